@@ -1,0 +1,119 @@
+/*
+ * mrs_model.h — flat, read-only view of a compiled MJCF model.
+ *
+ * This is the compiled-model contract shared by the product (the HIP step kernels, which pack it
+ * into a device constant block) and by the test oracle under oracle/ (which steps it on the CPU in
+ * fp64).  It plays the role of MuJoCo's mjModel for the subset of fields the hot path needs; field
+ * names follow mjModel so a maintainer can map them one-to-one.  The reference reads these mjModel
+ * fields directly (SURVEY.md §2 "mjModel fields read by the plugin"):
+ *   nq, nv, nu, nsensor, nsensordata, ncam            src/mujoco_system_interface.cpp:1193-1213
+ *   jnt_type, jnt_qposadr, jnt_dofadr                 src/mujoco_system_interface.cpp:1223-1226
+ *   actuator_trntype/trnid/biastype/biasprm           src/mujoco_system_interface.cpp:433-460,1200-1206
+ *   sensor_type, sensor_adr                           src/mujoco_lidar.cpp:130-200
+ *   cam_resolution, cam_fovy                          src/mujoco_cameras.cpp:45-47
+ *   vis.map.znear/zfar, stat.extent                   src/mujoco_cameras.cpp:222-223
+ *
+ * All arrays are owned by the model object that produced the view (mrs_model_view()).
+ * Layout: row-major, per-object blocks, doubles for reals (the model is compiled in fp64; the GPU
+ * packs a float32 copy).
+ */
+#ifndef MRS_MODEL_H
+#define MRS_MODEL_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* enum values follow MuJoCo 3.3 (mjtGeom, mjtJoint, mjtIntegrator, mjtSolver, mjtTrn, mjtGain,
+ * mjtBias, mjtDyn).  Sensor types are this project's own numbering (names match mjtSensor). */
+enum { MRS_GEOM_PLANE = 0, MRS_GEOM_HFIELD = 1, MRS_GEOM_SPHERE = 2, MRS_GEOM_CAPSULE = 3,
+       MRS_GEOM_ELLIPSOID = 4, MRS_GEOM_CYLINDER = 5, MRS_GEOM_BOX = 6, MRS_GEOM_MESH = 7 };
+enum { MRS_JNT_FREE = 0, MRS_JNT_BALL = 1, MRS_JNT_SLIDE = 2, MRS_JNT_HINGE = 3 };
+enum { MRS_INT_EULER = 0, MRS_INT_RK4 = 1, MRS_INT_IMPLICIT = 2, MRS_INT_IMPLICITFAST = 3 };
+enum { MRS_SOL_PGS = 0, MRS_SOL_CG = 1, MRS_SOL_NEWTON = 2 };
+enum { MRS_TRN_JOINT = 0 };
+enum { MRS_DYN_NONE = 0 };
+enum { MRS_GAIN_FIXED = 0, MRS_GAIN_AFFINE = 1 };
+enum { MRS_BIAS_NONE = 0, MRS_BIAS_AFFINE = 1 };
+enum { MRS_OBJ_UNKNOWN = 0, MRS_OBJ_BODY = 1, MRS_OBJ_JOINT = 3, MRS_OBJ_GEOM = 5, MRS_OBJ_SITE = 6,
+       MRS_OBJ_CAMERA = 7, MRS_OBJ_ACTUATOR = 19, MRS_OBJ_SENSOR = 20 };
+enum { MRS_SENS_ACCELEROMETER = 1, MRS_SENS_GYRO = 3, MRS_SENS_FORCE = 4, MRS_SENS_TORQUE = 5,
+       MRS_SENS_RANGEFINDER = 7, MRS_SENS_JOINTPOS = 9, MRS_SENS_JOINTVEL = 10,
+       MRS_SENS_ACTUATORFRC = 15, MRS_SENS_FRAMEPOS = 25, MRS_SENS_FRAMEQUAT = 26 };
+/* disable flags (mjtDisableBit subset) */
+enum { MRS_DSBL_CONSTRAINT = 1 << 0, MRS_DSBL_EQUALITY = 1 << 1, MRS_DSBL_FRICTIONLOSS = 1 << 2,
+       MRS_DSBL_LIMIT = 1 << 3, MRS_DSBL_CONTACT = 1 << 4, MRS_DSBL_PASSIVE = 1 << 5,
+       MRS_DSBL_GRAVITY = 1 << 6, MRS_DSBL_CLAMPCTRL = 1 << 7, MRS_DSBL_WARMSTART = 1 << 8,
+       MRS_DSBL_FILTERPARENT = 1 << 9, MRS_DSBL_ACTUATION = 1 << 10, MRS_DSBL_REFSAFE = 1 << 11,
+       MRS_DSBL_SENSOR = 1 << 12, MRS_DSBL_EULERDAMP = 1 << 15, MRS_DSBL_AUTORESET = 1 << 16 };
+
+#define MRS_NGAIN 10
+#define MRS_NBIAS 10
+#define MRS_NREF 2
+#define MRS_NIMP 5
+
+typedef struct mrs_model_view {
+  /* sizes */
+  int nq, nv, nu, na, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, nkey;
+  int nM;            /* nv*nv (dense joint-space matrices on this path) */
+  int max_depth;     /* longest root-to-leaf body chain (levels for tree-parallel passes) */
+
+  /* options (mjOption subset) */
+  double timestep, gravity[3], tolerance, impratio;
+  int integrator, solver, iterations, disableflags, cone;
+
+  /* statistic / visual (for the depth camera) */
+  double stat_extent, stat_center[3], stat_meaninertia, vis_znear, vis_zfar;
+
+  /* bodies: world is body 0 */
+  const int *body_parentid, *body_rootid, *body_weldid, *body_jntnum, *body_jntadr, *body_dofnum,
+      *body_dofadr, *body_geomnum, *body_geomadr, *body_depth;
+  const double *body_pos /*3*/, *body_quat /*4*/, *body_ipos /*3*/, *body_iquat /*4*/,
+      *body_mass, *body_subtreemass, *body_inertia /*3*/, *body_invweight0 /*2*/, *body_gravcomp;
+
+  /* joints */
+  const int *jnt_type, *jnt_qposadr, *jnt_dofadr, *jnt_bodyid, *jnt_limited, *jnt_actfrclimited;
+  const double *jnt_pos /*3*/, *jnt_axis /*3*/, *jnt_stiffness, *jnt_range /*2*/,
+      *jnt_actfrcrange /*2*/, *jnt_margin, *jnt_solref /*2*/, *jnt_solimp /*5*/;
+
+  /* dofs */
+  const int *dof_bodyid, *dof_jntid, *dof_parentid;
+  const double *dof_armature, *dof_damping, *dof_frictionloss, *dof_solref /*2*/,
+      *dof_solimp /*5*/, *dof_invweight0, *dof_M0;
+
+  /* geoms */
+  const int *geom_type, *geom_contype, *geom_conaffinity, *geom_condim, *geom_bodyid, *geom_group,
+      *geom_priority;
+  const double *geom_size /*3*/, *geom_pos /*3*/, *geom_quat /*4*/, *geom_rbound,
+      *geom_friction /*3*/, *geom_margin, *geom_gap, *geom_solmix, *geom_solref /*2*/,
+      *geom_solimp /*5*/, *geom_rgba /*4*/;
+
+  /* sites */
+  const int *site_bodyid;
+  const double *site_pos /*3*/, *site_quat /*4*/;
+
+  /* cameras */
+  const int *cam_bodyid, *cam_resolution /*2*/;
+  const double *cam_pos /*3*/, *cam_quat /*4*/, *cam_fovy;
+
+  /* actuators */
+  const int *actuator_trntype, *actuator_dyntype, *actuator_gaintype, *actuator_biastype,
+      *actuator_trnid /*2*/, *actuator_ctrllimited, *actuator_forcelimited;
+  const double *actuator_gear /*6*/, *actuator_gainprm /*10*/, *actuator_biasprm /*10*/,
+      *actuator_ctrlrange /*2*/, *actuator_forcerange /*2*/;
+
+  /* sensors */
+  const int *sensor_type, *sensor_objtype, *sensor_objid, *sensor_dim, *sensor_adr;
+  const double *sensor_cutoff;
+
+  /* default configuration */
+  const double *qpos0, *qpos_spring;
+
+  /* keyframes */
+  const double *key_time, *key_qpos, *key_qvel, *key_ctrl;
+} mrs_model_view;
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRS_MODEL_H */

@@ -1,0 +1,79 @@
+"""Build the product shared library libmrs.so in-tree (hipcc, gfx950) and the test oracle.
+
+`python -m mujoco_ros2_simulation_amd.build` compiles every C++/HIP source under csrc/ into
+mujoco_ros2_simulation_amd/libmrs.so; objects are cached under build/ keyed on source mtimes.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = ROOT / "build" / "obj"
+LIB = PKG / "libmrs.so"
+ARCH = os.environ.get("MRS_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
+CXX_SOURCES = ["capi.cc", "mjcf/compiler.cc", "mjcf/xml.cc"]
+HEADERS = ["hip/devmodel.h", "hip/batch.h", "mjcf/model.h", "mjcf/xml.h"]
+
+
+def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:
+    if not dst.exists():
+        return True
+    t = dst.stat().st_mtime
+    return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build failed: " + " ".join(cmd))
+
+
+def build_lib(verbose: bool = False) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    deps = [CSRC / h for h in HEADERS] + [ROOT / "include" / "mrs.h", ROOT / "include" / "mrs_model.h"]
+    objs = []
+    jobs = []
+    for rel in HIP_SOURCES + CXX_SOURCES:
+        src = CSRC / rel
+        obj = OBJ / (rel.replace("/", "_") + ".o")
+        objs.append(obj)
+        if not _newer(src, obj, deps):
+            continue
+        if rel.endswith(".hip"):
+            cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", str(src), "-o", str(obj)]
+        else:
+            cmd = ["hipcc", "-O2", "-std=c++17", "-fPIC", "-Wall", "-c", str(src), "-o", str(obj)]
+        jobs.append(cmd)
+    procs = [(cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)) for cmd in jobs]
+    failed = False
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            failed = True
+            sys.stderr.write(out)
+        elif verbose and out:
+            sys.stderr.write(out)
+    if failed:
+        raise RuntimeError("build of libmrs.so failed")
+    if jobs or not LIB.exists():
+        _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB)] + [str(o) for o in objs])
+    return LIB
+
+
+def build_oracle() -> Path:
+    """TEST INFRASTRUCTURE: the fp64 CPU oracle (oracle/Makefile)."""
+    _run(["make", "-s", "-C", str(ROOT / "oracle")])
+    return ROOT / "oracle" / "_build" / "liboracle.so"
+
+
+if __name__ == "__main__":
+    print(build_lib(verbose=True))
+    print(build_oracle())

@@ -1,0 +1,29 @@
+// Internal C++ interface between the C ABI (capi.cc) and the HIP batch implementation.
+#pragma once
+
+#include <stdexcept>
+#include <string>
+
+namespace mrs {
+
+struct Model;
+struct BatchImpl;
+
+struct DeviceError : std::runtime_error { using std::runtime_error::runtime_error; };
+struct UnsupportedError : std::runtime_error { using std::runtime_error::runtime_error; };
+
+BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_contacts);
+void batch_free(BatchImpl* b);
+int batch_num_envs(const BatchImpl* b);
+void batch_set_stream(BatchImpl* b, void* stream);
+void batch_reset(BatchImpl* b, int key, int env0, int n);
+void batch_set(BatchImpl* b, int field, const double* host, int env0, int n);
+void batch_get(BatchImpl* b, int field, double* host, int env0, int n);
+void* batch_device_ptr(BatchImpl* b, int field);
+void batch_set_ctrl_device(BatchImpl* b, const float* d_ctrl);
+void batch_launch(BatchImpl* b, int n_steps, bool forward_only);
+void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out);
+void batch_sync(BatchImpl* b);
+double batch_last_kernel_ms(BatchImpl* b, int kind);
+
+}  // namespace mrs

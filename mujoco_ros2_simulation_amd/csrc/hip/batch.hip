@@ -1,0 +1,646 @@
+// Batch of environments resident on one GPU: model packing, memory layouts, state transfer,
+// step/forward launches and the depth-camera kernel.  Host side of the C ABI in include/mrs.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/mrs.h"
+#include "../mjcf/model.h"
+#include "batch.h"
+#include "devmodel.h"
+
+namespace mrs {
+
+hipError_t launch_step(const DevModel& m, const LdsLayout& L, const ScratchLayout& S, const DevState& st,
+                       int n_envs, int n_steps, bool forward_only, hipStream_t stream);
+
+namespace {
+
+#define HIP_CHECK(x)                                                                         \
+  do {                                                                                       \
+    hipError_t err_ = (x);                                                                   \
+    if (err_ != hipSuccess)                                                                  \
+      throw DeviceError(std::string(#x) + " failed: " + hipGetErrorString(err_));            \
+  } while (0)
+
+// ------------------------------------------------------------------ depth camera kernel
+// One thread per pixel, one env per blockIdx.y; the env's geom poses are staged in LDS.
+// Eye-space depth: ray through the pixel centre with camera-frame direction (x, y, -1), so the ray
+// parameter of the nearest hit is the eye-space z that OpenGL + the plugin's linearisation
+// (src/mujoco_cameras.cpp:222-235) produce; rows in ROS order (flip of :229-240 applied).
+constexpr int kMaxRenderGeoms = 256;
+
+// analytic ray primitive (same restatement of engine_ray as the step kernel's rangefinder)
+__device__ float ray_prim(int type, const float* s, const float lp[3], const float lv[3]) {
+  auto quad = [](float a, float b, float c, float x[2]) {
+    float det = b * b - a * c;
+    if (det < 1e-15f) { x[0] = x[1] = -1; return -1.0f; }
+    det = sqrtf(det);
+    x[0] = (-b - det) / a;
+    x[1] = (-b + det) / a;
+    if (x[0] >= 0) return x[0];
+    if (x[1] >= 0) return x[1];
+    return -1.0f;
+  };
+  auto d3 = [](const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+  float x[2];
+  switch (type) {
+    case MRS_GEOM_PLANE: {
+      if (lv[2] > -1e-15f) return -1;
+      float t = -lp[2] / lv[2];
+      if (t < 0) return -1;
+      float p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
+      if ((s[0] <= 0 || fabsf(p0) <= s[0]) && (s[1] <= 0 || fabsf(p1) <= s[1])) return t;
+      return -1;
+    }
+    case MRS_GEOM_SPHERE: return quad(d3(lv, lv), d3(lv, lp), d3(lp, lp) - s[0] * s[0], x);
+    case MRS_GEOM_CAPSULE: {
+      float best = -1;
+      float a = lv[0] * lv[0] + lv[1] * lv[1];
+      if (a > 1e-15f) {
+        quad(a, lv[0] * lp[0] + lv[1] * lp[1], lp[0] * lp[0] + lp[1] * lp[1] - s[0] * s[0], x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && fabsf(lp[2] + x[i] * lv[2]) <= s[1] && (best < 0 || x[i] < best)) best = x[i];
+      }
+      for (int e = -1; e <= 1; e += 2) {
+        float q[3] = {lp[0], lp[1], lp[2] - e * s[1]};
+        quad(d3(lv, lv), d3(lv, q), d3(q, q) - s[0] * s[0], x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && e * (lp[2] + x[i] * lv[2] - e * s[1]) >= 0 && (best < 0 || x[i] < best)) best = x[i];
+      }
+      return best;
+    }
+    case MRS_GEOM_ELLIPSOID: {
+      float q[3] = {lp[0] / s[0], lp[1] / s[1], lp[2] / s[2]}, v[3] = {lv[0] / s[0], lv[1] / s[1], lv[2] / s[2]};
+      return quad(d3(v, v), d3(v, q), d3(q, q) - 1, x);
+    }
+    case MRS_GEOM_CYLINDER: {
+      float best = -1;
+      float a = lv[0] * lv[0] + lv[1] * lv[1];
+      if (a > 1e-15f) {
+        quad(a, lv[0] * lp[0] + lv[1] * lp[1], lp[0] * lp[0] + lp[1] * lp[1] - s[0] * s[0], x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && fabsf(lp[2] + x[i] * lv[2]) <= s[1] && (best < 0 || x[i] < best)) best = x[i];
+      }
+      if (fabsf(lv[2]) > 1e-15f)
+        for (int e = -1; e <= 1; e += 2) {
+          float t = (e * s[1] - lp[2]) / lv[2];
+          if (t < 0) continue;
+          float p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
+          if (p0 * p0 + p1 * p1 <= s[0] * s[0] && (best < 0 || t < best)) best = t;
+        }
+      return best;
+    }
+    case MRS_GEOM_BOX: {
+      float best = -1;
+      for (int i = 0; i < 3; ++i) {
+        if (fabsf(lv[i]) <= 1e-15f) continue;
+        int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+        for (int side = -1; side <= 1; side += 2) {
+          float t = (side * s[i] - lp[i]) / lv[i];
+          if (t < 0) continue;
+          float p1 = lp[i1] + t * lv[i1], p2 = lp[i2] + t * lv[i2];
+          if (fabsf(p1) <= s[i1] && fabsf(p2) <= s[i2] && (best < 0 || t < best)) best = t;
+        }
+      }
+      return best;
+    }
+  }
+  return -1;
+}
+
+
+__global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const int* geom_group,
+                                                    const float* geom_size, const float* geom_rbound,
+                                                    const float* geom_rgba, int ngeom, const float* geom_xpos,
+                                                    const float* geom_xmat, const float* cam_xpos,
+                                                    const float* cam_xmat, int ncam, int cam, int env0, int W,
+                                                    int H, float f, float znear, float zfar, float* out) {
+  __shared__ float gp[kMaxRenderGeoms * 3];
+  __shared__ float gm[kMaxRenderGeoms * 9];
+  __shared__ float cpos[3], cmat[9];
+  const int env = env0 + blockIdx.y;
+  const size_t eo = (size_t)env;
+  for (int i = threadIdx.x; i < 3 * ngeom; i += blockDim.x) gp[i] = geom_xpos[eo * 3 * ngeom + i];
+  for (int i = threadIdx.x; i < 9 * ngeom; i += blockDim.x) gm[i] = geom_xmat[eo * 9 * ngeom + i];
+  if (threadIdx.x < 3) cpos[threadIdx.x] = cam_xpos[(eo * ncam + cam) * 3 + threadIdx.x];
+  if (threadIdx.x < 9) cmat[threadIdx.x] = cam_xmat[(eo * ncam + cam) * 9 + threadIdx.x];
+  __syncthreads();
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= W * H) return;
+  const int row = pix / W, col = pix - row * W;
+  const float dc[3] = {(col + 0.5f - 0.5f * W) / f, (0.5f * H - row - 0.5f) / f, -1.0f};
+  const float vec[3] = {cmat[0] * dc[0] + cmat[1] * dc[1] + cmat[2] * dc[2],
+                        cmat[3] * dc[0] + cmat[4] * dc[1] + cmat[5] * dc[2],
+                        cmat[6] * dc[0] + cmat[7] * dc[1] + cmat[8] * dc[2]};
+  float best = -1;
+  for (int g = 0; g < ngeom; ++g) {
+    const int grp = geom_group[g];
+    if (grp < 0 || grp > 2 || geom_rgba[4 * g + 3] == 0) continue;
+    const float* p = gp + 3 * g;
+    const float* mm = gm + 9 * g;
+    const float dv[3] = {cpos[0] - p[0], cpos[1] - p[1], cpos[2] - p[2]};
+    const int t = geom_type[g];
+    if (t != MRS_GEOM_PLANE) {
+      // bounding-sphere reject: closest approach of the ray to the geom centre
+      const float vv = vec[0] * vec[0] + vec[1] * vec[1] + vec[2] * vec[2];
+      const float dvv = dv[0] * vec[0] + dv[1] * vec[1] + dv[2] * vec[2];
+      const float dd = dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2];
+      const float rb = geom_rbound[g];
+      if (dd - dvv * dvv / vv > rb * rb) continue;
+    }
+    const float lp[3] = {mm[0] * dv[0] + mm[3] * dv[1] + mm[6] * dv[2], mm[1] * dv[0] + mm[4] * dv[1] + mm[7] * dv[2],
+                         mm[2] * dv[0] + mm[5] * dv[1] + mm[8] * dv[2]};
+    const float lv[3] = {mm[0] * vec[0] + mm[3] * vec[1] + mm[6] * vec[2],
+                         mm[1] * vec[0] + mm[4] * vec[1] + mm[7] * vec[2],
+                         mm[2] * vec[0] + mm[5] * vec[1] + mm[8] * vec[2]};
+    const float tt = ray_prim(t, geom_size + 3 * g, lp, lv);
+    if (tt >= znear && (best < 0 || tt < best)) best = tt;
+  }
+  out[(size_t)blockIdx.y * W * H + pix] = (best < 0 || best > zfar) ? zfar : best;
+}
+
+// ------------------------------------------------------------------ packing helpers
+struct Packer {
+  std::vector<float> f;
+  std::vector<int> i;
+  std::vector<std::pair<const float**, size_t>> fptr;
+  std::vector<std::pair<const int**, size_t>> iptr;
+  void addf(const float** dst, const std::vector<double>& v) {
+    fptr.emplace_back(dst, f.size());
+    for (double x : v) f.push_back(static_cast<float>(x));
+    while (f.size() % 4) f.push_back(0);
+  }
+  void addf(const float** dst, const std::vector<float>& v) {
+    fptr.emplace_back(dst, f.size());
+    f.insert(f.end(), v.begin(), v.end());
+    while (f.size() % 4) f.push_back(0);
+  }
+  void addi(const int** dst, const std::vector<int>& v) {
+    iptr.emplace_back(dst, i.size());
+    i.insert(i.end(), v.begin(), v.end());
+    while (i.size() % 4) i.push_back(0);
+  }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ Batch implementation
+struct BatchImpl {
+  const Model* model = nullptr;
+  int n = 0, device = 0;
+  DevModel dm{};
+  LdsLayout L{};
+  ScratchLayout S{};
+  DevState st{};
+  void* dblock_f = nullptr;
+  void* dblock_i = nullptr;
+  std::vector<void*> allocs;
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
+  bool ev_valid[2] = {false, false};
+  std::vector<float> staging;
+};
+
+namespace {
+
+void* dalloc(BatchImpl& b, size_t bytes) {
+  void* p = nullptr;
+  HIP_CHECK(hipMalloc(&p, bytes ? bytes : 16));
+  HIP_CHECK(hipMemsetAsync(p, 0, bytes ? bytes : 16, b.stream));
+  b.allocs.push_back(p);
+  return p;
+}
+
+void build_devmodel(BatchImpl& b, int max_con_req) {
+  const Model& m = *b.model;
+  DevModel& d = b.dm;
+  if (m.nv > 64) throw UnsupportedError("nv > 64 is not supported by the one-wave-per-env kernel");
+  for (int s = 0; s < m.nsensor; ++s) {
+    int t = m.sensor_type[s];
+    if (t == MRS_SENS_ACCELEROMETER || t == MRS_SENS_FORCE || t == MRS_SENS_TORQUE)
+      throw UnsupportedError("accelerometer/force/torque sensors are not implemented on the GPU path yet");
+  }
+  d.nq = m.nq; d.nv = m.nv; d.nu = m.nu; d.nbody = m.nbody; d.njnt = m.njnt; d.ngeom = m.ngeom;
+  d.nsite = m.nsite; d.ncam = m.ncam; d.nsensor = m.nsensor; d.nsensordata = m.nsensordata;
+  d.max_depth = m.max_depth;
+  d.integrator = m.integrator; d.iterations = m.iterations; d.disableflags = m.disableflags;
+  d.timestep = static_cast<float>(m.timestep);
+  d.timestep_d = m.timestep;
+  d.tolerance = static_cast<float>(m.tolerance);
+  d.pgs_scale = static_cast<float>(1.0 / (m.stat_meaninertia * std::max(1, m.nv)));
+  for (int i = 0; i < 3; ++i) d.gravity[i] = static_cast<float>(m.gravity[i]);
+
+  // --- host precomputation of flat lists
+  std::vector<int> subtree_end(m.nbody);
+  for (int bI = m.nbody - 1; bI >= 0; --bI) {
+    int e = bI + 1;
+    while (e < m.nbody) {
+      int x = e;
+      bool inside = false;
+      while (x != 0) { if (x == bI) { inside = true; break; } x = m.body_parentid[x]; }
+      if (bI == 0) inside = true;
+      if (!inside) break;
+      ++e;
+    }
+    subtree_end[bI] = e;
+  }
+  std::vector<int> level_adr(m.max_depth + 2, 0), level_num(m.max_depth + 2, 0), level_body;
+  for (int lev = 1; lev <= m.max_depth; ++lev) {
+    level_adr[lev] = static_cast<int>(level_body.size());
+    for (int bI = 1; bI < m.nbody; ++bI)
+      if (m.body_depth[bI] == lev) level_body.push_back(bI);
+    level_num[lev] = static_cast<int>(level_body.size()) - level_adr[lev];
+  }
+  std::vector<int> Mpair;
+  for (int i = 0; i < m.nv; ++i)
+    for (int j = i; j >= 0; j = m.dof_parentid[j]) { Mpair.push_back(i); Mpair.push_back(j); }
+  d.nMpair = static_cast<int>(Mpair.size() / 2);
+  // static collision-pair filter (mj_collision broad phase minus the dynamic bounding test)
+  std::vector<int> pg1, pg2, pdim;
+  std::vector<float> pmargin, pgap, pfric, psolref, psolimp;
+  if (!(m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT))) {
+    for (int g1 = 0; g1 < m.ngeom; ++g1)
+      for (int g2 = g1 + 1; g2 < m.ngeom; ++g2) {
+        int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+        int w1 = m.body_weldid[b1], w2 = m.body_weldid[b2];
+        if (w1 == w2) continue;
+        if (!(m.disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
+            (w1 == m.body_weldid[m.body_parentid[w2]] || w2 == m.body_weldid[m.body_parentid[w1]]))
+          continue;
+        if (!((m.geom_contype[g1] & m.geom_conaffinity[g2]) || (m.geom_contype[g2] & m.geom_conaffinity[g1])))
+          continue;
+        int ga = g1, gb = g2;
+        if (m.geom_type[ga] > m.geom_type[gb]) std::swap(ga, gb);
+        int ta = m.geom_type[ga], tb = m.geom_type[gb];
+        bool ok = (ta == MRS_GEOM_PLANE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
+                  (ta == MRS_GEOM_SPHERE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
+                  (ta == MRS_GEOM_CAPSULE && (tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX));
+        if (!ok)
+          throw UnsupportedError("collision pair of geom types " + std::to_string(ta) + "/" + std::to_string(tb) +
+                                 " is not implemented (geoms " + std::to_string(g1) + "," + std::to_string(g2) + ")");
+        pg1.push_back(ga); pg2.push_back(gb);
+        pdim.push_back(std::max(m.geom_condim[ga], m.geom_condim[gb]));
+        pmargin.push_back(static_cast<float>(std::max(m.geom_margin[ga], m.geom_margin[gb])));
+        pgap.push_back(static_cast<float>(std::max(m.geom_gap[ga], m.geom_gap[gb])));
+        double s1 = m.geom_solmix[ga], s2 = m.geom_solmix[gb], mix;
+        if (s1 >= 1e-15 && s2 >= 1e-15) mix = s1 / (s1 + s2);
+        else if (s1 < 1e-15 && s2 < 1e-15) mix = 0.5;
+        else mix = s1 < 1e-15 ? 0 : 1;
+        for (int i = 0; i < 3; ++i)
+          pfric.push_back(static_cast<float>(std::max(m.geom_friction[3 * ga + i], m.geom_friction[3 * gb + i])));
+        for (int i = 0; i < 2; ++i)
+          psolref.push_back(static_cast<float>(mix * m.geom_solref[2 * ga + i] + (1 - mix) * m.geom_solref[2 * gb + i]));
+        for (int i = 0; i < 5; ++i)
+          psolimp.push_back(static_cast<float>(mix * m.geom_solimp[5 * ga + i] + (1 - mix) * m.geom_solimp[5 * gb + i]));
+      }
+  }
+  d.npair = static_cast<int>(pg1.size());
+  std::vector<int> fric, lim, rf;
+  for (int j = 0; j < m.nv; ++j) if (m.dof_frictionloss[j] > 0) fric.push_back(j);
+  for (int j = 0; j < m.njnt; ++j)
+    if (m.jnt_limited[j] && (m.jnt_type[j] == MRS_JNT_HINGE || m.jnt_type[j] == MRS_JNT_SLIDE)) lim.push_back(j);
+  for (int s = 0; s < m.nsensor; ++s) if (m.sensor_type[s] == MRS_SENS_RANGEFINDER) rf.push_back(s);
+  d.nfric = static_cast<int>(fric.size());
+  d.nlim = static_cast<int>(lim.size());
+  d.nrf = static_cast<int>(rf.size());
+  d.max_con = d.npair == 0 ? 0 : std::min(4 * d.npair, max_con_req);
+  d.max_efc = d.nfric + 2 * d.nlim + 4 * d.max_con;
+  // actuators
+  std::vector<int> act_dof, act_qadr;
+  std::vector<float> act_gear, act_gain, act_bias;
+  for (int a = 0; a < m.nu; ++a) {
+    int j = m.actuator_trnid[2 * a];
+    if (m.jnt_type[j] != MRS_JNT_HINGE && m.jnt_type[j] != MRS_JNT_SLIDE)
+      throw UnsupportedError("actuators on free/ball joints are not supported");
+    act_dof.push_back(m.jnt_dofadr[j]);
+    act_qadr.push_back(m.jnt_qposadr[j]);
+    act_gear.push_back(static_cast<float>(m.actuator_gear[6 * a]));
+    for (int i = 0; i < 3; ++i) {
+      act_gain.push_back(static_cast<float>(m.actuator_gainprm[MRS_NGAIN * a + i]));
+      act_bias.push_back(static_cast<float>(m.actuator_biasprm[MRS_NBIAS * a + i]));
+    }
+  }
+
+  Packer P;
+  P.addi(&d.body_parentid, m.body_parentid); P.addi(&d.body_rootid, m.body_rootid);
+  P.addi(&d.body_jntnum, m.body_jntnum); P.addi(&d.body_jntadr, m.body_jntadr);
+  P.addi(&d.body_dofnum, m.body_dofnum); P.addi(&d.body_dofadr, m.body_dofadr);
+  P.addi(&d.body_subtree_end, subtree_end); P.addi(&d.level_adr, level_adr);
+  P.addi(&d.level_num, level_num); P.addi(&d.level_body, level_body);
+  P.addf(&d.body_pos, m.body_pos); P.addf(&d.body_quat, m.body_quat); P.addf(&d.body_ipos, m.body_ipos);
+  P.addf(&d.body_iquat, m.body_iquat); P.addf(&d.body_mass, m.body_mass);
+  P.addf(&d.body_subtreemass, m.body_subtreemass); P.addf(&d.body_inertia, m.body_inertia);
+  P.addf(&d.body_gravcomp, m.body_gravcomp); P.addf(&d.body_invweight0, m.body_invweight0);
+  P.addi(&d.jnt_type, m.jnt_type); P.addi(&d.jnt_qposadr, m.jnt_qposadr); P.addi(&d.jnt_dofadr, m.jnt_dofadr);
+  P.addi(&d.jnt_bodyid, m.jnt_bodyid); P.addi(&d.jnt_actfrclimited, m.jnt_actfrclimited);
+  P.addf(&d.jnt_pos, m.jnt_pos); P.addf(&d.jnt_axis, m.jnt_axis); P.addf(&d.jnt_stiffness, m.jnt_stiffness);
+  P.addf(&d.jnt_range, m.jnt_range); P.addf(&d.jnt_margin, m.jnt_margin); P.addf(&d.jnt_solref, m.jnt_solref);
+  P.addf(&d.jnt_solimp, m.jnt_solimp); P.addf(&d.jnt_actfrcrange, m.jnt_actfrcrange);
+  P.addi(&d.dof_bodyid, m.dof_bodyid); P.addi(&d.dof_jntid, m.dof_jntid);
+  P.addf(&d.dof_armature, m.dof_armature); P.addf(&d.dof_damping, m.dof_damping);
+  P.addf(&d.dof_frictionloss, m.dof_frictionloss); P.addf(&d.dof_solref, m.dof_solref);
+  P.addf(&d.dof_solimp, m.dof_solimp); P.addf(&d.dof_invweight0, m.dof_invweight0);
+  P.addf(&d.qpos0, m.qpos0); P.addf(&d.qpos_spring, m.qpos_spring);
+  P.addi(&d.Mpair, Mpair);
+  P.addi(&d.geom_type, m.geom_type); P.addi(&d.geom_bodyid, m.geom_bodyid); P.addi(&d.geom_group, m.geom_group);
+  P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
+  P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
+  P.addi(&d.pair_g1, pg1); P.addi(&d.pair_g2, pg2); P.addi(&d.pair_dim, pdim);
+  P.addf(&d.pair_margin, pmargin); P.addf(&d.pair_gap, pgap); P.addf(&d.pair_friction, pfric);
+  P.addf(&d.pair_solref, psolref); P.addf(&d.pair_solimp, psolimp);
+  P.addi(&d.site_bodyid, m.site_bodyid); P.addf(&d.site_pos, m.site_pos); P.addf(&d.site_quat, m.site_quat);
+  P.addi(&d.cam_bodyid, m.cam_bodyid); P.addf(&d.cam_pos, m.cam_pos); P.addf(&d.cam_quat, m.cam_quat);
+  P.addi(&d.act_dof, act_dof); P.addi(&d.act_qadr, act_qadr);
+  P.addi(&d.act_gaintype, m.actuator_gaintype); P.addi(&d.act_biastype, m.actuator_biastype);
+  P.addi(&d.act_ctrllimited, m.actuator_ctrllimited); P.addi(&d.act_forcelimited, m.actuator_forcelimited);
+  P.addf(&d.act_gear, act_gear); P.addf(&d.act_gainprm, act_gain); P.addf(&d.act_biasprm, act_bias);
+  P.addf(&d.act_ctrlrange, m.actuator_ctrlrange); P.addf(&d.act_forcerange, m.actuator_forcerange);
+  P.addi(&d.sensor_type, m.sensor_type); P.addi(&d.sensor_objtype, m.sensor_objtype);
+  P.addi(&d.sensor_objid, m.sensor_objid); P.addi(&d.sensor_adr, m.sensor_adr); P.addi(&d.sensor_dim, m.sensor_dim);
+  P.addf(&d.sensor_cutoff, m.sensor_cutoff);
+  P.addi(&d.fric_dof, fric); P.addi(&d.lim_jnt, lim); P.addi(&d.rf_sensor, rf);
+
+  b.dblock_f = dalloc(b, P.f.size() * sizeof(float));
+  b.dblock_i = dalloc(b, P.i.size() * sizeof(int));
+  HIP_CHECK(hipMemcpyAsync(b.dblock_f, P.f.data(), P.f.size() * sizeof(float), hipMemcpyHostToDevice, b.stream));
+  HIP_CHECK(hipMemcpyAsync(b.dblock_i, P.i.data(), P.i.size() * sizeof(int), hipMemcpyHostToDevice, b.stream));
+  for (auto& kv : P.fptr) *kv.first = static_cast<const float*>(b.dblock_f) + kv.second;
+  for (auto& kv : P.iptr) *kv.first = static_cast<const int*>(b.dblock_i) + kv.second;
+  HIP_CHECK(hipStreamSynchronize(b.stream));
+
+  // --- LDS layout (floats)
+  LdsLayout& L = b.L;
+  int off = 0;
+  auto take = [&](int n) { int o = off; off += n; off = (off + 3) & ~3; return o; };
+  const int nb = m.nbody, nj = std::max(1, m.njnt), nv = std::max(1, m.nv), ng = std::max(1, m.ngeom);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.gxpos = take(3 * ng); L.gxmat = take(9 * ng);
+  L.scom = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb); L.cdof = take(6 * nv);
+  L.cdofdot = take(6 * nv); L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.cfrc = take(6 * nb);
+  L.M = take(nv * nv); L.L = take(nv * nv); L.qpos = take(std::max(1, m.nq)); L.qvel = take(nv);
+  L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);
+  L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
+  L.qacc = take(nv); L.qfrc_con = take(nv); L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
+  L.total = off;
+  if (static_cast<size_t>(L.total) * sizeof(float) * kEnvsPerBlock > 160 * 1024)
+    throw UnsupportedError("model too large for the per-wave LDS working set");
+  // --- scratch layout (floats)
+  ScratchLayout& S = b.S;
+  off = 0;
+  const int ne = std::max(1, d.max_efc);
+  S.efc_J = take(ne * nv); S.efc_MJ = take(ne * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
+  S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(ne); S.efc_aref = take(ne);
+  S.efc_b = take(ne); S.efc_f = take(ne); S.efc_ARii = take(ne); S.con = take(kConRec * std::max(1, d.max_con));
+  S.total = off;
+}
+
+int field_dim(const Model& m, int field) {
+  switch (field) {
+    case MRS_FIELD_QPOS: return m.nq;
+    case MRS_FIELD_QVEL: case MRS_FIELD_QFRC_APPLIED: case MRS_FIELD_QACC_WARMSTART: case MRS_FIELD_QACC:
+    case MRS_FIELD_QFRC_ACTUATOR: return m.nv;
+    case MRS_FIELD_CTRL: return m.nu;
+    case MRS_FIELD_SENSORDATA: return m.nsensordata;
+    case MRS_FIELD_TIME: return 1;
+    case MRS_FIELD_WARNING: return 4;
+    case MRS_FIELD_NCON: return 1;
+  }
+  return -1;
+}
+void* field_ptr(BatchImpl& b, int field) {
+  switch (field) {
+    case MRS_FIELD_QPOS: return b.st.qpos;
+    case MRS_FIELD_QVEL: return b.st.qvel;
+    case MRS_FIELD_CTRL: return b.st.ctrl;
+    case MRS_FIELD_QFRC_APPLIED: return b.st.qfrc_applied;
+    case MRS_FIELD_QACC_WARMSTART: return b.st.qacc_ws;
+    case MRS_FIELD_QACC: return b.st.qacc;
+    case MRS_FIELD_QFRC_ACTUATOR: return b.st.qfrc_act;
+    case MRS_FIELD_SENSORDATA: return b.st.sensordata;
+    case MRS_FIELD_TIME: return b.st.time;
+    case MRS_FIELD_WARNING: return b.st.warning;
+    case MRS_FIELD_NCON: return b.st.ncon;
+  }
+  return nullptr;
+}
+
+}  // namespace
+
+BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_contacts) {
+  if (n_envs < 1) throw std::invalid_argument("n_envs must be positive");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) throw DeviceError("no HIP device available");
+  if (device < 0 || device >= ndev) throw std::invalid_argument("device index out of range");
+  HIP_CHECK(hipSetDevice(device));
+  auto* b = new BatchImpl();
+  try {
+    b->model = model;
+    b->n = n_envs;
+    b->device = device;
+    HIP_CHECK(hipStreamCreateWithFlags(&b->own_stream, hipStreamNonBlocking));
+    b->stream = b->own_stream;
+    for (int k = 0; k < 2; ++k) { HIP_CHECK(hipEventCreate(&b->ev0[k])); HIP_CHECK(hipEventCreate(&b->ev1[k])); }
+    build_devmodel(*b, max_contacts);
+    const Model& m = *model;
+    const size_t n = static_cast<size_t>(n_envs);
+    b->st.qpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.nq) * sizeof(float)));
+    b->st.qvel = static_cast<float*>(dalloc(*b, n * std::max(1, m.nv) * sizeof(float)));
+    b->st.ctrl = static_cast<float*>(dalloc(*b, n * std::max(1, m.nu) * sizeof(float)));
+    b->st.qfrc_applied = static_cast<float*>(dalloc(*b, n * std::max(1, m.nv) * sizeof(float)));
+    b->st.qacc_ws = static_cast<float*>(dalloc(*b, n * std::max(1, m.nv) * sizeof(float)));
+    b->st.qacc = static_cast<float*>(dalloc(*b, n * std::max(1, m.nv) * sizeof(float)));
+    b->st.qfrc_act = static_cast<float*>(dalloc(*b, n * std::max(1, m.nv) * sizeof(float)));
+    b->st.sensordata = static_cast<float*>(dalloc(*b, n * std::max(1, m.nsensordata) * sizeof(float)));
+    b->st.time = static_cast<double*>(dalloc(*b, n * sizeof(double)));
+    b->st.warning = static_cast<int*>(dalloc(*b, n * 4 * sizeof(int)));
+    b->st.ncon = static_cast<int*>(dalloc(*b, n * sizeof(int)));
+    b->st.scratch = static_cast<float*>(dalloc(*b, n * b->S.total * sizeof(float)));
+    b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));
+    b->st.geom_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 9 * sizeof(float)));
+    b->st.cam_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ncam) * 3 * sizeof(float)));
+    b->st.cam_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ncam) * 9 * sizeof(float)));
+    batch_reset(b, -1, 0, n_envs);
+    batch_launch(b, 1, true);  // mj_forward after load (src/mujoco_system_interface.cpp:741)
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+  } catch (...) {
+    batch_free(b);
+    throw;
+  }
+  return b;
+}
+
+void batch_free(BatchImpl* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->device);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  for (void* p : b->allocs) (void)hipFree(p);
+  for (int k = 0; k < 2; ++k) {
+    if (b->ev0[k]) (void)hipEventDestroy(b->ev0[k]);
+    if (b->ev1[k]) (void)hipEventDestroy(b->ev1[k]);
+  }
+  if (b->own_stream) (void)hipStreamDestroy(b->own_stream);
+  delete b;
+}
+
+int batch_num_envs(const BatchImpl* b) { return b->n; }
+
+void batch_set_stream(BatchImpl* b, void* stream) {
+  b->stream = stream ? static_cast<hipStream_t>(stream) : b->own_stream;
+}
+
+void batch_reset(BatchImpl* b, int key, int env0, int n) {
+  const Model& m = *b->model;
+  if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
+  if (key >= m.nkey) throw std::invalid_argument("keyframe index out of range");
+  HIP_CHECK(hipSetDevice(b->device));
+  std::vector<double> qpos(static_cast<size_t>(n) * m.nq), qvel(static_cast<size_t>(n) * m.nv, 0.0),
+      ctrl(static_cast<size_t>(n) * m.nu, 0.0), zeros(static_cast<size_t>(n) * m.nv, 0.0), t(n, 0.0);
+  for (int e = 0; e < n; ++e) {
+    const double* q0 = key >= 0 ? &m.key_qpos[static_cast<size_t>(key) * m.nq] : m.qpos0.data();
+    std::copy(q0, q0 + m.nq, &qpos[static_cast<size_t>(e) * m.nq]);
+    if (key >= 0) {
+      std::copy(&m.key_qvel[static_cast<size_t>(key) * m.nv], &m.key_qvel[static_cast<size_t>(key) * m.nv] + m.nv,
+                &qvel[static_cast<size_t>(e) * m.nv]);
+      std::copy(&m.key_ctrl[static_cast<size_t>(key) * m.nu], &m.key_ctrl[static_cast<size_t>(key) * m.nu] + m.nu,
+                &ctrl[static_cast<size_t>(e) * m.nu]);
+      t[e] = m.key_time[key];
+    }
+  }
+  batch_set(b, MRS_FIELD_QPOS, qpos.data(), env0, n);
+  batch_set(b, MRS_FIELD_QVEL, qvel.data(), env0, n);
+  batch_set(b, MRS_FIELD_CTRL, ctrl.data(), env0, n);
+  batch_set(b, MRS_FIELD_QFRC_APPLIED, zeros.data(), env0, n);
+  batch_set(b, MRS_FIELD_QACC_WARMSTART, zeros.data(), env0, n);
+  batch_set(b, MRS_FIELD_TIME, t.data(), env0, n);
+  std::vector<double> w(static_cast<size_t>(n) * 4, 0.0);
+  batch_set(b, MRS_FIELD_WARNING, w.data(), env0, n);
+}
+
+void batch_set(BatchImpl* b, int field, const double* host, int env0, int n) {
+  const Model& m = *b->model;
+  int dim = field_dim(m, field);
+  if (dim < 0) throw std::invalid_argument("unknown field");
+  if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
+  if (n == 0 || dim == 0) return;
+  HIP_CHECK(hipSetDevice(b->device));
+  const size_t cnt = static_cast<size_t>(n) * dim;
+  char* dst = static_cast<char*>(field_ptr(*b, field));
+  if (field == MRS_FIELD_TIME) {
+    HIP_CHECK(hipMemcpyAsync(dst + sizeof(double) * env0, host, cnt * sizeof(double), hipMemcpyHostToDevice, b->stream));
+  } else if (field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON) {
+    std::vector<int> tmp(cnt);
+    for (size_t i = 0; i < cnt; ++i) tmp[i] = static_cast<int>(host[i]);
+    HIP_CHECK(hipMemcpyAsync(dst + sizeof(int) * static_cast<size_t>(env0) * dim, tmp.data(), cnt * sizeof(int),
+                             hipMemcpyHostToDevice, b->stream));
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+    return;
+  } else {
+    std::vector<float> tmp(cnt);
+    for (size_t i = 0; i < cnt; ++i) tmp[i] = static_cast<float>(host[i]);
+    HIP_CHECK(hipMemcpyAsync(dst + sizeof(float) * static_cast<size_t>(env0) * dim, tmp.data(), cnt * sizeof(float),
+                             hipMemcpyHostToDevice, b->stream));
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+    return;
+  }
+  HIP_CHECK(hipStreamSynchronize(b->stream));
+}
+
+void batch_get(BatchImpl* b, int field, double* host, int env0, int n) {
+  const Model& m = *b->model;
+  int dim = field_dim(m, field);
+  if (dim < 0) throw std::invalid_argument("unknown field");
+  if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
+  if (n == 0 || dim == 0) return;
+  HIP_CHECK(hipSetDevice(b->device));
+  const size_t cnt = static_cast<size_t>(n) * dim;
+  const char* src = static_cast<const char*>(field_ptr(*b, field));
+  if (field == MRS_FIELD_TIME) {
+    HIP_CHECK(hipMemcpyAsync(host, src + sizeof(double) * env0, cnt * sizeof(double), hipMemcpyDeviceToHost, b->stream));
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+  } else if (field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON) {
+    std::vector<int> tmp(cnt);
+    HIP_CHECK(hipMemcpyAsync(tmp.data(), src + sizeof(int) * static_cast<size_t>(env0) * dim, cnt * sizeof(int),
+                             hipMemcpyDeviceToHost, b->stream));
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+    for (size_t i = 0; i < cnt; ++i) host[i] = tmp[i];
+  } else {
+    std::vector<float> tmp(cnt);
+    HIP_CHECK(hipMemcpyAsync(tmp.data(), src + sizeof(float) * static_cast<size_t>(env0) * dim, cnt * sizeof(float),
+                             hipMemcpyDeviceToHost, b->stream));
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+    for (size_t i = 0; i < cnt; ++i) host[i] = tmp[i];
+  }
+}
+
+void* batch_device_ptr(BatchImpl* b, int field) { return field_ptr(*b, field); }
+
+void batch_set_ctrl_device(BatchImpl* b, const float* d_ctrl) {
+  const Model& m = *b->model;
+  if (m.nu == 0) return;
+  HIP_CHECK(hipSetDevice(b->device));
+  HIP_CHECK(hipMemcpyAsync(b->st.ctrl, d_ctrl, static_cast<size_t>(b->n) * m.nu * sizeof(float),
+                           hipMemcpyDeviceToDevice, b->stream));
+}
+
+void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
+  if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
+  HIP_CHECK(hipSetDevice(b->device));
+  HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
+  HIP_CHECK(launch_step(b->dm, b->L, b->S, b->st, b->n, n_steps, forward_only, b->stream));
+  HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
+  b->ev_valid[0] = true;
+}
+
+void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out) {
+  const Model& m = *b->model;
+  if (cam < 0 || cam >= m.ncam) throw std::invalid_argument("camera index out of range");
+  if (env0 < 0 || n < 1 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
+  if (m.ngeom > kMaxRenderGeoms) throw UnsupportedError("too many geoms for the depth kernel");
+  HIP_CHECK(hipSetDevice(b->device));
+  const int W = m.cam_resolution[2 * cam], H = m.cam_resolution[2 * cam + 1];
+  const size_t bytes = static_cast<size_t>(n) * W * H * sizeof(float);
+  float* dout = out;
+  void* tmp = nullptr;
+  if (!device_out) {
+    HIP_CHECK(hipMallocAsync(&tmp, bytes, b->stream));
+    dout = static_cast<float*>(tmp);
+  }
+  const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
+  const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
+  const DevModel& d = b->dm;
+  dim3 grid((W * H + 255) / 256, n);
+  HIP_CHECK(hipEventRecord(b->ev0[1], b->stream));
+  hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type, d.geom_group, d.geom_size, d.geom_rbound,
+                     d.geom_rgba, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
+                     cam, env0, W, H, f, znear, zfar, dout);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(b->ev1[1], b->stream));
+  b->ev_valid[1] = true;
+  if (!device_out) {
+    HIP_CHECK(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, b->stream));
+    HIP_CHECK(hipFreeAsync(tmp, b->stream));
+    HIP_CHECK(hipStreamSynchronize(b->stream));
+  }
+}
+
+void batch_sync(BatchImpl* b) {
+  HIP_CHECK(hipSetDevice(b->device));
+  HIP_CHECK(hipStreamSynchronize(b->stream));
+}
+
+double batch_last_kernel_ms(BatchImpl* b, int kind) {
+  if (kind < 0 || kind > 1 || !b->ev_valid[kind]) return -1;
+  HIP_CHECK(hipSetDevice(b->device));
+  HIP_CHECK(hipEventSynchronize(b->ev1[kind]));
+  float ms = -1;
+  if (hipEventElapsedTime(&ms, b->ev0[kind], b->ev1[kind]) != hipSuccess) return -1;
+  return ms;
+}
+
+}  // namespace mrs

@@ -1,0 +1,1431 @@
+// Fused batched mj_step for CDNA4 (gfx950): one wavefront per environment.
+//
+// Replaces the mj_step call of the reference's physics loop (src/mujoco_system_interface.cpp:1691,
+// 1731) and mj_forward (:741,1771) for N environments at once.  Each wave keeps its environment's
+// kinematic/dynamic working set in LDS (layout: devmodel.h LdsLayout) for all fused steps of a
+// launch; lanes work in parallel over bodies of one tree level, over geoms, dofs, mass-matrix
+// entries, constraint rows, collision pairs and rangefinder rays; reductions and broadcasts use
+// wavefront shuffles.  Constraint rows live in a per-env global scratch region (L2-resident).
+// State in HBM is read once and written once per launch.  Pipeline stages mirror MuJoCo 3.3.4
+// (see oracle/oracle.c for the fp64 restatement each stage is checked against).
+#include <hip/hip_runtime.h>
+
+#include "devmodel.h"
+
+namespace mrs {
+
+namespace {
+
+constexpr float kMinVal = 1e-15f;
+constexpr float kMaxVal = 1e10f;
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  total = __shfl(x, 63);
+  return x - v;
+}
+__device__ __forceinline__ float bcast(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+
+// ------------------------------------------------------------------ small math (fp32)
+__device__ __forceinline__ void quat_mul(float r[4], const float a[4], const float b[4]) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void quat_normalize(float q[4]) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < kMinVal) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float in = 1.0f / n;
+  q[0] *= in; q[1] *= in; q[2] *= in; q[3] *= in;
+}
+__device__ __forceinline__ void quat2mat(float m[9], const float q[4]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = w * w + x * x - y * y - z * z; m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = w * w - x * x + y * y - z * z; m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = w * w - x * x - y * y + z * z;
+}
+__device__ __forceinline__ void mat_vec(float r[3], const float m[9], const float v[3]) {
+  float a = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  float b = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  float c = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = a; r[1] = b; r[2] = c;
+}
+__device__ __forceinline__ void matT_vec(float r[3], const float m[9], const float v[3]) {
+  float a = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  float b = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  float c = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = a; r[1] = b; r[2] = c;
+}
+__device__ __forceinline__ void rot_quat(float r[3], const float v[3], const float q[4]) {
+  float m[9];
+  quat2mat(m, q);
+  mat_vec(r, m, v);
+}
+__device__ __forceinline__ void cross3(float r[3], const float a[3], const float b[3]) {
+  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  r[0] = x; r[1] = y; r[2] = z;
+}
+__device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+__device__ __forceinline__ float normalize3(float a[3]) {
+  float n = sqrtf(dot3(a, a));
+  if (n < kMinVal) { a[0] = 1; a[1] = a[2] = 0; return n; }
+  float in = 1.0f / n;
+  a[0] *= in; a[1] *= in; a[2] *= in;
+  return n;
+}
+__device__ __forceinline__ void axis_angle_quat(float q[4], const float ax[3], float ang) {
+  float s, c;
+  sincosf(0.5f * ang, &s, &c);
+  q[0] = c; q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
+}
+__device__ __forceinline__ void mul_inert_vec(float r[6], const float* i, const float v[6]) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* u) {
+  float t0 = -v[2] * u[1] + v[1] * u[2];
+  float t1 = v[2] * u[0] - v[0] * u[2];
+  float t2 = -v[1] * u[0] + v[0] * u[1];
+  float t3 = -v[2] * u[4] + v[1] * u[5] - v[5] * u[1] + v[4] * u[2];
+  float t4 = v[2] * u[3] - v[0] * u[5] + v[5] * u[0] - v[3] * u[2];
+  float t5 = -v[1] * u[3] + v[0] * u[4] - v[4] * u[0] + v[3] * u[1];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3; r[4] = t4; r[5] = t5;
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  float t0 = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
+  float t1 = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
+  float t2 = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
+  float t3 = -v[2] * f[4] + v[1] * f[5];
+  float t4 = v[2] * f[3] - v[0] * f[5];
+  float t5 = -v[1] * f[3] + v[0] * f[4];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3; r[4] = t4; r[5] = t5;
+}
+__device__ __forceinline__ bool is_bad(float x) { return !(x == x) || x > kMaxVal || x < -kMaxVal; }
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// ------------------------------------------------------------------ ray primitives (engine_ray)
+__device__ __forceinline__ float ray_quad(float a, float b, float c, float x[2]) {
+  float det = b * b - a * c;
+  if (det < kMinVal) { x[0] = x[1] = -1; return -1; }
+  det = sqrtf(det);
+  float ia = 1.0f / a;
+  x[0] = (-b - det) * ia;
+  x[1] = (-b + det) * ia;
+  if (x[0] >= 0) return x[0];
+  if (x[1] >= 0) return x[1];
+  return -1;
+}
+__device__ float ray_geom_local(int type, const float* s, const float lp[3], const float lv[3]) {
+  float x[2];
+  switch (type) {
+    case MRS_GEOM_PLANE: {
+      if (lv[2] > -kMinVal) return -1;
+      float t = -lp[2] / lv[2];
+      if (t < 0) return -1;
+      float p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
+      if ((s[0] <= 0 || fabsf(p0) <= s[0]) && (s[1] <= 0 || fabsf(p1) <= s[1])) return t;
+      return -1;
+    }
+    case MRS_GEOM_SPHERE:
+      return ray_quad(dot3(lv, lv), dot3(lv, lp), dot3(lp, lp) - s[0] * s[0], x);
+    case MRS_GEOM_CAPSULE: {
+      float best = -1;
+      float a = lv[0] * lv[0] + lv[1] * lv[1];
+      if (a > kMinVal) {
+        float b = lv[0] * lp[0] + lv[1] * lp[1], c = lp[0] * lp[0] + lp[1] * lp[1] - s[0] * s[0];
+        ray_quad(a, b, c, x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && fabsf(lp[2] + x[i] * lv[2]) <= s[1] && (best < 0 || x[i] < best)) best = x[i];
+      }
+      float vv = dot3(lv, lv);
+      for (int e = -1; e <= 1; e += 2) {
+        float q[3] = {lp[0], lp[1], lp[2] - e * s[1]};
+        ray_quad(vv, dot3(lv, q), dot3(q, q) - s[0] * s[0], x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && e * (lp[2] + x[i] * lv[2] - e * s[1]) >= 0 && (best < 0 || x[i] < best)) best = x[i];
+      }
+      return best;
+    }
+    case MRS_GEOM_ELLIPSOID: {
+      float q[3] = {lp[0] / s[0], lp[1] / s[1], lp[2] / s[2]}, v[3] = {lv[0] / s[0], lv[1] / s[1], lv[2] / s[2]};
+      return ray_quad(dot3(v, v), dot3(v, q), dot3(q, q) - 1, x);
+    }
+    case MRS_GEOM_CYLINDER: {
+      float best = -1;
+      float a = lv[0] * lv[0] + lv[1] * lv[1];
+      if (a > kMinVal) {
+        float b = lv[0] * lp[0] + lv[1] * lp[1], c = lp[0] * lp[0] + lp[1] * lp[1] - s[0] * s[0];
+        ray_quad(a, b, c, x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && fabsf(lp[2] + x[i] * lv[2]) <= s[1] && (best < 0 || x[i] < best)) best = x[i];
+      }
+      if (fabsf(lv[2]) > kMinVal)
+        for (int e = -1; e <= 1; e += 2) {
+          float t = (e * s[1] - lp[2]) / lv[2];
+          if (t < 0) continue;
+          float p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
+          if (p0 * p0 + p1 * p1 <= s[0] * s[0] && (best < 0 || t < best)) best = t;
+        }
+      return best;
+    }
+    case MRS_GEOM_BOX: {
+      float best = -1;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (fabsf(lv[i]) <= kMinVal) continue;
+        int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+        float inv = 1.0f / lv[i];
+#pragma unroll
+        for (int side = -1; side <= 1; side += 2) {
+          float t = (side * s[i] - lp[i]) * inv;
+          if (t < 0) continue;
+          float p1 = lp[i1] + t * lv[i1], p2 = lp[i2] + t * lv[i2];
+          if (fabsf(p1) <= s[i1] && fabsf(p2) <= s[i2] && (best < 0 || t < best)) best = t;
+        }
+      }
+      return best;
+    }
+  }
+  return -1;
+}
+
+// ------------------------------------------------------------------ collision primitives
+struct Con { float dist, pos[3], nrm[3]; };
+
+__device__ __forceinline__ int sphere_sphere(const float p1[3], float r1, const float p2[3], float r2,
+                                             float margin, Con* out, int n) {
+  float dv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  float len = sqrtf(dot3(dv, dv));
+  float dist = len - r1 - r2;
+  if (dist > margin || n >= 4) return n;
+  Con& c = out[n];
+  if (len < kMinVal) { c.nrm[0] = 1; c.nrm[1] = c.nrm[2] = 0; }
+  else { float il = 1.0f / len; c.nrm[0] = dv[0] * il; c.nrm[1] = dv[1] * il; c.nrm[2] = dv[2] * il; }
+  for (int i = 0; i < 3; ++i) c.pos[i] = p1[i] + c.nrm[i] * (r1 + dist / 2);
+  c.dist = dist;
+  return n + 1;
+}
+__device__ __forceinline__ void seg_point_closest(const float a[3], const float b[3], const float p[3], float c[3]) {
+  float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  float den = dot3(ab, ab), t = den > kMinVal ? dot3(ap, ab) / den : 0;
+  t = clampf(t, 0, 1);
+  for (int i = 0; i < 3; ++i) c[i] = a[i] + t * ab[i];
+}
+__device__ void seg_seg_closest(const float a0[3], const float a1[3], const float b0[3], const float b1[3],
+                                float ca[3], float cb[3]) {
+  float d1[3] = {a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]};
+  float d2[3] = {b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2]};
+  float r[3] = {a0[0] - b0[0], a0[1] - b0[1], a0[2] - b0[2]};
+  float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  float s = 0, t = 0;
+  if (a <= kMinVal && e <= kMinVal) { s = t = 0; }
+  else if (a <= kMinVal) { s = 0; t = clampf(f / e, 0, 1); }
+  else {
+    float c = dot3(d1, r);
+    if (e <= kMinVal) { t = 0; s = clampf(-c / a, 0, 1); }
+    else {
+      float bb = dot3(d1, d2), den = a * e - bb * bb;
+      s = den > kMinVal * a * e ? clampf((bb * f - c * e) / den, 0, 1) : 0;
+      t = (bb * s + f) / e;
+      if (t < 0) { t = 0; s = clampf(-c / a, 0, 1); }
+      else if (t > 1) { t = 1; s = clampf((bb - c) / a, 0, 1); }
+    }
+  }
+  for (int i = 0; i < 3; ++i) { ca[i] = a0[i] + s * d1[i]; cb[i] = b0[i] + t * d2[i]; }
+}
+__device__ __forceinline__ int plane_sphere(const float* pp, const float* pm, const float p[3], float r,
+                                            float margin, Con* out, int n) {
+  float nrm[3] = {pm[2], pm[5], pm[8]};
+  float dv[3] = {p[0] - pp[0], p[1] - pp[1], p[2] - pp[2]};
+  float dist = dot3(dv, nrm) - r;
+  if (dist > margin || n >= 4) return n;
+  Con& c = out[n];
+  for (int i = 0; i < 3; ++i) { c.pos[i] = p[i] - nrm[i] * (r + dist / 2); c.nrm[i] = nrm[i]; }
+  c.dist = dist;
+  return n + 1;
+}
+__device__ int plane_box(const float* pp, const float* pm, const float* bp, const float* bm, const float* size,
+                         float margin, Con* out, int n) {
+  float nrm[3] = {pm[2], pm[5], pm[8]};
+  float dv[3] = {bp[0] - pp[0], bp[1] - pp[1], bp[2] - pp[2]};
+  float cdist = dot3(dv, nrm);
+  for (int k = 0; k < 8 && n < 4; ++k) {
+    float v[3] = {(k & 1) ? size[0] : -size[0], (k & 2) ? size[1] : -size[1], (k & 4) ? size[2] : -size[2]};
+    float c[3];
+    mat_vec(c, bm, v);
+    float ld = dot3(nrm, c);
+    float dist = cdist + ld;
+    if (dist > margin || ld > 0) continue;
+    Con& o = out[n++];
+    for (int i = 0; i < 3; ++i) { o.pos[i] = bp[i] + c[i] - nrm[i] * dist / 2; o.nrm[i] = nrm[i]; }
+    o.dist = dist;
+  }
+  return n;
+}
+__device__ int sphere_box(const float p[3], float r, const float* bp, const float* bm, const float* size,
+                          float margin, Con* out, int n) {
+  float dv[3] = {p[0] - bp[0], p[1] - bp[1], p[2] - bp[2]}, l[3];
+  matT_vec(l, bm, dv);
+  float c[3];
+  bool inside = true;
+  for (int i = 0; i < 3; ++i) {
+    c[i] = clampf(l[i], -size[i], size[i]);
+    if (c[i] != l[i]) inside = false;
+  }
+  float nl[3], dist;
+  if (!inside) {
+    float dl[3] = {c[0] - l[0], c[1] - l[1], c[2] - l[2]};
+    float len = sqrtf(dot3(dl, dl));
+    dist = len - r;
+    if (dist > margin) return n;
+    for (int i = 0; i < 3; ++i) nl[i] = dl[i] / len;
+  } else {
+    int ax = 0;
+    float best = 1e30f;
+    for (int i = 0; i < 3; ++i) {
+      float pen = size[i] - fabsf(l[i]);
+      if (pen < best) { best = pen; ax = i; }
+    }
+    dist = -best - r;
+    nl[0] = nl[1] = nl[2] = 0;
+    nl[ax] = l[ax] >= 0 ? -1.0f : 1.0f;
+  }
+  if (n >= 4) return n;
+  Con& o = out[n];
+  mat_vec(o.nrm, bm, nl);
+  for (int i = 0; i < 3; ++i) o.pos[i] = p[i] + o.nrm[i] * (r + dist / 2);
+  o.dist = dist;
+  return n + 1;
+}
+__device__ __forceinline__ float box_dist2(const float l[3], const float* size) {
+  float s = 0;
+  for (int i = 0; i < 3; ++i) {
+    float e = fabsf(l[i]) - size[i];
+    if (e > 0) s += e * e;
+  }
+  return s;
+}
+__device__ int capsule_box(const float a[3], const float b[3], float r, const float* bp, const float* bm,
+                           const float* size, float margin, Con* out, int n) {
+  float lo = 0, hi = 1;
+  for (int it = 0; it < 40; ++it) {
+    float t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3, p1[3], p2[3], l1[3], l2[3];
+    for (int i = 0; i < 3; ++i) {
+      p1[i] = a[i] + t1 * (b[i] - a[i]) - bp[i];
+      p2[i] = a[i] + t2 * (b[i] - a[i]) - bp[i];
+    }
+    matT_vec(l1, bm, p1);
+    matT_vec(l2, bm, p2);
+    if (box_dist2(l1, size) <= box_dist2(l2, size)) hi = t2;
+    else lo = t1;
+  }
+  float t = 0.5f * (lo + hi), p[3];
+  for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
+  return sphere_box(p, r, bp, bm, size, margin, out, n);
+}
+__device__ __forceinline__ void capsule_ends(const float* pos, const float* mat, float hl, float a[3], float b[3]) {
+  for (int i = 0; i < 3; ++i) { a[i] = pos[i] - mat[3 * i + 2] * hl; b[i] = pos[i] + mat[3 * i + 2] * hl; }
+}
+__device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
+                           const float* m2, const float* s2, float margin, Con* out) {
+  float a1[3], b1[3], a2[3], b2[3], c1[3], c2[3];
+  int n = 0;
+  if (t1 == MRS_GEOM_PLANE) {
+    if (t2 == MRS_GEOM_SPHERE) return plane_sphere(p1, m1, p2, s2[0], margin, out, 0);
+    if (t2 == MRS_GEOM_CAPSULE) {
+      capsule_ends(p2, m2, s2[1], a2, b2);
+      n = plane_sphere(p1, m1, a2, s2[0], margin, out, 0);
+      return plane_sphere(p1, m1, b2, s2[0], margin, out, n);
+    }
+    if (t2 == MRS_GEOM_BOX) return plane_box(p1, m1, p2, m2, s2, margin, out, 0);
+  } else if (t1 == MRS_GEOM_SPHERE) {
+    if (t2 == MRS_GEOM_SPHERE) return sphere_sphere(p1, s1[0], p2, s2[0], margin, out, 0);
+    if (t2 == MRS_GEOM_CAPSULE) {
+      capsule_ends(p2, m2, s2[1], a2, b2);
+      seg_point_closest(a2, b2, p1, c2);
+      return sphere_sphere(p1, s1[0], c2, s2[0], margin, out, 0);
+    }
+    if (t2 == MRS_GEOM_BOX) return sphere_box(p1, s1[0], p2, m2, s2, margin, out, 0);
+  } else if (t1 == MRS_GEOM_CAPSULE) {
+    if (t2 == MRS_GEOM_CAPSULE) {
+      capsule_ends(p1, m1, s1[1], a1, b1);
+      capsule_ends(p2, m2, s2[1], a2, b2);
+      seg_seg_closest(a1, b1, a2, b2, c1, c2);
+      return sphere_sphere(c1, s1[0], c2, s2[0], margin, out, 0);
+    }
+    if (t2 == MRS_GEOM_BOX) {
+      capsule_ends(p1, m1, s1[1], a1, b1);
+      return capsule_box(a1, b1, s1[0], p2, m2, s2, margin, out, 0);
+    }
+  }
+  return 0;
+}
+// mju_makeFrame: tangent basis from the contact normal
+__device__ __forceinline__ void make_frame(float f[9]) {
+  normalize3(f);
+  if (fabsf(f[1]) < 0.5f) { f[3] = 0; f[4] = 1; f[5] = 0; }
+  else { f[3] = 0; f[4] = 0; f[5] = 1; }
+  float dd = dot3(f, f + 3);
+  for (int i = 0; i < 3; ++i) f[3 + i] -= dd * f[i];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+__device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
+  float dmin = clampf(si[0], 0.0001f, 0.9999f), dmax = clampf(si[1], 0.0001f, 0.9999f);
+  float width = si[2], mid = si[3], power = si[4];
+  if (dmin == dmax || width <= kMinVal) return 0.5f * (dmin + dmax);
+  float x = fabsf(pos - margin) / width;
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  float y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1);
+  else y = 1 - powf(1 - x, power) / powf(1 - mid, power - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
+
+// ------------------------------------------------------------------ environment context
+struct Env {
+  const DevModel& m;
+  const LdsLayout& L;
+  float* s;      // LDS base of this env
+  float* scr;    // global scratch of this env
+  const ScratchLayout& S;
+  int lane;
+  __device__ float* at(int off) const { return s + off; }
+};
+
+// Cholesky of the dense nv x nv matrix A (LDS) into Lf (LDS), column by column; lanes over rows.
+__device__ void cholesky(const Env& E, const float* A, float* Lf) {
+  const int nv = E.m.nv, lane = E.lane;
+  for (int k = 0; k < nv; ++k) {
+    float t = 0;
+    if (lane >= k && lane < nv) {
+      t = A[lane * nv + k];
+      for (int p = 0; p < k; ++p) t -= Lf[lane * nv + p] * Lf[k * nv + p];
+    }
+    float dk = bcast(t, k);
+    float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
+    if (lane == k) Lf[k * nv + k] = lkk;
+    else if (lane > k && lane < nv) Lf[lane * nv + k] = t / lkk;
+    wsync();
+  }
+}
+// x = A^-1 b with A = Lf Lf'; lane j holds b_j / returns x_j (lanes >= nv return 0)
+__device__ float chol_solve_lanes(const Env& E, const float* Lf, float b) {
+  const int nv = E.m.nv, lane = E.lane;
+  float x = lane < nv ? b : 0.0f;
+  for (int i = 0; i < nv; ++i) {
+    float xi = bcast(x, i) / Lf[i * nv + i];
+    if (lane == i) x = xi;
+    else if (lane > i && lane < nv) x -= Lf[lane * nv + i] * xi;
+  }
+  for (int i = nv - 1; i >= 0; --i) {
+    float xi = bcast(x, i) / Lf[i * nv + i];
+    if (lane == i) x = xi;
+    else if (lane < i) x -= Lf[i * nv + lane] * xi;
+  }
+  return x;
+}
+// serial solve by one lane (vectors in registers/scratch); used per constraint row
+__device__ void chol_solve_serial(const float* Lf, int nv, const float* b, float* x) {
+  for (int i = 0; i < nv; ++i) {
+    float sacc = b[i];
+    for (int k = 0; k < i; ++k) sacc -= Lf[i * nv + k] * x[k];
+    x[i] = sacc / Lf[i * nv + i];
+  }
+  for (int i = nv - 1; i >= 0; --i) {
+    float sacc = x[i];
+    for (int k = i + 1; k < nv; ++k) sacc -= Lf[k * nv + i] * x[k];
+    x[i] = sacc / Lf[i * nv + i];
+  }
+}
+
+// mj_kinematics + rotational part of cinert; bodies of one depth level per pass
+__device__ void kinematics(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane;
+  if (lane == 0) {
+    float* x = s + L.xpos; x[0] = x[1] = x[2] = 0;
+    float* q = s + L.xquat; q[0] = 1; q[1] = q[2] = q[3] = 0;
+    float* mm = s + L.xmat;
+    for (int i = 0; i < 9; ++i) mm[i] = (i % 4 == 0) ? 1.0f : 0.0f;
+    float* xi = s + L.xipos; xi[0] = xi[1] = xi[2] = 0;
+  }
+  wsync();
+  for (int lev = 1; lev <= m.max_depth; ++lev) {
+    const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+    for (int k = lane; k < nl; k += 64) {
+      const int b = m.level_body[a0 + k];
+      const int p = m.body_parentid[b];
+      float pos[3], q[4];
+      const int ja = m.body_jntadr[b], nj = m.body_jntnum[b];
+      if (nj > 0 && m.jnt_type[ja] == MRS_JNT_FREE) {
+        const float* qp = s + L.qpos + m.jnt_qposadr[ja];
+        pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
+        q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+        quat_normalize(q);
+        float* anc = s + L.xanchor + 3 * ja;
+        float* ax = s + L.xaxis + 3 * ja;
+        for (int i = 0; i < 3; ++i) { anc[i] = pos[i]; ax[i] = 0; }
+      } else {
+        float pq[4] = {s[L.xquat + 4 * p], s[L.xquat + 4 * p + 1], s[L.xquat + 4 * p + 2], s[L.xquat + 4 * p + 3]};
+        float bpos[3] = {m.body_pos[3 * b], m.body_pos[3 * b + 1], m.body_pos[3 * b + 2]};
+        float bq[4] = {m.body_quat[4 * b], m.body_quat[4 * b + 1], m.body_quat[4 * b + 2], m.body_quat[4 * b + 3]};
+        float r[3];
+        rot_quat(r, bpos, pq);
+        for (int i = 0; i < 3; ++i) pos[i] = s[L.xpos + 3 * p + i] + r[i];
+        quat_mul(q, pq, bq);
+        for (int k2 = 0; k2 < nj; ++k2) {
+          const int j = ja + k2, qa = m.jnt_qposadr[j];
+          float jp[3] = {m.jnt_pos[3 * j], m.jnt_pos[3 * j + 1], m.jnt_pos[3 * j + 2]};
+          float ja3[3] = {m.jnt_axis[3 * j], m.jnt_axis[3 * j + 1], m.jnt_axis[3 * j + 2]};
+          float anc[3], ax[3];
+          rot_quat(anc, jp, q);
+          for (int i = 0; i < 3; ++i) anc[i] += pos[i];
+          rot_quat(ax, ja3, q);
+          for (int i = 0; i < 3; ++i) { s[L.xanchor + 3 * j + i] = anc[i]; s[L.xaxis + 3 * j + i] = ax[i]; }
+          const int jt = m.jnt_type[j];
+          if (jt == MRS_JNT_SLIDE) {
+            float dq = s[L.qpos + qa] - m.qpos0[qa];
+            for (int i = 0; i < 3; ++i) pos[i] += ax[i] * dq;
+          } else {
+            float ql[4];
+            if (jt == MRS_JNT_BALL) {
+              for (int i = 0; i < 4; ++i) ql[i] = s[L.qpos + qa + i];
+              quat_normalize(ql);
+            } else {
+              axis_angle_quat(ql, ja3, s[L.qpos + qa] - m.qpos0[qa]);
+            }
+            quat_mul(q, q, ql);
+            float v[3];
+            rot_quat(v, jp, q);
+            for (int i = 0; i < 3; ++i) pos[i] = anc[i] - v[i];
+          }
+        }
+      }
+      quat_normalize(q);
+      float xm[9];
+      quat2mat(xm, q);
+      for (int i = 0; i < 3; ++i) s[L.xpos + 3 * b + i] = pos[i];
+      for (int i = 0; i < 4; ++i) s[L.xquat + 4 * b + i] = q[i];
+      for (int i = 0; i < 9; ++i) s[L.xmat + 9 * b + i] = xm[i];
+      // inertial frame; world-frame rotational inertia about the body com goes to cinert[0..5]
+      float ip[3] = {m.body_ipos[3 * b], m.body_ipos[3 * b + 1], m.body_ipos[3 * b + 2]};
+      float iq[4] = {m.body_iquat[4 * b], m.body_iquat[4 * b + 1], m.body_iquat[4 * b + 2], m.body_iquat[4 * b + 3]};
+      float r[3], qi[4], R[9];
+      mat_vec(r, xm, ip);
+      for (int i = 0; i < 3; ++i) s[L.xipos + 3 * b + i] = pos[i] + r[i];
+      quat_mul(qi, q, iq);
+      quat2mat(R, qi);
+      const float I0 = m.body_inertia[3 * b], I1 = m.body_inertia[3 * b + 1], I2 = m.body_inertia[3 * b + 2];
+      float* ci = s + L.cinert + 10 * b;
+      ci[0] = R[0] * I0 * R[0] + R[1] * I1 * R[1] + R[2] * I2 * R[2];
+      ci[1] = R[3] * I0 * R[3] + R[4] * I1 * R[4] + R[5] * I2 * R[5];
+      ci[2] = R[6] * I0 * R[6] + R[7] * I1 * R[7] + R[8] * I2 * R[8];
+      ci[3] = R[0] * I0 * R[3] + R[1] * I1 * R[4] + R[2] * I2 * R[5];
+      ci[4] = R[0] * I0 * R[6] + R[1] * I1 * R[7] + R[2] * I2 * R[8];
+      ci[5] = R[3] * I0 * R[6] + R[4] * I1 * R[7] + R[5] * I2 * R[8];
+    }
+    wsync();
+  }
+  // geoms
+  for (int g = lane; g < m.ngeom; g += 64) {
+    const int b = m.geom_bodyid[g];
+    float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+    float gp[3] = {m.geom_pos[3 * g], m.geom_pos[3 * g + 1], m.geom_pos[3 * g + 2]};
+    float gq[4] = {m.geom_quat[4 * g], m.geom_quat[4 * g + 1], m.geom_quat[4 * g + 2], m.geom_quat[4 * g + 3]};
+    float r[3], q[4], gm[9];
+    rot_quat(r, gp, bq);
+    for (int i = 0; i < 3; ++i) s[L.gxpos + 3 * g + i] = s[L.xpos + 3 * b + i] + r[i];
+    quat_mul(q, bq, gq);
+    quat2mat(gm, q);
+    for (int i = 0; i < 9; ++i) s[L.gxmat + 9 * g + i] = gm[i];
+  }
+  wsync();
+}
+
+// mj_comPos: subtree coms of tree roots, cinert (parallel-axis part), cdof
+__device__ void com_pos(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane;
+  for (int b = lane; b < m.nbody; b += 64) {
+    if (b != 0 && m.body_parentid[b] != 0) continue;
+    float c[3] = {0, 0, 0};
+    const int e = m.body_subtree_end[b];
+    for (int k = b; k < e; ++k) {
+      const float mk = m.body_mass[k];
+      for (int i = 0; i < 3; ++i) c[i] += mk * s[L.xipos + 3 * k + i];
+    }
+    const float sm = m.body_subtreemass[b];
+    for (int i = 0; i < 3; ++i) s[L.scom + 3 * b + i] = sm > kMinVal ? c[i] / sm : s[L.xipos + 3 * b + i];
+  }
+  wsync();
+  for (int b = lane; b < m.nbody; b += 64) {
+    float* ci = s + L.cinert + 10 * b;
+    if (b == 0) { for (int i = 0; i < 10; ++i) ci[i] = 0; continue; }
+    const int rt = m.body_rootid[b];
+    const float mass = m.body_mass[b];
+    float d[3];
+    for (int i = 0; i < 3; ++i) d[i] = s[L.xipos + 3 * b + i] - s[L.scom + 3 * rt + i];
+    ci[0] += mass * (d[1] * d[1] + d[2] * d[2]);
+    ci[1] += mass * (d[0] * d[0] + d[2] * d[2]);
+    ci[2] += mass * (d[0] * d[0] + d[1] * d[1]);
+    ci[3] -= mass * d[0] * d[1];
+    ci[4] -= mass * d[0] * d[2];
+    ci[5] -= mass * d[1] * d[2];
+    ci[6] = mass * d[0]; ci[7] = mass * d[1]; ci[8] = mass * d[2]; ci[9] = mass;
+  }
+  for (int j = lane; j < m.njnt; j += 64) {
+    const int b = m.jnt_bodyid[j], rt = m.body_rootid[b];
+    int dof = m.jnt_dofadr[j];
+    float off[3];
+    for (int i = 0; i < 3; ++i) off[i] = s[L.scom + 3 * rt + i] - s[L.xanchor + 3 * j + i];
+    const int jt = m.jnt_type[j];
+    if (jt == MRS_JNT_HINGE) {
+      float* cd = s + L.cdof + 6 * dof;
+      float ax[3] = {s[L.xaxis + 3 * j], s[L.xaxis + 3 * j + 1], s[L.xaxis + 3 * j + 2]}, c[3];
+      cross3(c, ax, off);
+      for (int i = 0; i < 3; ++i) { cd[i] = ax[i]; cd[3 + i] = c[i]; }
+    } else if (jt == MRS_JNT_SLIDE) {
+      float* cd = s + L.cdof + 6 * dof;
+      for (int i = 0; i < 3; ++i) { cd[i] = 0; cd[3 + i] = s[L.xaxis + 3 * j + i]; }
+    } else {
+      if (jt == MRS_JNT_FREE) {
+        for (int k = 0; k < 3; ++k)
+          for (int i = 0; i < 6; ++i) s[L.cdof + 6 * (dof + k) + i] = (i == 3 + k) ? 1.0f : 0.0f;
+        dof += 3;
+      }
+      for (int k = 0; k < 3; ++k) {
+        float ax[3] = {s[L.xmat + 9 * b + k], s[L.xmat + 9 * b + 3 + k], s[L.xmat + 9 * b + 6 + k]}, c[3];
+        cross3(c, ax, off);
+        float* cd = s + L.cdof + 6 * (dof + k);
+        for (int i = 0; i < 3; ++i) { cd[i] = ax[i]; cd[3 + i] = c[i]; }
+      }
+    }
+  }
+  wsync();
+}
+
+// mj_crb + armature: crb by subtree sums, M by (dof, ancestor-dof) pairs
+__device__ void make_M(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane, nv = m.nv;
+  for (int b = lane; b < m.nbody; b += 64) {
+    float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (b != 0) {
+      const int e = m.body_subtree_end[b];
+      for (int k = b; k < e; ++k)
+        for (int i = 0; i < 10; ++i) acc[i] += s[L.cinert + 10 * k + i];
+    }
+    for (int i = 0; i < 10; ++i) s[L.crb + 10 * b + i] = acc[i];
+  }
+  for (int i = lane; i < nv * nv; i += 64) s[L.M + i] = 0;
+  wsync();
+  for (int p = lane; p < m.nMpair; p += 64) {
+    const int i = m.Mpair[2 * p], j = m.Mpair[2 * p + 1];
+    float buf[6], cd[6];
+    for (int k = 0; k < 6; ++k) cd[k] = s[L.cdof + 6 * i + k];
+    mul_inert_vec(buf, s + L.crb + 10 * m.dof_bodyid[i], cd);
+    float v = 0;
+    for (int k = 0; k < 6; ++k) v += s[L.cdof + 6 * j + k] * buf[k];
+    if (i == j) v += m.dof_armature[i];
+    s[L.M + i * nv + j] = v;
+    s[L.M + j * nv + i] = v;
+  }
+  wsync();
+}
+
+// mj_comVel: level by level
+__device__ void com_vel(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane;
+  if (lane < 6) s[L.cvel + lane] = 0;
+  wsync();
+  for (int lev = 1; lev <= m.max_depth; ++lev) {
+    const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+    for (int k = lane; k < nl; k += 64) {
+      const int b = m.level_body[a0 + k];
+      const int p = m.body_parentid[b];
+      float cv[6];
+      for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
+      const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      for (int k2 = 0; k2 < nd; ++k2) {
+        const int j = da + k2;
+        const int jid = m.dof_jntid[j], jt = m.jnt_type[jid];
+        if (jt == MRS_JNT_FREE && j == m.jnt_dofadr[jid]) {
+          for (int t = 0; t < 3; ++t) {
+            const float qv = s[L.qvel + j + t];
+            for (int i = 0; i < 6; ++i) {
+              s[L.cdofdot + 6 * (j + t) + i] = 0;
+              cv[i] += s[L.cdof + 6 * (j + t) + i] * qv;
+            }
+          }
+          k2 += 2;
+          continue;
+        }
+        if (jt == MRS_JNT_BALL || jt == MRS_JNT_FREE) {
+          for (int t = 0; t < 3; ++t) cross_motion(s + L.cdofdot + 6 * (j + t), cv, s + L.cdof + 6 * (j + t));
+          for (int t = 0; t < 3; ++t) {
+            const float qv = s[L.qvel + j + t];
+            for (int i = 0; i < 6; ++i) cv[i] += s[L.cdof + 6 * (j + t) + i] * qv;
+          }
+          k2 += 2;
+          continue;
+        }
+        cross_motion(s + L.cdofdot + 6 * j, cv, s + L.cdof + 6 * j);
+        const float qv = s[L.qvel + j];
+        for (int i = 0; i < 6; ++i) cv[i] += s[L.cdof + 6 * j + i] * qv;
+      }
+      for (int i = 0; i < 6; ++i) s[L.cvel + 6 * b + i] = cv[i];
+    }
+    wsync();
+  }
+}
+
+// mj_rne (no acceleration term): qfrc_bias
+__device__ void rne(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane;
+  if (lane < 6) {
+    float g = (lane >= 3 && !(m.disableflags & MRS_DSBL_GRAVITY)) ? -m.gravity[lane - 3] : 0.0f;
+    s[L.cacc + lane] = g;
+  }
+  wsync();
+  for (int lev = 1; lev <= m.max_depth; ++lev) {
+    const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+    for (int k = lane; k < nl; k += 64) {
+      const int b = m.level_body[a0 + k];
+      float ca[6];
+      for (int i = 0; i < 6; ++i) ca[i] = s[L.cacc + 6 * m.body_parentid[b] + i];
+      const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      for (int k2 = 0; k2 < nd; ++k2) {
+        const float qv = s[L.qvel + da + k2];
+        for (int i = 0; i < 6; ++i) ca[i] += s[L.cdofdot + 6 * (da + k2) + i] * qv;
+      }
+      for (int i = 0; i < 6; ++i) s[L.cacc + 6 * b + i] = ca[i];
+      float f1[6], t[6], f2[6], cv[6];
+      for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * b + i];
+      mul_inert_vec(f1, s + L.cinert + 10 * b, ca);
+      mul_inert_vec(t, s + L.cinert + 10 * b, cv);
+      cross_force(f2, cv, t);
+      for (int i = 0; i < 6; ++i) s[L.cfrc + 6 * b + i] = f1[i] + f2[i];
+    }
+    wsync();
+  }
+  // subtree sums of body forces into crb storage (crb no longer needed)
+  for (int b = lane; b < m.nbody; b += 64) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    if (b != 0) {
+      const int e = m.body_subtree_end[b];
+      for (int k = b; k < e; ++k)
+        for (int i = 0; i < 6; ++i) acc[i] += s[L.cfrc + 6 * k + i];
+    }
+    for (int i = 0; i < 6; ++i) s[L.crb + 6 * b + i] = acc[i];
+  }
+  wsync();
+  for (int j = lane; j < m.nv; j += 64) {
+    const int b = m.dof_bodyid[j];
+    float v = 0;
+    for (int i = 0; i < 6; ++i) v += s[L.cdof + 6 * j + i] * s[L.crb + 6 * b + i];
+    s[L.qfrc_bias + j] = v;
+  }
+  wsync();
+}
+
+// translational point-Jacobian column of dof j for a point on body b (0 if j does not move b)
+__device__ __forceinline__ void jac_col(const Env& E, int b, const float pnt[3], int j, float col[3]) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  const int bj = m.dof_bodyid[j];
+  if (!(b >= bj && b < m.body_subtree_end[bj])) { col[0] = col[1] = col[2] = 0; return; }
+  const float* c = E.s + L.scom + 3 * m.body_rootid[b];
+  const float* cd = E.s + L.cdof + 6 * j;
+  float off[3] = {pnt[0] - c[0], pnt[1] - c[1], pnt[2] - c[2]}, ang[3] = {cd[0], cd[1], cd[2]}, cr[3];
+  cross3(cr, ang, off);
+  for (int i = 0; i < 3; ++i) col[i] = cd[3 + i] + cr[i];
+}
+
+// mj_passive + mj_fwdActuation + qfrc_smooth + qacc_smooth (lane per dof)
+__device__ float smooth_forces(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane, nv = m.nv;
+  // actuator forces (lane per actuator)
+  for (int a = lane; a < m.nu; a += 64) {
+    float force = 0;
+    if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
+      const float gear = m.act_gear[a];
+      const float len = gear * s[L.qpos + m.act_qadr[a]], vel = gear * s[L.qvel + m.act_dof[a]];
+      float ctrl = s[L.ctrl + a];
+      if (m.act_ctrllimited[a] && !(m.disableflags & MRS_DSBL_CLAMPCTRL))
+        ctrl = clampf(ctrl, m.act_ctrlrange[2 * a], m.act_ctrlrange[2 * a + 1]);
+      const float* g = m.act_gainprm + 3 * a;
+      const float* bp = m.act_biasprm + 3 * a;
+      float gain = m.act_gaintype[a] == MRS_GAIN_AFFINE ? g[0] + g[1] * len + g[2] * vel : g[0];
+      float bias = m.act_biastype[a] == MRS_BIAS_AFFINE ? bp[0] + bp[1] * len + bp[2] * vel : 0.0f;
+      force = gain * ctrl + bias;
+      if (m.act_forcelimited[a]) force = clampf(force, m.act_forcerange[2 * a], m.act_forcerange[2 * a + 1]);
+    }
+    s[L.act_force + a] = force;
+  }
+  wsync();
+  float qfs = 0;
+  if (lane < nv) {
+    const int j = lane;
+    float qa = 0;
+    for (int a = 0; a < m.nu; ++a)
+      if (m.act_dof[a] == j) qa += m.act_gear[a] * s[L.act_force + a];
+    const int jid = m.dof_jntid[j];
+    if (m.jnt_actfrclimited[jid]) qa = clampf(qa, m.jnt_actfrcrange[2 * jid], m.jnt_actfrcrange[2 * jid + 1]);
+    s[L.qfrc_act + j] = qa;
+    float pas = 0;
+    if (!(m.disableflags & MRS_DSBL_PASSIVE)) {
+      const int jt = m.jnt_type[jid];
+      if ((jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) && m.jnt_stiffness[jid] != 0) {
+        const int qadr = m.jnt_qposadr[jid];
+        pas -= m.jnt_stiffness[jid] * (s[L.qpos + qadr] - m.qpos_spring[qadr]);
+      }
+      pas -= m.dof_damping[j] * s[L.qvel + j];
+      if (!(m.disableflags & MRS_DSBL_GRAVITY)) {
+        const int bj = m.dof_bodyid[j], e = m.body_subtree_end[bj];
+        for (int b = bj; b < e; ++b) {
+          const float gc = m.body_gravcomp[b];
+          if (gc == 0) continue;
+          float f[3], col[3], pnt[3] = {s[L.xipos + 3 * b], s[L.xipos + 3 * b + 1], s[L.xipos + 3 * b + 2]};
+          for (int i = 0; i < 3; ++i) f[i] = -m.gravity[i] * m.body_mass[b] * gc;
+          jac_col(E, b, pnt, j, col);
+          pas += dot3(col, f);
+        }
+      }
+    }
+    s[L.qfrc_passive + j] = pas;
+    qfs = pas - s[L.qfrc_bias + j] + s[L.qfrc_applied + j] + qa;
+    s[L.qfrc_smooth + j] = qfs;
+  }
+  float qacc_s = chol_solve_lanes(E, s + L.L, qfs);
+  if (lane < nv) s[L.qacc_smooth + lane] = qacc_s;
+  wsync();
+  return qacc_s;
+}
+
+// mj_collision: candidate pairs (lane per pair), bounding-sphere test, narrow phase, compaction
+__device__ int collision(const Env& E) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  const ScratchLayout& S = E.S;
+  float* s = E.s;
+  const int lane = E.lane;
+  int ncon = 0;
+  if ((m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) || m.npair == 0) return 0;
+  for (int base = 0; base < m.npair; base += 64) {
+    const int p = base + lane;
+    Con c[4];
+    int n = 0;
+    if (p < m.npair) {
+      const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+      const float* p1 = s + L.gxpos + 3 * g1;
+      const float* p2 = s + L.gxpos + 3 * g2;
+      const float margin = m.pair_margin[p];
+      const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+      bool cand = true;
+      if (t1 != MRS_GEOM_PLANE) {
+        float dv[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+        float rb = m.geom_rbound[g1] + m.geom_rbound[g2] + margin;
+        cand = dot3(dv, dv) <= rb * rb;
+      }
+      if (cand)
+        n = narrowphase(t1, t2, p1, s + L.gxmat + 9 * g1, m.geom_size + 3 * g1, p2, s + L.gxmat + 9 * g2,
+                        m.geom_size + 3 * g2, margin, c);
+    }
+    int total;
+    int off = wave_scan_excl(n, lane, total);
+    for (int k = 0; k < n; ++k) {
+      const int slot = ncon + off + k;
+      if (slot >= m.max_con) break;
+      float* rec = E.scr + S.con + kConRec * slot;
+      float fr[9] = {c[k].nrm[0], c[k].nrm[1], c[k].nrm[2], 0, 0, 0, 0, 0, 0};
+      make_frame(fr);
+      rec[0] = __int_as_float(p);
+      rec[1] = c[k].dist;
+      for (int i = 0; i < 3; ++i) rec[2 + i] = c[k].pos[i];
+      for (int i = 0; i < 9; ++i) rec[5 + i] = fr[i];
+    }
+    ncon += total;
+  }
+  if (ncon > m.max_con) ncon = m.max_con;
+  wsync();
+  return ncon;
+}
+
+// mj_makeConstraint + mj_makeImpedance + PGS (matrix-free rows) -> qacc, qfrc_constraint
+__device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_out) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  const ScratchLayout& S = E.S;
+  float* s = E.s;
+  float* scr = E.scr;
+  const int lane = E.lane, nv = m.nv;
+  float* J = scr + S.efc_J;
+  float* MJ = scr + S.efc_MJ;
+  float* type = scr + S.efc_type;
+  float* pos = scr + S.efc_pos;
+  float* marg = scr + S.efc_margin;
+  float* floss = scr + S.efc_floss;
+  float* Rr = scr + S.efc_R;
+  float* aref = scr + S.efc_aref;
+  float* bb = scr + S.efc_b;
+  float* ff = scr + S.efc_f;
+  float* ARii = scr + S.efc_ARii;
+  int nefc = 0;
+  if (m.disableflags & MRS_DSBL_CONSTRAINT) { qacc_out = qacc_s; if (lane < nv) s[L.qfrc_con + lane] = 0; wsync(); return; }
+  // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
+  // keep ids in a small per-row int array inside the type slot (type*65536 + id)
+  // --- friction loss rows
+  if (!(m.disableflags & MRS_DSBL_FRICTIONLOSS)) {
+    for (int r = 0; r < m.nfric; ++r) {
+      const int j = m.fric_dof[r];
+      if (lane < nv) J[r * nv + lane] = (lane == j) ? 1.0f : 0.0f;
+      if (lane == 0) {
+        type[r] = __int_as_float(EFC_FRICTION * 65536 + j);
+        pos[r] = 0; marg[r] = 0; floss[r] = m.dof_frictionloss[j];
+      }
+    }
+    nefc = m.nfric;
+  }
+  // --- joint limit rows (lane per limited joint, compacted)
+  if (!(m.disableflags & MRS_DSBL_LIMIT)) {
+    for (int base = 0; base < m.nlim; base += 64) {
+      const int k = base + lane;
+      int cnt = 0;
+      float dist[2] = {0, 0};
+      int jid = -1;
+      bool act[2] = {false, false};
+      if (k < m.nlim) {
+        jid = m.lim_jnt[k];
+        const float q = s[L.qpos + m.jnt_qposadr[jid]], mg = m.jnt_margin[jid];
+        dist[0] = q - m.jnt_range[2 * jid];
+        dist[1] = m.jnt_range[2 * jid + 1] - q;
+        act[0] = dist[0] < mg;
+        act[1] = dist[1] < mg;
+        cnt = (int)act[0] + (int)act[1];
+      }
+      int total;
+      int off = wave_scan_excl(cnt, lane, total);
+      int r = nefc + off;
+      for (int sd = 0; sd < 2; ++sd) {
+        if (!act[sd]) continue;
+        type[r] = __int_as_float(EFC_LIMIT * 65536 + jid);
+        pos[r] = dist[sd];
+        marg[r] = m.jnt_margin[jid];
+        floss[r] = sd == 0 ? 1.0f : -1.0f;  // J sign, used below
+        ++r;
+      }
+      nefc += total;
+    }
+    wsync();
+    // dense J of limit rows
+    for (int r = m.nfric; r < nefc; ++r) {
+      const int code = __float_as_int(type[r]);
+      const int jid = code & 0xffff;
+      const int dof = m.jnt_dofadr[jid];
+      const float sg = floss[r];
+      if (lane < nv) J[r * nv + lane] = (lane == dof) ? sg : 0.0f;
+    }
+    wsync();
+    if (lane == 0)
+      for (int r = m.nfric; r < nefc; ++r) floss[r] = 0;
+  }
+  // --- contact rows: lane per dof, loop over contacts
+  for (int c = 0; c < ncon; ++c) {
+    const float* rec = scr + S.con + kConRec * c;
+    const int p = __float_as_int(rec[0]);
+    const int dim = m.pair_dim[p];
+    const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+    float cp[3] = {rec[2], rec[3], rec[4]};
+    float jc[3] = {0, 0, 0};
+    if (lane < nv) {
+      float c1[3], c2[3];
+      jac_col(E, b1, cp, lane, c1);
+      jac_col(E, b2, cp, lane, c2);
+      float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+      for (int r = 0; r < 3; ++r) jc[r] = rec[5 + 3 * r] * dc[0] + rec[6 + 3 * r] * dc[1] + rec[7 + 3 * r] * dc[2];
+    }
+    if (dim == 1) {
+      if (nefc < m.max_efc) {
+        if (lane < nv) J[nefc * nv + lane] = jc[0];
+        if (lane == 0) {
+          type[nefc] = __int_as_float(EFC_CONTACT * 65536 + c);
+          pos[nefc] = rec[1]; marg[nefc] = m.pair_margin[p] - m.pair_gap[p]; floss[nefc] = 0;
+        }
+        ++nefc;
+      }
+    } else {
+      for (int k = 1; k < 3; ++k)
+        for (int sg = 1; sg >= -1; sg -= 2) {
+          if (nefc >= m.max_efc) continue;
+          const float mu = m.pair_friction[3 * p + k - 1];
+          if (lane < nv) J[nefc * nv + lane] = jc[0] + sg * mu * jc[k];
+          if (lane == 0) {
+            type[nefc] = __int_as_float(EFC_CONTACT * 65536 + c);
+            pos[nefc] = rec[1]; marg[nefc] = m.pair_margin[p] - m.pair_gap[p]; floss[nefc] = 0;
+          }
+          ++nefc;
+        }
+    }
+  }
+  wsync();
+  if (nefc == 0) {
+    qacc_out = qacc_s;
+    if (lane < nv) s[L.qfrc_con + lane] = 0;
+    wsync();
+    return;
+  }
+  // --- impedance, R, aref, M^-1 J', ARii, b (lane per row)
+  for (int r = lane; r < nefc; r += 64) {
+    const int code = __float_as_int(type[r]);
+    const int t = code >> 16, id = code & 0xffff;
+    const float *sr, *si;
+    float diag;
+    if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
+    else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
+    else {
+      const float* rec = scr + S.con + kConRec * id;
+      const int p = __float_as_int(rec[0]);
+      sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
+      const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+      float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      diag = tran;
+      if (m.pair_dim[p] == 3) {
+        // edge k of this row: rows of a contact are laid out k=1:(+,-), k=2:(+,-)
+        int first = r;
+        while (first > 0 && __float_as_int(type[first - 1]) == code) --first;
+        const int k = 1 + (r - first) / 2;
+        const float mu = m.pair_friction[3 * p + k - 1];
+        diag = tran * (1 + mu * mu);
+      }
+    }
+    const float imp = impedance(si, pos[r], marg[r]);
+    float R = (1 - imp) * diag / imp;
+    R = R > kMinVal ? R : kMinVal;
+    Rr[r] = R;
+    const float dmax = clampf(si[1], 0.0001f, 0.9999f);
+    float K, B;
+    if (sr[0] > 0) {
+      float tc = sr[0], dr = sr[1];
+      if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -sr[0] / (dmax * dmax);
+      B = -sr[1] / dmax;
+    }
+    float vel = 0, jqs = 0;
+    const float* Jr = J + r * nv;
+    for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
+    const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
+    aref[r] = -B * vel - pterm;
+    bb[r] = jqs - aref[r];
+    // M^-1 J_r'
+    float* MJr = MJ + r * nv;
+    chol_solve_serial(s + L.L, nv, Jr, MJr);
+    float d = 0;
+    for (int j = 0; j < nv; ++j) d += Jr[j] * MJr[j];
+    ARii[r] = d + R;
+  }
+  wsync();
+  // --- warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if dual cost < 0
+  float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f, lane per dof
+  {
+    bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+    for (int r = lane; r < nefc; r += 64) {
+      float f = 0;
+      if (warm) {
+        const float* Jr = J + r * nv;
+        float jar = -aref[r];
+        for (int j = 0; j < nv; ++j) jar += Jr[j] * s[L.qacc_ws + j];
+        const int t = __float_as_int(type[r]) >> 16;
+        const float D = 1.0f / Rr[r];
+        if (t == EFC_FRICTION) {
+          const float fl = floss[r];
+          f = jar <= -Rr[r] * fl ? fl : (jar >= Rr[r] * fl ? -fl : -D * jar);
+        } else {
+          f = jar < 0 ? -D * jar : 0.0f;
+        }
+      }
+      ff[r] = f;
+    }
+    wsync();
+    if (warm) {
+      // v = M^-1 J' f (lane per dof); cost = sum_r f_r (0.5 (J_r v + R_r f_r) + b_r)
+      float v = 0;
+      if (lane < nv)
+        for (int r = 0; r < nefc; ++r) v += MJ[r * nv + lane] * ff[r];
+      float cost = 0;
+      for (int r = 0; r < nefc; ++r) {
+        const float jv = wave_sum(lane < nv ? J[r * nv + lane] * v : 0.0f);
+        cost += ff[r] * (0.5f * (jv + Rr[r] * ff[r]) + bb[r]);
+      }
+      if (cost > 0) {
+        for (int r = lane; r < nefc; r += 64) ff[r] = 0;
+      } else {
+        qa += v;
+      }
+      wsync();
+    }
+  }
+  // --- PGS sweeps (rows serial, dot products across lanes)
+  for (int it = 0; it < m.iterations; ++it) {
+    float improvement = 0;
+    for (int r = 0; r < nefc; ++r) {
+      const float jq = wave_sum(lane < nv ? J[r * nv + lane] * qa : 0.0f);
+      const float f0 = ff[r];
+      const float res = jq - aref[r] + Rr[r] * f0;
+      const float a = ARii[r];
+      float nf = f0 - res / a;
+      const int t = __float_as_int(type[r]) >> 16;
+      if (t == EFC_FRICTION) nf = clampf(nf, -floss[r], floss[r]);
+      else if (nf < 0) nf = 0;
+      const float delta = nf - f0;
+      if (delta != 0) {
+        if (lane < nv) qa += MJ[r * nv + lane] * delta;
+        if (lane == 0) ff[r] = nf;
+      }
+      improvement -= delta * res + 0.5f * delta * delta * a;
+      wsync();
+    }
+    if (improvement * m.pgs_scale < m.tolerance) break;
+  }
+  // --- qfrc_constraint = J' f
+  if (lane < nv) {
+    float v = 0;
+    for (int r = 0; r < nefc; ++r) v += J[r * nv + lane] * ff[r];
+    s[L.qfrc_con + lane] = v;
+  }
+  qacc_out = qa;
+  wsync();
+}
+
+// mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel
+__device__ void sensors(const Env& E, float* sensordata) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane;
+  if (m.disableflags & MRS_DSBL_SENSOR) return;
+  for (int k = lane; k < m.nrf; k += 64) {
+    const int sid = m.rf_sensor[k];
+    const int site = m.sensor_objid[sid];
+    const int b = m.site_bodyid[site];
+    float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+    float sp[3] = {m.site_pos[3 * site], m.site_pos[3 * site + 1], m.site_pos[3 * site + 2]};
+    float sq[4] = {m.site_quat[4 * site], m.site_quat[4 * site + 1], m.site_quat[4 * site + 2], m.site_quat[4 * site + 3]};
+    float r[3], q[4], sm[9], pnt[3];
+    rot_quat(r, sp, bq);
+    for (int i = 0; i < 3; ++i) pnt[i] = s[L.xpos + 3 * b + i] + r[i];
+    quat_mul(q, bq, sq);
+    quat2mat(sm, q);
+    const float vec[3] = {sm[2], sm[5], sm[8]};
+    float dist = -1;
+    for (int g = 0; g < m.ngeom; ++g) {
+      if (m.geom_bodyid[g] == b || m.geom_rgba[4 * g + 3] == 0) continue;
+      const float* gp = s + L.gxpos + 3 * g;
+      const float* gm = s + L.gxmat + 9 * g;
+      float dv[3] = {pnt[0] - gp[0], pnt[1] - gp[1], pnt[2] - gp[2]}, lp[3], lv[3];
+      matT_vec(lp, gm, dv);
+      matT_vec(lv, gm, vec);
+      const float t = ray_geom_local(m.geom_type[g], m.geom_size + 3 * g, lp, lv);
+      if (t >= 0 && (dist < 0 || t < dist)) dist = t;
+    }
+    sensordata[m.sensor_adr[sid]] = dist;
+  }
+  for (int sid = lane; sid < m.nsensor; sid += 64) {
+    const int t = m.sensor_type[sid], id = m.sensor_objid[sid];
+    float* out = sensordata + m.sensor_adr[sid];
+    float cutoff = m.sensor_cutoff[sid];
+    int dim = m.sensor_dim[sid];
+    switch (t) {
+      case MRS_SENS_RANGEFINDER: continue;
+      case MRS_SENS_JOINTPOS: out[0] = s[L.qpos + m.jnt_qposadr[id]]; break;
+      case MRS_SENS_JOINTVEL: out[0] = s[L.qvel + m.jnt_dofadr[id]]; break;
+      case MRS_SENS_ACTUATORFRC: out[0] = s[L.act_force + id]; break;
+      case MRS_SENS_FRAMEPOS:
+      case MRS_SENS_FRAMEQUAT:
+      case MRS_SENS_GYRO: {
+        const int ot = m.sensor_objtype[sid];
+        float p[3], q[4];
+        int b;
+        if (ot == MRS_OBJ_SITE || t == MRS_SENS_GYRO) {
+          b = m.site_bodyid[id];
+          float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+          float sp[3] = {m.site_pos[3 * id], m.site_pos[3 * id + 1], m.site_pos[3 * id + 2]};
+          float sq[4] = {m.site_quat[4 * id], m.site_quat[4 * id + 1], m.site_quat[4 * id + 2], m.site_quat[4 * id + 3]};
+          float r[3];
+          rot_quat(r, sp, bq);
+          for (int i = 0; i < 3; ++i) p[i] = s[L.xpos + 3 * b + i] + r[i];
+          quat_mul(q, bq, sq);
+        } else if (ot == MRS_OBJ_BODY) {
+          b = id;
+          for (int i = 0; i < 3; ++i) p[i] = s[L.xpos + 3 * b + i];
+          for (int i = 0; i < 4; ++i) q[i] = s[L.xquat + 4 * b + i];
+        } else {
+          b = m.geom_bodyid[id];
+          float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+          float gq[4] = {m.geom_quat[4 * id], m.geom_quat[4 * id + 1], m.geom_quat[4 * id + 2], m.geom_quat[4 * id + 3]};
+          for (int i = 0; i < 3; ++i) p[i] = s[L.gxpos + 3 * id + i];
+          quat_mul(q, bq, gq);
+        }
+        if (t == MRS_SENS_FRAMEPOS) { for (int i = 0; i < 3; ++i) out[i] = p[i]; }
+        else if (t == MRS_SENS_FRAMEQUAT) { quat_normalize(q); for (int i = 0; i < 4; ++i) out[i] = q[i]; cutoff = 0; }
+        else {
+          float sm[9], w[3] = {s[L.cvel + 6 * b], s[L.cvel + 6 * b + 1], s[L.cvel + 6 * b + 2]};
+          quat2mat(sm, q);
+          matT_vec(out, sm, w);
+        }
+        break;
+      }
+      default:
+        for (int i = 0; i < dim; ++i) out[i] = 0;
+    }
+    if (cutoff > 0)
+      for (int i = 0; i < dim; ++i) out[i] = clampf(out[i], -cutoff, cutoff);
+  }
+}
+
+// reset one env (mj_resetData; held inputs ctrl/qfrc_applied are re-applied by the caller's loop)
+__device__ void reset_env(const Env& E, double& time) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  for (int i = E.lane; i < m.nq; i += 64) s[L.qpos + i] = m.qpos0[i];
+  for (int i = E.lane; i < m.nv; i += 64) { s[L.qvel + i] = 0; s[L.qacc_ws + i] = 0; }
+  time = 0;
+  wsync();
+}
+
+__device__ bool any_bad(const Env& E, int off, int n) {
+  bool bad = false;
+  for (int i = E.lane; i < n; i += 64) bad |= is_bad(E.s[off + i]);
+  return __any(bad);
+}
+
+// full forward pass; returns qacc (lane per dof)
+__device__ float forward(const Env& E, float* sensordata, int& ncon) {
+  kinematics(E);
+  com_pos(E);
+  make_M(E);
+  cholesky(E, E.s + E.L.M, E.s + E.L.L);
+  com_vel(E);
+  rne(E);
+  float qacc_s = smooth_forces(E);
+  ncon = collision(E);
+  float qacc;
+  constraints(E, ncon, qacc_s, qacc);
+  sensors(E, sensordata);
+  if (E.lane < E.m.nv) E.s[E.L.qacc + E.lane] = qacc;
+  wsync();
+  return qacc;
+}
+
+// mj_Euler / mj_implicit(implicitfast) + mj_advance
+__device__ void integrate(const Env& E, float qacc, double& time) {
+  const DevModel& m = E.m;
+  const LdsLayout& L = E.L;
+  float* s = E.s;
+  const int lane = E.lane, nv = m.nv;
+  const float h = m.timestep;
+  bool need_solve = false;
+  float dg = 0;
+  if (lane < nv) {
+    if (m.integrator == MRS_INT_EULER) {
+      if (!(m.disableflags & MRS_DSBL_EULERDAMP) && m.dof_damping[lane] > 0) dg = m.dof_damping[lane];
+    } else {
+      if (!(m.disableflags & MRS_DSBL_PASSIVE)) dg = m.dof_damping[lane];
+      if (!(m.disableflags & MRS_DSBL_ACTUATION))
+        for (int a = 0; a < m.nu; ++a) {
+          if (m.act_dof[a] != lane) continue;
+          if (m.act_forcelimited[a]) {
+            const float f = s[L.act_force + a];
+            if (f <= m.act_forcerange[2 * a] || f >= m.act_forcerange[2 * a + 1]) continue;
+          }
+          const float bv = m.act_biastype[a] == MRS_BIAS_AFFINE ? m.act_biasprm[3 * a + 2] : 0.0f;
+          const float gv = m.act_gaintype[a] == MRS_GAIN_AFFINE ? m.act_gainprm[3 * a + 2] : 0.0f;
+          float ctrl = s[L.ctrl + a];
+          if (m.act_ctrllimited[a] && !(m.disableflags & MRS_DSBL_CLAMPCTRL))
+            ctrl = clampf(ctrl, m.act_ctrlrange[2 * a], m.act_ctrlrange[2 * a + 1]);
+          const float g = m.act_gear[a];
+          dg -= g * g * (bv + gv * ctrl);
+        }
+    }
+  }
+  need_solve = m.integrator != MRS_INT_EULER || __any(dg != 0);
+  float qacc_int = qacc;
+  if (need_solve) {
+    // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
+    if (lane < nv) s[L.M + lane * nv + lane] += h * dg;
+    wsync();
+    cholesky(E, s + L.M, s + L.L);
+    float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
+    qacc_int = chol_solve_lanes(E, s + L.L, rhs);
+  }
+  if (lane < nv) {
+    s[L.qacc_ws + lane] = qacc;
+    s[L.qvel + lane] += h * qacc_int;
+  }
+  wsync();
+  for (int j = lane; j < m.njnt; j += 64) {
+    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
+    const int jt = m.jnt_type[j];
+    if (jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) {
+      s[L.qpos + a] += h * s[L.qvel + da];
+      continue;
+    }
+    if (jt == MRS_JNT_FREE) {
+      for (int i = 0; i < 3; ++i) s[L.qpos + a + i] += h * s[L.qvel + da + i];
+      a += 3; da += 3;
+    }
+    float q[4] = {s[L.qpos + a], s[L.qpos + a + 1], s[L.qpos + a + 2], s[L.qpos + a + 3]};
+    float v[3] = {s[L.qvel + da], s[L.qvel + da + 1], s[L.qvel + da + 2]};
+    float ang = h * normalize3(v), dq[4];
+    axis_angle_quat(dq, v, ang);
+    quat_normalize(q);
+    quat_mul(q, q, dq);
+    quat_normalize(q);
+    for (int i = 0; i < 4; ++i) s[L.qpos + a + i] = q[i];
+  }
+  time += m.timestep_d;
+  wsync();
+}
+
+template <bool kForwardOnly>
+__global__ __launch_bounds__(64 * kEnvsPerBlock) void step_kernel(DevModel m, LdsLayout L, ScratchLayout S,
+                                                                  DevState st, int n_envs, int n_steps) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int env = blockIdx.x * kEnvsPerBlock + wid;
+  if (env >= n_envs) return;
+  float* s = smem + wid * L.total;
+  Env E{m, L, s, st.scratch + (size_t)env * S.total, S, lane};
+  const size_t e = (size_t)env;
+  for (int i = lane; i < m.nq; i += 64) s[L.qpos + i] = st.qpos[e * m.nq + i];
+  for (int i = lane; i < m.nv; i += 64) {
+    s[L.qvel + i] = st.qvel[e * m.nv + i];
+    s[L.qfrc_applied + i] = st.qfrc_applied[e * m.nv + i];
+    s[L.qacc_ws + i] = st.qacc_ws[e * m.nv + i];
+  }
+  for (int i = lane; i < m.nu; i += 64) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
+  double time = st.time[e];
+  float* sensordata = st.sensordata + e * m.nsensordata;
+  wsync();
+  int ncon = 0;
+  int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
+  for (int step = 0; step < n_steps; ++step) {
+    if (!kForwardOnly) {
+      if (any_bad(E, L.qpos, m.nq)) {
+        ++w_pos;
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) reset_env(E, time);
+      }
+      if (any_bad(E, L.qvel, m.nv)) {
+        ++w_vel;
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) reset_env(E, time);
+      }
+    }
+    float qacc = forward(E, sensordata, ncon);
+    if (kForwardOnly) break;
+    if (any_bad(E, L.qacc, m.nv)) {
+      ++w_acc;
+      if (!(m.disableflags & MRS_DSBL_AUTORESET)) {
+        reset_env(E, time);
+        qacc = forward(E, sensordata, ncon);
+      }
+    }
+    integrate(E, qacc, time);
+  }
+  // kinematics of the last forward pass (what mjv_updateScene would render after mj_step)
+  for (int i = lane; i < 3 * m.ngeom; i += 64) st.geom_xpos[e * 3 * m.ngeom + i] = s[L.gxpos + i];
+  for (int i = lane; i < 9 * m.ngeom; i += 64) st.geom_xmat[e * 9 * m.ngeom + i] = s[L.gxmat + i];
+  for (int c = lane; c < m.ncam; c += 64) {
+    const int b = m.cam_bodyid[c];
+    float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+    float cp[3] = {m.cam_pos[3 * c], m.cam_pos[3 * c + 1], m.cam_pos[3 * c + 2]};
+    float cq[4] = {m.cam_quat[4 * c], m.cam_quat[4 * c + 1], m.cam_quat[4 * c + 2], m.cam_quat[4 * c + 3]};
+    float r[3], q[4], cm[9];
+    rot_quat(r, cp, bq);
+    quat_mul(q, bq, cq);
+    quat2mat(cm, q);
+    for (int i = 0; i < 3; ++i) st.cam_xpos[(e * m.ncam + c) * 3 + i] = s[L.xpos + 3 * b + i] + r[i];
+    for (int i = 0; i < 9; ++i) st.cam_xmat[(e * m.ncam + c) * 9 + i] = cm[i];
+  }
+  for (int i = lane; i < m.nq; i += 64) st.qpos[e * m.nq + i] = s[L.qpos + i];
+  for (int i = lane; i < m.nv; i += 64) {
+    st.qvel[e * m.nv + i] = s[L.qvel + i];
+    st.qacc_ws[e * m.nv + i] = s[L.qacc_ws + i];
+    st.qacc[e * m.nv + i] = s[L.qacc + i];
+    st.qfrc_act[e * m.nv + i] = s[L.qfrc_act + i];
+  }
+  if (lane == 0) {
+    st.time[e] = time;
+    st.ncon[e] = ncon;
+    if (w_pos | w_vel | w_acc) {
+      st.warning[4 * e + 0] += w_pos;
+      st.warning[4 * e + 1] += w_vel;
+      st.warning[4 * e + 2] += w_acc;
+      st.warning[4 * e + 3] = w_info;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_step(const DevModel& m, const LdsLayout& L, const ScratchLayout& S, const DevState& st,
+                       int n_envs, int n_steps, bool forward_only, hipStream_t stream) {
+  const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  const size_t lds = sizeof(float) * (size_t)L.total * kEnvsPerBlock;
+  if (forward_only)
+    hipLaunchKernelGGL(step_kernel<true>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, m, L, S, st, n_envs, 1);
+  else
+    hipLaunchKernelGGL(step_kernel<false>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, m, L, S, st, n_envs,
+                       n_steps);
+  return hipGetLastError();
+}
+
+}  // namespace mrs

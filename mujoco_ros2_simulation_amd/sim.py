@@ -1,0 +1,283 @@
+"""ctypes binding of the C ABI (include/mrs.h) — the host-side mirror used by tests, bench and the
+plugin harness.  The product path is libmrs.so (HIP kernels for gfx950); there is no CPU fallback:
+if the library or a GPU is missing, the calls raise.
+
+Reference mapping (reference repo paths):
+  Model.load        -> mj_loadXML            src/mujoco_system_interface.cpp:318
+  Model.from_string -> mj_parseXMLString+mj_compile  :398-399
+  Model.name2id     -> mj_name2id            :1193,1213,1496-1497,1527-1529
+  Batch             -> N x mjData             mj_makeData :686-687
+  Batch.step        -> mj_step               :1691,1731
+  Batch.forward     -> mj_forward            :741,1771
+  Batch.render_depth-> mjr_render+mjr_readPixels+linearise  src/mujoco_cameras.cpp:211-240
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "libmrs.so"
+
+# enums mirrored from include/mrs_model.h / include/mrs.h
+GEOM_PLANE, GEOM_HFIELD, GEOM_SPHERE, GEOM_CAPSULE, GEOM_ELLIPSOID, GEOM_CYLINDER, GEOM_BOX, GEOM_MESH = range(8)
+JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = range(4)
+OBJ_BODY, OBJ_JOINT, OBJ_GEOM, OBJ_SITE, OBJ_CAMERA, OBJ_ACTUATOR, OBJ_SENSOR = 1, 3, 5, 6, 7, 19, 20
+SENS_ACCELEROMETER, SENS_GYRO, SENS_FORCE, SENS_TORQUE, SENS_RANGEFINDER = 1, 3, 4, 5, 7
+SENS_JOINTPOS, SENS_JOINTVEL, SENS_ACTUATORFRC, SENS_FRAMEPOS, SENS_FRAMEQUAT = 9, 10, 15, 25, 26
+BIAS_NONE, BIAS_AFFINE = 0, 1
+(FIELD_QPOS, FIELD_QVEL, FIELD_CTRL, FIELD_QFRC_APPLIED, FIELD_QACC_WARMSTART, FIELD_QACC,
+ FIELD_QFRC_ACTUATOR, FIELD_SENSORDATA, FIELD_TIME, FIELD_WARNING, FIELD_NCON) = range(11)
+# ActuatorType (include/mujoco_ros2_control/data.hpp:43-51 numbering)
+ACT_UNKNOWN, ACT_MOTOR, ACT_POSITION, ACT_VELOCITY, ACT_CUSTOM = range(5)
+
+MRS_OK = 0
+ERRORS = {-1: "invalid argument", -2: "load error", -3: "device error", -4: "unsupported"}
+
+
+class MrsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+# (name, kind, size-expression) in exactly the order of struct mrs_model_view
+_SIZES = ["nq", "nv", "nu", "na", "nbody", "njnt", "ngeom", "nsite", "ncam", "nsensor", "nsensordata", "nkey",
+          "nM", "max_depth"]
+_ARRAYS = [
+    ("body_parentid", "i", "nbody", 1), ("body_rootid", "i", "nbody", 1), ("body_weldid", "i", "nbody", 1),
+    ("body_jntnum", "i", "nbody", 1), ("body_jntadr", "i", "nbody", 1), ("body_dofnum", "i", "nbody", 1),
+    ("body_dofadr", "i", "nbody", 1), ("body_geomnum", "i", "nbody", 1), ("body_geomadr", "i", "nbody", 1),
+    ("body_depth", "i", "nbody", 1),
+    ("body_pos", "d", "nbody", 3), ("body_quat", "d", "nbody", 4), ("body_ipos", "d", "nbody", 3),
+    ("body_iquat", "d", "nbody", 4), ("body_mass", "d", "nbody", 1), ("body_subtreemass", "d", "nbody", 1),
+    ("body_inertia", "d", "nbody", 3), ("body_invweight0", "d", "nbody", 2), ("body_gravcomp", "d", "nbody", 1),
+    ("jnt_type", "i", "njnt", 1), ("jnt_qposadr", "i", "njnt", 1), ("jnt_dofadr", "i", "njnt", 1),
+    ("jnt_bodyid", "i", "njnt", 1), ("jnt_limited", "i", "njnt", 1), ("jnt_actfrclimited", "i", "njnt", 1),
+    ("jnt_pos", "d", "njnt", 3), ("jnt_axis", "d", "njnt", 3), ("jnt_stiffness", "d", "njnt", 1),
+    ("jnt_range", "d", "njnt", 2), ("jnt_actfrcrange", "d", "njnt", 2), ("jnt_margin", "d", "njnt", 1),
+    ("jnt_solref", "d", "njnt", 2), ("jnt_solimp", "d", "njnt", 5),
+    ("dof_bodyid", "i", "nv", 1), ("dof_jntid", "i", "nv", 1), ("dof_parentid", "i", "nv", 1),
+    ("dof_armature", "d", "nv", 1), ("dof_damping", "d", "nv", 1), ("dof_frictionloss", "d", "nv", 1),
+    ("dof_solref", "d", "nv", 2), ("dof_solimp", "d", "nv", 5), ("dof_invweight0", "d", "nv", 1),
+    ("dof_M0", "d", "nv", 1),
+    ("geom_type", "i", "ngeom", 1), ("geom_contype", "i", "ngeom", 1), ("geom_conaffinity", "i", "ngeom", 1),
+    ("geom_condim", "i", "ngeom", 1), ("geom_bodyid", "i", "ngeom", 1), ("geom_group", "i", "ngeom", 1),
+    ("geom_priority", "i", "ngeom", 1),
+    ("geom_size", "d", "ngeom", 3), ("geom_pos", "d", "ngeom", 3), ("geom_quat", "d", "ngeom", 4),
+    ("geom_rbound", "d", "ngeom", 1), ("geom_friction", "d", "ngeom", 3), ("geom_margin", "d", "ngeom", 1),
+    ("geom_gap", "d", "ngeom", 1), ("geom_solmix", "d", "ngeom", 1), ("geom_solref", "d", "ngeom", 2),
+    ("geom_solimp", "d", "ngeom", 5), ("geom_rgba", "d", "ngeom", 4),
+    ("site_bodyid", "i", "nsite", 1), ("site_pos", "d", "nsite", 3), ("site_quat", "d", "nsite", 4),
+    ("cam_bodyid", "i", "ncam", 1), ("cam_resolution", "i", "ncam", 2), ("cam_pos", "d", "ncam", 3),
+    ("cam_quat", "d", "ncam", 4), ("cam_fovy", "d", "ncam", 1),
+    ("actuator_trntype", "i", "nu", 1), ("actuator_dyntype", "i", "nu", 1), ("actuator_gaintype", "i", "nu", 1),
+    ("actuator_biastype", "i", "nu", 1), ("actuator_trnid", "i", "nu", 2), ("actuator_ctrllimited", "i", "nu", 1),
+    ("actuator_forcelimited", "i", "nu", 1),
+    ("actuator_gear", "d", "nu", 6), ("actuator_gainprm", "d", "nu", 10), ("actuator_biasprm", "d", "nu", 10),
+    ("actuator_ctrlrange", "d", "nu", 2), ("actuator_forcerange", "d", "nu", 2),
+    ("sensor_type", "i", "nsensor", 1), ("sensor_objtype", "i", "nsensor", 1), ("sensor_objid", "i", "nsensor", 1),
+    ("sensor_dim", "i", "nsensor", 1), ("sensor_adr", "i", "nsensor", 1), ("sensor_cutoff", "d", "nsensor", 1),
+    ("qpos0", "d", "nq", 1), ("qpos_spring", "d", "nq", 1),
+    ("key_time", "d", "nkey", 1), ("key_qpos", "d", "nkey", "nq"), ("key_qvel", "d", "nkey", "nv"),
+    ("key_ctrl", "d", "nkey", "nu"),
+]
+
+
+class ModelView(C.Structure):
+    _fields_ = ([(n, C.c_int) for n in _SIZES] +
+                [("timestep", C.c_double), ("gravity", C.c_double * 3), ("tolerance", C.c_double),
+                 ("impratio", C.c_double),
+                 ("integrator", C.c_int), ("solver", C.c_int), ("iterations", C.c_int), ("disableflags", C.c_int),
+                 ("cone", C.c_int),
+                 ("stat_extent", C.c_double), ("stat_center", C.c_double * 3), ("stat_meaninertia", C.c_double),
+                 ("vis_znear", C.c_double), ("vis_zfar", C.c_double)] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _ARRAYS])
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libmrs.so (built in-tree by build.py); raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise MrsError(-3, f"{LIB_PATH} not built; run `python -m mujoco_ros2_simulation_amd.build`")
+        L = C.CDLL(str(LIB_PATH))
+        L.mrs_last_error.restype = C.c_char_p
+        L.mrs_model_load_xml.restype = C.c_void_p
+        L.mrs_model_load_xml.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.mrs_model_load_xml_string.restype = C.c_void_p
+        L.mrs_model_load_xml_string.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+        L.mrs_model_free.argtypes = [C.c_void_p]
+        L.mrs_model_view_get.argtypes = [C.c_void_p, C.POINTER(ModelView)]
+        L.mrs_name2id.argtypes = [C.c_void_p, C.c_int, C.c_char_p]
+        L.mrs_id2name.restype = C.c_char_p
+        L.mrs_id2name.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.mrs_actuator_type.argtypes = [C.c_void_p, C.c_int]
+        L.mrs_batch_create.restype = C.c_void_p
+        L.mrs_batch_create.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.mrs_batch_free.argtypes = [C.c_void_p]
+        L.mrs_batch_num_envs.argtypes = [C.c_void_p]
+        L.mrs_batch_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+        L.mrs_batch_reset.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.mrs_batch_set_field.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.mrs_batch_get_field.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.mrs_batch_device_ptr.restype = C.c_void_p
+        L.mrs_batch_device_ptr.argtypes = [C.c_void_p, C.c_int]
+        L.mrs_batch_set_ctrl_device.argtypes = [C.c_void_p, C.c_void_p]
+        L.mrs_batch_step.argtypes = [C.c_void_p, C.c_int]
+        L.mrs_batch_forward.argtypes = [C.c_void_p]
+        L.mrs_batch_render_depth.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.mrs_batch_render_depth_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.mrs_batch_sync.argtypes = [C.c_void_p]
+        L.mrs_batch_last_kernel_ms.restype = C.c_double
+        L.mrs_batch_last_kernel_ms.argtypes = [C.c_void_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != MRS_OK:
+        raise MrsError(rc, lib().mrs_last_error().decode())
+
+
+class Model:
+    """Compiled MJCF model (mjModel analogue).  Arrays are exposed as read-only numpy views."""
+
+    def __init__(self, handle: int):
+        self._h = handle
+        self.view = ModelView()
+        _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
+        v = self.view
+        for n in _SIZES:
+            setattr(self, n, getattr(v, n))
+        for n in ["timestep", "tolerance", "impratio", "integrator", "solver", "iterations", "disableflags",
+                  "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
+            setattr(self, n, getattr(v, n))
+        self.gravity = np.array(v.gravity[:])
+        for name, kind, count, width in _ARRAYS:
+            n = getattr(v, count)
+            w = getattr(v, width) if isinstance(width, str) else width
+            ptr = getattr(v, name)
+            size = n * w
+            if size == 0 or not ptr:
+                arr = np.zeros((n, w) if w > 1 else (n,), dtype=np.int32 if kind == "i" else np.float64)
+            else:
+                arr = np.ctypeslib.as_array(ptr, shape=(size,)).copy()
+                if w > 1:
+                    arr = arr.reshape(n, w)
+            setattr(self, name, arr)
+
+    @classmethod
+    def load(cls, path: str | os.PathLike) -> "Model":
+        err = C.create_string_buffer(1024)
+        h = lib().mrs_model_load_xml(str(path).encode(), err, 1024)
+        if not h:
+            raise MrsError(-2, err.value.decode())
+        return cls(h)
+
+    @classmethod
+    def from_string(cls, xml: str, basedir: str | None = None) -> "Model":
+        err = C.create_string_buffer(1024)
+        h = lib().mrs_model_load_xml_string(xml.encode(), (basedir or ".").encode(), err, 1024)
+        if not h:
+            raise MrsError(-2, err.value.decode())
+        return cls(h)
+
+    def name2id(self, objtype: int, name: str) -> int:
+        return lib().mrs_name2id(self._h, objtype, name.encode())
+
+    def id2name(self, objtype: int, i: int) -> str | None:
+        r = lib().mrs_id2name(self._h, objtype, i)
+        return r.decode() if r else None
+
+    def actuator_type(self, i: int) -> int:
+        return lib().mrs_actuator_type(self._h, i)
+
+    @property
+    def handle(self) -> int:
+        return self._h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.mrs_model_free(self._h)
+            self._h = None
+
+
+_FIELD_DIM = {
+    FIELD_QPOS: "nq", FIELD_QVEL: "nv", FIELD_CTRL: "nu", FIELD_QFRC_APPLIED: "nv", FIELD_QACC_WARMSTART: "nv",
+    FIELD_QACC: "nv", FIELD_QFRC_ACTUATOR: "nv", FIELD_SENSORDATA: "nsensordata", FIELD_TIME: 1, FIELD_WARNING: 4,
+    FIELD_NCON: 1,
+}
+
+
+class Batch:
+    """N independent environments of one model on one GPU (N x mjData analogue)."""
+
+    def __init__(self, model: Model, n_envs: int, device: int = 0):
+        self.model = model
+        self.n = n_envs
+        h = lib().mrs_batch_create(model.handle, n_envs, device)
+        if not h:
+            raise MrsError(-3, lib().mrs_last_error().decode())
+        self._h = h
+
+    def _dim(self, field: int) -> int:
+        d = _FIELD_DIM[field]
+        return getattr(self.model, d) if isinstance(d, str) else d
+
+    def get(self, field: int, env0: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.n - env0 if n is None else n
+        out = np.empty((n, self._dim(field)), dtype=np.float64)
+        _check(lib().mrs_batch_get_field(self._h, field, out.ctypes.data, env0, n))
+        return out
+
+    def set(self, field: int, values, env0: int = 0) -> None:
+        a = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self._dim(field))
+        _check(lib().mrs_batch_set_field(self._h, field, a.ctypes.data, env0, a.shape[0]))
+
+    def reset(self, key: int = -1, env0: int = 0, n: int | None = None) -> None:
+        _check(lib().mrs_batch_reset(self._h, key, env0, self.n - env0 if n is None else n))
+
+    def step(self, n_steps: int = 1) -> None:
+        _check(lib().mrs_batch_step(self._h, n_steps))
+
+    def forward(self) -> None:
+        _check(lib().mrs_batch_forward(self._h))
+
+    def sync(self) -> None:
+        _check(lib().mrs_batch_sync(self._h))
+
+    def device_ptr(self, field: int) -> int:
+        return lib().mrs_batch_device_ptr(self._h, field)
+
+    def set_ctrl_device(self, ptr: int) -> None:
+        _check(lib().mrs_batch_set_ctrl_device(self._h, C.c_void_p(ptr)))
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        _check(lib().mrs_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def render_depth(self, cam: int, env0: int = 0, n: int = 1) -> np.ndarray:
+        W, H = self.model.cam_resolution[cam]
+        out = np.empty((n, H, W), dtype=np.float32)
+        _check(lib().mrs_batch_render_depth(self._h, cam, env0, n, out.ctypes.data))
+        return out
+
+    def render_depth_device(self, cam: int, env0: int, n: int, dptr: int) -> None:
+        _check(lib().mrs_batch_render_depth_device(self._h, cam, env0, n, C.c_void_p(dptr)))
+
+    def last_kernel_ms(self, kind: int = 0) -> float:
+        return lib().mrs_batch_last_kernel_ms(self._h, kind)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.mrs_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,1406 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h).  fp64 scalar CPU restatement of the
+ * MuJoCo 3.3.4 mj_step pipeline subset used by this repo's hot path.  One environment per call;
+ * orc_rollout() threads over environments for the CPU baseline.
+ *
+ * Reference anchors: the plugin calls this pipeline through mj_step at
+ * src/mujoco_system_interface.cpp:1691,1731 and mj_forward at :741,1771; rangefinder sensordata is
+ * consumed at src/mujoco_lidar.cpp:249; the depth image at src/mujoco_cameras.cpp:214-240.
+ * Upstream stage names are given on each function ([upstream] = MuJoCo 3.3.4 source layout).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define MINVAL 1e-15
+#define MAXVAL 1e10
+#define MAXCON 256
+#define MAXEFC 1024
+
+typedef struct {
+  int geom[2];
+  double dist, pos[3], frame[9], friction[3], solref[2], solimp[5], includemargin;
+  int dim;
+} orc_contact;
+
+typedef struct {
+  /* kinematics */
+  double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis, *geom_xpos, *geom_xmat;
+  double *subtree_com, *cinert, *cdof, *crb, *cvel, *cdof_dot, *cacc, *cfrc;
+  /* dynamics */
+  double *M, *L, *qfrc_bias, *qfrc_passive, *qfrc_smooth, *qacc_smooth, *qfrc_constraint,
+      *actuator_force, *tmp, *tmp2, *Mi, *Li;
+  /* constraints */
+  int nefc, ncon;
+  int efc_type[MAXEFC], efc_id[MAXEFC];
+  double *efc_J, *efc_MinvJT;
+  double efc_pos[MAXEFC], efc_margin[MAXEFC], efc_frictionloss[MAXEFC], efc_diag[MAXEFC],
+      efc_R[MAXEFC], efc_D[MAXEFC], efc_aref[MAXEFC], efc_b[MAXEFC], efc_force[MAXEFC],
+      efc_vel[MAXEFC], efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5], efc_KBIP[MAXEFC][4];
+  double* AR;
+  orc_contact con[MAXCON];
+} orc_ws;
+
+enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
+
+/* ------------------------------------------------------------------------ small math */
+static void quat_mul(double r[4], const double a[4], const double b[4]) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof t);
+}
+static void quat_normalize(double q[4]) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+}
+static void quat2mat(double m[9], const double q[4]) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = w * w + x * x - y * y - z * z; m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = w * w - x * x + y * y - z * z; m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = w * w - x * x - y * y + z * z;
+}
+static void mat_vec(double r[3], const double m[9], const double v[3]) {
+  double t[3] = {m[0] * v[0] + m[1] * v[1] + m[2] * v[2], m[3] * v[0] + m[4] * v[1] + m[5] * v[2],
+                 m[6] * v[0] + m[7] * v[1] + m[8] * v[2]};
+  memcpy(r, t, sizeof t);
+}
+static void matT_vec(double r[3], const double m[9], const double v[3]) {
+  double t[3] = {m[0] * v[0] + m[3] * v[1] + m[6] * v[2], m[1] * v[0] + m[4] * v[1] + m[7] * v[2],
+                 m[2] * v[0] + m[5] * v[1] + m[8] * v[2]};
+  memcpy(r, t, sizeof t);
+}
+static void rot_quat(double r[3], const double v[3], const double q[4]) {
+  double m[9];
+  quat2mat(m, q);
+  mat_vec(r, m, v);
+}
+static void cross3(double r[3], const double a[3], const double b[3]) {
+  double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  memcpy(r, t, sizeof t);
+}
+static double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double norm3(const double a[3]) { return sqrt(dot3(a, a)); }
+static double normalize3(double a[3]) {
+  double n = norm3(a);
+  if (n < MINVAL) { a[0] = 1; a[1] = a[2] = 0; return n; }
+  a[0] /= n; a[1] /= n; a[2] /= n;
+  return n;
+}
+static void axis_angle_quat(double q[4], const double ax[3], double ang) {
+  double s = sin(ang / 2);
+  q[0] = cos(ang / 2); q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
+}
+static void mat_mul(double r[9], const double a[9], const double b[9]) {
+  double t[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+  memcpy(r, t, sizeof t);
+}
+/* spatial algebra [upstream engine_util_spatial.c]: motion/force vectors are (angular, linear) */
+static void mul_inert_vec(double r[6], const double i[10], const double v[6]) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+static void cross_motion(double r[6], const double v[6], const double u[6]) {
+  double t[6];
+  t[0] = -v[2] * u[1] + v[1] * u[2];
+  t[1] = v[2] * u[0] - v[0] * u[2];
+  t[2] = -v[1] * u[0] + v[0] * u[1];
+  t[3] = -v[2] * u[4] + v[1] * u[5] - v[5] * u[1] + v[4] * u[2];
+  t[4] = v[2] * u[3] - v[0] * u[5] + v[5] * u[0] - v[3] * u[2];
+  t[5] = -v[1] * u[3] + v[0] * u[4] - v[4] * u[0] + v[3] * u[1];
+  memcpy(r, t, sizeof t);
+}
+static void cross_force(double r[6], const double v[6], const double f[6]) {
+  double t[6];
+  t[0] = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
+  t[1] = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
+  t[2] = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
+  t[3] = -v[2] * f[4] + v[1] * f[5];
+  t[4] = v[2] * f[3] - v[0] * f[5];
+  t[5] = -v[1] * f[3] + v[0] * f[4];
+  memcpy(r, t, sizeof t);
+}
+static int is_bad(double x) { return isnan(x) || x > MAXVAL || x < -MAXVAL; }
+
+/* ------------------------------------------------------------------------ data */
+static double* dalloc(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
+
+orc_data* orc_make_data(const mrs_model_view* m) {
+  orc_data* d = (orc_data*)calloc(1, sizeof(orc_data));
+  d->qpos = dalloc(m->nq); d->qvel = dalloc(m->nv); d->ctrl = dalloc(m->nu);
+  d->qfrc_applied = dalloc(m->nv); d->qacc_warmstart = dalloc(m->nv); d->qacc = dalloc(m->nv);
+  d->qfrc_actuator = dalloc(m->nv); d->sensordata = dalloc(m->nsensordata);
+  orc_ws* w = (orc_ws*)calloc(1, sizeof(orc_ws));
+  int nb = m->nbody, nv = m->nv, nj = m->njnt, ng = m->ngeom;
+  w->xpos = dalloc(3 * nb); w->xquat = dalloc(4 * nb); w->xmat = dalloc(9 * nb);
+  w->xipos = dalloc(3 * nb); w->ximat = dalloc(9 * nb); w->xanchor = dalloc(3 * nj);
+  w->xaxis = dalloc(3 * nj); w->geom_xpos = dalloc(3 * ng); w->geom_xmat = dalloc(9 * ng);
+  w->subtree_com = dalloc(3 * nb); w->cinert = dalloc(10 * nb); w->cdof = dalloc(6 * nv);
+  w->crb = dalloc(10 * nb); w->cvel = dalloc(6 * nb); w->cdof_dot = dalloc(6 * nv);
+  w->cacc = dalloc(6 * nb); w->cfrc = dalloc(6 * nb);
+  w->M = dalloc(nv * nv); w->L = dalloc(nv * nv); w->Mi = dalloc(nv * nv); w->Li = dalloc(nv * nv);
+  w->qfrc_bias = dalloc(nv); w->qfrc_passive = dalloc(nv); w->qfrc_smooth = dalloc(nv);
+  w->qacc_smooth = dalloc(nv); w->qfrc_constraint = dalloc(nv); w->actuator_force = dalloc(m->nu);
+  w->tmp = dalloc(nv > 6 ? nv : 6); w->tmp2 = dalloc(nv > 6 ? nv : 6);
+  w->efc_J = dalloc((size_t)MAXEFC * nv); w->efc_MinvJT = dalloc((size_t)MAXEFC * nv);
+  w->AR = NULL;
+  d->ws = w;
+  orc_reset(m, d, -1);
+  return d;
+}
+
+void orc_free_data(orc_data* d) {
+  if (!d) return;
+  orc_ws* w = (orc_ws*)d->ws;
+  double* arrs[] = {w->xpos, w->xquat, w->xmat, w->xipos, w->ximat, w->xanchor, w->xaxis,
+                    w->geom_xpos, w->geom_xmat, w->subtree_com, w->cinert, w->cdof, w->crb,
+                    w->cvel, w->cdof_dot, w->cacc, w->cfrc, w->M, w->L, w->Mi, w->Li,
+                    w->qfrc_bias, w->qfrc_passive, w->qfrc_smooth, w->qacc_smooth,
+                    w->qfrc_constraint, w->actuator_force, w->tmp, w->tmp2, w->efc_J,
+                    w->efc_MinvJT, w->AR};
+  for (size_t i = 0; i < sizeof arrs / sizeof arrs[0]; ++i) free(arrs[i]);
+  free(w);
+  free(d->qpos); free(d->qvel); free(d->ctrl); free(d->qfrc_applied); free(d->qacc_warmstart);
+  free(d->qacc); free(d->qfrc_actuator); free(d->sensordata);
+  free(d);
+}
+
+/* mj_resetData / mj_resetDataKeyframe [upstream engine_io.c] */
+void orc_reset(const mrs_model_view* m, orc_data* d, int key) {
+  memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
+  memset(d->qvel, 0, sizeof(double) * m->nv);
+  memset(d->ctrl, 0, sizeof(double) * m->nu);
+  memset(d->qfrc_applied, 0, sizeof(double) * m->nv);
+  memset(d->qacc_warmstart, 0, sizeof(double) * m->nv);
+  memset(d->qacc, 0, sizeof(double) * m->nv);
+  memset(d->qfrc_actuator, 0, sizeof(double) * m->nv);
+  memset(d->sensordata, 0, sizeof(double) * m->nsensordata);
+  d->time = 0;
+  if (key >= 0 && key < m->nkey) {
+    d->time = m->key_time[key];
+    memcpy(d->qpos, m->key_qpos + (size_t)key * m->nq, sizeof(double) * m->nq);
+    memcpy(d->qvel, m->key_qvel + (size_t)key * m->nv, sizeof(double) * m->nv);
+    memcpy(d->ctrl, m->key_ctrl + (size_t)key * m->nu, sizeof(double) * m->nu);
+  }
+}
+
+/* ------------------------------------------------------------------------ kinematics
+ * mj_kinematics [upstream engine_core_smooth.c]: body frames from parent, joints applied in order
+ * (hinge: rotate about axis through anchor by qpos-qpos0; slide: translate; ball: quaternion;
+ * free: world pose from qpos), then inertial frames and geom frames. */
+static void kinematics(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  w->xpos[0] = w->xpos[1] = w->xpos[2] = 0;
+  w->xquat[0] = 1; w->xquat[1] = w->xquat[2] = w->xquat[3] = 0;
+  quat2mat(w->xmat, w->xquat);
+  memcpy(w->ximat, w->xmat, 9 * sizeof(double));
+  memset(w->xipos, 0, 3 * sizeof(double));
+  for (int b = 1; b < m->nbody; ++b) {
+    int p = m->body_parentid[b];
+    double* pos = w->xpos + 3 * b;
+    double* q = w->xquat + 4 * b;
+    int ja = m->body_jntadr[b];
+    if (m->body_jntnum[b] > 0 && m->jnt_type[ja] == MRS_JNT_FREE) {
+      const double* qp = d->qpos + m->jnt_qposadr[ja];
+      pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
+      q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+      quat_normalize(q);
+      memcpy(w->xanchor + 3 * ja, pos, 3 * sizeof(double));
+      memset(w->xaxis + 3 * ja, 0, 3 * sizeof(double));
+    } else {
+      double r[3];
+      rot_quat(r, m->body_pos + 3 * b, w->xquat + 4 * p);
+      for (int i = 0; i < 3; ++i) pos[i] = w->xpos[3 * p + i] + r[i];
+      quat_mul(q, w->xquat + 4 * p, m->body_quat + 4 * b);
+      for (int k = 0; k < m->body_jntnum[b]; ++k) {
+        int j = ja + k, a = m->jnt_qposadr[j];
+        double* anc = w->xanchor + 3 * j;
+        double* ax = w->xaxis + 3 * j;
+        rot_quat(anc, m->jnt_pos + 3 * j, q);
+        for (int i = 0; i < 3; ++i) anc[i] += pos[i];
+        rot_quat(ax, m->jnt_axis + 3 * j, q);
+        if (m->jnt_type[j] == MRS_JNT_SLIDE) {
+          double dq = d->qpos[a] - m->qpos0[a];
+          for (int i = 0; i < 3; ++i) pos[i] += ax[i] * dq;
+        } else {
+          double qloc[4];
+          if (m->jnt_type[j] == MRS_JNT_BALL) {
+            memcpy(qloc, d->qpos + a, 4 * sizeof(double));
+            quat_normalize(qloc);
+          } else {
+            axis_angle_quat(qloc, m->jnt_axis + 3 * j, d->qpos[a] - m->qpos0[a]);
+          }
+          quat_mul(q, q, qloc);
+          double v[3];
+          rot_quat(v, m->jnt_pos + 3 * j, q);
+          for (int i = 0; i < 3; ++i) pos[i] = anc[i] - v[i];
+        }
+      }
+    }
+    quat_normalize(q);
+    quat2mat(w->xmat + 9 * b, q);
+    double r[3], iq[4];
+    rot_quat(r, m->body_ipos + 3 * b, q);
+    for (int i = 0; i < 3; ++i) w->xipos[3 * b + i] = pos[i] + r[i];
+    quat_mul(iq, q, m->body_iquat + 4 * b);
+    quat2mat(w->ximat + 9 * b, iq);
+  }
+  for (int g = 0; g < m->ngeom; ++g) {
+    int b = m->geom_bodyid[g];
+    double r[3], gq[4];
+    rot_quat(r, m->geom_pos + 3 * g, w->xquat + 4 * b);
+    for (int i = 0; i < 3; ++i) w->geom_xpos[3 * g + i] = w->xpos[3 * b + i] + r[i];
+    quat_mul(gq, w->xquat + 4 * b, m->geom_quat + 4 * g);
+    quat2mat(w->geom_xmat + 9 * g, gq);
+  }
+}
+
+/* site world pose (mj_kinematics site loop) */
+static void site_pose(const mrs_model_view* m, orc_ws* w, int s, double pos[3], double mat[9]) {
+  int b = m->site_bodyid[s];
+  double r[3], q[4];
+  rot_quat(r, m->site_pos + 3 * s, w->xquat + 4 * b);
+  for (int i = 0; i < 3; ++i) pos[i] = w->xpos[3 * b + i] + r[i];
+  quat_mul(q, w->xquat + 4 * b, m->site_quat + 4 * s);
+  quat2mat(mat, q);
+}
+
+/* mj_comPos [upstream]: subtree centres of mass, com-based inertias (cinert), motion dofs (cdof) */
+static void com_pos(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nb = m->nbody;
+  for (int b = 0; b < nb; ++b)
+    for (int i = 0; i < 3; ++i) w->subtree_com[3 * b + i] = m->body_mass[b] * w->xipos[3 * b + i];
+  for (int b = nb - 1; b > 0; --b)
+    for (int i = 0; i < 3; ++i) w->subtree_com[3 * m->body_parentid[b] + i] += w->subtree_com[3 * b + i];
+  for (int b = 0; b < nb; ++b)
+    for (int i = 0; i < 3; ++i)
+      w->subtree_com[3 * b + i] = m->body_subtreemass[b] > MINVAL
+                                      ? w->subtree_com[3 * b + i] / m->body_subtreemass[b]
+                                      : w->xipos[3 * b + i];
+  memset(w->cinert, 0, 10 * sizeof(double));
+  for (int b = 1; b < nb; ++b) {
+    const double* mat = w->ximat + 9 * b;
+    const double* in = m->body_inertia + 3 * b;
+    double mass = m->body_mass[b], dif[3], full[9];
+    for (int i = 0; i < 3; ++i) dif[i] = w->xipos[3 * b + i] - w->subtree_com[3 * m->body_rootid[b] + i];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c)
+        full[3 * r + c] = mat[3 * r] * in[0] * mat[3 * c] + mat[3 * r + 1] * in[1] * mat[3 * c + 1] +
+                          mat[3 * r + 2] * in[2] * mat[3 * c + 2];
+    double* ci = w->cinert + 10 * b;
+    ci[0] = full[0] + mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+    ci[1] = full[4] + mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+    ci[2] = full[8] + mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+    ci[3] = full[1] - mass * dif[0] * dif[1];
+    ci[4] = full[2] - mass * dif[0] * dif[2];
+    ci[5] = full[5] - mass * dif[1] * dif[2];
+    ci[6] = mass * dif[0]; ci[7] = mass * dif[1]; ci[8] = mass * dif[2]; ci[9] = mass;
+  }
+  for (int j = 0; j < m->njnt; ++j) {
+    int b = m->jnt_bodyid[j], dof = m->jnt_dofadr[j];
+    const double* c = w->subtree_com + 3 * m->body_rootid[b];
+    double off[3];
+    for (int i = 0; i < 3; ++i) off[i] = c[i] - w->xanchor[3 * j + i];
+    double* cd;
+    switch (m->jnt_type[j]) {
+      case MRS_JNT_HINGE:
+        cd = w->cdof + 6 * dof;
+        memcpy(cd, w->xaxis + 3 * j, 3 * sizeof(double));
+        cross3(cd + 3, cd, off);
+        break;
+      case MRS_JNT_SLIDE:
+        cd = w->cdof + 6 * dof;
+        cd[0] = cd[1] = cd[2] = 0;
+        memcpy(cd + 3, w->xaxis + 3 * j, 3 * sizeof(double));
+        break;
+      case MRS_JNT_FREE:
+        for (int k = 0; k < 3; ++k) {
+          cd = w->cdof + 6 * (dof + k);
+          for (int i = 0; i < 6; ++i) cd[i] = (i == 3 + k) ? 1 : 0;
+        }
+        dof += 3;
+        /* fall through */
+      case MRS_JNT_BALL:
+        for (int k = 0; k < 3; ++k) {
+          cd = w->cdof + 6 * (dof + k);
+          const double* xm = w->xmat + 9 * b;
+          cd[0] = xm[k]; cd[1] = xm[3 + k]; cd[2] = xm[6 + k];
+          cross3(cd + 3, cd, off);
+        }
+        break;
+    }
+  }
+}
+
+/* mj_crb + armature [upstream mj_makeM]: composite inertias, dense symmetric M */
+static void make_M(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nb = m->nbody, nv = m->nv;
+  memcpy(w->crb, w->cinert, 10 * nb * sizeof(double));
+  for (int b = nb - 1; b > 0; --b)
+    if (m->body_parentid[b] > 0)
+      for (int i = 0; i < 10; ++i) w->crb[10 * m->body_parentid[b] + i] += w->crb[10 * b + i];
+  memset(w->M, 0, (size_t)nv * nv * sizeof(double));
+  for (int i = 0; i < nv; ++i) {
+    double buf[6];
+    mul_inert_vec(buf, w->crb + 10 * m->dof_bodyid[i], w->cdof + 6 * i);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      double v = 0;
+      for (int k = 0; k < 6; ++k) v += w->cdof[6 * j + k] * buf[k];
+      w->M[i * nv + j] = w->M[j * nv + i] = v;
+    }
+    w->M[i * nv + i] += m->dof_armature[i];
+  }
+}
+
+/* dense Cholesky A = L L' (lower).  MuJoCo factors M as sparse L'DL (mj_factorM); the factor
+ * differs but the solves are mathematically identical. */
+static void cholesky(const double* A, double* L, int n) {
+  memset(L, 0, (size_t)n * n * sizeof(double));
+  for (int j = 0; j < n; ++j) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; ++k) s -= L[j * n + k] * L[j * n + k];
+    L[j * n + j] = sqrt(s > MINVAL ? s : MINVAL);
+    for (int i = j + 1; i < n; ++i) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; ++k) t -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = t / L[j * n + j];
+    }
+  }
+}
+static void chol_solve(const double* L, double* x, const double* b, int n) {
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i * n + k] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = x[i];
+    for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+}
+
+/* mj_comVel [upstream]: body spatial velocities and cdof_dot = cvel x cdof (parent velocity) */
+static void com_vel(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  memset(w->cvel, 0, 6 * sizeof(double));
+  for (int b = 1; b < m->nbody; ++b) {
+    double cv[6];
+    memcpy(cv, w->cvel + 6 * m->body_parentid[b], sizeof cv);
+    int da = m->body_dofadr[b];
+    for (int k = 0; k < m->body_dofnum[b]; ++k) {
+      int j = da + k;
+      int jt = m->jnt_type[m->dof_jntid[j]];
+      if (jt == MRS_JNT_FREE && j == m->jnt_dofadr[m->dof_jntid[j]]) {
+        for (int t = 0; t < 3; ++t) {
+          memset(w->cdof_dot + 6 * (j + t), 0, 6 * sizeof(double));
+          for (int i = 0; i < 6; ++i) cv[i] += w->cdof[6 * (j + t) + i] * d->qvel[j + t];
+        }
+        k += 2;
+        continue;
+      }
+      if (jt == MRS_JNT_BALL || jt == MRS_JNT_FREE) {
+        /* rotational triple: cdof_dot with the velocity before the triple is added */
+        for (int t = 0; t < 3; ++t) cross_motion(w->cdof_dot + 6 * (j + t), cv, w->cdof + 6 * (j + t));
+        for (int t = 0; t < 3; ++t)
+          for (int i = 0; i < 6; ++i) cv[i] += w->cdof[6 * (j + t) + i] * d->qvel[j + t];
+        k += 2;
+        continue;
+      }
+      cross_motion(w->cdof_dot + 6 * j, cv, w->cdof + 6 * j);
+      for (int i = 0; i < 6; ++i) cv[i] += w->cdof[6 * j + i] * d->qvel[j];
+    }
+    memcpy(w->cvel + 6 * b, cv, sizeof cv);
+  }
+}
+
+/* mj_rne with flg_acc = 0 [upstream]: qfrc_bias = C(q,v) + g(q) */
+static void rne(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nb = m->nbody;
+  memset(w->cacc, 0, 6 * sizeof(double));
+  if (!(m->disableflags & MRS_DSBL_GRAVITY))
+    for (int i = 0; i < 3; ++i) w->cacc[3 + i] = -m->gravity[i];
+  memset(w->cfrc, 0, 6 * sizeof(double));
+  for (int b = 1; b < nb; ++b) {
+    double* ca = w->cacc + 6 * b;
+    memcpy(ca, w->cacc + 6 * m->body_parentid[b], 6 * sizeof(double));
+    int da = m->body_dofadr[b];
+    for (int k = 0; k < m->body_dofnum[b]; ++k)
+      for (int i = 0; i < 6; ++i) ca[i] += w->cdof_dot[6 * (da + k) + i] * d->qvel[da + k];
+    double f1[6], t[6], f2[6];
+    mul_inert_vec(f1, w->cinert + 10 * b, ca);
+    mul_inert_vec(t, w->cinert + 10 * b, w->cvel + 6 * b);
+    cross_force(f2, w->cvel + 6 * b, t);
+    for (int i = 0; i < 6; ++i) w->cfrc[6 * b + i] = f1[i] + f2[i];
+  }
+  for (int b = nb - 1; b > 0; --b)
+    if (m->body_parentid[b] > 0)
+      for (int i = 0; i < 6; ++i) w->cfrc[6 * m->body_parentid[b] + i] += w->cfrc[6 * b + i];
+  for (int j = 0; j < m->nv; ++j) {
+    double v = 0;
+    for (int i = 0; i < 6; ++i) v += w->cdof[6 * j + i] * w->cfrc[6 * m->dof_bodyid[j] + i];
+    w->qfrc_bias[j] = v;
+  }
+}
+
+/* does dof j move body b (j in b's dof chain)? */
+static int dof_affects(const mrs_model_view* m, int j, int b) {
+  int bj = m->dof_bodyid[j];
+  for (int x = b; x != 0; x = m->body_parentid[x])
+    if (x == bj) return 1;
+  return 0;
+}
+
+/* mj_jac translational part [upstream engine_core_smooth.c]: column j of the point Jacobian of a
+ * point attached to body b */
+static void jac_point_col(const mrs_model_view* m, orc_ws* w, int b, const double pnt[3], int j,
+                          double col[3]) {
+  double off[3], cr[3];
+  for (int i = 0; i < 3; ++i) off[i] = pnt[i] - w->subtree_com[3 * m->body_rootid[b] + i];
+  cross3(cr, w->cdof + 6 * j, off);
+  for (int i = 0; i < 3; ++i) col[i] = w->cdof[6 * j + 3 + i] + cr[i];
+}
+
+/* mj_passive [upstream engine_passive.c]: joint springs, dampers, gravity compensation */
+static void passive(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  memset(w->qfrc_passive, 0, m->nv * sizeof(double));
+  if (m->disableflags & MRS_DSBL_PASSIVE) return;
+  for (int j = 0; j < m->njnt; ++j) {
+    int t = m->jnt_type[j];
+    if ((t == MRS_JNT_HINGE || t == MRS_JNT_SLIDE) && m->jnt_stiffness[j] != 0) {
+      int a = m->jnt_qposadr[j];
+      w->qfrc_passive[m->jnt_dofadr[j]] -= m->jnt_stiffness[j] * (d->qpos[a] - m->qpos_spring[a]);
+    }
+  }
+  for (int i = 0; i < m->nv; ++i) w->qfrc_passive[i] -= m->dof_damping[i] * d->qvel[i];
+  if (!(m->disableflags & MRS_DSBL_GRAVITY)) {
+    for (int b = 1; b < m->nbody; ++b) {
+      if (m->body_gravcomp[b] == 0) continue;
+      double f[3];
+      for (int i = 0; i < 3; ++i) f[i] = -m->gravity[i] * m->body_mass[b] * m->body_gravcomp[b];
+      for (int j = 0; j < m->nv; ++j) {
+        if (!dof_affects(m, j, b)) continue;
+        double col[3];
+        jac_point_col(m, w, b, w->xipos + 3 * b, j, col);
+        w->qfrc_passive[j] += dot3(col, f);
+      }
+    }
+  }
+}
+
+/* mj_fwdActuation [upstream engine_forward.c] for joint transmissions without dynamics */
+static void actuation(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  memset(d->qfrc_actuator, 0, m->nv * sizeof(double));
+  if (m->disableflags & MRS_DSBL_ACTUATION) { memset(w->actuator_force, 0, m->nu * sizeof(double)); return; }
+  for (int a = 0; a < m->nu; ++a) {
+    int j = m->actuator_trnid[2 * a];
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    double gear = m->actuator_gear[6 * a];
+    double len = gear * d->qpos[qa], vel = gear * d->qvel[da];
+    double ctrl = d->ctrl[a];
+    if (m->actuator_ctrllimited[a] && !(m->disableflags & MRS_DSBL_CLAMPCTRL)) {
+      const double* r = m->actuator_ctrlrange + 2 * a;
+      ctrl = ctrl < r[0] ? r[0] : ctrl > r[1] ? r[1] : ctrl;
+    }
+    const double* g = m->actuator_gainprm + MRS_NGAIN * a;
+    const double* bp = m->actuator_biasprm + MRS_NBIAS * a;
+    double gain = g[0];
+    if (m->actuator_gaintype[a] == MRS_GAIN_AFFINE) gain = g[0] + g[1] * len + g[2] * vel;
+    double bias = 0;
+    if (m->actuator_biastype[a] == MRS_BIAS_AFFINE) bias = bp[0] + bp[1] * len + bp[2] * vel;
+    double force = gain * ctrl + bias;
+    if (m->actuator_forcelimited[a]) {
+      const double* r = m->actuator_forcerange + 2 * a;
+      force = force < r[0] ? r[0] : force > r[1] ? r[1] : force;
+    }
+    w->actuator_force[a] = force;
+    d->qfrc_actuator[da] += gear * force;
+  }
+  for (int j = 0; j < m->njnt; ++j) {
+    if (!m->jnt_actfrclimited[j]) continue;
+    const double* r = m->jnt_actfrcrange + 2 * j;
+    int da = m->jnt_dofadr[j];
+    int n = m->jnt_type[j] == MRS_JNT_FREE ? 6 : m->jnt_type[j] == MRS_JNT_BALL ? 3 : 1;
+    for (int k = 0; k < n; ++k) {
+      double v = d->qfrc_actuator[da + k];
+      d->qfrc_actuator[da + k] = v < r[0] ? r[0] : v > r[1] ? r[1] : v;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ collision
+ * Broad phase: every geom pair (g1 < g2) passing MuJoCo's filters [upstream engine_collision_driver.c
+ * mj_collision/filterBodyPair]: distinct weld bodies, not both static, parent-child weld filter,
+ * contype/conaffinity, bounding-sphere distance with margin.  Narrow phase: analytic primitives
+ * (plane-sphere/capsule/box, sphere-sphere, sphere-capsule, capsule-capsule, sphere-box,
+ * capsule-box).  Contact order = pair order, then the primitive's own order. */
+static void make_frame(double f[9]) {
+  normalize3(f);
+  if (fabs(f[1]) < 0.5) { f[3] = 0; f[4] = 1; f[5] = 0; }
+  else { f[3] = 0; f[4] = 0; f[5] = 1; }
+  double dd = dot3(f, f + 3);
+  for (int i = 0; i < 3; ++i) f[3 + i] -= dd * f[i];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+static int add_contact(orc_contact* out, int n, double dist, const double pos[3], const double nrm[3]) {
+  if (n >= 4) return n;
+  orc_contact* c = out + n;
+  c->dist = dist;
+  memcpy(c->pos, pos, 3 * sizeof(double));
+  memcpy(c->frame, nrm, 3 * sizeof(double));
+  make_frame(c->frame);
+  return n + 1;
+}
+static int col_sphere_sphere(const double p1[3], double r1, const double p2[3], double r2,
+                             double margin, orc_contact* out, int n) {
+  double dv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  double len = norm3(dv);
+  double dist = len - r1 - r2;
+  if (dist > margin) return n;
+  double nrm[3];
+  if (len < MINVAL) { nrm[0] = 1; nrm[1] = nrm[2] = 0; }
+  else { nrm[0] = dv[0] / len; nrm[1] = dv[1] / len; nrm[2] = dv[2] / len; }
+  double pos[3];
+  for (int i = 0; i < 3; ++i) pos[i] = p1[i] + nrm[i] * (r1 + dist / 2);
+  return add_contact(out, n, dist, pos, nrm);
+}
+static void segment_point_closest(const double a[3], const double b[3], const double p[3], double c[3]) {
+  double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  double den = dot3(ab, ab), t = den > MINVAL ? dot3(ap, ab) / den : 0;
+  t = t < 0 ? 0 : t > 1 ? 1 : t;
+  for (int i = 0; i < 3; ++i) c[i] = a[i] + t * ab[i];
+}
+/* closest points of two segments (clamped parametric form) */
+static void segment_segment_closest(const double a0[3], const double a1[3], const double b0[3],
+                                    const double b1[3], double ca[3], double cb[3]) {
+  double d1[3] = {a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]};
+  double d2[3] = {b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2]};
+  double r[3] = {a0[0] - b0[0], a0[1] - b0[1], a0[2] - b0[2]};
+  double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  double s = 0, t = 0;
+  if (a <= MINVAL && e <= MINVAL) { s = t = 0; }
+  else if (a <= MINVAL) { s = 0; t = f / e; t = t < 0 ? 0 : t > 1 ? 1 : t; }
+  else {
+    double c = dot3(d1, r);
+    if (e <= MINVAL) { t = 0; s = -c / a; s = s < 0 ? 0 : s > 1 ? 1 : s; }
+    else {
+      double bb = dot3(d1, d2), den = a * e - bb * bb;
+      s = den > MINVAL * a * e ? (bb * f - c * e) / den : 0;
+      s = s < 0 ? 0 : s > 1 ? 1 : s;
+      t = (bb * s + f) / e;
+      if (t < 0) { t = 0; s = -c / a; s = s < 0 ? 0 : s > 1 ? 1 : s; }
+      else if (t > 1) { t = 1; s = (bb - c) / a; s = s < 0 ? 0 : s > 1 ? 1 : s; }
+    }
+  }
+  for (int i = 0; i < 3; ++i) { ca[i] = a0[i] + s * d1[i]; cb[i] = b0[i] + t * d2[i]; }
+}
+static void capsule_ends(const double* pos, const double* mat, double hl, double a[3], double b[3]) {
+  for (int i = 0; i < 3; ++i) { a[i] = pos[i] - mat[3 * i + 2] * hl; b[i] = pos[i] + mat[3 * i + 2] * hl; }
+}
+/* plane (geom1) vs sphere at p with radius r */
+static int col_plane_sphere(const double* ppos, const double* pmat, const double p[3], double r,
+                            double margin, orc_contact* out, int n) {
+  double nrm[3] = {pmat[2], pmat[5], pmat[8]};
+  double dv[3] = {p[0] - ppos[0], p[1] - ppos[1], p[2] - ppos[2]};
+  double dist = dot3(dv, nrm) - r;
+  if (dist > margin) return n;
+  double pos[3];
+  for (int i = 0; i < 3; ++i) pos[i] = p[i] - nrm[i] * (r + dist / 2);
+  return add_contact(out, n, dist, pos, nrm);
+}
+static int col_plane_box(const double* ppos, const double* pmat, const double* bpos, const double* bmat,
+                         const double* size, double margin, orc_contact* out, int n) {
+  double nrm[3] = {pmat[2], pmat[5], pmat[8]};
+  double dv[3] = {bpos[0] - ppos[0], bpos[1] - ppos[1], bpos[2] - ppos[2]};
+  double cdist = dot3(dv, nrm);
+  for (int k = 0; k < 8 && n < 4; ++k) {
+    double v[3] = {(k & 1) ? size[0] : -size[0], (k & 2) ? size[1] : -size[1], (k & 4) ? size[2] : -size[2]};
+    double c[3];
+    mat_vec(c, bmat, v);
+    double ld = dot3(nrm, c);
+    double dist = cdist + ld;
+    if (dist > margin || ld > 0) continue;
+    double pos[3];
+    for (int i = 0; i < 3; ++i) pos[i] = bpos[i] + c[i] - nrm[i] * dist / 2;
+    n = add_contact(out, n, dist, pos, nrm);
+  }
+  return n;
+}
+/* sphere (center p, radius r) vs box (geom2): normal points from sphere to box */
+static int col_sphere_box(const double p[3], double r, const double* bpos, const double* bmat,
+                          const double* size, double margin, orc_contact* out, int n) {
+  double dv[3] = {p[0] - bpos[0], p[1] - bpos[1], p[2] - bpos[2]}, l[3];
+  matT_vec(l, bmat, dv);
+  double c[3];
+  int inside = 1;
+  for (int i = 0; i < 3; ++i) {
+    c[i] = l[i] < -size[i] ? -size[i] : l[i] > size[i] ? size[i] : l[i];
+    if (c[i] != l[i]) inside = 0;
+  }
+  double nrm_l[3], dist;
+  if (!inside) {
+    double dl[3] = {c[0] - l[0], c[1] - l[1], c[2] - l[2]};
+    double len = norm3(dl);
+    dist = len - r;
+    if (dist > margin) return n;
+    for (int i = 0; i < 3; ++i) nrm_l[i] = dl[i] / len;
+  } else {
+    /* centre inside: push out through the nearest face */
+    int ax = 0;
+    double best = 1e300;
+    for (int i = 0; i < 3; ++i) {
+      double pen = size[i] - fabs(l[i]);
+      if (pen < best) { best = pen; ax = i; }
+    }
+    dist = -best - r;
+    nrm_l[0] = nrm_l[1] = nrm_l[2] = 0;
+    nrm_l[ax] = l[ax] >= 0 ? -1 : 1;
+    c[ax] = l[ax] >= 0 ? size[ax] : -size[ax];
+  }
+  double nrm[3], pos[3];
+  mat_vec(nrm, bmat, nrm_l);
+  /* contact point halfway between the sphere surface and the box surface */
+  for (int i = 0; i < 3; ++i) pos[i] = p[i] + nrm[i] * (r + dist / 2);
+  return add_contact(out, n, dist, pos, nrm);
+}
+/* distance^2 from point (box-local) to the box */
+static double box_dist2(const double l[3], const double* size) {
+  double s = 0;
+  for (int i = 0; i < 3; ++i) {
+    double e = fabs(l[i]) - size[i];
+    if (e > 0) s += e * e;
+  }
+  return s;
+}
+/* capsule (segment a-b, radius r) vs box: closest segment point by fixed-iteration ternary search
+ * on the convex distance function, then sphere-box at that point (restated primitive; MuJoCo's
+ * mjc_CapsuleBox may emit a second contact for flat poses) */
+static int col_capsule_box(const double a[3], const double b[3], double r, const double* bpos,
+                           const double* bmat, const double* size, double margin, orc_contact* out, int n) {
+  double lo = 0, hi = 1;
+  for (int it = 0; it < 40; ++it) {
+    double t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3, p1[3], p2[3], l1[3], l2[3];
+    for (int i = 0; i < 3; ++i) {
+      p1[i] = a[i] + t1 * (b[i] - a[i]) - bpos[i];
+      p2[i] = a[i] + t2 * (b[i] - a[i]) - bpos[i];
+    }
+    matT_vec(l1, bmat, p1);
+    matT_vec(l2, bmat, p2);
+    if (box_dist2(l1, size) <= box_dist2(l2, size)) hi = t2;
+    else lo = t1;
+  }
+  double t = 0.5 * (lo + hi), p[3];
+  for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
+  return col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
+}
+
+static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, double margin, orc_contact* out) {
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const double *p1 = w->geom_xpos + 3 * g1, *p2 = w->geom_xpos + 3 * g2;
+  const double *m1 = w->geom_xmat + 9 * g1, *m2 = w->geom_xmat + 9 * g2;
+  const double *s1 = m->geom_size + 3 * g1, *s2 = m->geom_size + 3 * g2;
+  double a1[3], b1[3], a2[3], b2[3], c1[3], c2[3];
+  int n = 0;
+  if (t1 == MRS_GEOM_PLANE) {
+    switch (t2) {
+      case MRS_GEOM_SPHERE: return col_plane_sphere(p1, m1, p2, s2[0], margin, out, 0);
+      case MRS_GEOM_CAPSULE:
+        capsule_ends(p2, m2, s2[1], a2, b2);
+        n = col_plane_sphere(p1, m1, a2, s2[0], margin, out, 0);
+        return col_plane_sphere(p1, m1, b2, s2[0], margin, out, n);
+      case MRS_GEOM_BOX: return col_plane_box(p1, m1, p2, m2, s2, margin, out, 0);
+    }
+  } else if (t1 == MRS_GEOM_SPHERE) {
+    switch (t2) {
+      case MRS_GEOM_SPHERE: return col_sphere_sphere(p1, s1[0], p2, s2[0], margin, out, 0);
+      case MRS_GEOM_CAPSULE:
+        capsule_ends(p2, m2, s2[1], a2, b2);
+        segment_point_closest(a2, b2, p1, c2);
+        return col_sphere_sphere(p1, s1[0], c2, s2[0], margin, out, 0);
+      case MRS_GEOM_BOX: return col_sphere_box(p1, s1[0], p2, m2, s2, margin, out, 0);
+    }
+  } else if (t1 == MRS_GEOM_CAPSULE) {
+    switch (t2) {
+      case MRS_GEOM_CAPSULE:
+        capsule_ends(p1, m1, s1[1], a1, b1);
+        capsule_ends(p2, m2, s2[1], a2, b2);
+        segment_segment_closest(a1, b1, a2, b2, c1, c2);
+        return col_sphere_sphere(c1, s1[0], c2, s2[0], margin, out, 0);
+      case MRS_GEOM_BOX:
+        capsule_ends(p1, m1, s1[1], a1, b1);
+        return col_capsule_box(a1, b1, s1[0], p2, m2, s2, margin, out, 0);
+    }
+  }
+  return -1; /* unsupported pair */
+}
+
+static void collision(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  w->ncon = 0;
+  if (m->disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) return;
+  for (int g1 = 0; g1 < m->ngeom; ++g1)
+    for (int g2 = g1 + 1; g2 < m->ngeom; ++g2) {
+      int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+      int w1 = m->body_weldid[b1], w2 = m->body_weldid[b2];
+      if (w1 == w2) continue;
+      if (!(m->disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
+          (w1 == m->body_weldid[m->body_parentid[w2]] || w2 == m->body_weldid[m->body_parentid[w1]]))
+        continue;
+      if (!((m->geom_contype[g1] & m->geom_conaffinity[g2]) || (m->geom_contype[g2] & m->geom_conaffinity[g1])))
+        continue;
+      double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
+      double gap = fmax(m->geom_gap[g1], m->geom_gap[g2]);
+      if (m->geom_type[g1] != MRS_GEOM_PLANE && m->geom_type[g2] != MRS_GEOM_PLANE) {
+        double dv[3];
+        for (int i = 0; i < 3; ++i) dv[i] = w->geom_xpos[3 * g1 + i] - w->geom_xpos[3 * g2 + i];
+        if (norm3(dv) > m->geom_rbound[g1] + m->geom_rbound[g2] + margin) continue;
+      }
+      int ga = g1, gb = g2;
+      if (m->geom_type[ga] > m->geom_type[gb]) { ga = g2; gb = g1; }
+      orc_contact tmp[4];
+      int nc = narrowphase(m, w, ga, gb, margin, tmp);
+      if (nc < 0) continue; /* unsupported pairs are rejected at batch creation in the product */
+      /* contact parameters [upstream mj_contactParam]: max friction/condim, solmix-weighted solref */
+      double mix, s1 = m->geom_solmix[ga], s2 = m->geom_solmix[gb];
+      if (s1 >= MINVAL && s2 >= MINVAL) mix = s1 / (s1 + s2);
+      else if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+      else mix = s1 < MINVAL ? 0 : 1;
+      for (int k = 0; k < nc && w->ncon < MAXCON; ++k) {
+        orc_contact* c = &w->con[w->ncon++];
+        *c = tmp[k];
+        c->geom[0] = ga; c->geom[1] = gb;
+        c->dim = m->geom_condim[ga] > m->geom_condim[gb] ? m->geom_condim[ga] : m->geom_condim[gb];
+        for (int i = 0; i < 3; ++i) c->friction[i] = fmax(m->geom_friction[3 * ga + i], m->geom_friction[3 * gb + i]);
+        for (int i = 0; i < 2; ++i) c->solref[i] = mix * m->geom_solref[2 * ga + i] + (1 - mix) * m->geom_solref[2 * gb + i];
+        for (int i = 0; i < 5; ++i) c->solimp[i] = mix * m->geom_solimp[5 * ga + i] + (1 - mix) * m->geom_solimp[5 * gb + i];
+        c->includemargin = margin - gap;
+      }
+    }
+}
+
+/* ------------------------------------------------------------------------ constraints
+ * mj_makeConstraint [upstream engine_core_constraint.c]: dof friction loss rows, joint limit rows
+ * (lower then upper, active when dist < margin), pyramidal contact rows (condim 3: four edges
+ * J_n +/- mu_k J_tk).  mj_makeImpedance: impedance from solimp, R = (1-imp)/imp * diagApprox,
+ * aref = -B v - K imp (pos - margin). */
+static double impedance(const double* solimp, double pos, double margin) {
+  double dmin = solimp[0], dmax = solimp[1], width = solimp[2], mid = solimp[3], power = solimp[4];
+  dmin = dmin < 0.0001 ? 0.0001 : dmin > 0.9999 ? 0.9999 : dmin;
+  dmax = dmax < 0.0001 ? 0.0001 : dmax > 0.9999 ? 0.9999 : dmax;
+  if (dmin == dmax || width <= MINVAL) return 0.5 * (dmin + dmax);
+  double x = fabs(pos - margin) / width;
+  if (x >= 1) return dmax;
+  if (x <= 0) return dmin;
+  double y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = pow(x, power) / pow(mid, power - 1);
+  else y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+static void add_row(orc_ws* w, int nv, int type, int id, const double* J, double pos, double margin,
+                    double floss, double diag, const double* solref, const double* solimp) {
+  if (w->nefc >= MAXEFC) return;
+  int r = w->nefc++;
+  memcpy(w->efc_J + (size_t)r * nv, J, nv * sizeof(double));
+  w->efc_type[r] = type; w->efc_id[r] = id;
+  w->efc_pos[r] = pos; w->efc_margin[r] = margin; w->efc_frictionloss[r] = floss;
+  w->efc_diag[r] = diag;
+  memcpy(w->efc_solref[r], solref, 2 * sizeof(double));
+  memcpy(w->efc_solimp[r], solimp, 5 * sizeof(double));
+}
+
+static void make_constraint(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nv = m->nv;
+  w->nefc = 0;
+  if (m->disableflags & MRS_DSBL_CONSTRAINT) return;
+  double* J = (double*)malloc(nv * sizeof(double) + 8);
+  if (!(m->disableflags & MRS_DSBL_FRICTIONLOSS))
+    for (int j = 0; j < nv; ++j) {
+      if (m->dof_frictionloss[j] <= 0) continue;
+      memset(J, 0, nv * sizeof(double));
+      J[j] = 1;
+      add_row(w, nv, EFC_FRICTION, j, J, 0, 0, m->dof_frictionloss[j], m->dof_invweight0[j],
+              m->dof_solref + 2 * j, m->dof_solimp + 5 * j);
+    }
+  if (!(m->disableflags & MRS_DSBL_LIMIT))
+    for (int j = 0; j < m->njnt; ++j) {
+      if (!m->jnt_limited[j]) continue;
+      int t = m->jnt_type[j];
+      if (t != MRS_JNT_HINGE && t != MRS_JNT_SLIDE) continue;
+      double q = d->qpos[m->jnt_qposadr[j]], margin = m->jnt_margin[j];
+      int da = m->jnt_dofadr[j];
+      for (int side = -1; side <= 1; side += 2) {
+        double dist = side * (m->jnt_range[2 * j + (side + 1) / 2] - q);
+        if (dist < margin) {
+          memset(J, 0, nv * sizeof(double));
+          J[da] = -side;
+          add_row(w, nv, EFC_LIMIT, j, J, dist, margin, 0, m->dof_invweight0[da],
+                  m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j);
+        }
+      }
+    }
+  /* contacts */
+  for (int c = 0; c < w->ncon; ++c) {
+    orc_contact* con = &w->con[c];
+    int b1 = m->geom_bodyid[con->geom[0]], b2 = m->geom_bodyid[con->geom[1]];
+    double tran = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
+    double* Jc = (double*)calloc(3 * (size_t)nv, sizeof(double)); /* rows: normal, t1, t2 */
+    for (int j = 0; j < nv; ++j) {
+      double col1[3] = {0, 0, 0}, col2[3] = {0, 0, 0};
+      if (dof_affects(m, j, b1)) jac_point_col(m, w, b1, con->pos, j, col1);
+      if (dof_affects(m, j, b2)) jac_point_col(m, w, b2, con->pos, j, col2);
+      double dc[3] = {col2[0] - col1[0], col2[1] - col1[1], col2[2] - col1[2]};
+      for (int r = 0; r < 3; ++r) Jc[r * nv + j] = dot3(con->frame + 3 * r, dc);
+    }
+    if (con->dim == 1) {
+      add_row(w, nv, EFC_CONTACT, c, Jc, con->dist, con->includemargin, 0, tran, con->solref, con->solimp);
+    } else {
+      for (int k = 1; k < 3; ++k)
+        for (int s = 1; s >= -1; s -= 2) {
+          for (int j = 0; j < nv; ++j) J[j] = Jc[j] + s * con->friction[k - 1] * Jc[k * nv + j];
+          add_row(w, nv, EFC_CONTACT, c, J, con->dist, con->includemargin, 0,
+                  tran * (1 + con->friction[k - 1] * con->friction[k - 1]), con->solref, con->solimp);
+        }
+    }
+    free(Jc);
+  }
+  free(J);
+  /* impedance, R, D, aref */
+  for (int r = 0; r < w->nefc; ++r) {
+    const double* sr = w->efc_solref[r];
+    double imp = impedance(w->efc_solimp[r], w->efc_pos[r], w->efc_margin[r]);
+    double R = (1 - imp) * w->efc_diag[r] / imp;
+    w->efc_R[r] = R > MINVAL ? R : MINVAL;
+    w->efc_D[r] = 1 / w->efc_R[r];
+    double K, B;
+    double dmax = w->efc_solimp[r][1];
+    dmax = dmax < 0.0001 ? 0.0001 : dmax > 0.9999 ? 0.9999 : dmax;
+    if (sr[0] > 0) {
+      double tc = sr[0], dr = sr[1];
+      if (!(m->disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m->timestep) tc = 2 * m->timestep;
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -sr[0] / (dmax * dmax);
+      B = -sr[1] / dmax;
+    }
+    double vel = 0;
+    for (int j = 0; j < nv; ++j) vel += w->efc_J[(size_t)r * nv + j] * d->qvel[j];
+    w->efc_vel[r] = vel;
+    double pterm = w->efc_type[r] == EFC_FRICTION ? 0 : K * imp * (w->efc_pos[r] - w->efc_margin[r]);
+    w->efc_aref[r] = -B * vel - pterm;
+    w->efc_KBIP[r][0] = K; w->efc_KBIP[r][1] = B; w->efc_KBIP[r][2] = imp; w->efc_KBIP[r][3] = 0;
+  }
+}
+
+/* force of one row for a given jar = J qacc - aref (mj_constraintUpdate primal states) */
+static double row_force(orc_ws* w, int r, double jar) {
+  double D = w->efc_D[r];
+  if (w->efc_type[r] == EFC_FRICTION) {
+    double fl = w->efc_frictionloss[r], Rr = w->efc_R[r];
+    if (jar <= -Rr * fl) return fl;
+    if (jar >= Rr * fl) return -fl;
+    return -D * jar;
+  }
+  return jar < 0 ? -D * jar : 0;
+}
+
+/* mj_solPGS [upstream engine_solver.c] on the dual problem
+ *   min 0.5 f'AR f + f'b,  AR = J M^-1 J' + diag(R),  b = J qacc_smooth - aref,
+ * friction rows boxed to [-frictionloss, frictionloss], limit/contact rows f >= 0; warm start from
+ * qacc_warmstart (forces of mj_constraintUpdate), kept only if its dual cost is negative; stop when
+ * the scaled cost improvement of a sweep falls below tolerance. */
+static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nv = m->nv, nefc = w->nefc;
+  if (nefc == 0) {
+    memcpy(d->qacc, w->qacc_smooth, nv * sizeof(double));
+    memset(w->qfrc_constraint, 0, nv * sizeof(double));
+    return;
+  }
+  /* M^-1 J' */
+  for (int r = 0; r < nefc; ++r) chol_solve(w->L, w->efc_MinvJT + (size_t)r * nv, w->efc_J + (size_t)r * nv, nv);
+  free(w->AR);
+  w->AR = dalloc((size_t)nefc * nefc);
+  for (int r = 0; r < nefc; ++r)
+    for (int s = 0; s < nefc; ++s) {
+      double v = 0;
+      for (int j = 0; j < nv; ++j) v += w->efc_J[(size_t)r * nv + j] * w->efc_MinvJT[(size_t)s * nv + j];
+      w->AR[(size_t)r * nefc + s] = v + (r == s ? w->efc_R[r] : 0);
+    }
+  for (int r = 0; r < nefc; ++r) {
+    double v = 0;
+    for (int j = 0; j < nv; ++j) v += w->efc_J[(size_t)r * nv + j] * w->qacc_smooth[j];
+    w->efc_b[r] = v - w->efc_aref[r];
+  }
+  double* f = w->efc_force;
+  memset(f, 0, nefc * sizeof(double));
+  if (!(m->disableflags & MRS_DSBL_WARMSTART)) {
+    for (int r = 0; r < nefc; ++r) {
+      double jar = -w->efc_aref[r];
+      for (int j = 0; j < nv; ++j) jar += w->efc_J[(size_t)r * nv + j] * d->qacc_warmstart[j];
+      f[r] = row_force(w, r, jar);
+    }
+    double cost = 0;
+    for (int r = 0; r < nefc; ++r) {
+      double arf = 0;
+      for (int s = 0; s < nefc; ++s) arf += w->AR[(size_t)r * nefc + s] * f[s];
+      cost += f[r] * (0.5 * arf + w->efc_b[r]);
+    }
+    if (cost > 0) memset(f, 0, nefc * sizeof(double));
+  }
+  double scale = 1 / (m->stat_meaninertia * (nv > 1 ? nv : 1));
+  for (int it = 0; it < m->iterations; ++it) {
+    double improvement = 0;
+    for (int r = 0; r < nefc; ++r) {
+      const double* ar = w->AR + (size_t)r * nefc;
+      double res = w->efc_b[r];
+      for (int s = 0; s < nefc; ++s) res += ar[s] * f[s];
+      double old = f[r];
+      double nf = old - res / ar[r];
+      if (w->efc_type[r] == EFC_FRICTION) {
+        double fl = w->efc_frictionloss[r];
+        nf = nf < -fl ? -fl : nf > fl ? fl : nf;
+      } else if (nf < 0) {
+        nf = 0;
+      }
+      double delta = nf - old;
+      f[r] = nf;
+      improvement -= delta * res + 0.5 * delta * delta * ar[r];
+    }
+    if (improvement * scale < m->tolerance) break;
+  }
+  for (int j = 0; j < nv; ++j) {
+    double v = 0;
+    for (int r = 0; r < nefc; ++r) v += w->efc_J[(size_t)r * nv + j] * f[r];
+    w->qfrc_constraint[j] = v;
+  }
+  chol_solve(w->L, w->tmp, w->qfrc_constraint, nv);
+  for (int j = 0; j < nv; ++j) d->qacc[j] = w->qacc_smooth[j] + w->tmp[j];
+}
+
+/* ------------------------------------------------------------------------ ray casting
+ * mj_ray / mju_rayGeom [upstream engine_ray.c]: ray in the geom's local frame against the
+ * analytic primitive; nearest non-negative hit; planes are clipped to their rendered rectangle. */
+static double ray_quad(double a, double b, double c, double x[2]) {
+  double det = b * b - a * c;
+  if (det < MINVAL) { x[0] = x[1] = -1; return -1; }
+  det = sqrt(det);
+  x[0] = (-b - det) / a;
+  x[1] = (-b + det) / a;
+  if (x[0] >= 0) return x[0];
+  if (x[1] >= 0) return x[1];
+  return -1;
+}
+static double ray_geom_local(int type, const double* s, const double lp[3], const double lv[3]) {
+  double x[2];
+  switch (type) {
+    case MRS_GEOM_PLANE: {
+      if (lv[2] > -MINVAL) return -1;
+      double t = -lp[2] / lv[2];
+      if (t < 0) return -1;
+      double p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
+      if ((s[0] <= 0 || fabs(p0) <= s[0]) && (s[1] <= 0 || fabs(p1) <= s[1])) return t;
+      return -1;
+    }
+    case MRS_GEOM_SPHERE:
+      return ray_quad(dot3(lv, lv), dot3(lv, lp), dot3(lp, lp) - s[0] * s[0], x);
+    case MRS_GEOM_CAPSULE: {
+      double best = -1;
+      /* cylinder part */
+      double a = lv[0] * lv[0] + lv[1] * lv[1];
+      if (a > MINVAL) {
+        double b = lv[0] * lp[0] + lv[1] * lp[1], c = lp[0] * lp[0] + lp[1] * lp[1] - s[0] * s[0];
+        ray_quad(a, b, c, x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && fabs(lp[2] + x[i] * lv[2]) <= s[1] && (best < 0 || x[i] < best)) best = x[i];
+      }
+      /* end caps */
+      for (int e = -1; e <= 1; e += 2) {
+        double q[3] = {lp[0], lp[1], lp[2] - e * s[1]};
+        ray_quad(dot3(lv, lv), dot3(lv, q), dot3(q, q) - s[0] * s[0], x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && e * (lp[2] + x[i] * lv[2] - e * s[1]) >= 0 && (best < 0 || x[i] < best)) best = x[i];
+      }
+      return best;
+    }
+    case MRS_GEOM_ELLIPSOID: {
+      double q[3] = {lp[0] / s[0], lp[1] / s[1], lp[2] / s[2]}, v[3] = {lv[0] / s[0], lv[1] / s[1], lv[2] / s[2]};
+      return ray_quad(dot3(v, v), dot3(v, q), dot3(q, q) - 1, x);
+    }
+    case MRS_GEOM_CYLINDER: {
+      double best = -1;
+      double a = lv[0] * lv[0] + lv[1] * lv[1];
+      if (a > MINVAL) {
+        double b = lv[0] * lp[0] + lv[1] * lp[1], c = lp[0] * lp[0] + lp[1] * lp[1] - s[0] * s[0];
+        ray_quad(a, b, c, x);
+        for (int i = 0; i < 2; ++i)
+          if (x[i] >= 0 && fabs(lp[2] + x[i] * lv[2]) <= s[1] && (best < 0 || x[i] < best)) best = x[i];
+      }
+      if (fabs(lv[2]) > MINVAL)
+        for (int e = -1; e <= 1; e += 2) {
+          double t = (e * s[1] - lp[2]) / lv[2];
+          if (t < 0) continue;
+          double p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
+          if (p0 * p0 + p1 * p1 <= s[0] * s[0] && (best < 0 || t < best)) best = t;
+        }
+      return best;
+    }
+    case MRS_GEOM_BOX: {
+      double best = -1;
+      for (int i = 0; i < 3; ++i) {
+        if (fabs(lv[i]) <= MINVAL) continue;
+        int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+        for (int side = -1; side <= 1; side += 2) {
+          double t = (side * s[i] - lp[i]) / lv[i];
+          if (t < 0) continue;
+          double p1 = lp[i1] + t * lv[i1], p2 = lp[i2] + t * lv[i2];
+          if (fabs(p1) <= s[i1] && fabs(p2) <= s[i2] && (best < 0 || t < best)) best = t;
+        }
+      }
+      return best;
+    }
+  }
+  return -1;
+}
+static double ray_geom(const mrs_model_view* m, orc_ws* w, int g, const double pnt[3], const double vec[3]) {
+  const double* gp = w->geom_xpos + 3 * g;
+  const double* gm = w->geom_xmat + 9 * g;
+  double dv[3] = {pnt[0] - gp[0], pnt[1] - gp[1], pnt[2] - gp[2]}, lp[3], lv[3];
+  matT_vec(lp, gm, dv);
+  matT_vec(lv, gm, vec);
+  return ray_geom_local(m->geom_type[g], m->geom_size + 3 * g, lp, lv);
+}
+/* geoms a ray may hit: not on the excluded body, not fully transparent (ray_eliminate) */
+static double ray_scene(const mrs_model_view* m, orc_ws* w, const double pnt[3], const double vec[3],
+                        int bodyexclude, int groupmask, double tmin, int* geomid) {
+  double dist = -1;
+  int id = -1;
+  for (int g = 0; g < m->ngeom; ++g) {
+    if (m->geom_bodyid[g] == bodyexclude) continue;
+    if (m->geom_rgba[4 * g + 3] == 0) continue;
+    if (groupmask && !(m->geom_group[g] >= 0 && m->geom_group[g] < 6 && ((groupmask >> m->geom_group[g]) & 1))) continue;
+    double t = ray_geom(m, w, g, pnt, vec);
+    if (t >= tmin && (dist < 0 || t < dist)) { dist = t; id = g; }
+  }
+  if (geomid) *geomid = id;
+  return dist;
+}
+double orc_ray(const mrs_model_view* m, orc_data* d, const double pnt[3], const double vec[3],
+               int bodyexclude, int* geomid) {
+  return ray_scene(m, (orc_ws*)d->ws, pnt, vec, bodyexclude, 0, 0, geomid);
+}
+
+/* ------------------------------------------------------------------------ sensors
+ * mj_sensorPos/Vel [upstream engine_sensor.c] for the implemented types */
+static void sensors(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  if (m->disableflags & MRS_DSBL_SENSOR) return;
+  for (int s = 0; s < m->nsensor; ++s) {
+    double* out = d->sensordata + m->sensor_adr[s];
+    int id = m->sensor_objid[s];
+    switch (m->sensor_type[s]) {
+      case MRS_SENS_RANGEFINDER: {
+        double pos[3], mat[9];
+        site_pose(m, w, id, pos, mat);
+        double vec[3] = {mat[2], mat[5], mat[8]};
+        out[0] = ray_scene(m, w, pos, vec, m->site_bodyid[id], 0, 0, NULL);
+        break;
+      }
+      case MRS_SENS_JOINTPOS: out[0] = d->qpos[m->jnt_qposadr[id]]; break;
+      case MRS_SENS_JOINTVEL: out[0] = d->qvel[m->jnt_dofadr[id]]; break;
+      case MRS_SENS_ACTUATORFRC: out[0] = w->actuator_force[id]; break;
+      case MRS_SENS_FRAMEPOS:
+      case MRS_SENS_FRAMEQUAT: {
+        double pos[3], q[4];
+        int ot = m->sensor_objtype[s];
+        if (ot == MRS_OBJ_SITE) {
+          int b = m->site_bodyid[id];
+          double r[3];
+          rot_quat(r, m->site_pos + 3 * id, w->xquat + 4 * b);
+          for (int i = 0; i < 3; ++i) pos[i] = w->xpos[3 * b + i] + r[i];
+          quat_mul(q, w->xquat + 4 * b, m->site_quat + 4 * id);
+        } else if (ot == MRS_OBJ_BODY) {
+          memcpy(pos, w->xpos + 3 * id, sizeof pos);
+          memcpy(q, w->xquat + 4 * id, sizeof q);
+        } else {
+          int b = m->geom_bodyid[id];
+          memcpy(pos, w->geom_xpos + 3 * id, sizeof pos);
+          quat_mul(q, w->xquat + 4 * b, m->geom_quat + 4 * id);
+        }
+        if (m->sensor_type[s] == MRS_SENS_FRAMEPOS) memcpy(out, pos, sizeof pos);
+        else { quat_normalize(q); memcpy(out, q, sizeof q); }
+        break;
+      }
+      case MRS_SENS_GYRO: {
+        double pos[3], mat[9];
+        site_pose(m, w, id, pos, mat);
+        matT_vec(out, mat, w->cvel + 6 * m->site_bodyid[id]);
+        break;
+      }
+      default: memset(out, 0, m->sensor_dim[s] * sizeof(double));
+    }
+    if (m->sensor_cutoff[s] > 0 && m->sensor_type[s] != MRS_SENS_RANGEFINDER &&
+        m->sensor_type[s] != MRS_SENS_FRAMEQUAT)
+      for (int i = 0; i < m->sensor_dim[s]; ++i) {
+        double c = m->sensor_cutoff[s];
+        out[i] = out[i] < -c ? -c : out[i] > c ? c : out[i];
+      }
+  }
+}
+
+/* ------------------------------------------------------------------------ forward / step */
+static void fwd_position(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  kinematics(m, d);
+  com_pos(m, d);
+  make_M(m, d);
+  cholesky(w->M, w->L, m->nv);
+  collision(m, d);
+  make_constraint(m, d);
+}
+
+void orc_forward(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nv = m->nv;
+  fwd_position(m, d);
+  com_vel(m, d);
+  passive(m, d);
+  rne(m, d);
+  actuation(m, d);
+  for (int j = 0; j < nv; ++j)
+    w->qfrc_smooth[j] = w->qfrc_passive[j] - w->qfrc_bias[j] + d->qfrc_applied[j] + d->qfrc_actuator[j];
+  chol_solve(w->L, w->qacc_smooth, w->qfrc_smooth, nv);
+  /* constraint impedance/aref need efc_vel from qvel: recompute after comVel (rows built above) */
+  fwd_constraint(m, d);
+  sensors(m, d);
+  d->ncon = w->ncon;
+  d->nefc = w->nefc;
+}
+
+/* mj_Euler (implicit in joint damping) and mj_implicit(implicitfast) [upstream engine_forward.c]:
+ *   (M + h*diag(B_eff)) qacc_int = qfrc_smooth + qfrc_constraint
+ * with B_eff = dof damping (Euler) or dof damping - d(actuator force)/d(qvel) (implicitfast; joint
+ * transmissions make it diagonal), then qvel += h qacc_int, integrate qpos, time += h. */
+static void integrate(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nv = m->nv;
+  double h = m->timestep;
+  double* qacc_int = w->tmp;
+  int need_solve = 0;
+  double* Dg = (double*)calloc(nv ? nv : 1, sizeof(double));
+  if (m->integrator == MRS_INT_EULER) {
+    if (!(m->disableflags & MRS_DSBL_EULERDAMP))
+      for (int j = 0; j < nv; ++j) if (m->dof_damping[j] > 0) { Dg[j] = m->dof_damping[j]; need_solve = 1; }
+  } else { /* implicitfast */
+    need_solve = 1;
+    if (!(m->disableflags & MRS_DSBL_PASSIVE))
+      for (int j = 0; j < nv; ++j) Dg[j] = m->dof_damping[j];
+    if (!(m->disableflags & MRS_DSBL_ACTUATION))
+      for (int a = 0; a < m->nu; ++a) {
+        if (m->actuator_forcelimited[a]) {
+          double f = w->actuator_force[a];
+          const double* r = m->actuator_forcerange + 2 * a;
+          if (f <= r[0] || f >= r[1]) continue;
+        }
+        double bv = m->actuator_biastype[a] == MRS_BIAS_AFFINE ? m->actuator_biasprm[MRS_NBIAS * a + 2] : 0;
+        double gv = m->actuator_gaintype[a] == MRS_GAIN_AFFINE ? m->actuator_gainprm[MRS_NGAIN * a + 2] : 0;
+        double ctrl = d->ctrl[a];
+        if (m->actuator_ctrllimited[a] && !(m->disableflags & MRS_DSBL_CLAMPCTRL)) {
+          const double* r = m->actuator_ctrlrange + 2 * a;
+          ctrl = ctrl < r[0] ? r[0] : ctrl > r[1] ? r[1] : ctrl;
+        }
+        double v = bv + gv * ctrl;
+        double gear = m->actuator_gear[6 * a];
+        Dg[m->jnt_dofadr[m->actuator_trnid[2 * a]]] -= gear * gear * v;
+      }
+  }
+  if (need_solve) {
+    memcpy(w->Mi, w->M, (size_t)nv * nv * sizeof(double));
+    for (int j = 0; j < nv; ++j) w->Mi[j * nv + j] += h * Dg[j];
+    cholesky(w->Mi, w->Li, nv);
+    for (int j = 0; j < nv; ++j) w->tmp2[j] = w->qfrc_smooth[j] + w->qfrc_constraint[j];
+    chol_solve(w->Li, qacc_int, w->tmp2, nv);
+  } else {
+    memcpy(qacc_int, d->qacc, nv * sizeof(double));
+  }
+  free(Dg);
+  /* mj_advance: warm start keeps the constraint solver's qacc */
+  memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(double));
+  for (int j = 0; j < nv; ++j) d->qvel[j] += h * qacc_int[j];
+  /* mj_integratePos */
+  for (int j = 0; j < m->njnt; ++j) {
+    int a = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    switch (m->jnt_type[j]) {
+      case MRS_JNT_FREE:
+        for (int i = 0; i < 3; ++i) d->qpos[a + i] += h * d->qvel[da + i];
+        a += 3; da += 3;
+        /* fall through */
+      case MRS_JNT_BALL: {
+        double* q = d->qpos + a;
+        double v[3] = {d->qvel[da], d->qvel[da + 1], d->qvel[da + 2]};
+        double ang = h * normalize3(v);
+        double dq[4];
+        axis_angle_quat(dq, v, ang);
+        quat_normalize(q);
+        quat_mul(q, q, dq);
+        quat_normalize(q);
+        break;
+      }
+      default: d->qpos[a] += h * d->qvel[da];
+    }
+  }
+  d->time += h;
+}
+
+/* mj_checkPos / mj_checkVel / mj_checkAcc with auto-reset [upstream engine_forward.c] */
+static int check(const mrs_model_view* m, orc_data* d, const double* x, int n, int which) {
+  for (int i = 0; i < n; ++i)
+    if (is_bad(x[i])) {
+      d->warning[which]++;
+      d->warning[3] = i;
+      if (!(m->disableflags & MRS_DSBL_AUTORESET)) {
+        int w0 = d->warning[0], w1 = d->warning[1], w2 = d->warning[2], w3 = d->warning[3];
+        orc_reset(m, d, -1);
+        d->warning[0] = w0; d->warning[1] = w1; d->warning[2] = w2; d->warning[3] = w3;
+      }
+      return 1;
+    }
+  return 0;
+}
+
+void orc_step(const mrs_model_view* m, orc_data* d) {
+  check(m, d, d->qpos, m->nq, 0);
+  check(m, d, d->qvel, m->nv, 1);
+  orc_forward(m, d);
+  if (check(m, d, d->qacc, m->nv, 2)) orc_forward(m, d);
+  integrate(m, d);
+}
+
+void orc_mass_matrix(const mrs_model_view* m, orc_data* d, double* M) {
+  orc_ws* w = (orc_ws*)d->ws;
+  kinematics(m, d);
+  com_pos(m, d);
+  make_M(m, d);
+  memcpy(M, w->M, (size_t)m->nv * m->nv * sizeof(double));
+}
+
+void orc_kinematics(const mrs_model_view* m, orc_data* d, double* xpos, double* xquat,
+                    double* geom_xpos, double* geom_xmat) {
+  orc_ws* w = (orc_ws*)d->ws;
+  kinematics(m, d);
+  com_pos(m, d);
+  if (xpos) memcpy(xpos, w->xpos, 3 * m->nbody * sizeof(double));
+  if (xquat) memcpy(xquat, w->xquat, 4 * m->nbody * sizeof(double));
+  if (geom_xpos) memcpy(geom_xpos, w->geom_xpos, 3 * m->ngeom * sizeof(double));
+  if (geom_xmat) memcpy(geom_xmat, w->geom_xmat, 9 * m->ngeom * sizeof(double));
+}
+
+int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, double* frame) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int n = w->ncon < max ? w->ncon : max;
+  for (int c = 0; c < n; ++c) {
+    if (geom) { geom[2 * c] = w->con[c].geom[0]; geom[2 * c + 1] = w->con[c].geom[1]; }
+    if (dist) dist[c] = w->con[c].dist;
+    if (pos) memcpy(pos + 3 * c, w->con[c].pos, 3 * sizeof(double));
+    if (frame) memcpy(frame + 9 * c, w->con[c].frame, 9 * sizeof(double));
+  }
+  return w->ncon;
+}
+
+/* ------------------------------------------------------------------------ depth camera
+ * Replaces mjr_render + mjr_readPixels + linearisation (src/mujoco_cameras.cpp:211-240): one ray
+ * per pixel centre through the pinhole (fovy, H; fx = fy = H/2 / tan(fovy/2) as in the plugin's
+ * intrinsics :119-123), eye-space depth = ray parameter along the camera -z axis, geoms of groups
+ * 0-2 (mjvOption default), hits nearer than znear*extent ignored, misses -> far = zfar*extent.
+ * Row 0 is the top row (the plugin's vertical flip, :229-240, already applied). */
+void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out) {
+  orc_ws* w = (orc_ws*)d->ws;
+  kinematics(m, d);
+  int W = m->cam_resolution[2 * cam], H = m->cam_resolution[2 * cam + 1];
+  int b = m->cam_bodyid[cam];
+  double cpos[3], cq[4], cmat[9], r[3];
+  rot_quat(r, m->cam_pos + 3 * cam, w->xquat + 4 * b);
+  for (int i = 0; i < 3; ++i) cpos[i] = w->xpos[3 * b + i] + r[i];
+  quat_mul(cq, w->xquat + 4 * b, m->cam_quat + 4 * cam);
+  quat2mat(cmat, cq);
+  double znear = m->vis_znear * m->stat_extent, zfar = m->vis_zfar * m->stat_extent;
+  double f = 0.5 * H / tan(m->cam_fovy[cam] * M_PI / 360.0);
+  for (int row = 0; row < H; ++row)
+    for (int col = 0; col < W; ++col) {
+      double dc[3] = {(col + 0.5 - 0.5 * W) / f, (0.5 * H - row - 0.5) / f, -1}, vec[3];
+      mat_vec(vec, cmat, dc);
+      double t = ray_scene(m, w, cpos, vec, -1, 0x7, znear, NULL);
+      out[(size_t)row * W + col] = (float)((t < 0 || t > zfar) ? zfar : t);
+    }
+}
+
+/* ------------------------------------------------------------------------ CPU baseline */
+typedef struct {
+  const mrs_model_view* m;
+  int env0, env1, n_steps, period, n_envs;
+  const double *ctrl_table, *qpos_init;
+  double *qpos_out, *qvel_out;
+} rollout_job;
+
+static void* rollout_worker(void* arg) {
+  rollout_job* j = (rollout_job*)arg;
+  const mrs_model_view* m = j->m;
+  orc_data* d = orc_make_data(m);
+  for (int e = j->env0; e < j->env1; ++e) {
+    orc_reset(m, d, -1);
+    if (j->qpos_init) memcpy(d->qpos, j->qpos_init + (size_t)e * m->nq, m->nq * sizeof(double));
+    for (int t = 0; t < j->n_steps; ++t) {
+      if (t % j->period == 0 && j->ctrl_table)
+        memcpy(d->ctrl, j->ctrl_table + ((size_t)(t / j->period) * j->n_envs + e) * m->nu, m->nu * sizeof(double));
+      orc_step(m, d);
+    }
+    if (j->qpos_out) memcpy(j->qpos_out + (size_t)e * m->nq, d->qpos, m->nq * sizeof(double));
+    if (j->qvel_out) memcpy(j->qvel_out + (size_t)e * m->nv, d->qvel, m->nv * sizeof(double));
+  }
+  orc_free_data(d);
+  return NULL;
+}
+
+double orc_rollout(const mrs_model_view* m, int n_envs, int n_steps, int period,
+                   const double* ctrl_table, const double* qpos_init, int n_threads,
+                   double* qpos_out, double* qvel_out) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > n_envs) n_threads = n_envs;
+  pthread_t th[256];
+  rollout_job jobs[256];
+  if (n_threads > 256) n_threads = 256;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int i = 0; i < n_threads; ++i) {
+    rollout_job* j = &jobs[i];
+    j->m = m; j->n_steps = n_steps; j->period = period > 0 ? period : 1; j->n_envs = n_envs;
+    j->ctrl_table = ctrl_table; j->qpos_init = qpos_init; j->qpos_out = qpos_out; j->qvel_out = qvel_out;
+    j->env0 = (int)((long)n_envs * i / n_threads);
+    j->env1 = (int)((long)n_envs * (i + 1) / n_threads);
+    pthread_create(&th[i], NULL, rollout_worker, j);
+  }
+  for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
