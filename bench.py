@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Benchmark: batched mj_step on MI355X (BASELINE.json metric "env-steps/sec (whole node),
+7-DoF arm+lidar scene").
+
+Workload (BASELINE.json configs[2]): scenes/arm7_lidar.xml — 7-DoF arm,
+360-beam rangefinder lidar, PGS — 8192 envs per GPU (weak scaling: every rank owns its own 8192
+envs, global env ids rank*8192 + i, no data-path collective).  One bench "step" = one controller
+period = 10 physics steps (mj_step) of every env with the period's synthetic action held (the
+reference's 500 Hz physics / 50 Hz controller ratio), i.e. one fused kernel launch.  Inputs (the
+whole synthetic action table) are resident in HBM before timing starts.
+
+Prints ONE JSON line on rank 0.  Launch: `python bench.py` (1 GPU) or
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "env-steps/sec (whole node), 7-DoF arm+lidar scene at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200, help="timed controller periods")
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--period", type=int, default=10, help="physics steps per controller period")
+    p.add_argument("--envs", type=int, default=8192, help="envs per GPU")
+    p.add_argument("--scene", default=str(ROOT / "scenes" / "arm7_lidar.xml"))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    return p.parse_args()
+
+
+def cpu_baseline(model, period: int, target_s: float):
+    """fp64 CPU oracle (oracle/oracle.c, 'port') on the host cores: bounded sample of the same
+    workload (same scene, same synthetic inputs), one env per pthread task."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import binding
+    from mujoco_ros2_simulation_amd import synth
+    cores = max(1, min(16, os.cpu_count() or 1))
+    # pilot: estimate env-step cost, then size the sample for ~target_s seconds
+    n_pilot = cores
+    steps = 100
+    q0 = synth.initial_qpos(model, np.arange(n_pilot))
+    tab = synth.ctrl_table(model, np.arange(n_pilot), steps // period + 1, period)
+    secs, _, _ = binding.rollout(model, q0, tab, steps, period, cores)
+    rate = n_pilot * steps / max(secs, 1e-6)
+    n_envs = max(cores, int(round(rate * target_s / 500 / cores)) * cores)
+    steps = 500
+    q0 = synth.initial_qpos(model, np.arange(n_envs))
+    tab = synth.ctrl_table(model, np.arange(n_envs), steps // period + 1, period)
+    secs, _, _ = binding.rollout(model, q0, tab, steps, period, cores)
+    return {"value": n_envs * steps / secs, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{n_envs} envs x {steps} steps of the same scene and synthetic inputs, fp64 oracle "
+                      f"(oracle/oracle.c), {cores} pthreads, {secs:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from mujoco_ros2_simulation_amd import build, roofline, sim, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    if not sim.LIB_PATH.exists():
+        if rank == 0:
+            build.build_lib()
+        if world > 1:
+            dist.barrier()
+
+    model = sim.Model.load(args.scene)
+    n = args.envs
+    env_ids = rank * n + np.arange(n)
+    P = args.warmup + args.steps
+    table = synth.ctrl_table(model, env_ids, P, args.period).astype(np.float32)   # [P, n, nu]
+    qpos0 = synth.initial_qpos(model, env_ids)
+
+    stream = torch.cuda.Stream(device=local)
+    batch = sim.Batch(model, n, device=local)
+    batch.set_stream(stream.cuda_stream)
+    batch.set(sim.FIELD_QPOS, qpos0)
+    d_table = torch.from_numpy(table).to(f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    def period(p: int, ev=None):
+        batch.set_ctrl_device(d_table[p].data_ptr())
+        if ev is not None:
+            ev[0].record(stream)
+        batch.step(args.period)
+        if ev is not None:
+            ev[1].record(stream)
+
+    with torch.cuda.stream(stream):
+        for p in range(args.warmup):
+            period(p)
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            period(args.warmup + k, events[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    # sanity: states finite after the run (a diverged run would be invalid)
+    q = batch.get(sim.FIELD_QPOS, 0, min(n, 64))
+    assert np.all(np.isfinite(q)), "non-finite state after benchmark"
+
+    env_steps = world * n * args.steps * args.period
+    value = env_steps / elapsed
+    flops = roofline.flops_per_env_step(model)
+    bytes_ = roofline.bytes_per_env_step(model, args.period)
+    achieved_tf = n * args.period * flops / (kern_ms * 1e-3) / 1e12
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Philox4x32-10 seeded actions and initial states; SURVEY.md §8d)",
+        "config": {
+            "workload": f"{Path(args.scene).stem} (C3: 7-DoF arm + {sum(1 for i in range(model.nsensor) if model.sensor_type[i] == sim.SENS_RANGEFINDER)}-ray lidar, PGS)",
+            "envs_per_gpu": n,
+            "global_envs": world * n,
+            "physics_steps_per_bench_step": args.period,
+            "timestep": model.timestep,
+            "parallelism": f"env-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "achieved": achieved_tf,
+            "peak": roofline.PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / roofline.PEAK_FP32_TFLOPS,
+            "traffic": None,
+            "kernel": "step_kernel<false> (fused 10-step launch)",
+            "kernel_ms": kern_ms,
+            "flops_per_env_step": flops,
+            "algorithmic_bytes_per_env_step": bytes_,
+            "note": "VALU-bound fp32 path; peak is the fp32 vector rate (= fp32 MFMA rate on gfx950)",
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(model, args.period, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    batch.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -166,10 +166,11 @@ class Model:
             ptr = getattr(v, name)
             size = n * w
             if size == 0 or not ptr:
-                arr = np.zeros((n, w) if w > 1 else (n,), dtype=np.int32 if kind == "i" else np.float64)
+                arr = np.zeros((n, w) if (w > 1 or isinstance(width, str)) else (n,),
+                               dtype=np.int32 if kind == "i" else np.float64)
             else:
                 arr = np.ctypeslib.as_array(ptr, shape=(size,)).copy()
-                if w > 1:
+                if w > 1 or isinstance(width, str):
                     arr = arr.reshape(n, w)
             setattr(self, name, arr)
 

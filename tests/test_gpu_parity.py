@@ -1,0 +1,185 @@
+"""GPU parity: the HIP path (libmrs.so through the C ABI) against the fp64 CPU oracle on the same
+seeded inputs.  Tolerances (fp32 device arithmetic vs fp64 oracle; SURVEY.md §8d, BASELINE.json
+north_star "qpos/qvel within 1e-5 rel"):
+
+  qpos, qvel        |gpu - cpu| <= RTOL * max(|cpu|, SCALE)      RTOL = 1e-5 (1000-step rollouts)
+  rangefinder       |gpu - cpu| <= 2e-5 * max(1, range) and identical hit/miss (-1) pattern
+  depth image       |gpu - cpu| <= 1e-5 * depth on >= 99.9% of pixels (silhouette edges may flip)
+  contact counts    identical (integer work is bit-exact)
+"""
+import numpy as np
+import pytest
+
+from conftest import ARM7, REF_SCENE
+from mujoco_ros2_simulation_amd import sim, synth
+import binding
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _oracle_rollout(model, qpos0, table, period, checkpoints):
+    """Per-env oracle rollout returning qpos/qvel/sensordata at each checkpoint (steps)."""
+    n = qpos0.shape[0]
+    out = {c: (np.zeros((n, model.nq)), np.zeros((n, model.nv)), np.zeros((n, model.nsensordata))) for c in checkpoints}
+    for e in range(n):
+        d = binding.OracleData(model)
+        d.qpos[:] = qpos0[e]
+        t = 0
+        for c in checkpoints:
+            while t < c:
+                if t % period == 0:
+                    d.ctrl[:] = table[t // period, e]
+                d.step()
+                t += 1
+            out[c][0][e] = d.qpos
+            out[c][1][e] = d.qvel
+            out[c][2][e] = d.sensordata
+    return out
+
+
+def _gpu_rollout(model, qpos0, table, period, checkpoints):
+    n = qpos0.shape[0]
+    b = sim.Batch(model, n)
+    b.set(sim.FIELD_QPOS, qpos0)
+    out = {}
+    t = 0
+    for c in checkpoints:
+        while t < c:
+            b.set(sim.FIELD_CTRL, table[t // period])
+            k = min(period - t % period, c - t)
+            b.step(k)
+            t += k
+        out[c] = (b.get(sim.FIELD_QPOS), b.get(sim.FIELD_QVEL), b.get(sim.FIELD_SENSORDATA))
+    b.close()
+    return out
+
+
+def _scale(x):
+    return np.maximum(np.abs(x), 1.0)
+
+
+@pytest.mark.parametrize("scene, n_envs, steps", [(REF_SCENE, 64, 1000), (ARM7, 16, 1000)])
+def test_rollout_parity(scene, n_envs, steps):
+    model = sim.Model.load(scene)
+    envs = np.arange(n_envs)
+    period = 10
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    checkpoints = [1, 10, 100, steps]
+    ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
+    got = _gpu_rollout(model, qpos0, table, period, checkpoints)
+    for c in checkpoints:
+        q_ref, v_ref, s_ref = ref[c]
+        q, v, s = got[c]
+        eq = np.max(np.abs(q - q_ref) / _scale(q_ref))
+        ev = np.max(np.abs(v - v_ref) / _scale(v_ref))
+        print(f"{scene.name} step {c}: max rel err qpos {eq:.2e} qvel {ev:.2e}")
+        assert eq <= RTOL, f"qpos rel err {eq} at step {c}"
+        assert ev <= RTOL, f"qvel rel err {ev} at step {c}"
+        rf = [i for i in range(model.nsensor) if model.sensor_type[i] == sim.SENS_RANGEFINDER]
+        adr = model.sensor_adr[rf]
+        np.testing.assert_array_equal(s[:, adr] < 0, s_ref[:, adr] < 0)
+        hit = s_ref[:, adr] >= 0
+        np.testing.assert_allclose(s[:, adr][hit], s_ref[:, adr][hit], rtol=2e-5, atol=2e-5)
+
+
+def test_forward_lidar_closed_form():
+    """GPU rangefinders of the reference scene at qpos=0 equal 1.95/cos(0.3 - 0.025 i)."""
+    model = sim.Model.load(REF_SCENE)
+    b = sim.Batch(model, 8)
+    b.forward()
+    s = b.get(sim.FIELD_SENSORDATA)
+    i = np.arange(24)
+    np.testing.assert_allclose(s, np.tile(1.95 / np.cos(0.3 - 0.025 * i), (8, 1)), atol=2e-5)
+
+
+def test_reference_position_pin_gpu():
+    """robot_launch_test.py:112-132 on the GPU path: [0.5, -0.5] reached within 0.05 rad in 2 s."""
+    model = sim.Model.load(REF_SCENE)
+    b = sim.Batch(model, 4)
+    b.set(sim.FIELD_CTRL, np.tile([0.5, -0.5], (4, 1)))
+    for _ in range(100):  # 50 Hz controller writes, 10 physics steps each = 2 s
+        b.step(10)
+    q = b.get(sim.FIELD_QPOS)
+    assert np.all(np.abs(q[:, 0] - 0.5) < 0.05) and np.all(np.abs(q[:, 1] + 0.5) < 0.05)
+    np.testing.assert_allclose(b.get(sim.FIELD_TIME)[:, 0], 2.0, rtol=1e-12)
+
+
+def test_full_size_batch_properties():
+    """4096 envs (config C2 size): identical envs give identical results wherever they sit in the
+    batch, results are deterministic across launches, and env 0 matches the oracle."""
+    model = sim.Model.load(REF_SCENE)
+    n = 4096
+    qpos0 = np.tile(synth.initial_qpos(model, np.arange(4)), (n // 4, 1))
+    ctrl = np.tile(synth.ctrl_table(model, np.arange(4), 1, 10)[0], (n // 4, 1))
+    outs = []
+    for _ in range(2):
+        b = sim.Batch(model, n)
+        b.set(sim.FIELD_QPOS, qpos0)
+        b.set(sim.FIELD_CTRL, ctrl)
+        b.step(200)
+        outs.append(b.get(sim.FIELD_QPOS))
+        b.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    q = outs[0].reshape(n // 4, 4, -1)
+    assert np.all(q == q[:1])
+    d = binding.OracleData(model)
+    d.qpos[:] = qpos0[0]
+    d.ctrl[:] = ctrl[0]
+    d.step(200)
+    np.testing.assert_allclose(outs[0][0], d.qpos, rtol=RTOL, atol=RTOL)
+
+
+def test_depth_parity_reference_camera():
+    model = sim.Model.load(REF_SCENE)
+    b = sim.Batch(model, 2)
+    q = np.array([[0.3, -0.7], [1.2, 0.4]])
+    b.set(sim.FIELD_QPOS, q)
+    b.forward()
+    imgs = b.render_depth(0, 0, 2)
+    for e in range(2):
+        d = binding.OracleData(model)
+        d.qpos[:] = q[e]
+        d.forward()
+        ref = d.render_depth(0)
+        close = np.abs(imgs[e] - ref) <= 1e-5 * np.maximum(ref, 1)
+        assert close.mean() >= 0.999, f"env {e}: {close.mean()}"
+
+
+CONTACT_SCENE = """<mujoco><compiler angle="radian"/><option timestep="0.002" solver="PGS" iterations="50"/>
+<worldbody><geom name="floor" type="plane" size="0 0 1"/>
+<geom name="ledge" type="box" pos="1 0 0.2" size="0.3 0.3 0.2"/>
+<body pos="0 0 0.4"><freejoint/><geom type="sphere" size="0.1"/></body>
+<body pos="1 0 0.8" euler="0.3 0.2 0"><freejoint/><geom type="capsule" size="0.05 0.2"/></body>
+<body pos="-1 0 0.5" euler="0.1 0.2 0.3"><freejoint/><geom type="box" size="0.1 0.15 0.05"/></body>
+</worldbody></mujoco>"""
+
+
+def test_contact_parity_short_horizon():
+    """Contact generation and PGS with free bodies: contact counts bit-exact, state within tolerance
+    over a short horizon (contact dynamics diverge chaotically in fp32 vs fp64 over long ones)."""
+    model = sim.Model.from_string(CONTACT_SCENE)
+    b = sim.Batch(model, 4)
+    d = binding.OracleData(model)
+    for chunk in range(12):
+        b.step(25)
+        d.step(25)
+        q = b.get(sim.FIELD_QPOS)[0]
+        ncon = int(b.get(sim.FIELD_NCON)[0, 0])
+        assert ncon == d.ncon, f"chunk {chunk}: ncon {ncon} vs {d.ncon}"
+        np.testing.assert_allclose(q, d.qpos, atol=2e-3)
+    assert d.ncon >= 3  # sphere on floor, capsule on ledge, box on floor (up to 4 corners)
+
+
+def test_autoreset_on_nan():
+    model = sim.Model.load(REF_SCENE)
+    b = sim.Batch(model, 3)
+    q = np.zeros((3, 2))
+    q[1, 0] = np.nan
+    b.set(sim.FIELD_QPOS, q)
+    b.step(1)
+    w = b.get(sim.FIELD_WARNING)
+    assert w[1, 0] == 1 and w[0, 0] == 0 and w[2, 0] == 0
+    assert np.all(np.isfinite(b.get(sim.FIELD_QPOS)))

@@ -1,0 +1,144 @@
+"""Pins the fp64 CPU oracle (oracle/oracle.c) before it is trusted as the parity checker:
+closed-form known answers and the reference's behavioural pin
+(test/src/robot_launch_test.py:112-132).  MuJoCo itself is not available anywhere in this pipeline
+(SURVEY.md §8c), so beyond these pins the oracle is 'parity unpinned' against upstream mj_step."""
+import numpy as np
+import pytest
+
+from mujoco_ros2_simulation_amd import sim
+import binding
+
+
+def test_lidar_ranges_closed_form(s2_model):
+    d = binding.OracleData(s2_model)
+    d.forward()
+    i = np.arange(24)
+    expect = 1.95 / np.cos(0.3 - 0.025 * i)  # every ray hits the upper arm's y=+0.05 face
+    # the MJCF quaternions are rounded to ~1e-6, which shifts ranges by < 1e-5
+    np.testing.assert_allclose(d.sensordata, expect, atol=1e-5)
+    # values printed in SURVEY.md Appendix B
+    np.testing.assert_allclose(d.sensordata[[0, 11, 12, 23]], [2.041168, 1.950610, 1.950000, 2.026129], atol=2e-6)
+
+
+@pytest.mark.parametrize("q2", [0.0, 0.4, -1.3, 2.5])
+def test_mass_matrix_closed_form(s2_model, q2):
+    d = binding.OracleData(s2_model)
+    d.qpos[:] = [0.7, q2]
+    M = d.mass_matrix()
+    c = np.cos(q2)
+    expect = np.array([[0.45 + 27 * (1.25 + c) + 6.75, 0.225 + 27 * (0.25 + 0.5 * c)],
+                       [0.225 + 27 * (0.25 + 0.5 * c), 6.975]])
+    np.testing.assert_allclose(M, expect, rtol=1e-12)
+
+
+SERVO = """<mujoco><compiler angle="radian"/><option timestep="0.002" integrator="{integ}" gravity="0 0 -9.81"/>
+<worldbody><body><joint name="j" axis="0 0 1" damping="{b}"/>
+<inertial pos="0 0 0" mass="1" diaginertia="0.1 0.1 {I}"/></body></worldbody>
+<actuator><position joint="j" kp="{kp}" kv="{kv}"/></actuator></mujoco>"""
+
+
+@pytest.mark.parametrize("integ", ["Euler", "implicitfast"])
+def test_servo_recurrence(integ):
+    I, b, kp, kv, h, c = 0.5, 0.3, 40.0, 2.0, 0.002, 0.8
+    m = sim.Model.from_string(SERVO.format(integ=integ, b=b, I=I, kp=kp, kv=kv))
+    d = binding.OracleData(m)
+    d.ctrl[:] = [c]
+    q, v = 0.0, 0.0
+    for _ in range(300):
+        f = kp * (c - q) - (b + kv) * v
+        a = f / (I + h * (b if integ == "Euler" else b + kv))
+        v = v + h * a
+        q = q + h * v
+        d.step()
+        assert d.qpos[0] == pytest.approx(q, rel=1e-12, abs=1e-14)
+        assert d.qvel[0] == pytest.approx(v, rel=1e-12, abs=1e-14)
+    assert d.time == pytest.approx(300 * h)
+
+
+def test_ballistic_free_body():
+    xml = """<mujoco><option timestep="0.01"/><worldbody><body pos="0 0 5"><freejoint/>
+    <geom type="sphere" size="0.1" contype="0" conaffinity="0"/></body></worldbody></mujoco>"""
+    m = sim.Model.from_string(xml)
+    d = binding.OracleData(m)
+    d.qvel[:] = [1.0, -0.5, 2.0, 0, 0, 3.0]  # translation + spin about z
+    h, g, n = 0.01, 9.81, 100
+    d.step(n)
+    # semi-implicit Euler: v_n = v0 - n h g, z_n = z0 + h sum_k v_k
+    z = 5 + h * sum(2.0 - k * h * g for k in range(1, n + 1))
+    assert d.qpos[2] == pytest.approx(z, rel=1e-12)
+    assert d.qpos[0] == pytest.approx(1.0 * n * h) and d.qpos[1] == pytest.approx(-0.5 * n * h)
+    # spin about the body z axis: quaternion (cos(wt/2), 0, 0, sin(wt/2))
+    ang = 3.0 * n * h
+    np.testing.assert_allclose(d.qpos[3:], [np.cos(ang / 2), 0, 0, np.sin(ang / 2)], atol=1e-12)
+
+
+def test_reference_position_pin(s2_model):
+    """robot_launch_test.py:112-132: command [0.5, -0.5]; after 2 s |q - cmd| < 0.05."""
+    d = binding.OracleData(s2_model)
+    d.ctrl[:] = [0.5, -0.5]
+    d.step(1000)  # 2 s at the default 0.002 s timestep
+    assert abs(d.qpos[0] - 0.5) < 0.05 and abs(d.qpos[1] + 0.5) < 0.05
+    assert d.nefc >= 1  # joint1 friction loss row is always present
+
+
+PLANE_CAM = """<mujoco><compiler angle="radian"/><statistic extent="1"/><visual><map znear="0.01" zfar="50"/></visual><worldbody>
+<geom type="plane" size="0 0 1" {tilt}/>
+<camera name="c" pos="0 0 {z0}" fovy="60" resolution="64 48"/></worldbody></mujoco>"""
+
+
+def test_depth_plane_constant():
+    z0 = 1.7
+    m = sim.Model.from_string(PLANE_CAM.format(z0=z0, tilt=""))
+    d = binding.OracleData(m)
+    d.forward()
+    img = d.render_depth(0)
+    np.testing.assert_allclose(img, z0, rtol=1e-6)  # eye-space z, not Euclidean range
+
+
+def test_depth_tilted_plane_rows():
+    z0, alpha = 2.0, 0.2
+    m = sim.Model.from_string(PLANE_CAM.format(z0=z0, tilt=f'euler="{alpha} 0 0"'))
+    d = binding.OracleData(m)
+    d.forward()
+    img = d.render_depth(0)
+    H, W = img.shape
+    f = 0.5 * H / np.tan(np.radians(30))
+    rows = np.arange(H)
+    y = (0.5 * H - rows - 0.5) / f  # camera-frame y of each row at z = -1
+    # plane through the origin with normal (0, -sin a, cos a); ray (x, y, -1) t from (0, 0, z0)
+    t = z0 * np.cos(alpha) / (np.cos(alpha) + y * np.sin(alpha))
+    np.testing.assert_allclose(img[:, W // 2], t, rtol=1e-6)
+    assert np.allclose(img, img[:, :1])  # depth constant along rows
+
+
+@pytest.mark.parametrize("geom, hit", [
+    ('type="sphere" size="0.5"', 2.5), ('type="box" size="0.3 0.4 0.5"', 2.7),
+    ('type="capsule" size="0.2 0.5" euler="0 1.5707963267948966 0"', 2.3),
+    ('type="cylinder" size="0.25 0.5" euler="0 1.5707963267948966 0"', 2.5),
+    ('type="capsule" size="0.2 0.5"', 2.8), ('type="cylinder" size="0.25 0.5"', 2.75),
+    ('type="ellipsoid" size="0.1 0.6 0.3"', 2.9),
+])
+def test_ray_primitives(geom, hit):
+    xml = f'<mujoco><compiler angle="radian"/><worldbody><geom {geom}/></worldbody></mujoco>'
+    m = sim.Model.from_string(xml)
+    d = binding.OracleData(m)
+    d.forward()
+    dist, gid = d.ray([-3.0, 0, 0], [1.0, 0, 0])
+    assert gid == 0 and dist == pytest.approx(hit, abs=1e-6)
+    dist, gid = d.ray([-3.0, 5, 0], [1.0, 0, 0])
+    assert gid == -1 and dist == -1
+
+
+def test_contact_sphere_on_plane():
+    xml = """<mujoco><option timestep="0.002"/><worldbody><geom type="plane" size="0 0 1"/>
+    <body pos="0 0 0.5"><freejoint/><geom type="sphere" size="0.1"/></body></worldbody></mujoco>"""
+    m = sim.Model.from_string(xml)
+    d = binding.OracleData(m)
+    d.step(1500)
+    # the sphere comes to rest on the plane with a small soft-contact penetration
+    assert d.qpos[2] == pytest.approx(0.1, abs=3e-3)
+    assert abs(d.qvel[2]) < 1e-2
+    assert d.ncon == 1
+    g, dist, pos, frame = d.contacts()
+    assert list(g[0]) == [0, 1]
+    np.testing.assert_allclose(frame[0, :3], [0, 0, 1], atol=1e-12)
