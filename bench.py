@@ -135,7 +135,8 @@ def main():
 
     env_steps = world * n * args.steps * args.period
     value = env_steps / elapsed
-    flops = roofline.flops_per_env_step(model)
+    detailed_flops = roofline.flops_per_env_step(model)
+    flops, survey_bytes = roofline.SURVEY_PER_ENV_STEP.get(Path(args.scene).stem, (detailed_flops, None))
     bytes_ = roofline.bytes_per_env_step(model, args.period)
     achieved_tf = n * args.period * flops / (kern_ms * 1e-3) / 1e12
     result = {
@@ -169,6 +170,8 @@ def main():
             "kernel": "step_kernel<false> (fused 10-step launch)",
             "kernel_ms": kern_ms,
             "flops_per_env_step": flops,
+            "flops_source": "SURVEY.md §8(d) per-unit figure x envs x steps per launch",
+            "flops_per_env_step_structural": detailed_flops,
             "algorithmic_bytes_per_env_step": bytes_,
             "note": "VALU-bound fp32 path; peak is the fp32 vector rate (= fp32 MFMA rate on gfx950)",
         },

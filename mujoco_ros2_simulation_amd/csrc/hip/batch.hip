@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -16,8 +17,8 @@
 
 namespace mrs {
 
-hipError_t launch_step(const DevModel& m, const LdsLayout& L, const ScratchLayout& S, const DevState& st,
-                       int n_envs, int n_steps, bool forward_only, hipStream_t stream);
+hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
+                       bool forward_only, hipStream_t stream);
 
 namespace {
 
@@ -51,7 +52,7 @@ __device__ float ray_prim(int type, const float* s, const float lp[3], const flo
   float x[2];
   switch (type) {
     case MRS_GEOM_PLANE: {
-      if (lv[2] > -1e-15f) return -1;
+      if (lv[2] >= 0 || lv[2] * lv[2] <= 1e-12f * d3(lv, lv)) return -1;
       float t = -lp[2] / lv[2];
       if (t < 0) return -1;
       float p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
@@ -169,19 +170,19 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
 struct Packer {
   std::vector<float> f;
   std::vector<int> i;
-  std::vector<std::pair<const float**, size_t>> fptr;
-  std::vector<std::pair<const int**, size_t>> iptr;
-  void addf(const float** dst, const std::vector<double>& v) {
+  std::vector<std::pair<CPtr<float>*, size_t>> fptr;
+  std::vector<std::pair<CPtr<int>*, size_t>> iptr;
+  void addf(CPtr<float>* dst, const std::vector<double>& v) {
     fptr.emplace_back(dst, f.size());
     for (double x : v) f.push_back(static_cast<float>(x));
     while (f.size() % 4) f.push_back(0);
   }
-  void addf(const float** dst, const std::vector<float>& v) {
+  void addf(CPtr<float>* dst, const std::vector<float>& v) {
     fptr.emplace_back(dst, f.size());
     f.insert(f.end(), v.begin(), v.end());
     while (f.size() % 4) f.push_back(0);
   }
-  void addi(const int** dst, const std::vector<int>& v) {
+  void addi(CPtr<int>* dst, const std::vector<int>& v) {
     iptr.emplace_back(dst, i.size());
     i.insert(i.end(), v.begin(), v.end());
     while (i.size() % 4) i.push_back(0);
@@ -195,8 +196,9 @@ struct BatchImpl {
   const Model* model = nullptr;
   int n = 0, device = 0;
   DevModel dm{};
-  LdsLayout L{};
-  ScratchLayout S{};
+  DevModel* d_dm = nullptr;  // device copy of dm
+  LdsLayout& L = dm.L;
+  ScratchLayout& S = dm.S;
   DevState st{};
   void* dblock_f = nullptr;
   void* dblock_i = nullptr;
@@ -230,6 +232,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nsite = m.nsite; d.ncam = m.ncam; d.nsensor = m.nsensor; d.nsensordata = m.nsensordata;
   d.max_depth = m.max_depth;
   d.integrator = m.integrator; d.iterations = m.iterations; d.disableflags = m.disableflags;
+  // diagnostic phase ablation for profiling only (bit 0 sensors, 1 collision, 2 constraints)
+  d.diag_skip = std::getenv("MRS_DIAG_SKIP") ? std::atoi(std::getenv("MRS_DIAG_SKIP")) : 0;
   d.timestep = static_cast<float>(m.timestep);
   d.timestep_d = m.timestep;
   d.tolerance = static_cast<float>(m.tolerance);
@@ -370,12 +374,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   b.dblock_i = dalloc(b, P.i.size() * sizeof(int));
   HIP_CHECK(hipMemcpyAsync(b.dblock_f, P.f.data(), P.f.size() * sizeof(float), hipMemcpyHostToDevice, b.stream));
   HIP_CHECK(hipMemcpyAsync(b.dblock_i, P.i.data(), P.i.size() * sizeof(int), hipMemcpyHostToDevice, b.stream));
-  for (auto& kv : P.fptr) *kv.first = static_cast<const float*>(b.dblock_f) + kv.second;
-  for (auto& kv : P.iptr) *kv.first = static_cast<const int*>(b.dblock_i) + kv.second;
+  for (auto& kv : P.fptr) kv.first->p = static_cast<const float*>(b.dblock_f) + kv.second;
+  for (auto& kv : P.iptr) kv.first->p = static_cast<const int*>(b.dblock_i) + kv.second;
   HIP_CHECK(hipStreamSynchronize(b.stream));
 
   // --- LDS layout (floats)
-  LdsLayout& L = b.L;
+  LdsLayout& L = b.dm.L;
   int off = 0;
   auto take = [&](int n) { int o = off; off += n; off = (off + 3) & ~3; return o; };
   const int nb = m.nbody, nj = std::max(1, m.njnt), nv = std::max(1, m.nv), ng = std::max(1, m.ngeom);
@@ -391,13 +395,17 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   if (static_cast<size_t>(L.total) * sizeof(float) * kEnvsPerBlock > 160 * 1024)
     throw UnsupportedError("model too large for the per-wave LDS working set");
   // --- scratch layout (floats)
-  ScratchLayout& S = b.S;
+  ScratchLayout& S = b.dm.S;
   off = 0;
   const int ne = std::max(1, d.max_efc);
   S.efc_J = take(ne * nv); S.efc_MJ = take(ne * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(ne); S.efc_aref = take(ne);
   S.efc_b = take(ne); S.efc_f = take(ne); S.efc_ARii = take(ne); S.con = take(kConRec * std::max(1, d.max_con));
+  S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);
   S.total = off;
+  b.d_dm = static_cast<DevModel*>(dalloc(b, sizeof(DevModel)));
+  HIP_CHECK(hipMemcpyAsync(b.d_dm, &b.dm, sizeof(DevModel), hipMemcpyHostToDevice, b.stream));
+  HIP_CHECK(hipStreamSynchronize(b.stream));
 }
 
 int field_dim(const Model& m, int field) {
@@ -592,7 +600,7 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
-  HIP_CHECK(launch_step(b->dm, b->L, b->S, b->st, b->n, n_steps, forward_only, b->stream));
+  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->st, b->n, n_steps, forward_only, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
 }
@@ -616,8 +624,8 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
   const DevModel& d = b->dm;
   dim3 grid((W * H + 255) / 256, n);
   HIP_CHECK(hipEventRecord(b->ev0[1], b->stream));
-  hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type, d.geom_group, d.geom_size, d.geom_rbound,
-                     d.geom_rgba, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
+  hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
+                     d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
                      cam, env0, W, H, f, znear, zfar, dout);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(b->ev1[1], b->stream));

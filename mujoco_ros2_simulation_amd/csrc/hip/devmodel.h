@@ -15,46 +15,22 @@
 
 namespace mrs {
 
-struct DevModel {
-  // sizes
-  int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth;
-  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc;
-  // options
-  int integrator, iterations, disableflags;
-  float timestep, tolerance, pgs_scale, gravity[3];
-  double timestep_d;  // time is accumulated in fp64 like mjData.time
-  // bodies
-  const int *body_parentid, *body_rootid, *body_jntnum, *body_jntadr, *body_dofnum, *body_dofadr,
-      *body_subtree_end, *level_adr, *level_num, *level_body;
-  const float *body_pos, *body_quat, *body_ipos, *body_iquat, *body_mass, *body_subtreemass,
-      *body_inertia, *body_gravcomp, *body_invweight0;
-  // joints / dofs
-  const int *jnt_type, *jnt_qposadr, *jnt_dofadr, *jnt_bodyid, *jnt_actfrclimited;
-  const float *jnt_pos, *jnt_axis, *jnt_stiffness, *jnt_range, *jnt_margin, *jnt_solref,
-      *jnt_solimp, *jnt_actfrcrange;
-  const int *dof_bodyid, *dof_jntid;
-  const float *dof_armature, *dof_damping, *dof_frictionloss, *dof_solref, *dof_solimp,
-      *dof_invweight0, *qpos0, *qpos_spring;
-  const int* Mpair;  // [nMpair][2] (i, j) with j = i or an ancestor dof of i
-  // geoms
-  const int *geom_type, *geom_bodyid, *geom_group;
-  const float *geom_size, *geom_pos, *geom_quat, *geom_rbound, *geom_rgba;
-  // candidate collision pairs (static filters applied; g1 has the smaller geom type)
-  const int *pair_g1, *pair_g2, *pair_dim;
-  const float *pair_margin, *pair_gap, *pair_friction /*3*/, *pair_solref /*2*/, *pair_solimp /*5*/;
-  // sites
-  const int* site_bodyid;
-  const float *site_pos, *site_quat;
-  // cameras
-  const int* cam_bodyid;
-  const float *cam_pos, *cam_quat;
-  // actuators (joint transmission)
-  const int *act_dof, *act_qadr, *act_gaintype, *act_biastype, *act_ctrllimited, *act_forcelimited;
-  const float *act_gear, *act_gainprm /*3*/, *act_biasprm /*3*/, *act_ctrlrange, *act_forcerange;
-  // sensors
-  const int *sensor_type, *sensor_objtype, *sensor_objid, *sensor_adr, *sensor_dim;
-  const float* sensor_cutoff;
-  const int *fric_dof, *lim_jnt, *rf_sensor;
+// Read-only model array.  On the device, element reads go through the AMDGPU constant address space
+// (4): wave-uniform indices become scalar loads (s_load through the scalar cache), per-lane indices
+// become global loads with an SGPR base.  Plain generic pointers loaded from a struct would compile to
+// flat loads with 64-bit per-lane addresses.  Host code sees an ordinary pointer.
+template <class T>
+struct CPtr {
+  const T* p;
+  CPtr& operator=(const T* q) { p = q; return *this; }
+  __device__ __forceinline__ T operator[](int i) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(4))) T*)p)[i];
+#else
+    return p[i];
+#endif
+  }
+  __device__ __forceinline__ CPtr operator+(int i) const { return CPtr{p + i}; }
 };
 
 // LDS layout of one environment (offsets in floats).  One wavefront owns one environment; the
@@ -70,10 +46,53 @@ struct LdsLayout {
 // region; the region of env e starts at e * total).
 struct ScratchLayout {
   int efc_J, efc_MJ, efc_type, efc_pos, efc_margin, efc_floss, efc_R, efc_aref, efc_b, efc_f,
-      efc_ARii, con;  // contact records: kConRec floats each
+      efc_ARii, con, stage;  // contact records (kConRec floats each); per-lane narrow-phase staging
   int total;
 };
 constexpr int kConRec = 16;  // pair id (int bits), dist, pos[3], frame[9], pad[2]
+
+// Everything the step kernel reads about the model.  Lives in device memory; the kernel receives
+// one pointer to it.
+struct DevModel {
+  LdsLayout L;
+  ScratchLayout S;
+  // sizes
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth;
+  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc;
+  // options
+  int integrator, iterations, disableflags;
+  int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
+  float timestep, tolerance, pgs_scale, gravity[3];
+  double timestep_d;  // time is accumulated in fp64 like mjData.time
+  // bodies
+  CPtr<int> body_parentid, body_rootid, body_jntnum, body_jntadr, body_dofnum, body_dofadr, body_subtree_end, level_adr, level_num, level_body;
+  CPtr<float> body_pos, body_quat, body_ipos, body_iquat, body_mass, body_subtreemass, body_inertia, body_gravcomp, body_invweight0;
+  // joints / dofs
+  CPtr<int> jnt_type, jnt_qposadr, jnt_dofadr, jnt_bodyid, jnt_actfrclimited;
+  CPtr<float> jnt_pos, jnt_axis, jnt_stiffness, jnt_range, jnt_margin, jnt_solref, jnt_solimp, jnt_actfrcrange;
+  CPtr<int> dof_bodyid, dof_jntid;
+  CPtr<float> dof_armature, dof_damping, dof_frictionloss, dof_solref, dof_solimp, dof_invweight0, qpos0, qpos_spring;
+  CPtr<int> Mpair;  // [nMpair][2] (i, j) with j = i or an ancestor dof of i
+  // geoms
+  CPtr<int> geom_type, geom_bodyid, geom_group;
+  CPtr<float> geom_size, geom_pos, geom_quat, geom_rbound, geom_rgba;
+  // candidate collision pairs (static filters applied; g1 has the smaller geom type)
+  CPtr<int> pair_g1, pair_g2, pair_dim;
+  CPtr<float> pair_margin, pair_gap, pair_friction /*3*/, pair_solref /*2*/, pair_solimp /*5*/;
+  // sites
+  CPtr<int> site_bodyid;
+  CPtr<float> site_pos, site_quat;
+  // cameras
+  CPtr<int> cam_bodyid;
+  CPtr<float> cam_pos, cam_quat;
+  // actuators (joint transmission)
+  CPtr<int> act_dof, act_qadr, act_gaintype, act_biastype, act_ctrllimited, act_forcelimited;
+  CPtr<float> act_gear, act_gainprm /*3*/, act_biasprm /*3*/, act_ctrlrange, act_forcerange;
+  // sensors
+  CPtr<int> sensor_type, sensor_objtype, sensor_objid, sensor_adr, sensor_dim;
+  CPtr<float> sensor_cutoff;
+  CPtr<int> fric_dof, lim_jnt, rf_sensor;
+};
 
 constexpr int kEnvsPerBlock = 4;  // 256-thread workgroups, one wave per environment
 

@@ -19,6 +19,10 @@ namespace {
 constexpr float kMinVal = 1e-15f;
 constexpr float kMaxVal = 1e10f;
 
+// LDS-qualified float: per-env working set pointers keep the LDS address space across the
+// out-of-line phase functions, so every access is a ds_read/ds_write (not a flat access).
+typedef __attribute__((address_space(3))) float lfloat;
+
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -69,7 +73,8 @@ __device__ __forceinline__ void mat_vec(float r[3], const float m[9], const floa
   float c = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
   r[0] = a; r[1] = b; r[2] = c;
 }
-__device__ __forceinline__ void matT_vec(float r[3], const float m[9], const float v[3]) {
+template <class PM>
+__device__ __forceinline__ void matT_vec(float r[3], const PM* m, const float v[3]) {
   float a = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
   float b = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
   float c = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
@@ -99,7 +104,8 @@ __device__ __forceinline__ void axis_angle_quat(float q[4], const float ax[3], f
   sincosf(0.5f * ang, &s, &c);
   q[0] = c; q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
 }
-__device__ __forceinline__ void mul_inert_vec(float r[6], const float* i, const float v[6]) {
+template <class PI>
+__device__ __forceinline__ void mul_inert_vec(float r[6], const PI* i, const float v[6]) {
   r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
   r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
   r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
@@ -107,7 +113,8 @@ __device__ __forceinline__ void mul_inert_vec(float r[6], const float* i, const 
   r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
   r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
 }
-__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* u) {
+template <class PR, class PV, class PU>
+__device__ __forceinline__ void cross_motion(PR* r, const PV* v, const PU* u) {
   float t0 = -v[2] * u[1] + v[1] * u[2];
   float t1 = v[2] * u[0] - v[0] * u[2];
   float t2 = -v[1] * u[0] + v[0] * u[1];
@@ -116,7 +123,8 @@ __device__ __forceinline__ void cross_motion(float* r, const float* v, const flo
   float t5 = -v[1] * u[3] + v[0] * u[4] - v[4] * u[0] + v[3] * u[1];
   r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3; r[4] = t4; r[5] = t5;
 }
-__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+template <class PR, class PV, class PF>
+__device__ __forceinline__ void cross_force(PR* r, const PV* v, const PF* f) {
   float t0 = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
   float t1 = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
   float t2 = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
@@ -140,11 +148,13 @@ __device__ __forceinline__ float ray_quad(float a, float b, float c, float x[2])
   if (x[1] >= 0) return x[1];
   return -1;
 }
-__device__ float ray_geom_local(int type, const float* s, const float lp[3], const float lv[3]) {
+template <class PS>
+__device__ float ray_geom_local(int type, const PS s, const float lp[3], const float lv[3]) {
   float x[2];
   switch (type) {
     case MRS_GEOM_PLANE: {
-      if (lv[2] > -kMinVal) return -1;
+      // parallel (within 1e-6 rad) or facing away: miss (fp32-safe form of MuJoCo's lv[2] > -mjMINVAL)
+      if (lv[2] >= 0 || lv[2] * lv[2] <= 1e-12f * dot3(lv, lv)) return -1;
       float t = -lp[2] / lv[2];
       if (t < 0) return -1;
       float p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];
@@ -396,7 +406,8 @@ __device__ __forceinline__ void make_frame(float f[9]) {
   cross3(f + 6, f, f + 3);
 }
 
-__device__ __forceinline__ float impedance(const float* si, float pos, float margin) {
+template <class PS>
+__device__ __forceinline__ float impedance(const PS si, float pos, float margin) {
   float dmin = clampf(si[0], 0.0001f, 0.9999f), dmax = clampf(si[1], 0.0001f, 0.9999f);
   float width = si[2], mid = si[3], power = si[4];
   if (dmin == dmax || width <= kMinVal) return 0.5f * (dmin + dmax);
@@ -413,19 +424,50 @@ __device__ __forceinline__ float impedance(const float* si, float pos, float mar
 enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 
 // ------------------------------------------------------------------ environment context
-struct Env {
-  const DevModel& m;
-  const LdsLayout& L;
-  float* s;      // LDS base of this env
-  float* scr;    // global scratch of this env
-  const ScratchLayout& S;
-  int lane;
-  __device__ float* at(int off) const { return s + off; }
-};
+// Phases are separate non-inlined functions (own register allocation, nothing live across them
+// but these four values).  The model (with its LDS/scratch layouts) stays in device memory behind
+// one pointer: wave-uniform model reads become scalar loads instead of SGPR-resident kernel args.
+#define ENV_PARAMS const DevModel* __restrict__ mp, lfloat* __restrict__ s, float* __restrict__ scr, int lane
+#define ENV_ARGS mp, s, scr, lane
+// Function arguments arrive in VGPRs, so the compiler cannot know they are wave-uniform; the phase
+// prologue re-establishes uniformity with readfirstlane (every phase is entered by the whole wave).
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v));
+  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v >> 32));
+  return reinterpret_cast<T*>((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+__device__ __forceinline__ lfloat* uniform_lds(lfloat* p) {
+  return (lfloat*)(unsigned long)__builtin_amdgcn_readfirstlane((unsigned)(unsigned long)p);
+}
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// by-value copy of the model descriptor read through the constant address space: only the fields a
+// phase uses are loaded (scalar loads), and they stay in SGPRs for the whole phase
+__device__ __forceinline__ DevModel load_model(const DevModel* mp) {
+  DevModel m;
+  __builtin_memcpy(&m, (const __attribute__((address_space(4))) DevModel*)mp, sizeof(DevModel));
+  return m;
+}
+
+#define ENV_UNPACK                  \
+  mp = uniform_ptr(mp);             \
+  s = uniform_lds(s);               \
+  scr = uniform_ptr(scr);           \
+  lane = __lane_id();               \
+  const DevModel m = load_model(mp); \
+  const LdsLayout& L = m.L;         \
+  const ScratchLayout& S = m.S;     \
+  (void)L; (void)S; (void)scr; (void)lane
 
 // Cholesky of the dense nv x nv matrix A (LDS) into Lf (LDS), column by column; lanes over rows.
-__device__ void cholesky(const Env& E, const float* A, float* Lf) {
-  const int nv = E.m.nv, lane = E.lane;
+__device__ __noinline__ void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
+  mp = uniform_ptr(mp);
+  A = uniform_lds(const_cast<lfloat*>(A));
+  Lf = uniform_lds(Lf);
+  lane = __lane_id();
+  const int nv = load_model(mp).nv;
+  #pragma unroll 1
   for (int k = 0; k < nv; ++k) {
     float t = 0;
     if (lane >= k && lane < nv) {
@@ -440,9 +482,13 @@ __device__ void cholesky(const Env& E, const float* A, float* Lf) {
   }
 }
 // x = A^-1 b with A = Lf Lf'; lane j holds b_j / returns x_j (lanes >= nv return 0)
-__device__ float chol_solve_lanes(const Env& E, const float* Lf, float b) {
-  const int nv = E.m.nv, lane = E.lane;
+__device__ __noinline__ float chol_solve_lanes(const DevModel* __restrict__ mp, const lfloat* Lf, float b, int lane) {
+  mp = uniform_ptr(mp);
+  Lf = uniform_lds(const_cast<lfloat*>(Lf));
+  lane = __lane_id();
+  const int nv = load_model(mp).nv;
   float x = lane < nv ? b : 0.0f;
+  #pragma unroll 1
   for (int i = 0; i < nv; ++i) {
     float xi = bcast(x, i) / Lf[i * nv + i];
     if (lane == i) x = xi;
@@ -456,7 +502,8 @@ __device__ float chol_solve_lanes(const Env& E, const float* Lf, float b) {
   return x;
 }
 // serial solve by one lane (vectors in registers/scratch); used per constraint row
-__device__ void chol_solve_serial(const float* Lf, int nv, const float* b, float* x) {
+__device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, const float* b, float* x) {
+  #pragma unroll 1
   for (int i = 0; i < nv; ++i) {
     float sacc = b[i];
     for (int k = 0; k < i; ++k) sacc -= Lf[i * nv + k] * x[k];
@@ -464,39 +511,38 @@ __device__ void chol_solve_serial(const float* Lf, int nv, const float* b, float
   }
   for (int i = nv - 1; i >= 0; --i) {
     float sacc = x[i];
+    #pragma unroll 1
     for (int k = i + 1; k < nv; ++k) sacc -= Lf[k * nv + i] * x[k];
     x[i] = sacc / Lf[i * nv + i];
   }
 }
 
 // mj_kinematics + rotational part of cinert; bodies of one depth level per pass
-__device__ void kinematics(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane;
+__device__ __noinline__ void kinematics(ENV_PARAMS) {
+  ENV_UNPACK;
   if (lane == 0) {
-    float* x = s + L.xpos; x[0] = x[1] = x[2] = 0;
-    float* q = s + L.xquat; q[0] = 1; q[1] = q[2] = q[3] = 0;
-    float* mm = s + L.xmat;
+    lfloat* x = s + L.xpos; x[0] = x[1] = x[2] = 0;
+    lfloat* q = s + L.xquat; q[0] = 1; q[1] = q[2] = q[3] = 0;
+    lfloat* mm = s + L.xmat;
     for (int i = 0; i < 9; ++i) mm[i] = (i % 4 == 0) ? 1.0f : 0.0f;
-    float* xi = s + L.xipos; xi[0] = xi[1] = xi[2] = 0;
+    lfloat* xi = s + L.xipos; xi[0] = xi[1] = xi[2] = 0;
   }
   wsync();
   for (int lev = 1; lev <= m.max_depth; ++lev) {
     const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+    #pragma unroll 1
     for (int k = lane; k < nl; k += 64) {
       const int b = m.level_body[a0 + k];
       const int p = m.body_parentid[b];
       float pos[3], q[4];
       const int ja = m.body_jntadr[b], nj = m.body_jntnum[b];
       if (nj > 0 && m.jnt_type[ja] == MRS_JNT_FREE) {
-        const float* qp = s + L.qpos + m.jnt_qposadr[ja];
+        const lfloat* qp = s + L.qpos + m.jnt_qposadr[ja];
         pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
         q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
         quat_normalize(q);
-        float* anc = s + L.xanchor + 3 * ja;
-        float* ax = s + L.xaxis + 3 * ja;
+        lfloat* anc = s + L.xanchor + 3 * ja;
+        lfloat* ax = s + L.xaxis + 3 * ja;
         for (int i = 0; i < 3; ++i) { anc[i] = pos[i]; ax[i] = 0; }
       } else {
         float pq[4] = {s[L.xquat + 4 * p], s[L.xquat + 4 * p + 1], s[L.xquat + 4 * p + 2], s[L.xquat + 4 * p + 3]};
@@ -506,6 +552,7 @@ __device__ void kinematics(const Env& E) {
         rot_quat(r, bpos, pq);
         for (int i = 0; i < 3; ++i) pos[i] = s[L.xpos + 3 * p + i] + r[i];
         quat_mul(q, pq, bq);
+        #pragma unroll 1
         for (int k2 = 0; k2 < nj; ++k2) {
           const int j = ja + k2, qa = m.jnt_qposadr[j];
           float jp[3] = {m.jnt_pos[3 * j], m.jnt_pos[3 * j + 1], m.jnt_pos[3 * j + 2]};
@@ -549,7 +596,7 @@ __device__ void kinematics(const Env& E) {
       quat_mul(qi, q, iq);
       quat2mat(R, qi);
       const float I0 = m.body_inertia[3 * b], I1 = m.body_inertia[3 * b + 1], I2 = m.body_inertia[3 * b + 2];
-      float* ci = s + L.cinert + 10 * b;
+      lfloat* ci = s + L.cinert + 10 * b;
       ci[0] = R[0] * I0 * R[0] + R[1] * I1 * R[1] + R[2] * I2 * R[2];
       ci[1] = R[3] * I0 * R[3] + R[4] * I1 * R[4] + R[5] * I2 * R[5];
       ci[2] = R[6] * I0 * R[6] + R[7] * I1 * R[7] + R[8] * I2 * R[8];
@@ -560,6 +607,7 @@ __device__ void kinematics(const Env& E) {
     wsync();
   }
   // geoms
+  #pragma unroll 1
   for (int g = lane; g < m.ngeom; g += 64) {
     const int b = m.geom_bodyid[g];
     float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
@@ -576,15 +624,14 @@ __device__ void kinematics(const Env& E) {
 }
 
 // mj_comPos: subtree coms of tree roots, cinert (parallel-axis part), cdof
-__device__ void com_pos(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane;
+__device__ __noinline__ void com_pos(ENV_PARAMS) {
+  ENV_UNPACK;
+  #pragma unroll 1
   for (int b = lane; b < m.nbody; b += 64) {
     if (b != 0 && m.body_parentid[b] != 0) continue;
     float c[3] = {0, 0, 0};
     const int e = m.body_subtree_end[b];
+    #pragma unroll 1
     for (int k = b; k < e; ++k) {
       const float mk = m.body_mass[k];
       for (int i = 0; i < 3; ++i) c[i] += mk * s[L.xipos + 3 * k + i];
@@ -593,8 +640,9 @@ __device__ void com_pos(const Env& E) {
     for (int i = 0; i < 3; ++i) s[L.scom + 3 * b + i] = sm > kMinVal ? c[i] / sm : s[L.xipos + 3 * b + i];
   }
   wsync();
+  #pragma unroll 1
   for (int b = lane; b < m.nbody; b += 64) {
-    float* ci = s + L.cinert + 10 * b;
+    lfloat* ci = s + L.cinert + 10 * b;
     if (b == 0) { for (int i = 0; i < 10; ++i) ci[i] = 0; continue; }
     const int rt = m.body_rootid[b];
     const float mass = m.body_mass[b];
@@ -608,6 +656,7 @@ __device__ void com_pos(const Env& E) {
     ci[5] -= mass * d[1] * d[2];
     ci[6] = mass * d[0]; ci[7] = mass * d[1]; ci[8] = mass * d[2]; ci[9] = mass;
   }
+  #pragma unroll 1
   for (int j = lane; j < m.njnt; j += 64) {
     const int b = m.jnt_bodyid[j], rt = m.body_rootid[b];
     int dof = m.jnt_dofadr[j];
@@ -615,12 +664,12 @@ __device__ void com_pos(const Env& E) {
     for (int i = 0; i < 3; ++i) off[i] = s[L.scom + 3 * rt + i] - s[L.xanchor + 3 * j + i];
     const int jt = m.jnt_type[j];
     if (jt == MRS_JNT_HINGE) {
-      float* cd = s + L.cdof + 6 * dof;
+      lfloat* cd = s + L.cdof + 6 * dof;
       float ax[3] = {s[L.xaxis + 3 * j], s[L.xaxis + 3 * j + 1], s[L.xaxis + 3 * j + 2]}, c[3];
       cross3(c, ax, off);
       for (int i = 0; i < 3; ++i) { cd[i] = ax[i]; cd[3 + i] = c[i]; }
     } else if (jt == MRS_JNT_SLIDE) {
-      float* cd = s + L.cdof + 6 * dof;
+      lfloat* cd = s + L.cdof + 6 * dof;
       for (int i = 0; i < 3; ++i) { cd[i] = 0; cd[3 + i] = s[L.xaxis + 3 * j + i]; }
     } else {
       if (jt == MRS_JNT_FREE) {
@@ -631,7 +680,7 @@ __device__ void com_pos(const Env& E) {
       for (int k = 0; k < 3; ++k) {
         float ax[3] = {s[L.xmat + 9 * b + k], s[L.xmat + 9 * b + 3 + k], s[L.xmat + 9 * b + 6 + k]}, c[3];
         cross3(c, ax, off);
-        float* cd = s + L.cdof + 6 * (dof + k);
+        lfloat* cd = s + L.cdof + 6 * (dof + k);
         for (int i = 0; i < 3; ++i) { cd[i] = ax[i]; cd[3 + i] = c[i]; }
       }
     }
@@ -640,22 +689,24 @@ __device__ void com_pos(const Env& E) {
 }
 
 // mj_crb + armature: crb by subtree sums, M by (dof, ancestor-dof) pairs
-__device__ void make_M(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane, nv = m.nv;
+__device__ __noinline__ void make_M(ENV_PARAMS) {
+  ENV_UNPACK;
+  const int nv = m.nv;
+  #pragma unroll 1
   for (int b = lane; b < m.nbody; b += 64) {
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (b != 0) {
       const int e = m.body_subtree_end[b];
+      #pragma unroll 1
       for (int k = b; k < e; ++k)
         for (int i = 0; i < 10; ++i) acc[i] += s[L.cinert + 10 * k + i];
     }
     for (int i = 0; i < 10; ++i) s[L.crb + 10 * b + i] = acc[i];
   }
+  #pragma unroll 1
   for (int i = lane; i < nv * nv; i += 64) s[L.M + i] = 0;
   wsync();
+  #pragma unroll 1
   for (int p = lane; p < m.nMpair; p += 64) {
     const int i = m.Mpair[2 * p], j = m.Mpair[2 * p + 1];
     float buf[6], cd[6];
@@ -671,21 +722,20 @@ __device__ void make_M(const Env& E) {
 }
 
 // mj_comVel: level by level
-__device__ void com_vel(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane;
+__device__ __noinline__ void com_vel(ENV_PARAMS) {
+  ENV_UNPACK;
   if (lane < 6) s[L.cvel + lane] = 0;
   wsync();
   for (int lev = 1; lev <= m.max_depth; ++lev) {
     const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+    #pragma unroll 1
     for (int k = lane; k < nl; k += 64) {
       const int b = m.level_body[a0 + k];
       const int p = m.body_parentid[b];
       float cv[6];
       for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
       const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      #pragma unroll 1
       for (int k2 = 0; k2 < nd; ++k2) {
         const int j = da + k2;
         const int jid = m.dof_jntid[j], jt = m.jnt_type[jid];
@@ -720,23 +770,24 @@ __device__ void com_vel(const Env& E) {
 }
 
 // mj_rne (no acceleration term): qfrc_bias
-__device__ void rne(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane;
+__device__ __noinline__ void rne(ENV_PARAMS) {
+  ENV_UNPACK;
   if (lane < 6) {
-    float g = (lane >= 3 && !(m.disableflags & MRS_DSBL_GRAVITY)) ? -m.gravity[lane - 3] : 0.0f;
+    const float gx = m.gravity[0], gy = m.gravity[1], gz = m.gravity[2];
+    float g = lane == 3 ? -gx : (lane == 4 ? -gy : (lane == 5 ? -gz : 0.0f));
+    if (m.disableflags & MRS_DSBL_GRAVITY) g = 0;
     s[L.cacc + lane] = g;
   }
   wsync();
   for (int lev = 1; lev <= m.max_depth; ++lev) {
     const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+    #pragma unroll 1
     for (int k = lane; k < nl; k += 64) {
       const int b = m.level_body[a0 + k];
       float ca[6];
       for (int i = 0; i < 6; ++i) ca[i] = s[L.cacc + 6 * m.body_parentid[b] + i];
       const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      #pragma unroll 1
       for (int k2 = 0; k2 < nd; ++k2) {
         const float qv = s[L.qvel + da + k2];
         for (int i = 0; i < 6; ++i) ca[i] += s[L.cdofdot + 6 * (da + k2) + i] * qv;
@@ -752,16 +803,19 @@ __device__ void rne(const Env& E) {
     wsync();
   }
   // subtree sums of body forces into crb storage (crb no longer needed)
+  #pragma unroll 1
   for (int b = lane; b < m.nbody; b += 64) {
     float acc[6] = {0, 0, 0, 0, 0, 0};
     if (b != 0) {
       const int e = m.body_subtree_end[b];
+      #pragma unroll 1
       for (int k = b; k < e; ++k)
         for (int i = 0; i < 6; ++i) acc[i] += s[L.cfrc + 6 * k + i];
     }
     for (int i = 0; i < 6; ++i) s[L.crb + 6 * b + i] = acc[i];
   }
   wsync();
+  #pragma unroll 1
   for (int j = lane; j < m.nv; j += 64) {
     const int b = m.dof_bodyid[j];
     float v = 0;
@@ -772,25 +826,22 @@ __device__ void rne(const Env& E) {
 }
 
 // translational point-Jacobian column of dof j for a point on body b (0 if j does not move b)
-__device__ __forceinline__ void jac_col(const Env& E, int b, const float pnt[3], int j, float col[3]) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
+__device__ __forceinline__ void jac_col(const DevModel& m, const lfloat* s, int b, const float pnt[3], int j, float col[3]) {
   const int bj = m.dof_bodyid[j];
   if (!(b >= bj && b < m.body_subtree_end[bj])) { col[0] = col[1] = col[2] = 0; return; }
-  const float* c = E.s + L.scom + 3 * m.body_rootid[b];
-  const float* cd = E.s + L.cdof + 6 * j;
+  const lfloat* c = s + m.L.scom + 3 * m.body_rootid[b];
+  const lfloat* cd = s + m.L.cdof + 6 * j;
   float off[3] = {pnt[0] - c[0], pnt[1] - c[1], pnt[2] - c[2]}, ang[3] = {cd[0], cd[1], cd[2]}, cr[3];
   cross3(cr, ang, off);
   for (int i = 0; i < 3; ++i) col[i] = cd[3 + i] + cr[i];
 }
 
 // mj_passive + mj_fwdActuation + qfrc_smooth + qacc_smooth (lane per dof)
-__device__ float smooth_forces(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane, nv = m.nv;
+__device__ __noinline__ float smooth_forces(ENV_PARAMS) {
+  ENV_UNPACK;
+  const int nv = m.nv;
   // actuator forces (lane per actuator)
+  #pragma unroll 1
   for (int a = lane; a < m.nu; a += 64) {
     float force = 0;
     if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
@@ -799,8 +850,8 @@ __device__ float smooth_forces(const Env& E) {
       float ctrl = s[L.ctrl + a];
       if (m.act_ctrllimited[a] && !(m.disableflags & MRS_DSBL_CLAMPCTRL))
         ctrl = clampf(ctrl, m.act_ctrlrange[2 * a], m.act_ctrlrange[2 * a + 1]);
-      const float* g = m.act_gainprm + 3 * a;
-      const float* bp = m.act_biasprm + 3 * a;
+      const CPtr<float> g = m.act_gainprm + 3 * a;
+      const CPtr<float> bp = m.act_biasprm + 3 * a;
       float gain = m.act_gaintype[a] == MRS_GAIN_AFFINE ? g[0] + g[1] * len + g[2] * vel : g[0];
       float bias = m.act_biastype[a] == MRS_BIAS_AFFINE ? bp[0] + bp[1] * len + bp[2] * vel : 0.0f;
       force = gain * ctrl + bias;
@@ -813,6 +864,7 @@ __device__ float smooth_forces(const Env& E) {
   if (lane < nv) {
     const int j = lane;
     float qa = 0;
+    #pragma unroll 1
     for (int a = 0; a < m.nu; ++a)
       if (m.act_dof[a] == j) qa += m.act_gear[a] * s[L.act_force + a];
     const int jid = m.dof_jntid[j];
@@ -828,12 +880,13 @@ __device__ float smooth_forces(const Env& E) {
       pas -= m.dof_damping[j] * s[L.qvel + j];
       if (!(m.disableflags & MRS_DSBL_GRAVITY)) {
         const int bj = m.dof_bodyid[j], e = m.body_subtree_end[bj];
+        #pragma unroll 1
         for (int b = bj; b < e; ++b) {
           const float gc = m.body_gravcomp[b];
           if (gc == 0) continue;
           float f[3], col[3], pnt[3] = {s[L.xipos + 3 * b], s[L.xipos + 3 * b + 1], s[L.xipos + 3 * b + 2]};
           for (int i = 0; i < 3; ++i) f[i] = -m.gravity[i] * m.body_mass[b] * gc;
-          jac_col(E, b, pnt, j, col);
+          jac_col(m, s, b, pnt, j, col);
           pas += dot3(col, f);
         }
       }
@@ -842,29 +895,26 @@ __device__ float smooth_forces(const Env& E) {
     qfs = pas - s[L.qfrc_bias + j] + s[L.qfrc_applied + j] + qa;
     s[L.qfrc_smooth + j] = qfs;
   }
-  float qacc_s = chol_solve_lanes(E, s + L.L, qfs);
+  float qacc_s = chol_solve_lanes(mp, s + L.L, qfs, lane);
   if (lane < nv) s[L.qacc_smooth + lane] = qacc_s;
   wsync();
   return qacc_s;
 }
 
 // mj_collision: candidate pairs (lane per pair), bounding-sphere test, narrow phase, compaction
-__device__ int collision(const Env& E) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  const ScratchLayout& S = E.S;
-  float* s = E.s;
-  const int lane = E.lane;
+__device__ __noinline__ int collision(ENV_PARAMS) {
+  ENV_UNPACK;
   int ncon = 0;
   if ((m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) || m.npair == 0) return 0;
+  #pragma unroll 1
   for (int base = 0; base < m.npair; base += 64) {
     const int p = base + lane;
-    Con c[4];
+    Con* c = reinterpret_cast<Con*>(scr + S.stage) + 4 * lane;  // per-lane staging in global scratch
     int n = 0;
     if (p < m.npair) {
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-      const float* p1 = s + L.gxpos + 3 * g1;
-      const float* p2 = s + L.gxpos + 3 * g2;
+      float p1[3], p2[3], m1[9], m2[9];
+      for (int i = 0; i < 3; ++i) { p1[i] = s[L.gxpos + 3 * g1 + i]; p2[i] = s[L.gxpos + 3 * g2 + i]; }
       const float margin = m.pair_margin[p];
       const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
       bool cand = true;
@@ -873,16 +923,20 @@ __device__ int collision(const Env& E) {
         float rb = m.geom_rbound[g1] + m.geom_rbound[g2] + margin;
         cand = dot3(dv, dv) <= rb * rb;
       }
-      if (cand)
-        n = narrowphase(t1, t2, p1, s + L.gxmat + 9 * g1, m.geom_size + 3 * g1, p2, s + L.gxmat + 9 * g2,
-                        m.geom_size + 3 * g2, margin, c);
+      if (cand) {
+        for (int i = 0; i < 9; ++i) { m1[i] = s[L.gxmat + 9 * g1 + i]; m2[i] = s[L.gxmat + 9 * g2 + i]; }
+        float s1[3] = {m.geom_size[3 * g1], m.geom_size[3 * g1 + 1], m.geom_size[3 * g1 + 2]};
+        float s2[3] = {m.geom_size[3 * g2], m.geom_size[3 * g2 + 1], m.geom_size[3 * g2 + 2]};
+        n = narrowphase(t1, t2, p1, m1, s1, p2, m2, s2, margin, c);
+      }
     }
     int total;
     int off = wave_scan_excl(n, lane, total);
+    #pragma unroll 1
     for (int k = 0; k < n; ++k) {
       const int slot = ncon + off + k;
       if (slot >= m.max_con) break;
-      float* rec = E.scr + S.con + kConRec * slot;
+      float* rec = scr + S.con + kConRec * slot;
       float fr[9] = {c[k].nrm[0], c[k].nrm[1], c[k].nrm[2], 0, 0, 0, 0, 0, 0};
       make_frame(fr);
       rec[0] = __int_as_float(p);
@@ -898,13 +952,10 @@ __device__ int collision(const Env& E) {
 }
 
 // mj_makeConstraint + mj_makeImpedance + PGS (matrix-free rows) -> qacc, qfrc_constraint
-__device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_out) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  const ScratchLayout& S = E.S;
-  float* s = E.s;
-  float* scr = E.scr;
-  const int lane = E.lane, nv = m.nv;
+__device__ __noinline__ float constraints(ENV_PARAMS, int ncon, float qacc_s) {
+  ENV_UNPACK;
+  ncon = uniform_int(ncon);
+  const int nv = m.nv;
   float* J = scr + S.efc_J;
   float* MJ = scr + S.efc_MJ;
   float* type = scr + S.efc_type;
@@ -917,11 +968,12 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
   float* ff = scr + S.efc_f;
   float* ARii = scr + S.efc_ARii;
   int nefc = 0;
-  if (m.disableflags & MRS_DSBL_CONSTRAINT) { qacc_out = qacc_s; if (lane < nv) s[L.qfrc_con + lane] = 0; wsync(); return; }
+  if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) s[L.qfrc_con + lane] = 0; wsync(); return qacc_s; }
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
   // keep ids in a small per-row int array inside the type slot (type*65536 + id)
   // --- friction loss rows
   if (!(m.disableflags & MRS_DSBL_FRICTIONLOSS)) {
+    #pragma unroll 1
     for (int r = 0; r < m.nfric; ++r) {
       const int j = m.fric_dof[r];
       if (lane < nv) J[r * nv + lane] = (lane == j) ? 1.0f : 0.0f;
@@ -934,6 +986,7 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
   }
   // --- joint limit rows (lane per limited joint, compacted)
   if (!(m.disableflags & MRS_DSBL_LIMIT)) {
+    #pragma unroll 1
     for (int base = 0; base < m.nlim; base += 64) {
       const int k = base + lane;
       int cnt = 0;
@@ -964,6 +1017,7 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
     }
     wsync();
     // dense J of limit rows
+    #pragma unroll 1
     for (int r = m.nfric; r < nefc; ++r) {
       const int code = __float_as_int(type[r]);
       const int jid = code & 0xffff;
@@ -973,9 +1027,11 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
     }
     wsync();
     if (lane == 0)
+      #pragma unroll 1
       for (int r = m.nfric; r < nefc; ++r) floss[r] = 0;
   }
   // --- contact rows: lane per dof, loop over contacts
+  #pragma unroll 1
   for (int c = 0; c < ncon; ++c) {
     const float* rec = scr + S.con + kConRec * c;
     const int p = __float_as_int(rec[0]);
@@ -985,8 +1041,8 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
     float jc[3] = {0, 0, 0};
     if (lane < nv) {
       float c1[3], c2[3];
-      jac_col(E, b1, cp, lane, c1);
-      jac_col(E, b2, cp, lane, c2);
+      jac_col(m, s, b1, cp, lane, c1);
+      jac_col(m, s, b2, cp, lane, c2);
       float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
       for (int r = 0; r < 3; ++r) jc[r] = rec[5 + 3 * r] * dc[0] + rec[6 + 3 * r] * dc[1] + rec[7 + 3 * r] * dc[2];
     }
@@ -1015,16 +1071,16 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
   }
   wsync();
   if (nefc == 0) {
-    qacc_out = qacc_s;
     if (lane < nv) s[L.qfrc_con + lane] = 0;
     wsync();
-    return;
+    return qacc_s;
   }
   // --- impedance, R, aref, M^-1 J', ARii, b (lane per row)
+  #pragma unroll 1
   for (int r = lane; r < nefc; r += 64) {
     const int code = __float_as_int(type[r]);
     const int t = code >> 16, id = code & 0xffff;
-    const float *sr, *si;
+    CPtr<float> sr, si;
     float diag;
     if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
     else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
@@ -1061,6 +1117,7 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
     }
     float vel = 0, jqs = 0;
     const float* Jr = J + r * nv;
+    #pragma unroll 1
     for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
     const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
     aref[r] = -B * vel - pterm;
@@ -1069,6 +1126,7 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
     float* MJr = MJ + r * nv;
     chol_solve_serial(s + L.L, nv, Jr, MJr);
     float d = 0;
+    #pragma unroll 1
     for (int j = 0; j < nv; ++j) d += Jr[j] * MJr[j];
     ARii[r] = d + R;
   }
@@ -1077,11 +1135,13 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
   float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f, lane per dof
   {
     bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+    #pragma unroll 1
     for (int r = lane; r < nefc; r += 64) {
       float f = 0;
       if (warm) {
         const float* Jr = J + r * nv;
         float jar = -aref[r];
+        #pragma unroll 1
         for (int j = 0; j < nv; ++j) jar += Jr[j] * s[L.qacc_ws + j];
         const int t = __float_as_int(type[r]) >> 16;
         const float D = 1.0f / Rr[r];
@@ -1099,13 +1159,16 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
       // v = M^-1 J' f (lane per dof); cost = sum_r f_r (0.5 (J_r v + R_r f_r) + b_r)
       float v = 0;
       if (lane < nv)
+        #pragma unroll 1
         for (int r = 0; r < nefc; ++r) v += MJ[r * nv + lane] * ff[r];
       float cost = 0;
+      #pragma unroll 1
       for (int r = 0; r < nefc; ++r) {
         const float jv = wave_sum(lane < nv ? J[r * nv + lane] * v : 0.0f);
         cost += ff[r] * (0.5f * (jv + Rr[r] * ff[r]) + bb[r]);
       }
       if (cost > 0) {
+        #pragma unroll 1
         for (int r = lane; r < nefc; r += 64) ff[r] = 0;
       } else {
         qa += v;
@@ -1114,8 +1177,10 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
     }
   }
   // --- PGS sweeps (rows serial, dot products across lanes)
+  #pragma unroll 1
   for (int it = 0; it < m.iterations; ++it) {
     float improvement = 0;
+    #pragma unroll 1
     for (int r = 0; r < nefc; ++r) {
       const float jq = wave_sum(lane < nv ? J[r * nv + lane] * qa : 0.0f);
       const float f0 = ff[r];
@@ -1138,20 +1203,20 @@ __device__ void constraints(const Env& E, int ncon, float qacc_s, float& qacc_ou
   // --- qfrc_constraint = J' f
   if (lane < nv) {
     float v = 0;
+    #pragma unroll 1
     for (int r = 0; r < nefc; ++r) v += J[r * nv + lane] * ff[r];
     s[L.qfrc_con + lane] = v;
   }
-  qacc_out = qa;
   wsync();
+  return qa;
 }
 
 // mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel
-__device__ void sensors(const Env& E, float* sensordata) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane;
+__device__ __noinline__ void sensors(ENV_PARAMS, float* sensordata) {
+  ENV_UNPACK;
+  sensordata = uniform_ptr(sensordata);
   if (m.disableflags & MRS_DSBL_SENSOR) return;
+  #pragma unroll 1
   for (int k = lane; k < m.nrf; k += 64) {
     const int sid = m.rf_sensor[k];
     const int site = m.sensor_objid[sid];
@@ -1166,18 +1231,36 @@ __device__ void sensors(const Env& E, float* sensordata) {
     quat2mat(sm, q);
     const float vec[3] = {sm[2], sm[5], sm[8]};
     float dist = -1;
+    const float vv = dot3(vec, vec);
+    #pragma unroll 1
     for (int g = 0; g < m.ngeom; ++g) {
-      if (m.geom_bodyid[g] == b || m.geom_rgba[4 * g + 3] == 0) continue;
-      const float* gp = s + L.gxpos + 3 * g;
-      const float* gm = s + L.gxmat + 9 * g;
-      float dv[3] = {pnt[0] - gp[0], pnt[1] - gp[1], pnt[2] - gp[2]}, lp[3], lv[3];
+      if (m.geom_rgba[4 * g + 3] == 0) continue;
+      const int type = m.geom_type[g];
+      const lfloat* gp = s + L.gxpos + 3 * g;
+      float dv[3] = {pnt[0] - gp[0], pnt[1] - gp[1], pnt[2] - gp[2]};
+      bool cand = m.geom_bodyid[g] != b;
+      if (type != MRS_GEOM_PLANE) {
+        // bounding-sphere cull (conservative): closest approach of the ray line to the geom centre,
+        // and no chance of beating the current nearest hit; the primitive test runs only if some
+        // lane of the wave still needs it
+        const float rb = m.geom_rbound[g] * 1.0001f + 1e-6f;
+        const float tp = -dot3(dv, vec);  // projection (times |vec|^2) of the centre on the ray
+        const float d2 = dot3(dv, dv) - tp * tp / vv;
+        cand = cand && d2 <= rb * rb && tp >= -rb * sqrtf(vv) &&
+               (dist < 0 || tp - rb * sqrtf(vv) <= dist * vv);
+      }
+      if (!__any(cand)) continue;
+      if (!cand) continue;
+      const lfloat* gm = s + L.gxmat + 9 * g;
+      float lp[3], lv[3];
       matT_vec(lp, gm, dv);
       matT_vec(lv, gm, vec);
-      const float t = ray_geom_local(m.geom_type[g], m.geom_size + 3 * g, lp, lv);
+      const float t = ray_geom_local(type, m.geom_size + 3 * g, lp, lv);
       if (t >= 0 && (dist < 0 || t < dist)) dist = t;
     }
     sensordata[m.sensor_adr[sid]] = dist;
   }
+  #pragma unroll 1
   for (int sid = lane; sid < m.nsensor; sid += 64) {
     const int t = m.sensor_type[sid], id = m.sensor_objid[sid];
     float* out = sensordata + m.sensor_adr[sid];
@@ -1232,47 +1315,50 @@ __device__ void sensors(const Env& E, float* sensordata) {
 }
 
 // reset one env (mj_resetData; held inputs ctrl/qfrc_applied are re-applied by the caller's loop)
-__device__ void reset_env(const Env& E, double& time) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  for (int i = E.lane; i < m.nq; i += 64) s[L.qpos + i] = m.qpos0[i];
-  for (int i = E.lane; i < m.nv; i += 64) { s[L.qvel + i] = 0; s[L.qacc_ws + i] = 0; }
-  time = 0;
+__device__ __noinline__ void reset_env(ENV_PARAMS) {
+  ENV_UNPACK;
+  #pragma unroll 1
+  for (int i = lane; i < m.nq; i += 64) s[L.qpos + i] = m.qpos0[i];
+  #pragma unroll 1
+  for (int i = lane; i < m.nv; i += 64) { s[L.qvel + i] = 0; s[L.qacc_ws + i] = 0; }
   wsync();
 }
 
-__device__ bool any_bad(const Env& E, int off, int n) {
+__device__ __noinline__ bool any_bad(ENV_PARAMS, int off, int n) {
+  ENV_UNPACK;
+  off = uniform_int(off);
+  n = uniform_int(n);
   bool bad = false;
-  for (int i = E.lane; i < n; i += 64) bad |= is_bad(E.s[off + i]);
+  #pragma unroll 1
+  for (int i = lane; i < n; i += 64) bad |= is_bad(s[off + i]);
   return __any(bad);
 }
 
 // full forward pass; returns qacc (lane per dof)
-__device__ float forward(const Env& E, float* sensordata, int& ncon) {
-  kinematics(E);
-  com_pos(E);
-  make_M(E);
-  cholesky(E, E.s + E.L.M, E.s + E.L.L);
-  com_vel(E);
-  rne(E);
-  float qacc_s = smooth_forces(E);
-  ncon = collision(E);
-  float qacc;
-  constraints(E, ncon, qacc_s, qacc);
-  sensors(E, sensordata);
-  if (E.lane < E.m.nv) E.s[E.L.qacc + E.lane] = qacc;
+__device__ __noinline__ int forward(ENV_PARAMS, float* sensordata) {
+  ENV_UNPACK;
+  sensordata = uniform_ptr(sensordata);
+  kinematics(ENV_ARGS);
+  com_pos(ENV_ARGS);
+  make_M(ENV_ARGS);
+  cholesky(mp, s + L.M, s + L.L, lane);
+  com_vel(ENV_ARGS);
+  rne(ENV_ARGS);
+  const float qacc_s = smooth_forces(ENV_ARGS);
+  const int ncon = (m.diag_skip & 2) ? 0 : collision(ENV_ARGS);
+  const float qacc = (m.diag_skip & 4) ? qacc_s : constraints(ENV_ARGS, ncon, qacc_s);
+  if (!(m.diag_skip & 1)) sensors(ENV_ARGS, sensordata);
+  if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
-  return qacc;
+  return ncon;
 }
 
 // mj_Euler / mj_implicit(implicitfast) + mj_advance
-__device__ void integrate(const Env& E, float qacc, double& time) {
-  const DevModel& m = E.m;
-  const LdsLayout& L = E.L;
-  float* s = E.s;
-  const int lane = E.lane, nv = m.nv;
+__device__ __noinline__ void integrate(ENV_PARAMS) {
+  ENV_UNPACK;
+  const int nv = m.nv;
   const float h = m.timestep;
+  const float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
   bool need_solve = false;
   float dg = 0;
   if (lane < nv) {
@@ -1281,6 +1367,7 @@ __device__ void integrate(const Env& E, float qacc, double& time) {
     } else {
       if (!(m.disableflags & MRS_DSBL_PASSIVE)) dg = m.dof_damping[lane];
       if (!(m.disableflags & MRS_DSBL_ACTUATION))
+        #pragma unroll 1
         for (int a = 0; a < m.nu; ++a) {
           if (m.act_dof[a] != lane) continue;
           if (m.act_forcelimited[a]) {
@@ -1303,15 +1390,16 @@ __device__ void integrate(const Env& E, float qacc, double& time) {
     // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
     if (lane < nv) s[L.M + lane * nv + lane] += h * dg;
     wsync();
-    cholesky(E, s + L.M, s + L.L);
+    cholesky(mp, s + L.M, s + L.L, lane);
     float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
-    qacc_int = chol_solve_lanes(E, s + L.L, rhs);
+    qacc_int = chol_solve_lanes(mp, s + L.L, rhs, lane);
   }
   if (lane < nv) {
     s[L.qacc_ws + lane] = qacc;
     s[L.qvel + lane] += h * qacc_int;
   }
   wsync();
+  #pragma unroll 1
   for (int j = lane; j < m.njnt; j += 64) {
     int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
     const int jt = m.jnt_type[j];
@@ -1332,26 +1420,34 @@ __device__ void integrate(const Env& E, float qacc, double& time) {
     quat_normalize(q);
     for (int i = 0; i < 4; ++i) s[L.qpos + a + i] = q[i];
   }
-  time += m.timestep_d;
   wsync();
 }
 
+#ifndef MRS_MIN_WAVES_PER_EU
+#define MRS_MIN_WAVES_PER_EU 8
+#endif
+
 template <bool kForwardOnly>
-__global__ __launch_bounds__(64 * kEnvsPerBlock) void step_kernel(DevModel m, LdsLayout L, ScratchLayout S,
-                                                                  DevState st, int n_envs, int n_steps) {
+__global__ __launch_bounds__(64 * kEnvsPerBlock, MRS_MIN_WAVES_PER_EU) void step_kernel(const DevModel* __restrict__ mp, DevState st,
+                                                                  int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const DevModel& m = *mp;
+  const LdsLayout& L = m.L;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int env = blockIdx.x * kEnvsPerBlock + wid;
   if (env >= n_envs) return;
-  float* s = smem + wid * L.total;
-  Env E{m, L, s, st.scratch + (size_t)env * S.total, S, lane};
+  lfloat* s = (lfloat*)(smem + wid * L.total);
+  float* scr = st.scratch + (size_t)env * m.S.total;
   const size_t e = (size_t)env;
+  #pragma unroll 1
   for (int i = lane; i < m.nq; i += 64) s[L.qpos + i] = st.qpos[e * m.nq + i];
+  #pragma unroll 1
   for (int i = lane; i < m.nv; i += 64) {
     s[L.qvel + i] = st.qvel[e * m.nv + i];
     s[L.qfrc_applied + i] = st.qfrc_applied[e * m.nv + i];
     s[L.qacc_ws + i] = st.qacc_ws[e * m.nv + i];
   }
+  #pragma unroll 1
   for (int i = lane; i < m.nu; i += 64) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
   double time = st.time[e];
   float* sensordata = st.sensordata + e * m.nsensordata;
@@ -1360,29 +1456,34 @@ __global__ __launch_bounds__(64 * kEnvsPerBlock) void step_kernel(DevModel m, Ld
   int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
   for (int step = 0; step < n_steps; ++step) {
     if (!kForwardOnly) {
-      if (any_bad(E, L.qpos, m.nq)) {
+      if (any_bad(ENV_ARGS, L.qpos, m.nq)) {
         ++w_pos;
-        if (!(m.disableflags & MRS_DSBL_AUTORESET)) reset_env(E, time);
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env(ENV_ARGS); time = 0; }
       }
-      if (any_bad(E, L.qvel, m.nv)) {
+      if (any_bad(ENV_ARGS, L.qvel, m.nv)) {
         ++w_vel;
-        if (!(m.disableflags & MRS_DSBL_AUTORESET)) reset_env(E, time);
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env(ENV_ARGS); time = 0; }
       }
     }
-    float qacc = forward(E, sensordata, ncon);
+    ncon = forward(ENV_ARGS, sensordata);
     if (kForwardOnly) break;
-    if (any_bad(E, L.qacc, m.nv)) {
+    if (any_bad(ENV_ARGS, L.qacc, m.nv)) {
       ++w_acc;
       if (!(m.disableflags & MRS_DSBL_AUTORESET)) {
-        reset_env(E, time);
-        qacc = forward(E, sensordata, ncon);
+        reset_env(ENV_ARGS);
+        time = 0;
+        ncon = forward(ENV_ARGS, sensordata);
       }
     }
-    integrate(E, qacc, time);
+    integrate(ENV_ARGS);
+    time += m.timestep_d;
   }
   // kinematics of the last forward pass (what mjv_updateScene would render after mj_step)
+  #pragma unroll 1
   for (int i = lane; i < 3 * m.ngeom; i += 64) st.geom_xpos[e * 3 * m.ngeom + i] = s[L.gxpos + i];
+  #pragma unroll 1
   for (int i = lane; i < 9 * m.ngeom; i += 64) st.geom_xmat[e * 9 * m.ngeom + i] = s[L.gxmat + i];
+  #pragma unroll 1
   for (int c = lane; c < m.ncam; c += 64) {
     const int b = m.cam_bodyid[c];
     float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
@@ -1395,7 +1496,9 @@ __global__ __launch_bounds__(64 * kEnvsPerBlock) void step_kernel(DevModel m, Ld
     for (int i = 0; i < 3; ++i) st.cam_xpos[(e * m.ncam + c) * 3 + i] = s[L.xpos + 3 * b + i] + r[i];
     for (int i = 0; i < 9; ++i) st.cam_xmat[(e * m.ncam + c) * 9 + i] = cm[i];
   }
+  #pragma unroll 1
   for (int i = lane; i < m.nq; i += 64) st.qpos[e * m.nq + i] = s[L.qpos + i];
+  #pragma unroll 1
   for (int i = lane; i < m.nv; i += 64) {
     st.qvel[e * m.nv + i] = s[L.qvel + i];
     st.qacc_ws[e * m.nv + i] = s[L.qacc_ws + i];
@@ -1416,14 +1519,14 @@ __global__ __launch_bounds__(64 * kEnvsPerBlock) void step_kernel(DevModel m, Ld
 
 }  // namespace
 
-hipError_t launch_step(const DevModel& m, const LdsLayout& L, const ScratchLayout& S, const DevState& st,
-                       int n_envs, int n_steps, bool forward_only, hipStream_t stream) {
+hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
+                       bool forward_only, hipStream_t stream) {
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  const size_t lds = sizeof(float) * (size_t)L.total * kEnvsPerBlock;
+  const size_t lds = sizeof(float) * (size_t)lds_floats * kEnvsPerBlock;
   if (forward_only)
-    hipLaunchKernelGGL(step_kernel<true>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, m, L, S, st, n_envs, 1);
+    hipLaunchKernelGGL(step_kernel<true>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, d_model, st, n_envs, 1);
   else
-    hipLaunchKernelGGL(step_kernel<false>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, m, L, S, st, n_envs,
+    hipLaunchKernelGGL(step_kernel<false>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, d_model, st, n_envs,
                        n_steps);
   return hipGetLastError();
 }

@@ -72,5 +72,12 @@ def _ancestors(m, i):
         j = m.dof_parentid[j]
 
 
+# SURVEY.md §8(d) per-unit algorithmic figures (flops, bytes per env-step) for the configs; the
+# bench's roofline uses these, the structural count above is reported beside them for reference
+SURVEY_PER_ENV_STEP = {
+    "scene": (2.0e3, 72.0),          # C2: reference 2-DoF scene, dynamics only
+    "arm7_lidar": (1.9e5, 1692.0),   # C3: 7-DoF arm + 360-ray lidar
+}
+
 PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0      # HBM3E spec peak

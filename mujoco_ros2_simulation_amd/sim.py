@@ -20,7 +20,7 @@ from pathlib import Path
 import numpy as np
 
 _PKG = Path(__file__).resolve().parent
-LIB_PATH = _PKG / "libmrs.so"
+LIB_PATH = Path(os.environ["MRS_LIB"]) if os.environ.get("MRS_LIB") else _PKG / "libmrs.so"
 
 # enums mirrored from include/mrs_model.h / include/mrs.h
 GEOM_PLANE, GEOM_HFIELD, GEOM_SPHERE, GEOM_CAPSULE, GEOM_ELLIPSOID, GEOM_CYLINDER, GEOM_BOX, GEOM_MESH = range(8)

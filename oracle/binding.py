@@ -20,7 +20,8 @@ class OrcData(C.Structure):
                 ("time", C.c_double),
                 ("qacc", C.POINTER(C.c_double)), ("qfrc_actuator", C.POINTER(C.c_double)),
                 ("sensordata", C.POINTER(C.c_double)),
-                ("warning", C.c_int * 4), ("ncon", C.c_int), ("nefc", C.c_int), ("ws", C.c_void_p)]
+                ("warning", C.c_int * 4), ("ncon", C.c_int), ("nefc", C.c_int), ("solver_niter", C.c_int),
+                ("ws", C.c_void_p)]
 
 
 _lib = None
@@ -92,6 +93,8 @@ class OracleData:
     def ncon(self): return self._d.contents.ncon
     @property
     def nefc(self): return self._d.contents.nefc
+    @property
+    def solver_niter(self): return self._d.contents.solver_niter
 
     def reset(self, key: int = -1):
         lib().orc_reset(self._mv, self._d, key)

@@ -970,6 +970,7 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
     if (cost > 0) memset(f, 0, nefc * sizeof(double));
   }
   double scale = 1 / (m->stat_meaninertia * (nv > 1 ? nv : 1));
+  d->solver_niter = 0;
   for (int it = 0; it < m->iterations; ++it) {
     double improvement = 0;
     for (int r = 0; r < nefc; ++r) {
@@ -988,7 +989,8 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
       f[r] = nf;
       improvement -= delta * res + 0.5 * delta * delta * ar[r];
     }
-    if (improvement * scale < m->tolerance) break;
+    if (improvement * scale < m->tolerance) { d->solver_niter = it + 1; break; }
+    d->solver_niter = it + 1;
   }
   for (int j = 0; j < nv; ++j) {
     double v = 0;
@@ -1016,7 +1018,10 @@ static double ray_geom_local(int type, const double* s, const double lp[3], cons
   double x[2];
   switch (type) {
     case MRS_GEOM_PLANE: {
-      if (lv[2] > -MINVAL) return -1;
+      /* parallel within 1e-6 rad or facing away: miss.  MuJoCo tests lv[2] > -mjMINVAL (1e-15);
+         the relative form keeps fp32 (device) and fp64 (oracle) decisions identical for rays that
+         are horizontal up to rounding (the lidar of scenes/arm7_lidar.xml). */
+      if (lv[2] >= 0 || lv[2] * lv[2] <= 1e-12 * dot3(lv, lv)) return -1;
       double t = -lp[2] / lv[2];
       if (t < 0) return -1;
       double p0 = lp[0] + t * lv[0], p1 = lp[1] + t * lv[1];

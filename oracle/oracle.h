@@ -29,6 +29,7 @@ typedef struct orc_data {
   double *qacc, *qfrc_actuator, *sensordata;
   int warning[4]; /* bad qpos count, bad qvel count, bad qacc count, last info */
   int ncon, nefc;
+  int solver_niter; /* PGS sweeps of the last step */
   void* ws;       /* private workspace */
 } orc_data;
 
