@@ -23,6 +23,16 @@ constexpr float kMaxVal = 1e10f;
 // out-of-line phase functions, so every access is a ds_read/ds_write (not a flat access).
 typedef __attribute__((address_space(3))) float lfloat;
 
+// Phase functions are out of line by default: each gets its own register allocation under the
+// 64-VGPR budget of 8 waves/SIMD.  Measured on C3 (8192 envs): out-of-line 2.19 ms per 10-step
+// launch vs 2.39 (inlined, 8 waves), 2.64 (inlined, 4 waves), 3.04 (inlined, 6 waves).
+// -DMRS_PHASE_INLINE builds the inlined variant.
+#ifdef MRS_PHASE_INLINE
+#define MRS_PHASE __forceinline__
+#else
+#define MRS_PHASE __noinline__
+#endif
+
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -461,7 +471,7 @@ __device__ __forceinline__ DevModel load_model(const DevModel* mp) {
   (void)L; (void)S; (void)scr; (void)lane
 
 // Cholesky of the dense nv x nv matrix A (LDS) into Lf (LDS), column by column; lanes over rows.
-__device__ __noinline__ void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
+__device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
   mp = uniform_ptr(mp);
   A = uniform_lds(const_cast<lfloat*>(A));
   Lf = uniform_lds(Lf);
@@ -482,7 +492,7 @@ __device__ __noinline__ void cholesky(const DevModel* __restrict__ mp, const lfl
   }
 }
 // x = A^-1 b with A = Lf Lf'; lane j holds b_j / returns x_j (lanes >= nv return 0)
-__device__ __noinline__ float chol_solve_lanes(const DevModel* __restrict__ mp, const lfloat* Lf, float b, int lane) {
+__device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, const lfloat* Lf, float b, int lane) {
   mp = uniform_ptr(mp);
   Lf = uniform_lds(const_cast<lfloat*>(Lf));
   lane = __lane_id();
@@ -518,7 +528,7 @@ __device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, cons
 }
 
 // mj_kinematics + rotational part of cinert; bodies of one depth level per pass
-__device__ __noinline__ void kinematics(ENV_PARAMS) {
+__device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   ENV_UNPACK;
   if (lane == 0) {
     lfloat* x = s + L.xpos; x[0] = x[1] = x[2] = 0;
@@ -624,7 +634,7 @@ __device__ __noinline__ void kinematics(ENV_PARAMS) {
 }
 
 // mj_comPos: subtree coms of tree roots, cinert (parallel-axis part), cdof
-__device__ __noinline__ void com_pos(ENV_PARAMS) {
+__device__ MRS_PHASE void com_pos(ENV_PARAMS) {
   ENV_UNPACK;
   #pragma unroll 1
   for (int b = lane; b < m.nbody; b += 64) {
@@ -689,7 +699,7 @@ __device__ __noinline__ void com_pos(ENV_PARAMS) {
 }
 
 // mj_crb + armature: crb by subtree sums, M by (dof, ancestor-dof) pairs
-__device__ __noinline__ void make_M(ENV_PARAMS) {
+__device__ MRS_PHASE void make_M(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
   #pragma unroll 1
@@ -722,7 +732,7 @@ __device__ __noinline__ void make_M(ENV_PARAMS) {
 }
 
 // mj_comVel: level by level
-__device__ __noinline__ void com_vel(ENV_PARAMS) {
+__device__ MRS_PHASE void com_vel(ENV_PARAMS) {
   ENV_UNPACK;
   if (lane < 6) s[L.cvel + lane] = 0;
   wsync();
@@ -770,7 +780,7 @@ __device__ __noinline__ void com_vel(ENV_PARAMS) {
 }
 
 // mj_rne (no acceleration term): qfrc_bias
-__device__ __noinline__ void rne(ENV_PARAMS) {
+__device__ MRS_PHASE void rne(ENV_PARAMS) {
   ENV_UNPACK;
   if (lane < 6) {
     const float gx = m.gravity[0], gy = m.gravity[1], gz = m.gravity[2];
@@ -837,7 +847,7 @@ __device__ __forceinline__ void jac_col(const DevModel& m, const lfloat* s, int 
 }
 
 // mj_passive + mj_fwdActuation + qfrc_smooth + qacc_smooth (lane per dof)
-__device__ __noinline__ float smooth_forces(ENV_PARAMS) {
+__device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
   // actuator forces (lane per actuator)
@@ -902,7 +912,7 @@ __device__ __noinline__ float smooth_forces(ENV_PARAMS) {
 }
 
 // mj_collision: candidate pairs (lane per pair), bounding-sphere test, narrow phase, compaction
-__device__ __noinline__ int collision(ENV_PARAMS) {
+__device__ MRS_PHASE int collision(ENV_PARAMS) {
   ENV_UNPACK;
   int ncon = 0;
   if ((m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) || m.npair == 0) return 0;
@@ -952,7 +962,7 @@ __device__ __noinline__ int collision(ENV_PARAMS) {
 }
 
 // mj_makeConstraint + mj_makeImpedance + PGS (matrix-free rows) -> qacc, qfrc_constraint
-__device__ __noinline__ float constraints(ENV_PARAMS, int ncon, float qacc_s) {
+__device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   ncon = uniform_int(ncon);
   const int nv = m.nv;
@@ -1212,7 +1222,7 @@ __device__ __noinline__ float constraints(ENV_PARAMS, int ncon, float qacc_s) {
 }
 
 // mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel
-__device__ __noinline__ void sensors(ENV_PARAMS, float* sensordata) {
+__device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
   ENV_UNPACK;
   sensordata = uniform_ptr(sensordata);
   if (m.disableflags & MRS_DSBL_SENSOR) return;
@@ -1315,7 +1325,7 @@ __device__ __noinline__ void sensors(ENV_PARAMS, float* sensordata) {
 }
 
 // reset one env (mj_resetData; held inputs ctrl/qfrc_applied are re-applied by the caller's loop)
-__device__ __noinline__ void reset_env(ENV_PARAMS) {
+__device__ MRS_PHASE void reset_env(ENV_PARAMS) {
   ENV_UNPACK;
   #pragma unroll 1
   for (int i = lane; i < m.nq; i += 64) s[L.qpos + i] = m.qpos0[i];
@@ -1324,7 +1334,7 @@ __device__ __noinline__ void reset_env(ENV_PARAMS) {
   wsync();
 }
 
-__device__ __noinline__ bool any_bad(ENV_PARAMS, int off, int n) {
+__device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
   ENV_UNPACK;
   off = uniform_int(off);
   n = uniform_int(n);
@@ -1335,7 +1345,7 @@ __device__ __noinline__ bool any_bad(ENV_PARAMS, int off, int n) {
 }
 
 // full forward pass; returns qacc (lane per dof)
-__device__ __noinline__ int forward(ENV_PARAMS, float* sensordata) {
+__device__ MRS_PHASE int forward(ENV_PARAMS, float* sensordata) {
   ENV_UNPACK;
   sensordata = uniform_ptr(sensordata);
   kinematics(ENV_ARGS);
@@ -1354,7 +1364,7 @@ __device__ __noinline__ int forward(ENV_PARAMS, float* sensordata) {
 }
 
 // mj_Euler / mj_implicit(implicitfast) + mj_advance
-__device__ __noinline__ void integrate(ENV_PARAMS) {
+__device__ MRS_PHASE void integrate(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
   const float h = m.timestep;
