@@ -1,0 +1,94 @@
+/* C entry points for driving the MujocoSystemInterface plugin host without a controller manager.
+ *
+ * The plugin (mujoco_ros2_simulation_amd/csrc/plugin) is the C++ hardware_interface::SystemInterface
+ * that replaces the reference's src/mujoco_system_interface.cpp; on a ROS 2 box the controller
+ * manager loads it through pluginlib.  These functions play the controller manager's part —
+ * parse the <ros2_control> block of a URDF (what hardware_interface::parse_control_resources_from_urdf
+ * does after xacro), run the lifecycle, and call read()/write() — so the plugin's host logic can be
+ * tested and scripted from Python (tests/test_plugin.py) or any FFI.
+ *
+ * Library: mujoco_ros2_simulation_amd/libmrs_plugin.so (links libmrs.so).  All functions return 0 /
+ * a valid pointer on success and set a thread-local message readable with mrsp_last_error().
+ */
+#ifndef MRS_PLUGIN_H_
+#define MRS_PLUGIN_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mrsp_system mrsp_system;
+
+const char* mrsp_last_error(void);
+
+/* Parse `urdf_path`, expanding the xacro constructs the reference's test robot uses
+ * (test/test_robot.urdf: <xacro:arg> defaults, <xacro:if>/<xacro:unless>, $(arg x), $(find pkg)).
+ * xacro_args: "name:=value" pairs separated by spaces (overrides <xacro:arg> defaults);
+ * package_dirs: "pkg=/dir" pairs separated by ';' for $(find pkg).  The first <ros2_control> block
+ * becomes the plugin's HardwareInfo.  Returns NULL on a parse error. */
+mrsp_system* mrsp_load_urdf(const char* urdf_path, const char* xacro_args, const char* package_dirs);
+void mrsp_free(mrsp_system* s);
+
+/* read / override a <hardware><param> before on_init (e.g. physics_thread=false, device=0) */
+int mrsp_set_hardware_param(mrsp_system* s, const char* key, const char* value);
+int mrsp_get_hardware_param(const mrsp_system* s, const char* key, char* buf, int len);
+int mrsp_num_joints(const mrsp_system* s);
+int mrsp_num_sensors(const mrsp_system* s);
+
+/* lifecycle: returns 0 SUCCESS, 1 FAILURE, 2 ERROR (hardware_interface::CallbackReturn) and -1 if
+ * on_init threw (the message is in mrsp_last_error).  on_init also exports the interfaces. */
+int mrsp_on_init(mrsp_system* s);
+int mrsp_on_activate(mrsp_system* s);
+
+/* exported interfaces, in export order; names are "<prefix>/<interface>" */
+int mrsp_num_state_interfaces(const mrsp_system* s);
+int mrsp_num_command_interfaces(const mrsp_system* s);
+int mrsp_state_interface_name(const mrsp_system* s, int i, char* buf, int len);
+int mrsp_command_interface_name(const mrsp_system* s, int i, char* buf, int len);
+double mrsp_get_state(const mrsp_system* s, int i);
+double mrsp_get_command(const mrsp_system* s, int i);
+int mrsp_set_command(mrsp_system* s, int i, double value);
+/* perform_command_mode_switch with ';'-separated interface lists */
+int mrsp_switch_mode(mrsp_system* s, const char* start, const char* stop);
+
+/* one controller-manager cycle's halves */
+int mrsp_read(mrsp_system* s);
+int mrsp_write(mrsp_system* s, double period_s);
+/* advance the simulation synchronously by n physics steps (requires hardware param
+ * physics_thread=false); returns 0, or 1 if the step reported divergence */
+int mrsp_step(mrsp_system* s, int n_steps);
+double mrsp_sim_time(const mrsp_system* s);
+/* last /clock message (seconds) and the number published */
+double mrsp_clock(const mrsp_system* s, long* count);
+
+/* lidar: gather + publish once; read back the last LaserScan on `topic`.
+ * meta[7] = angle_min, angle_max, angle_increment, range_min, range_max, scan_time, time_increment.
+ * Returns the number of ranges (copied up to max), -1 if nothing was published on the topic. */
+int mrsp_lidar_update(mrsp_system* s);
+int mrsp_last_scan(const mrsp_system* s, const char* topic, float* ranges, int max, float* meta);
+/* cameras: render + publish once; read back the last depth image / camera info on the topics.
+ * depth: H*W floats (copied up to max); returns H*W or -1.  info: k[9], p[12]; wh[2]. */
+int mrsp_camera_update(mrsp_system* s);
+int mrsp_last_depth(const mrsp_system* s, const char* topic, float* depth, int max, int* wh);
+int mrsp_last_camera_info(const mrsp_system* s, const char* topic, double* k9, double* p12, int* wh);
+int mrsp_last_image(const mrsp_system* s, const char* topic, int* wh_step, char* encoding, int len);
+
+/* host-logic hooks (no GPU needed):
+ * parse_lidar_name: "<name>-<digits>" -> index (or -1), name copied to buf (reference
+ *   src/mujoco_lidar.cpp:29-47);
+ * lidar_config: get_lidar_data for sensor `name` of the parsed URDF (reference :52-112):
+ *   out[6] = min_angle, max_angle, angle_increment, range_min, range_max, num_rangefinders;
+ *   topic copied to buf; -1 if a required parameter is missing;
+ * ros_param: value of dotted `key` in a ROS 2 params file as the plugin flattens it (the
+ *   pids_config_file, reference :653-675); -1 if absent. */
+int mrsp_parse_lidar_name(const char* sensor_name, char* buf, int len);
+int mrsp_lidar_config(const mrsp_system* s, const char* name, double* out, char* topic, int len);
+int mrsp_ros_param(const char* params_file, const char* key, char* buf, int len);
+
+/* the plugin's batch (physics of env 0) for direct mrs_batch_* access */
+struct mrs_batch* mrsp_batch(mrsp_system* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

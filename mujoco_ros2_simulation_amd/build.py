@@ -71,6 +71,42 @@ def build_lib(verbose: bool = False) -> Path:
     return LIB
 
 
+PLUGIN_LIB = PKG / "libmrs_plugin.so"
+PLUGIN_SOURCES = ["plugin/src/mujoco_system_interface.cpp", "plugin/src/mujoco_lidar.cpp",
+                  "plugin/src/mujoco_cameras.cpp", "plugin/src/plugin_capi.cc", "mjcf/xml.cc"]
+
+
+def build_plugin(verbose: bool = False) -> Path:
+    """The MujocoSystemInterface plugin host against the ROS API shim (csrc/plugin/ros_shim) and
+    libmrs.so; host C++ only (no device code), linked with rpath $ORIGIN."""
+    lib = build_lib(verbose)
+    inc = [f"-I{CSRC / 'plugin' / 'include'}", f"-I{CSRC / 'plugin' / 'ros_shim'}", f"-I{ROOT / 'include'}"]
+    deps = [p for p in (CSRC / "plugin").rglob("*.hpp")] + [ROOT / "include" / "mrs.h",
+                                                          ROOT / "include" / "mrs_plugin.h", CSRC / "mjcf" / "xml.h"]
+    objs, procs = [], []
+    for rel in PLUGIN_SOURCES:
+        src = CSRC / rel
+        obj = OBJ / ("plugin_" + rel.replace("/", "_") + ".o")
+        objs.append(obj)
+        if _newer(src, obj, deps):
+            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-pthread", *inc, "-c", str(src), "-o", str(obj)]
+            procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    failed = False
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            failed = True
+            sys.stderr.write(out)
+        elif verbose and out:
+            sys.stderr.write(out)
+    if failed:
+        raise RuntimeError("build of libmrs_plugin.so failed")
+    if procs or not PLUGIN_LIB.exists() or PLUGIN_LIB.stat().st_mtime < lib.stat().st_mtime:
+        _run(["g++", "-shared", "-fPIC", "-pthread", "-o", str(PLUGIN_LIB), *[str(o) for o in objs],
+              f"-L{PKG}", "-lmrs", "-Wl,-rpath,$ORIGIN"])
+    return PLUGIN_LIB
+
+
 def build_oracle() -> Path:
     """TEST INFRASTRUCTURE: the fp64 CPU oracle (oracle/Makefile)."""
     _run(["make", "-s", "-C", str(ROOT / "oracle")])
@@ -79,4 +115,5 @@ def build_oracle() -> Path:
 
 if __name__ == "__main__":
     print(build_lib(verbose=True))
+    print(build_plugin(verbose=True))
     print(build_oracle())

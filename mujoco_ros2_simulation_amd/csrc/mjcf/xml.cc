@@ -99,9 +99,9 @@ std::unique_ptr<XmlElement> parse_element(Cursor& c) {
     e->attrs.emplace_back(key, decode_entities(val));
   }
   // content
+  std::string text;
   for (;;) {
-    // text is ignored (MJCF carries no element text the hot path needs)
-    while (!c.eof() && c.peek() != '<') c.get();
+    while (!c.eof() && c.peek() != '<') text += c.get();
     if (c.eof()) c.fail("unterminated element <" + e->tag + ">");
     if (c.starts("<!--")) { c.skip_until("-->"); continue; }
     if (c.starts("<![CDATA[")) { c.skip_until("]]>"); continue; }
@@ -114,6 +114,8 @@ std::unique_ptr<XmlElement> parse_element(Cursor& c) {
       c.ws();
       if (c.peek() != '>') c.fail("expected '>'");
       c.get();
+      const auto b = text.find_first_not_of(" \t\r\n"), t = text.find_last_not_of(" \t\r\n");
+      if (b != std::string::npos) e->text = decode_entities(text.substr(b, t - b + 1));
       return e;
     }
     e->children.push_back(parse_element(c));

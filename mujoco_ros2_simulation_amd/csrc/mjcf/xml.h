@@ -1,7 +1,7 @@
 // Minimal XML DOM for MJCF files (no tinyxml2 in this image; the reference links tinyxml2 for the
 // keyframe override file, src/mujoco_system_interface.cpp:1552-1575, and MuJoCo's own parser reads
 // the MJCF).  Supports elements, attributes, comments, declarations, CDATA-free text and the five
-// predefined entities.  Errors carry a line number.
+// predefined entities.  Element text is kept (URDF <param> values).  Errors carry a line number.
 #pragma once
 
 #include <memory>
@@ -16,6 +16,7 @@ struct XmlElement {
   std::string tag;
   std::vector<std::pair<std::string, std::string>> attrs;
   std::vector<std::unique_ptr<XmlElement>> children;
+  std::string text;  // concatenated character data, whitespace-trimmed, entities decoded
   int line = 0;
 
   const std::string* attr(const std::string& key) const {
@@ -30,7 +31,7 @@ struct XmlElement {
   }
   std::unique_ptr<XmlElement> clone() const {
     auto e = std::make_unique<XmlElement>();
-    e->tag = tag; e->attrs = attrs; e->line = line;
+    e->tag = tag; e->attrs = attrs; e->text = text; e->line = line;
     for (auto& c : children) e->children.push_back(c->clone());
     return e;
   }

@@ -1,0 +1,254 @@
+"""ctypes binding of the plugin host's C entry points (include/mrs_plugin.h).
+
+`System` plays the controller manager around the C++ MujocoSystemInterface: it parses the URDF's
+<ros2_control> block, runs on_init / on_activate, exposes the exported state and command
+interfaces by name, and drives read() / write() cycles.  Physics, lidar and depth all run through
+libmrs.so on the GPU; there is no Python fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("MRS_PLUGIN_LIB", PKG / "libmrs_plugin.so"))
+
+SUCCESS, FAILURE, ERROR = 0, 1, 2
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} not built; run `python -m mujoco_ros2_simulation_amd.build`")
+        L = C.CDLL(str(LIB_PATH))
+        P, S, I, D, F = C.c_void_p, C.c_char_p, C.c_int, C.c_double, C.POINTER(C.c_float)
+        sigs = {
+            "mrsp_last_error": (S, []),
+            "mrsp_load_urdf": (P, [S, S, S]),
+            "mrsp_free": (None, [P]),
+            "mrsp_set_hardware_param": (I, [P, S, S]),
+            "mrsp_get_hardware_param": (I, [P, S, S, I]),
+            "mrsp_num_joints": (I, [P]),
+            "mrsp_num_sensors": (I, [P]),
+            "mrsp_on_init": (I, [P]),
+            "mrsp_on_activate": (I, [P]),
+            "mrsp_num_state_interfaces": (I, [P]),
+            "mrsp_num_command_interfaces": (I, [P]),
+            "mrsp_state_interface_name": (I, [P, I, S, I]),
+            "mrsp_command_interface_name": (I, [P, I, S, I]),
+            "mrsp_get_state": (D, [P, I]),
+            "mrsp_get_command": (D, [P, I]),
+            "mrsp_set_command": (I, [P, I, D]),
+            "mrsp_switch_mode": (I, [P, S, S]),
+            "mrsp_read": (I, [P]),
+            "mrsp_write": (I, [P, D]),
+            "mrsp_step": (I, [P, I]),
+            "mrsp_sim_time": (D, [P]),
+            "mrsp_clock": (D, [P, C.POINTER(C.c_long)]),
+            "mrsp_lidar_update": (I, [P]),
+            "mrsp_last_scan": (I, [P, S, F, I, F]),
+            "mrsp_camera_update": (I, [P]),
+            "mrsp_last_depth": (I, [P, S, F, I, C.POINTER(C.c_int)]),
+            "mrsp_last_camera_info": (I, [P, S, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+            "mrsp_last_image": (I, [P, S, C.POINTER(C.c_int), S, I]),
+            "mrsp_batch": (P, [P]),
+            "mrsp_parse_lidar_name": (I, [S, S, I]),
+            "mrsp_lidar_config": (I, [P, S, C.POINTER(C.c_double), S, I]),
+            "mrsp_ros_param": (I, [S, S, S, I]),
+        }
+        for name, (res, args) in sigs.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class PluginError(RuntimeError):
+    pass
+
+
+def _err() -> str:
+    return lib().mrsp_last_error().decode()
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def parse_lidar_name(name: str) -> tuple[str, int]:
+    buf = C.create_string_buffer(512)
+    idx = lib().mrsp_parse_lidar_name(name.encode(), buf, 512)
+    return buf.value.decode(), idx
+
+
+def ros_param(params_file: str | Path, key: str) -> str | None:
+    buf = C.create_string_buffer(1024)
+    if lib().mrsp_ros_param(str(params_file).encode(), key.encode(), buf, 1024) < 0:
+        return None
+    return buf.value.decode()
+
+
+class System:
+    def __init__(self, urdf: str | Path, xacro_args: dict | None = None, packages: dict | None = None):
+        args = " ".join(f"{k}:={v}" for k, v in (xacro_args or {}).items())
+        pk = ";".join(f"{k}={v}" for k, v in (packages or {}).items())
+        self._h = lib().mrsp_load_urdf(str(urdf).encode(), args.encode(), pk.encode())
+        if not self._h:
+            raise PluginError(_err())
+        self.state_names: list[str] = []
+        self.command_names: list[str] = []
+
+    # -- hardware info
+    def set_param(self, key: str, value) -> None:
+        lib().mrsp_set_hardware_param(self._h, key.encode(), str(value).encode())
+
+    def param(self, key: str) -> str | None:
+        buf = C.create_string_buffer(4096)
+        if lib().mrsp_get_hardware_param(self._h, key.encode(), buf, 4096) < 0:
+            return None
+        return buf.value.decode()
+
+    @property
+    def num_joints(self) -> int:
+        return lib().mrsp_num_joints(self._h)
+
+    @property
+    def num_sensors(self) -> int:
+        return lib().mrsp_num_sensors(self._h)
+
+    def lidar_config(self, name: str) -> dict | None:
+        out = np.zeros(6)
+        buf = C.create_string_buffer(512)
+        if lib().mrsp_lidar_config(self._h, name.encode(), out.ctypes.data_as(C.POINTER(C.c_double)), buf, 512) < 0:
+            return None
+        keys = ["min_angle", "max_angle", "angle_increment", "range_min", "range_max"]
+        d = dict(zip(keys, out[:5].tolist()))
+        d["num_rangefinders"] = int(out[5])
+        d["laserscan_topic"] = buf.value.decode()
+        return d
+
+    # -- lifecycle
+    def on_init(self) -> int:
+        r = lib().mrsp_on_init(self._h)
+        if r < 0:
+            raise PluginError(_err())
+        if r == SUCCESS:
+            buf = C.create_string_buffer(512)
+            self.state_names = []
+            for i in range(lib().mrsp_num_state_interfaces(self._h)):
+                lib().mrsp_state_interface_name(self._h, i, buf, 512)
+                self.state_names.append(buf.value.decode())
+            self.command_names = []
+            for i in range(lib().mrsp_num_command_interfaces(self._h)):
+                lib().mrsp_command_interface_name(self._h, i, buf, 512)
+                self.command_names.append(buf.value.decode())
+        return r
+
+    def on_activate(self) -> int:
+        return lib().mrsp_on_activate(self._h)
+
+    # -- interfaces
+    def state(self, name: str) -> float:
+        return lib().mrsp_get_state(self._h, self.state_names.index(name))
+
+    def command(self, name: str) -> float:
+        return lib().mrsp_get_command(self._h, self.command_names.index(name))
+
+    def set_command(self, name: str, value: float) -> None:
+        if lib().mrsp_set_command(self._h, self.command_names.index(name), float(value)) != 0:
+            raise PluginError(_err())
+
+    def switch_mode(self, start=(), stop=()) -> int:
+        return lib().mrsp_switch_mode(self._h, ";".join(start).encode(), ";".join(stop).encode())
+
+    # -- cycle
+    def read(self) -> int:
+        return lib().mrsp_read(self._h)
+
+    def write(self, period: float) -> int:
+        return lib().mrsp_write(self._h, period)
+
+    def step(self, n: int) -> int:
+        r = lib().mrsp_step(self._h, n)
+        if r < 0:
+            raise PluginError(_err())
+        return r
+
+    def cycle(self, period: float, n_steps: int) -> None:
+        """one controller-manager cycle with a synchronous physics advance: write, step, read"""
+        self.write(period)
+        self.step(n_steps)
+        self.read()
+
+    @property
+    def sim_time(self) -> float:
+        return lib().mrsp_sim_time(self._h)
+
+    def clock(self) -> tuple[float, int]:
+        n = C.c_long(0)
+        t = lib().mrsp_clock(self._h, C.byref(n))
+        return t, n.value
+
+    # -- sensors
+    def lidar_update(self) -> None:
+        lib().mrsp_lidar_update(self._h)
+
+    def last_scan(self, topic: str = "/scan"):
+        meta = np.zeros(7, np.float32)
+        n = lib().mrsp_last_scan(self._h, topic.encode(), None, 0, _fptr(meta))
+        if n < 0:
+            raise PluginError(_err())
+        out = np.zeros(n, np.float32)
+        lib().mrsp_last_scan(self._h, topic.encode(), _fptr(out), n, _fptr(meta))
+        keys = ["angle_min", "angle_max", "angle_increment", "range_min", "range_max", "scan_time", "time_increment"]
+        return out, dict(zip(keys, meta.tolist()))
+
+    def camera_update(self) -> None:
+        lib().mrsp_camera_update(self._h)
+
+    def last_depth(self, topic: str) -> np.ndarray:
+        wh = (C.c_int * 2)()
+        n = lib().mrsp_last_depth(self._h, topic.encode(), None, 0, wh)
+        if n < 0:
+            raise PluginError(_err())
+        out = np.zeros(n, np.float32)
+        lib().mrsp_last_depth(self._h, topic.encode(), _fptr(out), n, wh)
+        return out.reshape(wh[1], wh[0])
+
+    def last_camera_info(self, topic: str):
+        k = np.zeros(9)
+        p = np.zeros(12)
+        wh = (C.c_int * 2)()
+        if lib().mrsp_last_camera_info(self._h, topic.encode(), k.ctypes.data_as(C.POINTER(C.c_double)),
+                                       p.ctypes.data_as(C.POINTER(C.c_double)), wh) < 0:
+            raise PluginError(_err())
+        return k.reshape(3, 3), p.reshape(3, 4), (wh[0], wh[1])
+
+    def last_image(self, topic: str):
+        whs = (C.c_int * 3)()
+        enc = C.create_string_buffer(64)
+        n = lib().mrsp_last_image(self._h, topic.encode(), whs, enc, 64)
+        if n < 0:
+            raise PluginError(_err())
+        return {"width": whs[0], "height": whs[1], "step": whs[2], "encoding": enc.value.decode(), "bytes": n}
+
+    def batch_handle(self):
+        return lib().mrsp_batch(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            lib().mrsp_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -23,6 +23,7 @@ def pytest_configure(config):
 def built():
     from mujoco_ros2_simulation_amd import build
     build.build_lib()
+    build.build_plugin()
     build.build_oracle()
     return True
 
