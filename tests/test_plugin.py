@@ -192,6 +192,7 @@ def emulate(scene, mode, cmd, cycles, steps):
     d.forward()
     pids = [PidRestated(f"pid_gains.{mode.split('_')[0]}.joint{j}") for j in (1, 2)] if mode.endswith("pid") else None
     traj = []
+    emulate.data = d
     for _ in range(cycles):
         if mode == "position":
             d.ctrl[:] = cmd
@@ -286,9 +287,9 @@ def test_override_start_positions(pkg_dir):
 def test_lidar_scan_matches_oracle(pkg_dir, s2_model):
     """LaserScan from the plugin = GPU rangefinders of env 0, filtered to [range_min, range_max]"""
     from mujoco_ros2_simulation_amd import plugin
-    import binding
     s = make_system(pkg_dir, physics_thread="false")
     assert s.on_init() == plugin.SUCCESS
+    s.read()
     s.set_command("joint1/position", 0.8)
     run_cycles(s, 1.0, 10)
     s.lidar_update()
@@ -296,13 +297,11 @@ def test_lidar_scan_matches_oracle(pkg_dir, s2_model):
     assert len(ranges) == 24
     assert meta["angle_min"] == pytest.approx(-0.3) and meta["angle_increment"] == pytest.approx(0.025)
     assert meta["scan_time"] == pytest.approx(1.0)       # 1 / lidar_publish_rate
-    # oracle: rangefinders at the plugin's current state
+    # oracle: the same 50 cycles; sensordata after mj_step belongs to the state before the last
+    # integration, so it is compared with the oracle's own step, not a forward() at the final qpos
     from mujoco_ros2_simulation_amd import sim
-    st = np.array([s.state(f"joint{j}/position") for j in (1, 2)])
-    d = binding.OracleData(s2_model)
-    d.qpos[:] = st
-    d.forward()
-    sens = d.sensordata.copy()
+    emulate(REF_SCENE, "position", [0.8, 0.0], 50, 10)
+    sens = emulate.data.sensordata.copy()
     rf = [i for i in range(s2_model.nsensor) if s2_model.sensor_type[i] == sim.SENS_RANGEFINDER]
     names = [s2_model.id2name(sim.OBJ_SENSOR, i) for i in rf]
     order = sorted(range(len(rf)), key=lambda k: int(names[k].rsplit("-", 1)[1]))
