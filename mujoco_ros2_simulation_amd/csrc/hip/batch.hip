@@ -18,7 +18,7 @@
 namespace mrs {
 
 hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
-                       bool forward_only, hipStream_t stream);
+                       bool forward_only, int group, hipStream_t stream);
 
 namespace {
 
@@ -195,6 +195,7 @@ struct Packer {
 struct BatchImpl {
   const Model* model = nullptr;
   int n = 0, device = 0;
+  int group = 64;  // lanes per environment in the step kernel (64/group envs per wavefront)
   DevModel dm{};
   DevModel* d_dm = nullptr;  // device copy of dm
   LdsLayout& L = dm.L;
@@ -369,6 +370,16 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.sensor_objid, m.sensor_objid); P.addi(&d.sensor_adr, m.sensor_adr); P.addi(&d.sensor_dim, m.sensor_dim);
   P.addf(&d.sensor_cutoff, m.sensor_cutoff);
   P.addi(&d.fric_dof, fric); P.addi(&d.lim_jnt, lim); P.addi(&d.rf_sensor, rf);
+  std::vector<float> rgeom;
+  auto bits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+  for (int g = 0; g < m.ngeom; ++g) {
+    if (m.geom_rgba[4 * g + 3] == 0) continue;
+    rgeom.insert(rgeom.end(), {bits(g), bits(m.geom_type[g]), bits(m.geom_bodyid[g]),
+                               static_cast<float>(m.geom_rbound[g]), static_cast<float>(m.geom_size[3 * g]),
+                               static_cast<float>(m.geom_size[3 * g + 1]), static_cast<float>(m.geom_size[3 * g + 2]), 0.0f});
+  }
+  d.nrgeom = static_cast<int>(rgeom.size() / 8);
+  P.addf(&d.rgeom, rgeom);
 
   b.dblock_f = dalloc(b, P.f.size() * sizeof(float));
   b.dblock_i = dalloc(b, P.i.size() * sizeof(int));
@@ -392,8 +403,19 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
   L.qacc = take(nv); L.qfrc_con = take(nv); L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
   L.total = off;
-  if (static_cast<size_t>(L.total) * sizeof(float) * kEnvsPerBlock > 160 * 1024)
-    throw UnsupportedError("model too large for the per-wave LDS working set");
+  // lanes per environment: the narrowest group that still gives every dof its own lane (the
+  // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
+  // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
+  auto lds_bytes = [&](int g) { return static_cast<size_t>(L.total) * sizeof(float) * kWavesPerBlock * (64 / g); };
+  b.group = 64;
+  for (int g : {32, 16})
+    if (m.nv <= g && lds_bytes(g) <= 80 * 1024) b.group = g;
+  if (const char* e = std::getenv("MRS_GROUP")) {
+    const int g = std::atoi(e);
+    if ((g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
+  }
+  if (lds_bytes(b.group) > 160 * 1024)
+    throw UnsupportedError("model too large for the per-environment LDS working set");
   // --- scratch layout (floats)
   ScratchLayout& S = b.dm.S;
   off = 0;
@@ -401,7 +423,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_J = take(ne * nv); S.efc_MJ = take(ne * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(ne); S.efc_aref = take(ne);
   S.efc_b = take(ne); S.efc_f = take(ne); S.efc_ARii = take(ne); S.con = take(kConRec * std::max(1, d.max_con));
-  S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);
+  S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);  // <= 64 lanes x 4 contacts x 7 floats
+  S.sens = take(std::max(1, m.nsensordata));
   S.total = off;
   b.d_dm = static_cast<DevModel*>(dalloc(b, sizeof(DevModel)));
   HIP_CHECK(hipMemcpyAsync(b.d_dm, &b.dm, sizeof(DevModel), hipMemcpyHostToDevice, b.stream));
@@ -468,7 +491,9 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     b->st.time = static_cast<double*>(dalloc(*b, n * sizeof(double)));
     b->st.warning = static_cast<int*>(dalloc(*b, n * 4 * sizeof(int)));
     b->st.ncon = static_cast<int*>(dalloc(*b, n * sizeof(int)));
-    b->st.scratch = static_cast<float*>(dalloc(*b, n * b->S.total * sizeof(float)));
+    // padded to whole workgroups (16 envs at the narrowest group width): idle groups use it
+    const size_t n_pad = (static_cast<size_t>(n) + 15) / 16 * 16;
+    b->st.scratch = static_cast<float*>(dalloc(*b, n_pad * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));
     b->st.geom_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 9 * sizeof(float)));
     b->st.cam_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ncam) * 3 * sizeof(float)));
@@ -600,7 +625,7 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
-  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->st, b->n, n_steps, forward_only, b->stream));
+  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->st, b->n, n_steps, forward_only, b->group, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
 }

@@ -34,7 +34,7 @@ struct CPtr {
 };
 
 // LDS layout of one environment (offsets in floats).  One wavefront owns one environment; the
-// workgroup holds kEnvsPerBlock environments back to back.
+// workgroup holds 4*64/G environments back to back.
 struct LdsLayout {
   int xpos, xquat, xmat, xipos, xanchor, xaxis, gxpos, gxmat, scom, cinert, crb, cdof, cdofdot,
       cvel, cacc, cfrc, M, L, qpos, qvel, ctrl, qfrc_applied, qacc_ws, qfrc_bias, qfrc_passive,
@@ -46,7 +46,8 @@ struct LdsLayout {
 // region; the region of env e starts at e * total).
 struct ScratchLayout {
   int efc_J, efc_MJ, efc_type, efc_pos, efc_margin, efc_floss, efc_R, efc_aref, efc_b, efc_f,
-      efc_ARii, con, stage;  // contact records (kConRec floats each); per-lane narrow-phase staging
+      efc_ARii, con, stage,  // contact records (kConRec floats each); per-lane narrow-phase staging
+      sens;                  // sensordata sink of idle lane groups (envs past n_envs)
   int total;
 };
 constexpr int kConRec = 16;  // pair id (int bits), dist, pos[3], frame[9], pad[2]
@@ -58,7 +59,7 @@ struct DevModel {
   ScratchLayout S;
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth;
-  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc;
+  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom;
   // options
   int integrator, iterations, disableflags;
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
@@ -92,9 +93,12 @@ struct DevModel {
   CPtr<int> sensor_type, sensor_objtype, sensor_objid, sensor_adr, sensor_dim;
   CPtr<float> sensor_cutoff;
   CPtr<int> fric_dof, lim_jnt, rf_sensor;
+  // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
+  // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
+  CPtr<float> rgeom;
 };
 
-constexpr int kEnvsPerBlock = 4;  // 256-thread workgroups, one wave per environment
+constexpr int kWavesPerBlock = 4;  // 256-thread workgroups; 64/G environments per wavefront
 
 // device state of a batch (all [n_envs][dim], fp32 unless noted)
 struct DevState {

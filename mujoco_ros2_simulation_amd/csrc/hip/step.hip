@@ -38,23 +38,43 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-__device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  total = __shfl(x, 63);
-  return x - v;
-}
 __device__ __forceinline__ float bcast(float v, int src) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+
+// ---- lane groups: G consecutive lanes own one environment (64/G environments per wavefront).
+// Group-local reductions, scans, broadcasts and votes; for G = 64 they are the wave-wide forms.
+template <int G>
+__device__ __forceinline__ float gsum(float v) {
+#pragma unroll
+  for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+template <int G>
+__device__ __forceinline__ int gscan_excl(int v, int glane, int& total) {
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < G; off <<= 1) {
+    int y = __shfl_up(x, off, G);
+    if (glane >= off) x += y;
+  }
+  total = __shfl(x, G - 1, G);
+  return x - v;
+}
+template <int G>
+__device__ __forceinline__ float gbcast(float v, int src) {
+  if constexpr (G == 64) return bcast(v, src);
+  else return __shfl(v, src, G);
+}
+template <int G>
+__device__ __forceinline__ bool gany(bool c) {
+  if constexpr (G == 64) {
+    return __any(c);
+  } else {
+    const unsigned long long b = __ballot(c);
+    const int base = __lane_id() & ~(G - 1);
+    return ((b >> base) & ((1ull << G) - 1)) != 0;
+  }
 }
 
 // ------------------------------------------------------------------ small math (fp32)
@@ -441,6 +461,8 @@ enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 #define ENV_ARGS mp, s, scr, lane
 // Function arguments arrive in VGPRs, so the compiler cannot know they are wave-uniform; the phase
 // prologue re-establishes uniformity with readfirstlane (every phase is entered by the whole wave).
+// With several environments per wave (G < 64) only the model pointer is wave-uniform; the LDS base
+// and scratch pointers of each group stay per-lane.
 template <class T>
 __device__ __forceinline__ T* uniform_ptr(T* p) {
   const unsigned long long v = reinterpret_cast<unsigned long long>(p);
@@ -460,22 +482,27 @@ __device__ __forceinline__ DevModel load_model(const DevModel* mp) {
   return m;
 }
 
-#define ENV_UNPACK                  \
-  mp = uniform_ptr(mp);             \
-  s = uniform_lds(s);               \
-  scr = uniform_ptr(scr);           \
-  lane = __lane_id();               \
+#define ENV_UNPACK                        \
+  mp = uniform_ptr(mp);                   \
+  if constexpr (G == 64) {                \
+    s = uniform_lds(s);                   \
+    scr = uniform_ptr(scr);               \
+  }                                       \
+  lane = __lane_id() & (G - 1);           \
   const DevModel m = load_model(mp); \
   const LdsLayout& L = m.L;         \
   const ScratchLayout& S = m.S;     \
   (void)L; (void)S; (void)scr; (void)lane
 
 // Cholesky of the dense nv x nv matrix A (LDS) into Lf (LDS), column by column; lanes over rows.
+template <int G>
 __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
   mp = uniform_ptr(mp);
-  A = uniform_lds(const_cast<lfloat*>(A));
-  Lf = uniform_lds(Lf);
-  lane = __lane_id();
+  if constexpr (G == 64) {
+    A = uniform_lds(const_cast<lfloat*>(A));
+    Lf = uniform_lds(Lf);
+  }
+  lane = __lane_id() & (G - 1);
   const int nv = load_model(mp).nv;
   #pragma unroll 1
   for (int k = 0; k < nv; ++k) {
@@ -484,7 +511,7 @@ __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat
       t = A[lane * nv + k];
       for (int p = 0; p < k; ++p) t -= Lf[lane * nv + p] * Lf[k * nv + p];
     }
-    float dk = bcast(t, k);
+    float dk = gbcast<G>(t, k);
     float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
     if (lane == k) Lf[k * nv + k] = lkk;
     else if (lane > k && lane < nv) Lf[lane * nv + k] = t / lkk;
@@ -492,20 +519,21 @@ __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat
   }
 }
 // x = A^-1 b with A = Lf Lf'; lane j holds b_j / returns x_j (lanes >= nv return 0)
+template <int G>
 __device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, const lfloat* Lf, float b, int lane) {
   mp = uniform_ptr(mp);
-  Lf = uniform_lds(const_cast<lfloat*>(Lf));
-  lane = __lane_id();
+  if constexpr (G == 64) Lf = uniform_lds(const_cast<lfloat*>(Lf));
+  lane = __lane_id() & (G - 1);
   const int nv = load_model(mp).nv;
   float x = lane < nv ? b : 0.0f;
   #pragma unroll 1
   for (int i = 0; i < nv; ++i) {
-    float xi = bcast(x, i) / Lf[i * nv + i];
+    float xi = gbcast<G>(x, i) / Lf[i * nv + i];
     if (lane == i) x = xi;
     else if (lane > i && lane < nv) x -= Lf[lane * nv + i] * xi;
   }
   for (int i = nv - 1; i >= 0; --i) {
-    float xi = bcast(x, i) / Lf[i * nv + i];
+    float xi = gbcast<G>(x, i) / Lf[i * nv + i];
     if (lane == i) x = xi;
     else if (lane < i) x -= Lf[i * nv + lane] * xi;
   }
@@ -528,6 +556,7 @@ __device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, cons
 }
 
 // mj_kinematics + rotational part of cinert; bodies of one depth level per pass
+template <int G>
 __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   ENV_UNPACK;
   if (lane == 0) {
@@ -541,7 +570,7 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   for (int lev = 1; lev <= m.max_depth; ++lev) {
     const int a0 = m.level_adr[lev], nl = m.level_num[lev];
     #pragma unroll 1
-    for (int k = lane; k < nl; k += 64) {
+    for (int k = lane; k < nl; k += G) {
       const int b = m.level_body[a0 + k];
       const int p = m.body_parentid[b];
       float pos[3], q[4];
@@ -618,7 +647,7 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   }
   // geoms
   #pragma unroll 1
-  for (int g = lane; g < m.ngeom; g += 64) {
+  for (int g = lane; g < m.ngeom; g += G) {
     const int b = m.geom_bodyid[g];
     float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
     float gp[3] = {m.geom_pos[3 * g], m.geom_pos[3 * g + 1], m.geom_pos[3 * g + 2]};
@@ -634,10 +663,11 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
 }
 
 // mj_comPos: subtree coms of tree roots, cinert (parallel-axis part), cdof
+template <int G>
 __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
   ENV_UNPACK;
   #pragma unroll 1
-  for (int b = lane; b < m.nbody; b += 64) {
+  for (int b = lane; b < m.nbody; b += G) {
     if (b != 0 && m.body_parentid[b] != 0) continue;
     float c[3] = {0, 0, 0};
     const int e = m.body_subtree_end[b];
@@ -651,7 +681,7 @@ __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
   }
   wsync();
   #pragma unroll 1
-  for (int b = lane; b < m.nbody; b += 64) {
+  for (int b = lane; b < m.nbody; b += G) {
     lfloat* ci = s + L.cinert + 10 * b;
     if (b == 0) { for (int i = 0; i < 10; ++i) ci[i] = 0; continue; }
     const int rt = m.body_rootid[b];
@@ -667,7 +697,7 @@ __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
     ci[6] = mass * d[0]; ci[7] = mass * d[1]; ci[8] = mass * d[2]; ci[9] = mass;
   }
   #pragma unroll 1
-  for (int j = lane; j < m.njnt; j += 64) {
+  for (int j = lane; j < m.njnt; j += G) {
     const int b = m.jnt_bodyid[j], rt = m.body_rootid[b];
     int dof = m.jnt_dofadr[j];
     float off[3];
@@ -699,11 +729,12 @@ __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
 }
 
 // mj_crb + armature: crb by subtree sums, M by (dof, ancestor-dof) pairs
+template <int G>
 __device__ MRS_PHASE void make_M(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
   #pragma unroll 1
-  for (int b = lane; b < m.nbody; b += 64) {
+  for (int b = lane; b < m.nbody; b += G) {
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (b != 0) {
       const int e = m.body_subtree_end[b];
@@ -714,10 +745,10 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
     for (int i = 0; i < 10; ++i) s[L.crb + 10 * b + i] = acc[i];
   }
   #pragma unroll 1
-  for (int i = lane; i < nv * nv; i += 64) s[L.M + i] = 0;
+  for (int i = lane; i < nv * nv; i += G) s[L.M + i] = 0;
   wsync();
   #pragma unroll 1
-  for (int p = lane; p < m.nMpair; p += 64) {
+  for (int p = lane; p < m.nMpair; p += G) {
     const int i = m.Mpair[2 * p], j = m.Mpair[2 * p + 1];
     float buf[6], cd[6];
     for (int k = 0; k < 6; ++k) cd[k] = s[L.cdof + 6 * i + k];
@@ -732,6 +763,7 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
 }
 
 // mj_comVel: level by level
+template <int G>
 __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
   ENV_UNPACK;
   if (lane < 6) s[L.cvel + lane] = 0;
@@ -739,7 +771,7 @@ __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
   for (int lev = 1; lev <= m.max_depth; ++lev) {
     const int a0 = m.level_adr[lev], nl = m.level_num[lev];
     #pragma unroll 1
-    for (int k = lane; k < nl; k += 64) {
+    for (int k = lane; k < nl; k += G) {
       const int b = m.level_body[a0 + k];
       const int p = m.body_parentid[b];
       float cv[6];
@@ -780,6 +812,7 @@ __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
 }
 
 // mj_rne (no acceleration term): qfrc_bias
+template <int G>
 __device__ MRS_PHASE void rne(ENV_PARAMS) {
   ENV_UNPACK;
   if (lane < 6) {
@@ -792,7 +825,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
   for (int lev = 1; lev <= m.max_depth; ++lev) {
     const int a0 = m.level_adr[lev], nl = m.level_num[lev];
     #pragma unroll 1
-    for (int k = lane; k < nl; k += 64) {
+    for (int k = lane; k < nl; k += G) {
       const int b = m.level_body[a0 + k];
       float ca[6];
       for (int i = 0; i < 6; ++i) ca[i] = s[L.cacc + 6 * m.body_parentid[b] + i];
@@ -814,7 +847,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
   }
   // subtree sums of body forces into crb storage (crb no longer needed)
   #pragma unroll 1
-  for (int b = lane; b < m.nbody; b += 64) {
+  for (int b = lane; b < m.nbody; b += G) {
     float acc[6] = {0, 0, 0, 0, 0, 0};
     if (b != 0) {
       const int e = m.body_subtree_end[b];
@@ -826,7 +859,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
   }
   wsync();
   #pragma unroll 1
-  for (int j = lane; j < m.nv; j += 64) {
+  for (int j = lane; j < m.nv; j += G) {
     const int b = m.dof_bodyid[j];
     float v = 0;
     for (int i = 0; i < 6; ++i) v += s[L.cdof + 6 * j + i] * s[L.crb + 6 * b + i];
@@ -847,12 +880,13 @@ __device__ __forceinline__ void jac_col(const DevModel& m, const lfloat* s, int 
 }
 
 // mj_passive + mj_fwdActuation + qfrc_smooth + qacc_smooth (lane per dof)
+template <int G>
 __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
   // actuator forces (lane per actuator)
   #pragma unroll 1
-  for (int a = lane; a < m.nu; a += 64) {
+  for (int a = lane; a < m.nu; a += G) {
     float force = 0;
     if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
       const float gear = m.act_gear[a];
@@ -905,19 +939,20 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
     qfs = pas - s[L.qfrc_bias + j] + s[L.qfrc_applied + j] + qa;
     s[L.qfrc_smooth + j] = qfs;
   }
-  float qacc_s = chol_solve_lanes(mp, s + L.L, qfs, lane);
+  float qacc_s = chol_solve_lanes<G>(mp, s + L.L, qfs, lane);
   if (lane < nv) s[L.qacc_smooth + lane] = qacc_s;
   wsync();
   return qacc_s;
 }
 
 // mj_collision: candidate pairs (lane per pair), bounding-sphere test, narrow phase, compaction
+template <int G>
 __device__ MRS_PHASE int collision(ENV_PARAMS) {
   ENV_UNPACK;
   int ncon = 0;
   if ((m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) || m.npair == 0) return 0;
   #pragma unroll 1
-  for (int base = 0; base < m.npair; base += 64) {
+  for (int base = 0; base < m.npair; base += G) {
     const int p = base + lane;
     Con* c = reinterpret_cast<Con*>(scr + S.stage) + 4 * lane;  // per-lane staging in global scratch
     int n = 0;
@@ -941,7 +976,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
       }
     }
     int total;
-    int off = wave_scan_excl(n, lane, total);
+    int off = gscan_excl<G>(n, lane, total);
     #pragma unroll 1
     for (int k = 0; k < n; ++k) {
       const int slot = ncon + off + k;
@@ -962,9 +997,10 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
 }
 
 // mj_makeConstraint + mj_makeImpedance + PGS (matrix-free rows) -> qacc, qfrc_constraint
+template <int G>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
-  ncon = uniform_int(ncon);
+  if constexpr (G == 64) ncon = uniform_int(ncon);
   const int nv = m.nv;
   float* J = scr + S.efc_J;
   float* MJ = scr + S.efc_MJ;
@@ -997,7 +1033,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   // --- joint limit rows (lane per limited joint, compacted)
   if (!(m.disableflags & MRS_DSBL_LIMIT)) {
     #pragma unroll 1
-    for (int base = 0; base < m.nlim; base += 64) {
+    for (int base = 0; base < m.nlim; base += G) {
       const int k = base + lane;
       int cnt = 0;
       float dist[2] = {0, 0};
@@ -1013,7 +1049,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
         cnt = (int)act[0] + (int)act[1];
       }
       int total;
-      int off = wave_scan_excl(cnt, lane, total);
+      int off = gscan_excl<G>(cnt, lane, total);
       int r = nefc + off;
       for (int sd = 0; sd < 2; ++sd) {
         if (!act[sd]) continue;
@@ -1087,7 +1123,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   }
   // --- impedance, R, aref, M^-1 J', ARii, b (lane per row)
   #pragma unroll 1
-  for (int r = lane; r < nefc; r += 64) {
+  for (int r = lane; r < nefc; r += G) {
     const int code = __float_as_int(type[r]);
     const int t = code >> 16, id = code & 0xffff;
     CPtr<float> sr, si;
@@ -1146,7 +1182,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   {
     bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
     #pragma unroll 1
-    for (int r = lane; r < nefc; r += 64) {
+    for (int r = lane; r < nefc; r += G) {
       float f = 0;
       if (warm) {
         const float* Jr = J + r * nv;
@@ -1174,12 +1210,12 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       float cost = 0;
       #pragma unroll 1
       for (int r = 0; r < nefc; ++r) {
-        const float jv = wave_sum(lane < nv ? J[r * nv + lane] * v : 0.0f);
+        const float jv = gsum<G>(lane < nv ? J[r * nv + lane] * v : 0.0f);
         cost += ff[r] * (0.5f * (jv + Rr[r] * ff[r]) + bb[r]);
       }
       if (cost > 0) {
         #pragma unroll 1
-        for (int r = lane; r < nefc; r += 64) ff[r] = 0;
+        for (int r = lane; r < nefc; r += G) ff[r] = 0;
       } else {
         qa += v;
       }
@@ -1192,7 +1228,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     float improvement = 0;
     #pragma unroll 1
     for (int r = 0; r < nefc; ++r) {
-      const float jq = wave_sum(lane < nv ? J[r * nv + lane] * qa : 0.0f);
+      const float jq = gsum<G>(lane < nv ? J[r * nv + lane] * qa : 0.0f);
       const float f0 = ff[r];
       const float res = jq - aref[r] + Rr[r] * f0;
       const float a = ARii[r];
@@ -1221,57 +1257,95 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   return qa;
 }
 
-// mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel
-__device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
-  ENV_UNPACK;
-  sensordata = uniform_ptr(sensordata);
-  if (m.disableflags & MRS_DSBL_SENSOR) return;
-  #pragma unroll 1
-  for (int k = lane; k < m.nrf; k += 64) {
-    const int sid = m.rf_sensor[k];
+// rays per lane per pass over the geoms: 4 with lane groups (measured C3: 1.59 ms per launch vs
+// 1.98 at 1, 1.71 at 2), 2 at one env per wave (64-VGPR budget: 2.15 ms vs 2.38 at 1, 2.95 at 4)
+template <int G>
+struct RayBatch { static constexpr int value = G == 64 ? 2 : 4; };
+
+// R rangefinders per lane in one pass over the geoms (mj_ray per sensor: nearest hit along the
+// site's +z over all visible geoms not on the site's body).  Each geom's pose is read from LDS once
+// for the R rays, and the R independent rays give the scheduler parallel work.  Rays k0 + j*stride.
+template <int R>
+__device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, float* sd, int k0, int stride) {
+  const LdsLayout& L = m.L;
+  float pnt[R][3], vec[R][3], dist[R];
+  int bod[R], adr[R];
+  bool act[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int k = k0 + j * stride;
+    act[j] = k < m.nrf;
+    const int sid = m.rf_sensor[act[j] ? k : 0];
     const int site = m.sensor_objid[sid];
     const int b = m.site_bodyid[site];
-    float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+    bod[j] = b;
+    adr[j] = m.sensor_adr[sid];
+    float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
     float sp[3] = {m.site_pos[3 * site], m.site_pos[3 * site + 1], m.site_pos[3 * site + 2]};
     float sq[4] = {m.site_quat[4 * site], m.site_quat[4 * site + 1], m.site_quat[4 * site + 2], m.site_quat[4 * site + 3]};
-    float r[3], q[4], sm[9], pnt[3];
+    float r[3], q[4], sm[9];
     rot_quat(r, sp, bq);
-    for (int i = 0; i < 3; ++i) pnt[i] = s[L.xpos + 3 * b + i] + r[i];
+    for (int i = 0; i < 3; ++i) pnt[j][i] = se[L.xpos + 3 * b + i] + r[i];
     quat_mul(q, bq, sq);
     quat2mat(sm, q);
-    const float vec[3] = {sm[2], sm[5], sm[8]};
-    float dist = -1;
-    const float vv = dot3(vec, vec);
-    #pragma unroll 1
-    for (int g = 0; g < m.ngeom; ++g) {
-      if (m.geom_rgba[4 * g + 3] == 0) continue;
-      const int type = m.geom_type[g];
-      const lfloat* gp = s + L.gxpos + 3 * g;
-      float dv[3] = {pnt[0] - gp[0], pnt[1] - gp[1], pnt[2] - gp[2]};
-      bool cand = m.geom_bodyid[g] != b;
-      if (type != MRS_GEOM_PLANE) {
-        // bounding-sphere cull (conservative): closest approach of the ray line to the geom centre,
-        // and no chance of beating the current nearest hit; the primitive test runs only if some
-        // lane of the wave still needs it
-        const float rb = m.geom_rbound[g] * 1.0001f + 1e-6f;
-        const float tp = -dot3(dv, vec);  // projection (times |vec|^2) of the centre on the ray
-        const float d2 = dot3(dv, dv) - tp * tp / vv;
-        cand = cand && d2 <= rb * rb && tp >= -rb * sqrtf(vv) &&
-               (dist < 0 || tp - rb * sqrtf(vv) <= dist * vv);
-      }
-      if (!__any(cand)) continue;
-      if (!cand) continue;
-      const lfloat* gm = s + L.gxmat + 9 * g;
-      float lp[3], lv[3];
-      matT_vec(lp, gm, dv);
-      matT_vec(lv, gm, vec);
-      const float t = ray_geom_local(type, m.geom_size + 3 * g, lp, lv);
-      if (t >= 0 && (dist < 0 || t < dist)) dist = t;
-    }
-    sensordata[m.sensor_adr[sid]] = dist;
+    vec[j][0] = sm[2]; vec[j][1] = sm[5]; vec[j][2] = sm[8];
+    dist[j] = -1;
   }
   #pragma unroll 1
-  for (int sid = lane; sid < m.nsensor; sid += 64) {
+  for (int i = 0; i < m.nrgeom; ++i) {
+    const CPtr<float> rec = m.rgeom + 8 * i;
+    const int g = __float_as_int(rec[0]), type = __float_as_int(rec[1]), gb = __float_as_int(rec[2]);
+    const float rb = rec[3] * 1.0001f + 1e-6f;
+    const float gp[3] = {se[L.gxpos + 3 * g], se[L.gxpos + 3 * g + 1], se[L.gxpos + 3 * g + 2]};
+    // bounding-sphere cull (conservative, branch-free): closest approach of the ray line to the
+    // geom centre within rb, centre not behind the origin by more than rb, and no chance of beating
+    // the current nearest hit; ray directions are unit (rotation-matrix columns)
+    unsigned cmask = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const float dv[3] = {pnt[j][0] - gp[0], pnt[j][1] - gp[1], pnt[j][2] - gp[2]};
+      const float tp = -dot3(dv, vec[j]);
+      const float d2 = dot3(dv, dv) - tp * tp;
+      const bool near = (d2 <= rb * rb) & (tp >= -rb) & ((dist[j] < 0) | (tp - rb <= dist[j]));
+      const bool c = act[j] & (gb != bod[j]) & ((type == MRS_GEOM_PLANE) | near);
+      cmask |= static_cast<unsigned>(c) << j;
+    }
+    if (!__any(cmask != 0)) continue;
+    float gm[9];
+    for (int k = 0; k < 9; ++k) gm[k] = se[L.gxmat + 9 * g + k];
+    const CPtr<float> gs = rec + 4;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (!((cmask >> j) & 1)) continue;
+      const float dv[3] = {pnt[j][0] - gp[0], pnt[j][1] - gp[1], pnt[j][2] - gp[2]};
+      float lp[3], lv[3];
+      matT_vec(lp, gm, dv);
+      matT_vec(lv, gm, vec[j]);
+      const float t = ray_geom_local(type, gs, lp, lv);
+      if (t >= 0 && (dist[j] < 0 || t < dist[j])) dist[j] = t;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+    if (act[j]) sd[adr[j]] = dist[j];
+}
+
+// mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel within the group,
+// RayBatch<G> rays per lane per pass
+template <int G>
+__device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
+  ENV_UNPACK;
+  if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
+  if (m.disableflags & MRS_DSBL_SENSOR) return;
+#ifdef MRS_RAY_BATCH
+  constexpr int R = MRS_RAY_BATCH;
+#else
+  constexpr int R = RayBatch<G>::value;
+#endif
+  #pragma unroll 1
+  for (int k0 = lane; k0 < m.nrf; k0 += G * R) rangefinders<R>(m, s, sensordata, k0, G);
+  #pragma unroll 1
+  for (int sid = lane; sid < m.nsensor; sid += G) {
     const int t = m.sensor_type[sid], id = m.sensor_objid[sid];
     float* out = sensordata + m.sensor_adr[sid];
     float cutoff = m.sensor_cutoff[sid];
@@ -1325,45 +1399,49 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
 }
 
 // reset one env (mj_resetData; held inputs ctrl/qfrc_applied are re-applied by the caller's loop)
+template <int G>
 __device__ MRS_PHASE void reset_env(ENV_PARAMS) {
   ENV_UNPACK;
   #pragma unroll 1
-  for (int i = lane; i < m.nq; i += 64) s[L.qpos + i] = m.qpos0[i];
+  for (int i = lane; i < m.nq; i += G) s[L.qpos + i] = m.qpos0[i];
   #pragma unroll 1
-  for (int i = lane; i < m.nv; i += 64) { s[L.qvel + i] = 0; s[L.qacc_ws + i] = 0; }
+  for (int i = lane; i < m.nv; i += G) { s[L.qvel + i] = 0; s[L.qacc_ws + i] = 0; }
   wsync();
 }
 
+template <int G>
 __device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
   ENV_UNPACK;
   off = uniform_int(off);
   n = uniform_int(n);
   bool bad = false;
   #pragma unroll 1
-  for (int i = lane; i < n; i += 64) bad |= is_bad(s[off + i]);
-  return __any(bad);
+  for (int i = lane; i < n; i += G) bad |= is_bad(s[off + i]);
+  return gany<G>(bad);
 }
 
 // full forward pass; returns qacc (lane per dof)
+template <int G>
 __device__ MRS_PHASE int forward(ENV_PARAMS, float* sensordata) {
   ENV_UNPACK;
-  sensordata = uniform_ptr(sensordata);
-  kinematics(ENV_ARGS);
-  com_pos(ENV_ARGS);
-  make_M(ENV_ARGS);
-  cholesky(mp, s + L.M, s + L.L, lane);
-  com_vel(ENV_ARGS);
-  rne(ENV_ARGS);
-  const float qacc_s = smooth_forces(ENV_ARGS);
-  const int ncon = (m.diag_skip & 2) ? 0 : collision(ENV_ARGS);
-  const float qacc = (m.diag_skip & 4) ? qacc_s : constraints(ENV_ARGS, ncon, qacc_s);
-  if (!(m.diag_skip & 1)) sensors(ENV_ARGS, sensordata);
+  if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
+  kinematics<G>(ENV_ARGS);
+  com_pos<G>(ENV_ARGS);
+  make_M<G>(ENV_ARGS);
+  cholesky<G>(mp, s + L.M, s + L.L, lane);
+  com_vel<G>(ENV_ARGS);
+  rne<G>(ENV_ARGS);
+  const float qacc_s = smooth_forces<G>(ENV_ARGS);
+  const int ncon = (m.diag_skip & 2) ? 0 : collision<G>(ENV_ARGS);
+  const float qacc = (m.diag_skip & 4) ? qacc_s : constraints<G>(ENV_ARGS, ncon, qacc_s);
+  if (!(m.diag_skip & 1)) sensors<G>(ENV_ARGS, sensordata);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
   return ncon;
 }
 
 // mj_Euler / mj_implicit(implicitfast) + mj_advance
+template <int G>
 __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
@@ -1394,15 +1472,15 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
         }
     }
   }
-  need_solve = m.integrator != MRS_INT_EULER || __any(dg != 0);
+  need_solve = m.integrator != MRS_INT_EULER || gany<G>(dg != 0);
   float qacc_int = qacc;
   if (need_solve) {
     // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
     if (lane < nv) s[L.M + lane * nv + lane] += h * dg;
     wsync();
-    cholesky(mp, s + L.M, s + L.L, lane);
+    cholesky<G>(mp, s + L.M, s + L.L, lane);
     float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
-    qacc_int = chol_solve_lanes(mp, s + L.L, rhs, lane);
+    qacc_int = chol_solve_lanes<G>(mp, s + L.L, rhs, lane);
   }
   if (lane < nv) {
     s[L.qacc_ws + lane] = qacc;
@@ -1410,7 +1488,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   }
   wsync();
   #pragma unroll 1
-  for (int j = lane; j < m.njnt; j += 64) {
+  for (int j = lane; j < m.njnt; j += G) {
     int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
     const int jt = m.jnt_type[j];
     if (jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) {
@@ -1433,68 +1511,78 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   wsync();
 }
 
-#ifndef MRS_MIN_WAVES_PER_EU
-#define MRS_MIN_WAVES_PER_EU 8
-#endif
+// waves per SIMD the register budget is sized for: 8 waves at one env per wave (64 VGPRs); with
+// G < 64 the LDS of 4*64/G envs per workgroup bounds residency instead (e.g. G = 16: 16 envs x 4.5 KB
+// per workgroup -> 2 workgroups per CU -> 2 waves per SIMD, 256 VGPRs)
+template <int G>
+struct Occupancy { static constexpr int waves = G == 64 ? 8 : (G == 32 ? 4 : 2); };
 
-template <bool kForwardOnly>
-__global__ __launch_bounds__(64 * kEnvsPerBlock, MRS_MIN_WAVES_PER_EU) void step_kernel(const DevModel* __restrict__ mp, DevState st,
-                                                                  int n_envs, int n_steps) {
+template <int G, bool kForwardOnly>
+__global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step_kernel(
+    const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int kEnvsPerBlock = kWavesPerBlock * 64 / G;
   const DevModel& m = *mp;
   const LdsLayout& L = m.L;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int env = blockIdx.x * kEnvsPerBlock + wid;
-  if (env >= n_envs) return;
-  lfloat* s = (lfloat*)(smem + wid * L.total);
+  const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
+  const int env = blockIdx.x * kEnvsPerBlock + slot;
+  // groups past n_envs stay alive (the wave-cooperative ray phase needs every lane) and mirror the
+  // last env with their own scratch (allocated for the padded count); they write nothing back
+  const bool valid = env < n_envs;
+  lfloat* s = (lfloat*)(smem + slot * L.total);
   float* scr = st.scratch + (size_t)env * m.S.total;
-  const size_t e = (size_t)env;
+  const size_t e = (size_t)(valid ? env : n_envs - 1);
   #pragma unroll 1
-  for (int i = lane; i < m.nq; i += 64) s[L.qpos + i] = st.qpos[e * m.nq + i];
+  for (int i = lane; i < m.nq; i += G) s[L.qpos + i] = st.qpos[e * m.nq + i];
   #pragma unroll 1
-  for (int i = lane; i < m.nv; i += 64) {
+  for (int i = lane; i < m.nv; i += G) {
     s[L.qvel + i] = st.qvel[e * m.nv + i];
     s[L.qfrc_applied + i] = st.qfrc_applied[e * m.nv + i];
     s[L.qacc_ws + i] = st.qacc_ws[e * m.nv + i];
   }
   #pragma unroll 1
-  for (int i = lane; i < m.nu; i += 64) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
+  for (int i = lane; i < m.nu; i += G) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
   double time = st.time[e];
-  float* sensordata = st.sensordata + e * m.nsensordata;
+  float* sensordata = valid ? st.sensordata + e * m.nsensordata : scr + m.S.sens;
   wsync();
   int ncon = 0;
   int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
   for (int step = 0; step < n_steps; ++step) {
     if (!kForwardOnly) {
-      if (any_bad(ENV_ARGS, L.qpos, m.nq)) {
+      if (any_bad<G>(ENV_ARGS, L.qpos, m.nq)) {
         ++w_pos;
-        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env(ENV_ARGS); time = 0; }
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env<G>(ENV_ARGS); time = 0; }
       }
-      if (any_bad(ENV_ARGS, L.qvel, m.nv)) {
+      if (any_bad<G>(ENV_ARGS, L.qvel, m.nv)) {
         ++w_vel;
-        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env(ENV_ARGS); time = 0; }
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env<G>(ENV_ARGS); time = 0; }
       }
     }
-    ncon = forward(ENV_ARGS, sensordata);
+    ncon = forward<G>(ENV_ARGS, sensordata);
     if (kForwardOnly) break;
-    if (any_bad(ENV_ARGS, L.qacc, m.nv)) {
+    bool redo = false;
+    if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
       ++w_acc;
       if (!(m.disableflags & MRS_DSBL_AUTORESET)) {
-        reset_env(ENV_ARGS);
+        reset_env<G>(ENV_ARGS);
         time = 0;
-        ncon = forward(ENV_ARGS, sensordata);
+        redo = true;
       }
     }
-    integrate(ENV_ARGS);
+    // forward() is entered by the whole wave; for envs that were not reset it recomputes the
+    // same outputs from the same state
+    if (__any(redo)) ncon = forward<G>(ENV_ARGS, sensordata);
+    integrate<G>(ENV_ARGS);
     time += m.timestep_d;
   }
+  if (!valid) return;
   // kinematics of the last forward pass (what mjv_updateScene would render after mj_step)
   #pragma unroll 1
-  for (int i = lane; i < 3 * m.ngeom; i += 64) st.geom_xpos[e * 3 * m.ngeom + i] = s[L.gxpos + i];
+  for (int i = lane; i < 3 * m.ngeom; i += G) st.geom_xpos[e * 3 * m.ngeom + i] = s[L.gxpos + i];
   #pragma unroll 1
-  for (int i = lane; i < 9 * m.ngeom; i += 64) st.geom_xmat[e * 9 * m.ngeom + i] = s[L.gxmat + i];
+  for (int i = lane; i < 9 * m.ngeom; i += G) st.geom_xmat[e * 9 * m.ngeom + i] = s[L.gxmat + i];
   #pragma unroll 1
-  for (int c = lane; c < m.ncam; c += 64) {
+  for (int c = lane; c < m.ncam; c += G) {
     const int b = m.cam_bodyid[c];
     float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
     float cp[3] = {m.cam_pos[3 * c], m.cam_pos[3 * c + 1], m.cam_pos[3 * c + 2]};
@@ -1507,9 +1595,9 @@ __global__ __launch_bounds__(64 * kEnvsPerBlock, MRS_MIN_WAVES_PER_EU) void step
     for (int i = 0; i < 9; ++i) st.cam_xmat[(e * m.ncam + c) * 9 + i] = cm[i];
   }
   #pragma unroll 1
-  for (int i = lane; i < m.nq; i += 64) st.qpos[e * m.nq + i] = s[L.qpos + i];
+  for (int i = lane; i < m.nq; i += G) st.qpos[e * m.nq + i] = s[L.qpos + i];
   #pragma unroll 1
-  for (int i = lane; i < m.nv; i += 64) {
+  for (int i = lane; i < m.nv; i += G) {
     st.qvel[e * m.nv + i] = s[L.qvel + i];
     st.qacc_ws[e * m.nv + i] = s[L.qacc_ws + i];
     st.qacc[e * m.nv + i] = s[L.qacc + i];
@@ -1529,15 +1617,27 @@ __global__ __launch_bounds__(64 * kEnvsPerBlock, MRS_MIN_WAVES_PER_EU) void step
 
 }  // namespace
 
-hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
-                       bool forward_only, hipStream_t stream) {
+template <int G>
+static void launch_g(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
+                     bool forward_only, hipStream_t stream) {
+  constexpr int kEnvsPerBlock = kWavesPerBlock * 64 / G;
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * (size_t)lds_floats * kEnvsPerBlock;
   if (forward_only)
-    hipLaunchKernelGGL(step_kernel<true>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, d_model, st, n_envs, 1);
+    hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * kWavesPerBlock), lds, stream, d_model, st, n_envs, 1);
   else
-    hipLaunchKernelGGL(step_kernel<false>, dim3(blocks), dim3(64 * kEnvsPerBlock), lds, stream, d_model, st, n_envs,
+    hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * kWavesPerBlock), lds, stream, d_model, st, n_envs,
                        n_steps);
+}
+
+hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
+                       bool forward_only, int group, hipStream_t stream) {
+  switch (group) {
+    case 16: launch_g<16>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 32: launch_g<32>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 64: launch_g<64>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
