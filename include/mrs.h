@@ -113,6 +113,11 @@ int mrs_batch_sync(mrs_batch* b);
 /* duration in ms of the last step / render kernel measured with HIP events on the batch stream
  * (kind 0 = step, 1 = depth), -1 if unavailable */
 double mrs_batch_last_kernel_ms(mrs_batch* b, int kind);
+/* diagnostics (no reference counterpart): per-phase wave-cycle totals of the step kernel since the
+ * last reset, in phase order kinematics, com_pos, make_M, cholesky, com_vel, rne, smooth_forces,
+ * collision, constraints, sensors, integrate, checks.  Only a library built with
+ * -DMRS_PHASE_TIMING records them; returns the number of phases written (0 otherwise, <0 on error). */
+int mrs_debug_phase_cycles(double* out, int n, int reset);
 
 #ifdef __cplusplus
 }

@@ -217,4 +217,9 @@ double mrs_batch_last_kernel_ms(mrs_batch* b, int kind) {
   return ms;
 }
 
+int mrs_debug_phase_cycles(double* out, int n, int reset) {
+  if (!out || n < 0) return MRS_ERR_INVALID;
+  return mrs::phase_cycles(out, n, reset != 0);
+}
+
 }  // extern "C"

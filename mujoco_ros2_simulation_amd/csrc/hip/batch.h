@@ -25,5 +25,6 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only);
 void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out);
 void batch_sync(BatchImpl* b);
 double batch_last_kernel_ms(BatchImpl* b, int kind);
+int phase_cycles(double* out, int n, bool reset);  // step.hip; profiling builds only
 
 }  // namespace mrs

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <array>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -380,6 +382,64 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.nrgeom = static_cast<int>(rgeom.size() / 8);
   P.addf(&d.rgeom, rgeom);
+  // ray blocks (kRayBlock consecutive rangefinders) for the level-1 cone cull: when every ray of a
+  // block starts at the same point of the same body, the block is bounded by a cone (origin, unit
+  // axis, half-angle) fixed in that body's frame; blocks that are not are flagged and test every geom
+  std::vector<float> rfblk;
+  d.nrfblk = 0;
+  if (d.nrgeom <= 32 && d.nrf > 0) {
+    d.nrfblk = (d.nrf + kRayBlock - 1) / kRayBlock;
+    for (int blk = 0; blk < d.nrfblk; ++blk) {
+      const int k0 = blk * kRayBlock, k1 = std::min(d.nrf, k0 + kRayBlock);
+      const int site0 = m.sensor_objid[rf[k0]], body = m.site_bodyid[site0];
+      bool ok = true;
+      double axis[3] = {0, 0, 0};
+      std::vector<std::array<double, 3>> dirs;
+      for (int k = k0; k < k1; ++k) {
+        const int site = m.sensor_objid[rf[k]];
+        if (m.site_bodyid[site] != body) ok = false;
+        for (int i = 0; i < 3; ++i)
+          if (std::abs(m.site_pos[3 * site + i] - m.site_pos[3 * site0 + i]) > 1e-9) ok = false;
+        const double* q = &m.site_quat[4 * site];  // z column of the site rotation (ray direction)
+        std::array<double, 3> dz = {2 * (q[1] * q[3] + q[0] * q[2]), 2 * (q[2] * q[3] - q[0] * q[1]),
+                                    q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3]};
+        const double n = std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]);
+        for (int i = 0; i < 3; ++i) { dz[i] /= n; axis[i] += dz[i]; }
+        dirs.push_back(dz);
+      }
+      const double an = std::sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+      double theta = 0;
+      if (an < 1e-6) ok = false;
+      else {
+        for (int i = 0; i < 3; ++i) axis[i] /= an;
+        for (auto& dz : dirs) {
+          const double c = dz[0] * axis[0] + dz[1] * axis[1] + dz[2] * axis[2];
+          theta = std::max(theta, std::acos(std::max(-1.0, std::min(1.0, c))));
+        }
+        if (theta > 1.4) ok = false;  // too wide for the cone bound to pay
+      }
+      rfblk.insert(rfblk.end(), {bits(body), bits(ok ? 1 : 0), static_cast<float>(m.site_pos[3 * site0]),
+                                 static_cast<float>(m.site_pos[3 * site0 + 1]), static_cast<float>(m.site_pos[3 * site0 + 2]),
+                                 static_cast<float>(axis[0]), static_cast<float>(axis[1]), static_cast<float>(axis[2]),
+                                 static_cast<float>(theta + 1e-4), 0.0f, 0.0f, 0.0f});
+    }
+  }
+  P.addf(&d.rfblk, rfblk);
+  // per-ray records: body, sensordata address (int bits), origin and unit direction in the body
+  // frame (site pos, z column of the site rotation)
+  std::vector<float> rfray;
+  for (int k = 0; k < d.nrf; ++k) {
+    const int site = m.sensor_objid[rf[k]];
+    const double* q = &m.site_quat[4 * site];
+    double dz[3] = {2 * (q[1] * q[3] + q[0] * q[2]), 2 * (q[2] * q[3] - q[0] * q[1]),
+                    q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3]};
+    const double n = std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]);
+    rfray.insert(rfray.end(), {bits(m.site_bodyid[site]), bits(m.sensor_adr[rf[k]]),
+                               static_cast<float>(m.site_pos[3 * site]), static_cast<float>(m.site_pos[3 * site + 1]),
+                               static_cast<float>(m.site_pos[3 * site + 2]), static_cast<float>(dz[0] / n),
+                               static_cast<float>(dz[1] / n), static_cast<float>(dz[2] / n)});
+  }
+  P.addf(&d.rfray, rfray);
 
   b.dblock_f = dalloc(b, P.f.size() * sizeof(float));
   b.dblock_i = dalloc(b, P.i.size() * sizeof(int));
@@ -402,6 +462,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);
   L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
   L.qacc = take(nv); L.qfrc_con = take(nv); L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
+  L.rfmask = take(std::max(1, d.nrfblk));
   L.total = off;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB

@@ -38,7 +38,8 @@ struct CPtr {
 struct LdsLayout {
   int xpos, xquat, xmat, xipos, xanchor, xaxis, gxpos, gxmat, scom, cinert, crb, cdof, cdofdot,
       cvel, cacc, cfrc, M, L, qpos, qvel, ctrl, qfrc_applied, qacc_ws, qfrc_bias, qfrc_passive,
-      qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force, Dg;
+      qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force, Dg,
+      rfmask;  // per ray block: bitmask of candidate ray geoms (int bits)
   int total;  // floats per env (multiple of 4)
 };
 
@@ -59,7 +60,7 @@ struct DevModel {
   ScratchLayout S;
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth;
-  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom;
+  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk;
   // options
   int integrator, iterations, disableflags;
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
@@ -96,7 +97,14 @@ struct DevModel {
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;
+  // ray blocks of kRayBlock consecutive rangefinders, 12 floats each: body, cone flag (int bits),
+  // origin[3] and unit axis[3] in the body frame, half-angle
+  CPtr<float> rfblk;
+  // per rangefinder, 8 floats: body, sensordata address (int bits), origin[3] and unit
+  // direction[3] in the body frame
+  CPtr<float> rfray;
 };
+constexpr int kRayBlock = 64;
 
 constexpr int kWavesPerBlock = 4;  // 256-thread workgroups; 64/G environments per wavefront
 

@@ -44,10 +44,24 @@ __device__ __forceinline__ float bcast(float v, int src) {
 
 // ---- lane groups: G consecutive lanes own one environment (64/G environments per wavefront).
 // Group-local reductions, scans, broadcasts and votes; for G = 64 they are the wave-wide forms.
+// DPP move within rows of 16 lanes (no LDS traffic, unlike ds_bpermute-based shuffles)
+template <int kCtrl>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xf, 0xf, false));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // lane i <-> 7-i within each 8
+constexpr int kDppMirror = 0x140;     // lane i <-> 15-i within each 16
 template <int G>
 __device__ __forceinline__ float gsum(float v) {
-#pragma unroll
-  for (int off = G / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  // full sum of each row of 16 in every lane of the row: quads, then halves, then rows
+  v += dpp<kDppXor1>(v);
+  v += dpp<kDppXor2>(v);
+  v += dpp<kDppHalfMirror>(v);
+  v += dpp<kDppMirror>(v);
+  if constexpr (G >= 32) v += __shfl_xor(v, 16);
+  if constexpr (G == 64) v += __shfl_xor(v, 32);
   return v;
 }
 template <int G>
@@ -61,10 +75,23 @@ __device__ __forceinline__ int gscan_excl(int v, int glane, int& total) {
   total = __shfl(x, G - 1, G);
   return x - v;
 }
+// value of lane `src` of the caller's group, in every lane of the group: one readlane per group and
+// a per-lane select (readlane reads a lane's register whatever the exec mask, and each group only
+// selects its own group's value)
 template <int G>
 __device__ __forceinline__ float gbcast(float v, int src) {
-  if constexpr (G == 64) return bcast(v, src);
-  else return __shfl(v, src, G);
+  if constexpr (G == 64) {
+    return bcast(v, src);
+  } else {
+    const int grp = __lane_id() / G;
+    float r = bcast(v, src);
+#pragma unroll
+    for (int i = 1; i < 64 / G; ++i) {
+      const float ri = bcast(v, src + i * G);
+      r = grp == i ? ri : r;
+    }
+    return r;
+  }
 }
 template <int G>
 __device__ __forceinline__ bool gany(bool c) {
@@ -452,6 +479,28 @@ __device__ __forceinline__ float impedance(const PS si, float pos, float margin)
 }
 
 enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
+
+// Per-phase cycle accounting, built only with -DMRS_PHASE_TIMING (profiling variant): s_memtime
+// around each phase, summed per wave and added to a device table at the end of the kernel.
+enum { PH_KIN, PH_COMPOS, PH_MAKEM, PH_CHOL, PH_COMVEL, PH_RNE, PH_SMOOTH, PH_COLL, PH_CONSTR, PH_SENS,
+       PH_INTEG, PH_CHECK, PH_COUNT };
+#ifdef MRS_PHASE_TIMING
+__device__ unsigned long long g_phase_cycles[PH_COUNT];
+#define PH_BEGIN() unsigned long long ph_t0_ = __builtin_amdgcn_s_memtime()
+#define PH_END(acc, id)                                         \
+  do {                                                          \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    (acc)[id] += t1_ - ph_t0_;                                  \
+    ph_t0_ = t1_;                                               \
+  } while (0)
+#define PH_ACC_PARAM , unsigned long long* ph_acc
+#define PH_ACC_ARG , ph_acc
+#else
+#define PH_BEGIN() (void)0
+#define PH_END(acc, id) (void)0
+#define PH_ACC_PARAM
+#define PH_ACC_ARG
+#endif
 
 // ------------------------------------------------------------------ environment context
 // Phases are separate non-inlined functions (own register allocation, nothing live across them
@@ -1265,8 +1314,9 @@ struct RayBatch { static constexpr int value = G == 64 ? 2 : 4; };
 // R rangefinders per lane in one pass over the geoms (mj_ray per sensor: nearest hit along the
 // site's +z over all visible geoms not on the site's body).  Each geom's pose is read from LDS once
 // for the R rays, and the R independent rays give the scheduler parallel work.  Rays k0 + j*stride.
-template <int R>
-__device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, float* sd, int k0, int stride) {
+template <int G, int R>
+__device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, float* sd, int k0, int stride,
+                                             unsigned gmask) {
   const LdsLayout& L = m.L;
   float pnt[R][3], vec[R][3], dist[R];
   int bod[R], adr[R];
@@ -1275,24 +1325,31 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
   for (int j = 0; j < R; ++j) {
     const int k = k0 + j * stride;
     act[j] = k < m.nrf;
-    const int sid = m.rf_sensor[act[j] ? k : 0];
-    const int site = m.sensor_objid[sid];
-    const int b = m.site_bodyid[site];
+    const CPtr<float> rr = m.rfray + 8 * (act[j] ? k : 0);
+    const int b = __float_as_int(rr[0]);
     bod[j] = b;
-    adr[j] = m.sensor_adr[sid];
+    adr[j] = __float_as_int(rr[1]);
+    const float ol[3] = {rr[2], rr[3], rr[4]}, dl[3] = {rr[5], rr[6], rr[7]};
     float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
-    float sp[3] = {m.site_pos[3 * site], m.site_pos[3 * site + 1], m.site_pos[3 * site + 2]};
-    float sq[4] = {m.site_quat[4 * site], m.site_quat[4 * site + 1], m.site_quat[4 * site + 2], m.site_quat[4 * site + 3]};
-    float r[3], q[4], sm[9];
-    rot_quat(r, sp, bq);
-    for (int i = 0; i < 3; ++i) pnt[j][i] = se[L.xpos + 3 * b + i] + r[i];
-    quat_mul(q, bq, sq);
-    quat2mat(sm, q);
-    vec[j][0] = sm[2]; vec[j][1] = sm[5]; vec[j][2] = sm[8];
+    float bm[9];
+    quat2mat(bm, bq);
+    mat_vec(pnt[j], bm, ol);
+    for (int i = 0; i < 3; ++i) pnt[j][i] += se[L.xpos + 3 * b + i];
+    mat_vec(vec[j], bm, dl);
     dist[j] = -1;
   }
+  // geoms some group of the wave still needs (union of the groups' level-1 masks), in order
+  unsigned wmask = gmask;
+  if constexpr (G < 64) {
+#pragma unroll
+    for (int i = 0; i < 64 / G; ++i) wmask |= __builtin_amdgcn_readlane(gmask, i * G);
+  }
+  wmask = __builtin_amdgcn_readfirstlane(wmask);
   #pragma unroll 1
-  for (int i = 0; i < m.nrgeom; ++i) {
+  while (wmask) {
+    const int i = __builtin_ctz(wmask);
+    wmask &= wmask - 1;
+    const bool gsel = (gmask >> i) & 1u;
     const CPtr<float> rec = m.rgeom + 8 * i;
     const int g = __float_as_int(rec[0]), type = __float_as_int(rec[1]), gb = __float_as_int(rec[2]);
     const float rb = rec[3] * 1.0001f + 1e-6f;
@@ -1307,7 +1364,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       const float tp = -dot3(dv, vec[j]);
       const float d2 = dot3(dv, dv) - tp * tp;
       const bool near = (d2 <= rb * rb) & (tp >= -rb) & ((dist[j] < 0) | (tp - rb <= dist[j]));
-      const bool c = act[j] & (gb != bod[j]) & ((type == MRS_GEOM_PLANE) | near);
+      const bool c = gsel & act[j] & (gb != bod[j]) & ((type == MRS_GEOM_PLANE) | near);
       cmask |= static_cast<unsigned>(c) << j;
     }
     if (!__any(cmask != 0)) continue;
@@ -1342,8 +1399,59 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
 #else
   constexpr int R = RayBatch<G>::value;
 #endif
+  // level 1: which ray geoms can a ray block reach at all (cone of the block vs bounding sphere of
+  // the geom; planes always), one bitmask per block; lanes over geoms
+  const unsigned all = m.nrgeom >= 32 ? 0xffffffffu : ((1u << m.nrgeom) - 1u);
   #pragma unroll 1
-  for (int k0 = lane; k0 < m.nrf; k0 += G * R) rangefinders<R>(m, s, sensordata, k0, G);
+  for (int blk = 0; blk < m.nrfblk; ++blk) {
+    const CPtr<float> br = m.rfblk + 12 * blk;
+    unsigned mask = all;
+    if (__float_as_int(br[1])) {
+      const int b = __float_as_int(br[0]);
+      const float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+      const float ol[3] = {br[2], br[3], br[4]}, al[3] = {br[5], br[6], br[7]};
+      const float theta = br[8];
+      float o[3], a[3];
+      rot_quat(o, ol, bq);
+      for (int i = 0; i < 3; ++i) o[i] += s[L.xpos + 3 * b + i];
+      rot_quat(a, al, bq);
+      mask = 0;
+      #pragma unroll 1
+      for (int c0 = 0; c0 < m.nrgeom; c0 += G) {
+        const int i = c0 + lane;
+        bool cand = false;
+        if (i < m.nrgeom) {
+          const CPtr<float> rec = m.rgeom + 8 * i;
+          const int g = __float_as_int(rec[0]), type = __float_as_int(rec[1]);
+          const float rb = rec[3] * 1.0001f + 1e-6f;
+          const float v[3] = {s[L.gxpos + 3 * g] - o[0], s[L.gxpos + 3 * g + 1] - o[1], s[L.gxpos + 3 * g + 2] - o[2]};
+          const float l2 = dot3(v, v);
+          if (type == MRS_GEOM_PLANE || l2 <= rb * rb) {
+            cand = true;
+          } else {
+            const float lv = sqrtf(l2);
+            const float phi = acosf(clampf(dot3(v, a) / lv, -1.0f, 1.0f));
+            cand = phi <= theta + asinf(fminf(1.0f, rb / lv)) + 1e-3f;
+          }
+        }
+        const unsigned long long bal = __ballot(cand);
+        const unsigned bits = static_cast<unsigned>((bal >> (__lane_id() & ~(G - 1))) & ((G == 64) ? ~0ull : ((1ull << G) - 1)));
+        mask |= c0 < 32 ? bits << c0 : 0u;
+      }
+    }
+    if (lane == 0) s[L.rfmask + blk] = __int_as_float(static_cast<int>(mask));
+  }
+  wsync();
+  #pragma unroll 1
+  for (int base = 0; base < m.nrf; base += G * R) {
+    unsigned gmask = all;
+    if (m.nrfblk > 0) {
+      gmask = 0;
+      const int b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
+      for (int blk = base / kRayBlock; blk < b1; ++blk) gmask |= static_cast<unsigned>(__float_as_int(s[L.rfmask + blk]));
+    }
+    rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask);
+  }
   #pragma unroll 1
   for (int sid = lane; sid < m.nsensor; sid += G) {
     const int t = m.sensor_type[sid], id = m.sensor_objid[sid];
@@ -1422,19 +1530,30 @@ __device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
 
 // full forward pass; returns qacc (lane per dof)
 template <int G>
-__device__ MRS_PHASE int forward(ENV_PARAMS, float* sensordata) {
+__device__ MRS_PHASE int forward(ENV_PARAMS, float* sensordata PH_ACC_PARAM) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
+  PH_BEGIN();
   kinematics<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_KIN);
   com_pos<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_COMPOS);
   make_M<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_MAKEM);
   cholesky<G>(mp, s + L.M, s + L.L, lane);
+  PH_END(ph_acc, PH_CHOL);
   com_vel<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_COMVEL);
   rne<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_RNE);
   const float qacc_s = smooth_forces<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_SMOOTH);
   const int ncon = (m.diag_skip & 2) ? 0 : collision<G>(ENV_ARGS);
+  PH_END(ph_acc, PH_COLL);
   const float qacc = (m.diag_skip & 4) ? qacc_s : constraints<G>(ENV_ARGS, ncon, qacc_s);
+  PH_END(ph_acc, PH_CONSTR);
   if (!(m.diag_skip & 1)) sensors<G>(ENV_ARGS, sensordata);
+  PH_END(ph_acc, PH_SENS);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
   return ncon;
@@ -1547,6 +1666,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
   wsync();
   int ncon = 0;
   int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
+#ifdef MRS_PHASE_TIMING
+  unsigned long long ph_acc[PH_COUNT] = {};
+#endif
   for (int step = 0; step < n_steps; ++step) {
     if (!kForwardOnly) {
       if (any_bad<G>(ENV_ARGS, L.qpos, m.nq)) {
@@ -1558,7 +1680,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
         if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env<G>(ENV_ARGS); time = 0; }
       }
     }
-    ncon = forward<G>(ENV_ARGS, sensordata);
+    ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG);
     if (kForwardOnly) break;
     bool redo = false;
     if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
@@ -1571,10 +1693,18 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
     }
     // forward() is entered by the whole wave; for envs that were not reset it recomputes the
     // same outputs from the same state
-    if (__any(redo)) ncon = forward<G>(ENV_ARGS, sensordata);
-    integrate<G>(ENV_ARGS);
+    if (__any(redo)) ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG);
+    {
+      PH_BEGIN();
+      integrate<G>(ENV_ARGS);
+      PH_END(ph_acc, PH_INTEG);
+    }
     time += m.timestep_d;
   }
+#ifdef MRS_PHASE_TIMING
+  if (__lane_id() == 0)
+    for (int i = 0; i < PH_COUNT; ++i) atomicAdd(&g_phase_cycles[i], ph_acc[i]);
+#endif
   if (!valid) return;
   // kinematics of the last forward pass (what mjv_updateScene would render after mj_step)
   #pragma unroll 1
@@ -1628,6 +1758,24 @@ static void launch_g(const DevModel* d_model, int lds_floats, const DevState& st
   else
     hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * kWavesPerBlock), lds, stream, d_model, st, n_envs,
                        n_steps);
+}
+
+// profiling variant only: per-phase wave-cycle totals since the last reset (s_memtime ticks summed
+// over waves); returns the number of phases, 0 in normal builds
+int phase_cycles(double* out, int n, bool reset) {
+#ifdef MRS_PHASE_TIMING
+  unsigned long long h[PH_COUNT];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_cycles), sizeof h) != hipSuccess) return -1;
+  for (int i = 0; i < PH_COUNT && i < n; ++i) out[i] = static_cast<double>(h[i]);
+  if (reset) {
+    unsigned long long z[PH_COUNT] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z) != hipSuccess) return -1;
+  }
+  return PH_COUNT;
+#else
+  (void)out; (void)n; (void)reset;
+  return 0;
+#endif
 }
 
 hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,

@@ -137,8 +137,22 @@ def lib() -> C.CDLL:
         L.mrs_batch_sync.argtypes = [C.c_void_p]
         L.mrs_batch_last_kernel_ms.restype = C.c_double
         L.mrs_batch_last_kernel_ms.argtypes = [C.c_void_p, C.c_int]
+        L.mrs_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int, C.c_int]
         _lib = L
     return _lib
+
+
+PHASES = ["kinematics", "com_pos", "make_M", "cholesky", "com_vel", "rne", "smooth_forces", "collision",
+          "constraints", "sensors", "integrate", "checks"]
+
+
+def phase_cycles(reset: bool = False) -> dict | None:
+    """per-phase wave-cycle totals of the step kernel (profiling builds, -DMRS_PHASE_TIMING)"""
+    out = np.zeros(len(PHASES))
+    n = lib().mrs_debug_phase_cycles(out.ctypes.data_as(C.c_void_p), len(PHASES), int(reset))
+    if n <= 0:
+        return None
+    return dict(zip(PHASES, out[:n].tolist()))
 
 
 def _check(rc: int) -> None:
