@@ -312,7 +312,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   for (int j = 0; j < m.nv; ++j) if (m.dof_frictionloss[j] > 0) fric.push_back(j);
   for (int j = 0; j < m.njnt; ++j)
     if (m.jnt_limited[j] && (m.jnt_type[j] == MRS_JNT_HINGE || m.jnt_type[j] == MRS_JNT_SLIDE)) lim.push_back(j);
-  for (int s = 0; s < m.nsensor; ++s) if (m.sensor_type[s] == MRS_SENS_RANGEFINDER) rf.push_back(s);
+  std::vector<int> other_sens;
+  for (int s = 0; s < m.nsensor; ++s) {
+    if (m.sensor_type[s] == MRS_SENS_RANGEFINDER) rf.push_back(s);
+    else other_sens.push_back(s);
+  }
+  d.nsens_other = static_cast<int>(other_sens.size());
   d.nfric = static_cast<int>(fric.size());
   d.nlim = static_cast<int>(lim.size());
   d.nrf = static_cast<int>(rf.size());
@@ -372,6 +377,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.sensor_objid, m.sensor_objid); P.addi(&d.sensor_adr, m.sensor_adr); P.addi(&d.sensor_dim, m.sensor_dim);
   P.addf(&d.sensor_cutoff, m.sensor_cutoff);
   P.addi(&d.fric_dof, fric); P.addi(&d.lim_jnt, lim); P.addi(&d.rf_sensor, rf);
+  P.addi(&d.sens_other, other_sens);
   std::vector<float> rgeom;
   auto bits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
   for (int g = 0; g < m.ngeom; ++g) {

@@ -60,7 +60,7 @@ struct DevModel {
   ScratchLayout S;
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth;
-  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk;
+  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other;
   // options
   int integrator, iterations, disableflags;
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
@@ -93,7 +93,7 @@ struct DevModel {
   // sensors
   CPtr<int> sensor_type, sensor_objtype, sensor_objid, sensor_adr, sensor_dim;
   CPtr<float> sensor_cutoff;
-  CPtr<int> fric_dof, lim_jnt, rf_sensor;
+  CPtr<int> fric_dof, lim_jnt, rf_sensor, sens_other;  // sens_other: non-rangefinder sensor ids
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;

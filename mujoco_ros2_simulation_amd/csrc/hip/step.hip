@@ -22,6 +22,9 @@ constexpr float kMaxVal = 1e10f;
 // LDS-qualified float: per-env working set pointers keep the LDS address space across the
 // out-of-line phase functions, so every access is a ds_read/ds_write (not a flat access).
 typedef __attribute__((address_space(3))) float lfloat;
+// Global-qualified float: per-env scratch and output pointers compile to global_load/store (not flat
+// accesses, which also hold the LDS counter and so stall LDS waits behind memory latency).
+typedef __attribute__((address_space(1))) float gfloat;
 
 // Phase functions are out of line by default: each gets its own register allocation under the
 // 64-VGPR budget of 8 waves/SIMD.  Measured on C3 (8192 envs): out-of-line 2.19 ms per 10-step
@@ -283,14 +286,15 @@ __device__ float ray_geom_local(int type, const PS s, const float lp[3], const f
 
 // ------------------------------------------------------------------ collision primitives
 struct Con { float dist, pos[3], nrm[3]; };
+typedef __attribute__((address_space(1))) Con gCon;  // narrow-phase staging lives in global scratch
 
 __device__ __forceinline__ int sphere_sphere(const float p1[3], float r1, const float p2[3], float r2,
-                                             float margin, Con* out, int n) {
+                                             float margin, gCon* out, int n) {
   float dv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   float len = sqrtf(dot3(dv, dv));
   float dist = len - r1 - r2;
   if (dist > margin || n >= 4) return n;
-  Con& c = out[n];
+  gCon& c = out[n];
   if (len < kMinVal) { c.nrm[0] = 1; c.nrm[1] = c.nrm[2] = 0; }
   else { float il = 1.0f / len; c.nrm[0] = dv[0] * il; c.nrm[1] = dv[1] * il; c.nrm[2] = dv[2] * il; }
   for (int i = 0; i < 3; ++i) c.pos[i] = p1[i] + c.nrm[i] * (r1 + dist / 2);
@@ -326,18 +330,18 @@ __device__ void seg_seg_closest(const float a0[3], const float a1[3], const floa
   for (int i = 0; i < 3; ++i) { ca[i] = a0[i] + s * d1[i]; cb[i] = b0[i] + t * d2[i]; }
 }
 __device__ __forceinline__ int plane_sphere(const float* pp, const float* pm, const float p[3], float r,
-                                            float margin, Con* out, int n) {
+                                            float margin, gCon* out, int n) {
   float nrm[3] = {pm[2], pm[5], pm[8]};
   float dv[3] = {p[0] - pp[0], p[1] - pp[1], p[2] - pp[2]};
   float dist = dot3(dv, nrm) - r;
   if (dist > margin || n >= 4) return n;
-  Con& c = out[n];
+  gCon& c = out[n];
   for (int i = 0; i < 3; ++i) { c.pos[i] = p[i] - nrm[i] * (r + dist / 2); c.nrm[i] = nrm[i]; }
   c.dist = dist;
   return n + 1;
 }
 __device__ int plane_box(const float* pp, const float* pm, const float* bp, const float* bm, const float* size,
-                         float margin, Con* out, int n) {
+                         float margin, gCon* out, int n) {
   float nrm[3] = {pm[2], pm[5], pm[8]};
   float dv[3] = {bp[0] - pp[0], bp[1] - pp[1], bp[2] - pp[2]};
   float cdist = dot3(dv, nrm);
@@ -348,14 +352,14 @@ __device__ int plane_box(const float* pp, const float* pm, const float* bp, cons
     float ld = dot3(nrm, c);
     float dist = cdist + ld;
     if (dist > margin || ld > 0) continue;
-    Con& o = out[n++];
+    gCon& o = out[n++];
     for (int i = 0; i < 3; ++i) { o.pos[i] = bp[i] + c[i] - nrm[i] * dist / 2; o.nrm[i] = nrm[i]; }
     o.dist = dist;
   }
   return n;
 }
 __device__ int sphere_box(const float p[3], float r, const float* bp, const float* bm, const float* size,
-                          float margin, Con* out, int n) {
+                          float margin, gCon* out, int n) {
   float dv[3] = {p[0] - bp[0], p[1] - bp[1], p[2] - bp[2]}, l[3];
   matT_vec(l, bm, dv);
   float c[3];
@@ -383,9 +387,10 @@ __device__ int sphere_box(const float p[3], float r, const float* bp, const floa
     nl[ax] = l[ax] >= 0 ? -1.0f : 1.0f;
   }
   if (n >= 4) return n;
-  Con& o = out[n];
-  mat_vec(o.nrm, bm, nl);
-  for (int i = 0; i < 3; ++i) o.pos[i] = p[i] + o.nrm[i] * (r + dist / 2);
+  gCon& o = out[n];
+  float nw[3];
+  mat_vec(nw, bm, nl);
+  for (int i = 0; i < 3; ++i) { o.nrm[i] = nw[i]; o.pos[i] = p[i] + nw[i] * (r + dist / 2); }
   o.dist = dist;
   return n + 1;
 }
@@ -398,7 +403,7 @@ __device__ __forceinline__ float box_dist2(const float l[3], const float* size) 
   return s;
 }
 __device__ int capsule_box(const float a[3], const float b[3], float r, const float* bp, const float* bm,
-                           const float* size, float margin, Con* out, int n) {
+                           const float* size, float margin, gCon* out, int n) {
   float lo = 0, hi = 1;
   for (int it = 0; it < 40; ++it) {
     float t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3, p1[3], p2[3], l1[3], l2[3];
@@ -419,7 +424,7 @@ __device__ __forceinline__ void capsule_ends(const float* pos, const float* mat,
   for (int i = 0; i < 3; ++i) { a[i] = pos[i] - mat[3 * i + 2] * hl; b[i] = pos[i] + mat[3 * i + 2] * hl; }
 }
 __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
-                           const float* m2, const float* s2, float margin, Con* out) {
+                           const float* m2, const float* s2, float margin, gCon* out) {
   float a1[3], b1[3], a2[3], b2[3], c1[3], c2[3];
   int n = 0;
   if (t1 == MRS_GEOM_PLANE) {
@@ -483,9 +488,20 @@ enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 // Per-phase cycle accounting, built only with -DMRS_PHASE_TIMING (profiling variant): s_memtime
 // around each phase, summed per wave and added to a device table at the end of the kernel.
 enum { PH_KIN, PH_COMPOS, PH_MAKEM, PH_CHOL, PH_COMVEL, PH_RNE, PH_SMOOTH, PH_COLL, PH_CONSTR, PH_SENS,
-       PH_INTEG, PH_CHECK, PH_COUNT };
+       PH_INTEG, PH_CHECK, PH_SENS_L1, PH_SENS_SETUP, PH_SENS_GEOMS, PH_COUNT };
 #ifdef MRS_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[PH_COUNT];
+#define SUB_T() __builtin_amdgcn_s_memtime()
+#define SUB_ADD(id, t0)                                                              \
+  do {                                                                               \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                     \
+    if (__lane_id() == 0) atomicAdd(&g_phase_cycles[id], t1_ - (t0));                \
+  } while (0)
+#else
+#define SUB_T() 0ull
+#define SUB_ADD(id, t0) (void)(t0)
+#endif
+#ifdef MRS_PHASE_TIMING
 #define PH_BEGIN() unsigned long long ph_t0_ = __builtin_amdgcn_s_memtime()
 #define PH_END(acc, id)                                         \
   do {                                                          \
@@ -506,7 +522,7 @@ __device__ unsigned long long g_phase_cycles[PH_COUNT];
 // Phases are separate non-inlined functions (own register allocation, nothing live across them
 // but these four values).  The model (with its LDS/scratch layouts) stays in device memory behind
 // one pointer: wave-uniform model reads become scalar loads instead of SGPR-resident kernel args.
-#define ENV_PARAMS const DevModel* __restrict__ mp, lfloat* __restrict__ s, float* __restrict__ scr, int lane
+#define ENV_PARAMS const DevModel* __restrict__ mp, lfloat* __restrict__ s, gfloat* __restrict__ scr, int lane
 #define ENV_ARGS mp, s, scr, lane
 // Function arguments arrive in VGPRs, so the compiler cannot know they are wave-uniform; the phase
 // prologue re-establishes uniformity with readfirstlane (every phase is entered by the whole wave).
@@ -589,7 +605,7 @@ __device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, con
   return x;
 }
 // serial solve by one lane (vectors in registers/scratch); used per constraint row
-__device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, const float* b, float* x) {
+__device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, const gfloat* b, gfloat* x) {
   #pragma unroll 1
   for (int i = 0; i < nv; ++i) {
     float sacc = b[i];
@@ -1003,7 +1019,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
   #pragma unroll 1
   for (int base = 0; base < m.npair; base += G) {
     const int p = base + lane;
-    Con* c = reinterpret_cast<Con*>(scr + S.stage) + 4 * lane;  // per-lane staging in global scratch
+    gCon* c = (gCon*)(scr + S.stage) + 4 * lane;  // per-lane staging in global scratch
     int n = 0;
     if (p < m.npair) {
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
@@ -1030,7 +1046,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
     for (int k = 0; k < n; ++k) {
       const int slot = ncon + off + k;
       if (slot >= m.max_con) break;
-      float* rec = scr + S.con + kConRec * slot;
+      gfloat* rec = scr + S.con + kConRec * slot;
       float fr[9] = {c[k].nrm[0], c[k].nrm[1], c[k].nrm[2], 0, 0, 0, 0, 0, 0};
       make_frame(fr);
       rec[0] = __int_as_float(p);
@@ -1051,17 +1067,17 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) ncon = uniform_int(ncon);
   const int nv = m.nv;
-  float* J = scr + S.efc_J;
-  float* MJ = scr + S.efc_MJ;
-  float* type = scr + S.efc_type;
-  float* pos = scr + S.efc_pos;
-  float* marg = scr + S.efc_margin;
-  float* floss = scr + S.efc_floss;
-  float* Rr = scr + S.efc_R;
-  float* aref = scr + S.efc_aref;
-  float* bb = scr + S.efc_b;
-  float* ff = scr + S.efc_f;
-  float* ARii = scr + S.efc_ARii;
+  gfloat* J = scr + S.efc_J;
+  gfloat* MJ = scr + S.efc_MJ;
+  gfloat* type = scr + S.efc_type;
+  gfloat* pos = scr + S.efc_pos;
+  gfloat* marg = scr + S.efc_margin;
+  gfloat* floss = scr + S.efc_floss;
+  gfloat* Rr = scr + S.efc_R;
+  gfloat* aref = scr + S.efc_aref;
+  gfloat* bb = scr + S.efc_b;
+  gfloat* ff = scr + S.efc_f;
+  gfloat* ARii = scr + S.efc_ARii;
   int nefc = 0;
   if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) s[L.qfrc_con + lane] = 0; wsync(); return qacc_s; }
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
@@ -1128,7 +1144,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   // --- contact rows: lane per dof, loop over contacts
   #pragma unroll 1
   for (int c = 0; c < ncon; ++c) {
-    const float* rec = scr + S.con + kConRec * c;
+    const gfloat* rec = scr + S.con + kConRec * c;
     const int p = __float_as_int(rec[0]);
     const int dim = m.pair_dim[p];
     const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
@@ -1180,7 +1196,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
     else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
     else {
-      const float* rec = scr + S.con + kConRec * id;
+      const gfloat* rec = scr + S.con + kConRec * id;
       const int p = __float_as_int(rec[0]);
       sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
       const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
@@ -1211,14 +1227,14 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       B = -sr[1] / dmax;
     }
     float vel = 0, jqs = 0;
-    const float* Jr = J + r * nv;
+    const gfloat* Jr = J + r * nv;
     #pragma unroll 1
     for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
     const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
     aref[r] = -B * vel - pterm;
     bb[r] = jqs - aref[r];
     // M^-1 J_r'
-    float* MJr = MJ + r * nv;
+    gfloat* MJr = MJ + r * nv;
     chol_solve_serial(s + L.L, nv, Jr, MJr);
     float d = 0;
     #pragma unroll 1
@@ -1234,7 +1250,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     for (int r = lane; r < nefc; r += G) {
       float f = 0;
       if (warm) {
-        const float* Jr = J + r * nv;
+        const gfloat* Jr = J + r * nv;
         float jar = -aref[r];
         #pragma unroll 1
         for (int j = 0; j < nv; ++j) jar += Jr[j] * s[L.qacc_ws + j];
@@ -1315,12 +1331,13 @@ struct RayBatch { static constexpr int value = G == 64 ? 2 : 4; };
 // site's +z over all visible geoms not on the site's body).  Each geom's pose is read from LDS once
 // for the R rays, and the R independent rays give the scheduler parallel work.  Rays k0 + j*stride.
 template <int G, int R>
-__device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, float* sd, int k0, int stride,
+__device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, gfloat* sd, int k0, int stride,
                                              unsigned gmask) {
   const LdsLayout& L = m.L;
   float pnt[R][3], vec[R][3], dist[R];
   int bod[R], adr[R];
   bool act[R];
+  unsigned long long t_setup = SUB_T();
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int k = k0 + j * stride;
@@ -1338,6 +1355,8 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     mat_vec(vec[j], bm, dl);
     dist[j] = -1;
   }
+  SUB_ADD(PH_SENS_SETUP, t_setup);
+  unsigned long long t_geoms = SUB_T();
   // geoms some group of the wave still needs (union of the groups' level-1 masks), in order
   unsigned wmask = gmask;
   if constexpr (G < 64) {
@@ -1385,12 +1404,13 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
 #pragma unroll
   for (int j = 0; j < R; ++j)
     if (act[j]) sd[adr[j]] = dist[j];
+  SUB_ADD(PH_SENS_GEOMS, t_geoms);
 }
 
 // mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel within the group,
 // RayBatch<G> rays per lane per pass
 template <int G>
-__device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
+__device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   if (m.disableflags & MRS_DSBL_SENSOR) return;
@@ -1402,6 +1422,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
   // level 1: which ray geoms can a ray block reach at all (cone of the block vs bounding sphere of
   // the geom; planes always), one bitmask per block; lanes over geoms
   const unsigned all = m.nrgeom >= 32 ? 0xffffffffu : ((1u << m.nrgeom) - 1u);
+  unsigned long long t_l1 = SUB_T();
   #pragma unroll 1
   for (int blk = 0; blk < m.nrfblk; ++blk) {
     const CPtr<float> br = m.rfblk + 12 * blk;
@@ -1442,6 +1463,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
     if (lane == 0) s[L.rfmask + blk] = __int_as_float(static_cast<int>(mask));
   }
   wsync();
+  SUB_ADD(PH_SENS_L1, t_l1);
   #pragma unroll 1
   for (int base = 0; base < m.nrf; base += G * R) {
     unsigned gmask = all;
@@ -1453,9 +1475,10 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
     rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask);
   }
   #pragma unroll 1
-  for (int sid = lane; sid < m.nsensor; sid += G) {
+  for (int ks = lane; ks < m.nsens_other; ks += G) {
+    const int sid = m.sens_other[ks];
     const int t = m.sensor_type[sid], id = m.sensor_objid[sid];
-    float* out = sensordata + m.sensor_adr[sid];
+    gfloat* out = sensordata + m.sensor_adr[sid];
     float cutoff = m.sensor_cutoff[sid];
     int dim = m.sensor_dim[sid];
     switch (t) {
@@ -1494,7 +1517,9 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, float* sensordata) {
         else {
           float sm[9], w[3] = {s[L.cvel + 6 * b], s[L.cvel + 6 * b + 1], s[L.cvel + 6 * b + 2]};
           quat2mat(sm, q);
-          matT_vec(out, sm, w);
+          float o3[3];
+          matT_vec(o3, sm, w);
+          for (int i = 0; i < 3; ++i) out[i] = o3[i];
         }
         break;
       }
@@ -1530,7 +1555,7 @@ __device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
 
 // full forward pass; returns qacc (lane per dof)
 template <int G>
-__device__ MRS_PHASE int forward(ENV_PARAMS, float* sensordata PH_ACC_PARAM) {
+__device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   PH_BEGIN();
@@ -1649,7 +1674,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
   // last env with their own scratch (allocated for the padded count); they write nothing back
   const bool valid = env < n_envs;
   lfloat* s = (lfloat*)(smem + slot * L.total);
-  float* scr = st.scratch + (size_t)env * m.S.total;
+  gfloat* scr = (gfloat*)(st.scratch + (size_t)env * m.S.total);
   const size_t e = (size_t)(valid ? env : n_envs - 1);
   #pragma unroll 1
   for (int i = lane; i < m.nq; i += G) s[L.qpos + i] = st.qpos[e * m.nq + i];
@@ -1662,7 +1687,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
   #pragma unroll 1
   for (int i = lane; i < m.nu; i += G) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
   double time = st.time[e];
-  float* sensordata = valid ? st.sensordata + e * m.nsensordata : scr + m.S.sens;
+  gfloat* sensordata = valid ? (gfloat*)(st.sensordata + e * m.nsensordata) : scr + m.S.sens;
   wsync();
   int ncon = 0;
   int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;

@@ -143,7 +143,7 @@ def lib() -> C.CDLL:
 
 
 PHASES = ["kinematics", "com_pos", "make_M", "cholesky", "com_vel", "rne", "smooth_forces", "collision",
-          "constraints", "sensors", "integrate", "checks"]
+          "constraints", "sensors", "integrate", "checks", "sensors.level1", "sensors.setup", "sensors.geoms"]
 
 
 def phase_cycles(reset: bool = False) -> dict | None:

@@ -24,5 +24,5 @@ for p in range(launches):
     b.step(period)
 b.sync()
 pc = sim.phase_cycles()
-tot = sum(pc.values())
+tot = sum(v for k, v in pc.items() if "." not in k)
 print(json.dumps({k: round(v / tot, 4) for k, v in pc.items()}))
