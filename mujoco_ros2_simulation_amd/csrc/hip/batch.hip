@@ -479,7 +479,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     if (m.nv <= g && lds_bytes(g) <= 80 * 1024) b.group = g;
   if (const char* e = std::getenv("MRS_GROUP")) {
     const int g = std::atoi(e);
-    if ((g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
+    if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
   }
   if (lds_bytes(b.group) > 160 * 1024)
     throw UnsupportedError("model too large for the per-environment LDS working set");
@@ -558,8 +558,8 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     b->st.time = static_cast<double*>(dalloc(*b, n * sizeof(double)));
     b->st.warning = static_cast<int*>(dalloc(*b, n * 4 * sizeof(int)));
     b->st.ncon = static_cast<int*>(dalloc(*b, n * sizeof(int)));
-    // padded to whole workgroups (16 envs at the narrowest group width): idle groups use it
-    const size_t n_pad = (static_cast<size_t>(n) + 15) / 16 * 16;
+    // padded to whole workgroups (32 envs at the narrowest group width): idle groups use it
+    const size_t n_pad = (static_cast<size_t>(n) + 31) / 32 * 32;
     b->st.scratch = static_cast<float*>(dalloc(*b, n_pad * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));
     b->st.geom_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 9 * sizeof(float)));

@@ -10,6 +10,9 @@
 // (see oracle/oracle.c for the fp64 restatement each stage is checked against).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+#include <utility>
+
 #include "devmodel.h"
 
 namespace mrs {
@@ -62,7 +65,7 @@ __device__ __forceinline__ float gsum(float v) {
   v += dpp<kDppXor1>(v);
   v += dpp<kDppXor2>(v);
   v += dpp<kDppHalfMirror>(v);
-  v += dpp<kDppMirror>(v);
+  if constexpr (G >= 16) v += dpp<kDppMirror>(v);
   if constexpr (G >= 32) v += __shfl_xor(v, 16);
   if constexpr (G == 64) v += __shfl_xor(v, 32);
   return v;
@@ -106,6 +109,19 @@ __device__ __forceinline__ bool gany(bool c) {
     return ((b >> base) & ((1ull << G) - 1)) != 0;
   }
 }
+
+// compile-time unrolling: f(integral_constant<int, 0..N-1>) in order
+template <class F, int... K>
+__device__ __forceinline__ void unroll_impl(F& f, std::integer_sequence<int, K...>) {
+  (f(std::integral_constant<int, K>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void unroll(F&& f) {
+  unroll_impl(f, std::make_integer_sequence<int, N>{});
+}
+// lane K of each row of 16 (= each group when G == 16), in every lane of the row: DPP row_newbcast
+template <int K>
+__device__ __forceinline__ float rowb(float v) { return dpp<0x150 + K>(v); }
 
 // ------------------------------------------------------------------ small math (fp32)
 __device__ __forceinline__ void quat_mul(float r[4], const float a[4], const float b[4]) {
@@ -1062,6 +1078,120 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
 }
 
 // mj_makeConstraint + mj_makeImpedance + PGS (matrix-free rows) -> qacc, qfrc_constraint
+// Small constraint systems on G = 16 groups (nv <= 16, nefc <= 16): lane j holds column j of J and
+// of M^-1 J' for every row (registers, rows unrolled), row scalars are replicated in every lane of
+// the group, row broadcasts are DPP row_newbcast and dot products DPP row reductions, so warm start
+// and the PGS sweeps touch no memory.  Inputs: the dense rows J (global scratch, row-major) and,
+// in lane r, row r's R, aref, b and friction-loss bound (0 for unilateral rows).  Returns qacc of
+// lane j's dof and writes qfrc_constraint.  Rows past the group's nefc (up to the wave's maximum)
+// are zero rows with R = 1, which never move.
+__device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, int nefc, int rmax,
+                                             float myR, float myaref, float myb, float myfl, float qacc_s,
+                                             int lane) {
+  const LdsLayout& L = m.L;
+  const int nv = m.nv;
+  constexpr int KR = 16;
+  float Jt[KR], MJt[KR], Rr[KR], ar[KR], bq[KR], fl[KR], iA[KR], Ai[KR], f[KR];
+  if (lane >= nefc) { myR = 1; myaref = 0; myb = 0; myfl = 0; }
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    Jt[r] = (r < nefc && lane < nv) ? J[r * nv + lane] : 0.0f;
+    MJt[r] = Jt[r];
+    Rr[r] = rowb<r>(myR);
+    ar[r] = rowb<r>(myaref);
+    bq[r] = rowb<r>(myb);
+    fl[r] = rowb<r>(myfl);
+    f[r] = 0;
+  });
+  // M^-1 J' for all rows at once: forward then backward substitution with L (Cholesky of M, LDS)
+  unroll<KR>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i < nv) {
+      const float inv = 1.0f / s[L.L + i * nv + i];
+      const float lji = (lane > i && lane < nv) ? s[L.L + lane * nv + i] : 0.0f;
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (r < rmax) {
+          const float xi = rowb<i>(MJt[r]) * inv;
+          MJt[r] = lane == i ? xi : MJt[r] - lji * xi;
+        }
+      });
+    }
+  });
+  unroll<KR>([&](auto ic) {
+    constexpr int i = KR - 1 - decltype(ic)::value;
+    if (i < nv) {
+      const float inv = 1.0f / s[L.L + i * nv + i];
+      const float lij = lane < i ? s[L.L + i * nv + lane] : 0.0f;
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (r < rmax) {
+          const float zi = rowb<i>(MJt[r]) * inv;
+          MJt[r] = lane == i ? zi : MJt[r] - lij * zi;
+        }
+      });
+    }
+  });
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if (r < rmax) {
+      Ai[r] = gsum<16>(Jt[r] * MJt[r]) + Rr[r];
+      iA[r] = 1.0f / Ai[r];
+    }
+  });
+  float qa = lane < nv ? qacc_s : 0.0f;
+  // warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost is negative
+  if (!(m.disableflags & MRS_DSBL_WARMSTART)) {
+    const float qw = lane < nv ? s[L.qacc_ws + lane] : 0.0f;
+    float v = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) {
+        const float jar = gsum<16>(Jt[r] * qw) - ar[r];
+        const float D = 1.0f / Rr[r];
+        f[r] = fl[r] > 0 ? (jar <= -Rr[r] * fl[r] ? fl[r] : (jar >= Rr[r] * fl[r] ? -fl[r] : -D * jar))
+                         : (jar < 0 ? -D * jar : 0.0f);
+        v += MJt[r] * f[r];
+      }
+    });
+    float cost = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) cost += f[r] * (0.5f * (gsum<16>(Jt[r] * v) + Rr[r] * f[r]) + bq[r]);
+    });
+    if (cost > 0) {
+      unroll<KR>([&](auto rc) { f[decltype(rc)::value] = 0; });
+    } else {
+      qa += v;
+    }
+  }
+  // PGS sweeps
+  #pragma unroll 1
+  for (int it = 0; it < m.iterations; ++it) {
+    float improvement = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) {
+        const float res = gsum<16>(Jt[r] * qa) - ar[r] + Rr[r] * f[r];
+        float nf = f[r] - res * iA[r];
+        nf = fl[r] > 0 ? clampf(nf, -fl[r], fl[r]) : (nf < 0 ? 0.0f : nf);
+        const float delta = nf - f[r];
+        qa += MJt[r] * delta;
+        f[r] = nf;
+        improvement -= delta * res + 0.5f * delta * delta * Ai[r];
+      }
+    });
+    if (improvement * m.pgs_scale < m.tolerance) break;
+  }
+  float qc = 0;
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if (r < rmax) qc += Jt[r] * f[r];
+  });
+  if (lane < nv) s[L.qfrc_con + lane] = qc;
+  return qa;
+}
+
 template <int G>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
@@ -1187,6 +1317,8 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     return qacc_s;
   }
   // --- impedance, R, aref, M^-1 J', ARii, b (lane per row)
+  const bool small = G == 16 && nefc <= 16;
+  float my_R = 1, my_aref = 0, my_b = 0, my_fl = 0;
   #pragma unroll 1
   for (int r = lane; r < nefc; r += G) {
     const int code = __float_as_int(type[r]);
@@ -1214,7 +1346,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     const float imp = impedance(si, pos[r], marg[r]);
     float R = (1 - imp) * diag / imp;
     R = R > kMinVal ? R : kMinVal;
-    Rr[r] = R;
+    if (!small) Rr[r] = R;
     const float dmax = clampf(si[1], 0.0001f, 0.9999f);
     float K, B;
     if (sr[0] > 0) {
@@ -1231,6 +1363,13 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     #pragma unroll 1
     for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
     const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
+    if (small) {
+      my_R = R;
+      my_aref = -B * vel - pterm;
+      my_b = jqs - my_aref;
+      my_fl = t == EFC_FRICTION ? floss[r] : 0.0f;
+      continue;
+    }
     aref[r] = -B * vel - pterm;
     bb[r] = jqs - aref[r];
     // M^-1 J_r'
@@ -1242,6 +1381,20 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     ARii[r] = d + R;
   }
   wsync();
+  if constexpr (G == 16) {
+    // rows unrolled up to the largest small system among the wave's active groups (wave-uniform
+    // bound; binary search with ballots, which only see active lanes)
+    const int mine = small ? nefc : 0;
+    int rmax = 0;
+#pragma unroll
+    for (int bit = 16; bit >= 1; bit >>= 1)
+      if (__ballot(mine >= rmax + bit) != 0) rmax += bit;
+    if (small) {
+      const float qa = pgs_small16(m, s, J, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      wsync();
+      return qa;
+    }
+  }
   // --- warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if dual cost < 0
   float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f, lane per dof
   {
@@ -1659,7 +1812,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
 // G < 64 the LDS of 4*64/G envs per workgroup bounds residency instead (e.g. G = 16: 16 envs x 4.5 KB
 // per workgroup -> 2 workgroups per CU -> 2 waves per SIMD, 256 VGPRs)
 template <int G>
-struct Occupancy { static constexpr int waves = G == 64 ? 8 : (G == 32 ? 4 : 2); };
+struct Occupancy { static constexpr int waves = G == 64 ? 8 : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
 template <int G, bool kForwardOnly>
 __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step_kernel(
@@ -1806,6 +1959,7 @@ int phase_cycles(double* out, int n, bool reset) {
 hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
                        bool forward_only, int group, hipStream_t stream) {
   switch (group) {
+    case 8: launch_g<8>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
     case 16: launch_g<16>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
     case 32: launch_g<32>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
     case 64: launch_g<64>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
