@@ -388,9 +388,11 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.nrgeom = static_cast<int>(rgeom.size() / 8);
   P.addf(&d.rgeom, rgeom);
-  // ray blocks (kRayBlock consecutive rangefinders) for the level-1 cone cull: when every ray of a
-  // block starts at the same point of the same body, the block is bounded by a cone (origin, unit
-  // axis, half-angle) fixed in that body's frame; blocks that are not are flagged and test every geom
+  // ray blocks (kRayBlock consecutive rangefinders) for the level-1 cull.  When every ray of a block
+  // starts at the same point of the same body the block is bounded by a fan fixed in that body's
+  // frame: unit axis a, in-plane direction b and normal c (the least-spread direction of the rays),
+  // in-plane half-angle theta around a and out-of-plane slope eps = max |d.c| (a planar lidar fan
+  // has eps ~ 0).  Blocks without a common origin, or wider than +-80 degrees, test every geom.
   std::vector<float> rfblk;
   d.nrfblk = 0;
   if (d.nrgeom <= 32 && d.nrf > 0) {
@@ -399,8 +401,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       const int k0 = blk * kRayBlock, k1 = std::min(d.nrf, k0 + kRayBlock);
       const int site0 = m.sensor_objid[rf[k0]], body = m.site_bodyid[site0];
       bool ok = true;
-      double axis[3] = {0, 0, 0};
       std::vector<std::array<double, 3>> dirs;
+      double axis[3] = {0, 0, 0}, cov[3][3] = {};
       for (int k = k0; k < k1; ++k) {
         const int site = m.sensor_objid[rf[k]];
         if (m.site_bodyid[site] != body) ok = false;
@@ -411,23 +413,65 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
                                     q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3]};
         const double n = std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]);
         for (int i = 0; i < 3; ++i) { dz[i] /= n; axis[i] += dz[i]; }
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) cov[i][j] += dz[i] * dz[j];
         dirs.push_back(dz);
       }
-      const double an = std::sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
-      double theta = 0;
+      double an = std::sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+      double c[3] = {0, 0, 1}, bv[3] = {0, 1, 0}, theta = 0, eps = 0;
       if (an < 1e-6) ok = false;
-      else {
+      if (ok) {
         for (int i = 0; i < 3; ++i) axis[i] /= an;
-        for (auto& dz : dirs) {
-          const double c = dz[0] * axis[0] + dz[1] * axis[1] + dz[2] * axis[2];
-          theta = std::max(theta, std::acos(std::max(-1.0, std::min(1.0, c))));
+        // normal of the fan: eigenvector of the smallest eigenvalue of sum d d' (cyclic Jacobi)
+        double A[3][3], V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+        std::memcpy(A, cov, sizeof A);
+        for (int sweep = 0; sweep < 50; ++sweep)
+          for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+              if (std::abs(A[p][q]) < 1e-15) continue;
+              const double th = 0.5 * std::atan2(2 * A[p][q], A[q][q] - A[p][p]);
+              const double cs = std::cos(th), sn = std::sin(th);
+              for (int k = 0; k < 3; ++k) {
+                const double akp = A[k][p], akq = A[k][q];
+                A[k][p] = cs * akp - sn * akq; A[k][q] = sn * akp + cs * akq;
+              }
+              for (int k = 0; k < 3; ++k) {
+                const double apk = A[p][k], aqk = A[q][k];
+                A[p][k] = cs * apk - sn * aqk; A[q][k] = sn * apk + cs * aqk;
+              }
+              for (int k = 0; k < 3; ++k) {
+                const double vkp = V[k][p], vkq = V[k][q];
+                V[k][p] = cs * vkp - sn * vkq; V[k][q] = sn * vkp + cs * vkq;
+              }
+            }
+        int imin = 0;
+        for (int i = 1; i < 3; ++i) if (A[i][i] < A[imin][imin]) imin = i;
+        for (int i = 0; i < 3; ++i) c[i] = V[i][imin];
+        const double ca = c[0] * axis[0] + c[1] * axis[1] + c[2] * axis[2];
+        for (int i = 0; i < 3; ++i) c[i] -= ca * axis[i];
+        const double cn = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+        if (cn < 1e-6) ok = false;
+        else {
+          for (int i = 0; i < 3; ++i) c[i] /= cn;
+          bv[0] = c[1] * axis[2] - c[2] * axis[1];
+          bv[1] = c[2] * axis[0] - c[0] * axis[2];
+          bv[2] = c[0] * axis[1] - c[1] * axis[0];
+          for (auto& dz : dirs) {
+            const double da = dz[0] * axis[0] + dz[1] * axis[1] + dz[2] * axis[2];
+            const double db = dz[0] * bv[0] + dz[1] * bv[1] + dz[2] * bv[2];
+            const double dc = dz[0] * c[0] + dz[1] * c[1] + dz[2] * c[2];
+            theta = std::max(theta, std::abs(std::atan2(db, da)));
+            eps = std::max(eps, std::abs(dc));
+          }
+          if (theta > 1.4) ok = false;
         }
-        if (theta > 1.4) ok = false;  // too wide for the cone bound to pay
       }
       rfblk.insert(rfblk.end(), {bits(body), bits(ok ? 1 : 0), static_cast<float>(m.site_pos[3 * site0]),
                                  static_cast<float>(m.site_pos[3 * site0 + 1]), static_cast<float>(m.site_pos[3 * site0 + 2]),
                                  static_cast<float>(axis[0]), static_cast<float>(axis[1]), static_cast<float>(axis[2]),
-                                 static_cast<float>(theta + 1e-4), 0.0f, 0.0f, 0.0f});
+                                 static_cast<float>(bv[0]), static_cast<float>(bv[1]), static_cast<float>(bv[2]),
+                                 static_cast<float>(c[0]), static_cast<float>(c[1]), static_cast<float>(c[2]),
+                                 static_cast<float>(theta + 1e-4), static_cast<float>(eps + 1e-6)});
     }
   }
   P.addf(&d.rfblk, rfblk);

@@ -97,8 +97,8 @@ struct DevModel {
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;
-  // ray blocks of kRayBlock consecutive rangefinders, 12 floats each: body, cone flag (int bits),
-  // origin[3] and unit axis[3] in the body frame, half-angle
+  // ray blocks of kRayBlock consecutive rangefinders, 16 floats each: body, fan flag (int bits),
+  // origin[3], axis a[3], in-plane b[3], normal c[3] in the body frame, half-angle, out-of-plane eps
   CPtr<float> rfblk;
   // per rangefinder, 8 floats: body, sensordata address (int bits), origin[3] and unit
   // direction[3] in the body frame

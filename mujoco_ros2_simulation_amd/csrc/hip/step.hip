@@ -1572,23 +1572,28 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
 #else
   constexpr int R = RayBatch<G>::value;
 #endif
-  // level 1: which ray geoms can a ray block reach at all (cone of the block vs bounding sphere of
-  // the geom; planes always), one bitmask per block; lanes over geoms
+  // level 1: which ray geoms can a ray block reach at all (fan bound of the block vs bounding sphere
+  // of the geom; planes by the direction range of the fan), one bitmask per block; lanes over geoms
   const unsigned all = m.nrgeom >= 32 ? 0xffffffffu : ((1u << m.nrgeom) - 1u);
   unsigned long long t_l1 = SUB_T();
   #pragma unroll 1
   for (int blk = 0; blk < m.nrfblk; ++blk) {
-    const CPtr<float> br = m.rfblk + 12 * blk;
+    const CPtr<float> br = m.rfblk + 16 * blk;
     unsigned mask = all;
     if (__float_as_int(br[1])) {
       const int b = __float_as_int(br[0]);
       const float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+      float bmat[9];
+      quat2mat(bmat, bq);
       const float ol[3] = {br[2], br[3], br[4]}, al[3] = {br[5], br[6], br[7]};
-      const float theta = br[8];
-      float o[3], a[3];
-      rot_quat(o, ol, bq);
+      const float bl[3] = {br[8], br[9], br[10]}, cl[3] = {br[11], br[12], br[13]};
+      const float theta = br[14], eps = br[15];
+      float o[3], a[3], bb[3], c[3];
+      mat_vec(o, bmat, ol);
       for (int i = 0; i < 3; ++i) o[i] += s[L.xpos + 3 * b + i];
-      rot_quat(a, al, bq);
+      mat_vec(a, bmat, al);
+      mat_vec(bb, bmat, bl);
+      mat_vec(c, bmat, cl);
       mask = 0;
       #pragma unroll 1
       for (int c0 = 0; c0 < m.nrgeom; c0 += G) {
@@ -1597,15 +1602,26 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
         if (i < m.nrgeom) {
           const CPtr<float> rec = m.rgeom + 8 * i;
           const int g = __float_as_int(rec[0]), type = __float_as_int(rec[1]);
-          const float rb = rec[3] * 1.0001f + 1e-6f;
           const float v[3] = {s[L.gxpos + 3 * g] - o[0], s[L.gxpos + 3 * g + 1] - o[1], s[L.gxpos + 3 * g + 2] - o[2]};
-          const float l2 = dot3(v, v);
-          if (type == MRS_GEOM_PLANE || l2 <= rb * rb) {
-            cand = true;
+          if (type == MRS_GEOM_PLANE) {
+            // hit needs the origin in front of the plane and some ray direction with d.n < -1e-6
+            // (the ray-plane test's parallel tolerance): d.n >= -(|(a.n, b.n)| + eps |c.n|)
+            const float n[3] = {s[L.gxmat + 9 * g + 2], s[L.gxmat + 9 * g + 5], s[L.gxmat + 9 * g + 8]};
+            const float An = dot3(a, n), Bn = dot3(bb, n), Cn = dot3(c, n);
+            cand = -dot3(v, n) > 0 && sqrtf(An * An + Bn * Bn) + eps * fabsf(Cn) > 1e-6f;
           } else {
-            const float lv = sqrtf(l2);
-            const float phi = acosf(clampf(dot3(v, a) / lv, -1.0f, 1.0f));
-            cand = phi <= theta + asinf(fminf(1.0f, rb / lv)) + 1e-3f;
+            const float rb = rec[3] * 1.0001f + 1e-6f;
+            const float l2 = dot3(v, v);
+            if (l2 <= rb * rb) {
+              cand = true;
+            } else {
+              const float lv = sqrtf(l2);
+              const float rr = rb + eps * (lv + rb);  // sphere radius plus out-of-plane drift
+              const float wa = dot3(v, a), wb = dot3(v, bb), h = dot3(v, c);
+              const float wn = sqrtf(wa * wa + wb * wb);
+              cand = fabsf(h) <= rr &&
+                     (wn <= rb || fabsf(atan2f(wb, wa)) <= theta + asinf(fminf(1.0f, rb / wn)) + 1e-3f);
+            }
           }
         }
         const unsigned long long bal = __ballot(cand);
@@ -1624,6 +1640,20 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       gmask = 0;
       const int b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
       for (int blk = base / kRayBlock; blk < b1; ++blk) gmask |= static_cast<unsigned>(__float_as_int(s[L.rfmask + blk]));
+    }
+    // no geom reachable from this pass in any group of the wave: every ray misses (-1)
+    unsigned wm = gmask;
+    if constexpr (G < 64) {
+#pragma unroll
+      for (int i = 0; i < 64 / G; ++i) wm |= __builtin_amdgcn_readlane(gmask, i * G);
+    }
+    if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int k = base + lane + j * G;
+        if (k < m.nrf) sensordata[__float_as_int(m.rfray[8 * k + 1])] = -1.0f;
+      }
+      continue;
     }
     rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask);
   }
