@@ -475,8 +475,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     }
   }
   P.addf(&d.rfblk, rfblk);
-  // per-ray records: body, sensordata address (int bits), origin and unit direction in the body
-  // frame (site pos, z column of the site rotation)
+  // per-ray records: unit direction (z column of the site rotation) and sensordata address first
+  // (one 16-byte load when the ray's pass shares body and origin), then body and origin in the body
+  // frame
   std::vector<float> rfray;
   for (int k = 0; k < d.nrf; ++k) {
     const int site = m.sensor_objid[rf[k]];
@@ -484,10 +485,10 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     double dz[3] = {2 * (q[1] * q[3] + q[0] * q[2]), 2 * (q[2] * q[3] - q[0] * q[1]),
                     q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3]};
     const double n = std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]);
-    rfray.insert(rfray.end(), {bits(m.site_bodyid[site]), bits(m.sensor_adr[rf[k]]),
+    rfray.insert(rfray.end(), {static_cast<float>(dz[0] / n), static_cast<float>(dz[1] / n), static_cast<float>(dz[2] / n),
+                               bits(m.sensor_adr[rf[k]]), bits(m.site_bodyid[site]),
                                static_cast<float>(m.site_pos[3 * site]), static_cast<float>(m.site_pos[3 * site + 1]),
-                               static_cast<float>(m.site_pos[3 * site + 2]), static_cast<float>(dz[0] / n),
-                               static_cast<float>(dz[1] / n), static_cast<float>(dz[2] / n)});
+                               static_cast<float>(m.site_pos[3 * site + 2])});
   }
   P.addf(&d.rfray, rfray);
 

@@ -100,8 +100,8 @@ struct DevModel {
   // ray blocks of kRayBlock consecutive rangefinders, 16 floats each: body, fan flag (int bits),
   // origin[3], axis a[3], in-plane b[3], normal c[3] in the body frame, half-angle, out-of-plane eps
   CPtr<float> rfblk;
-  // per rangefinder, 8 floats: body, sensordata address (int bits), origin[3] and unit
-  // direction[3] in the body frame
+  // per rangefinder, 8 floats: unit direction[3], sensordata address (int bits), body (int bits),
+  // origin[3], in the body frame
   CPtr<float> rfray;
 };
 constexpr int kRayBlock = 64;

@@ -1485,28 +1485,50 @@ struct RayBatch { static constexpr int value = G == 64 ? 2 : 4; };
 // for the R rays, and the R independent rays give the scheduler parallel work.  Rays k0 + j*stride.
 template <int G, int R>
 __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, gfloat* sd, int k0, int stride,
-                                             unsigned gmask) {
+                                             unsigned gmask, int common_body, const float* common_o) {
   const LdsLayout& L = m.L;
   float pnt[R][3], vec[R][3], dist[R];
   int bod[R], adr[R];
   bool act[R];
   unsigned long long t_setup = SUB_T();
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int k = k0 + j * stride;
-    act[j] = k < m.nrf;
-    const CPtr<float> rr = m.rfray + 8 * (act[j] ? k : 0);
-    const int b = __float_as_int(rr[0]);
-    bod[j] = b;
-    adr[j] = __float_as_int(rr[1]);
-    const float ol[3] = {rr[2], rr[3], rr[4]}, dl[3] = {rr[5], rr[6], rr[7]};
+  if (common_body >= 0) {
+    // every ray of the pass starts at the same point of the same body: one rotation for all
+    const int b = common_body;
     float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
-    float bm[9];
+    float bm[9], o[3];
     quat2mat(bm, bq);
-    mat_vec(pnt[j], bm, ol);
-    for (int i = 0; i < 3; ++i) pnt[j][i] += se[L.xpos + 3 * b + i];
-    mat_vec(vec[j], bm, dl);
-    dist[j] = -1;
+    mat_vec(o, bm, common_o);
+    for (int i = 0; i < 3; ++i) o[i] += se[L.xpos + 3 * b + i];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int k = k0 + j * stride;
+      act[j] = k < m.nrf;
+      const CPtr<float> rr = m.rfray + 8 * (act[j] ? k : 0);
+      const float dl[3] = {rr[0], rr[1], rr[2]};
+      adr[j] = __float_as_int(rr[3]);
+      bod[j] = b;
+      mat_vec(vec[j], bm, dl);
+      for (int i = 0; i < 3; ++i) pnt[j][i] = o[i];
+      dist[j] = -1;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int k = k0 + j * stride;
+      act[j] = k < m.nrf;
+      const CPtr<float> rr = m.rfray + 8 * (act[j] ? k : 0);
+      const float dl[3] = {rr[0], rr[1], rr[2]}, ol[3] = {rr[5], rr[6], rr[7]};
+      adr[j] = __float_as_int(rr[3]);
+      const int b = __float_as_int(rr[4]);
+      bod[j] = b;
+      float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
+      float bm[9];
+      quat2mat(bm, bq);
+      mat_vec(pnt[j], bm, ol);
+      for (int i = 0; i < 3; ++i) pnt[j][i] += se[L.xpos + 3 * b + i];
+      mat_vec(vec[j], bm, dl);
+      dist[j] = -1;
+    }
   }
   SUB_ADD(PH_SENS_SETUP, t_setup);
   unsigned long long t_geoms = SUB_T();
@@ -1651,11 +1673,28 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const int k = base + lane + j * G;
-        if (k < m.nrf) sensordata[__float_as_int(m.rfray[8 * k + 1])] = -1.0f;
+        if (k < m.nrf) sensordata[__float_as_int(m.rfray[8 * k + 3])] = -1.0f;
       }
       continue;
     }
-    rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask);
+    // shared body and origin for the whole pass when all its blocks are fans from one point
+    int common_body = -1;
+    float common_o[3] = {0, 0, 0};
+    if (m.nrfblk > 0) {
+      const int b0 = base / kRayBlock, b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
+      const CPtr<float> r0 = m.rfblk + 16 * b0;
+      bool same = __float_as_int(r0[1]) != 0;
+      for (int blk = b0 + 1; blk < b1 && same; ++blk) {
+        const CPtr<float> ri = m.rfblk + 16 * blk;
+        same = __float_as_int(ri[1]) != 0 && __float_as_int(ri[0]) == __float_as_int(r0[0]) && ri[2] == r0[2] &&
+               ri[3] == r0[3] && ri[4] == r0[4];
+      }
+      if (same) {
+        common_body = __float_as_int(r0[0]);
+        common_o[0] = r0[2]; common_o[1] = r0[3]; common_o[2] = r0[4];
+      }
+    }
+    rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask, common_body, common_o);
   }
   #pragma unroll 1
   for (int ks = lane; ks < m.nsens_other; ks += G) {
