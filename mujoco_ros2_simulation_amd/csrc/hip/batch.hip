@@ -264,6 +264,18 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       if (m.body_depth[bI] == lev) level_body.push_back(bI);
     level_num[lev] = static_cast<int>(level_body.size()) - level_adr[lev];
   }
+  // pointer-jumping tables for the tree passes: jump[r][b] = ancestor of b at distance 2^r when b
+  // is deeper than 2^r (that ancestor is not the world body), else -1; ceil(log2(max_depth)) rounds
+  d.njump = 0;
+  while ((1 << d.njump) < m.max_depth) ++d.njump;
+  std::vector<int> jump(std::max(1, d.njump * m.nbody), -1);
+  for (int r = 0; r < d.njump; ++r)
+    for (int bI = 1; bI < m.nbody; ++bI) {
+      if (m.body_depth[bI] <= (1 << r)) continue;
+      int a = bI;
+      for (int k = 0; k < (1 << r); ++k) a = m.body_parentid[a];
+      jump[r * m.nbody + bI] = a;
+    }
   std::vector<int> Mpair;
   for (int i = 0; i < m.nv; ++i)
     for (int j = i; j >= 0; j = m.dof_parentid[j]) { Mpair.push_back(i); Mpair.push_back(j); }
@@ -344,7 +356,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.body_jntnum, m.body_jntnum); P.addi(&d.body_jntadr, m.body_jntadr);
   P.addi(&d.body_dofnum, m.body_dofnum); P.addi(&d.body_dofadr, m.body_dofadr);
   P.addi(&d.body_subtree_end, subtree_end); P.addi(&d.level_adr, level_adr);
-  P.addi(&d.level_num, level_num); P.addi(&d.level_body, level_body);
+  P.addi(&d.level_num, level_num); P.addi(&d.level_body, level_body); P.addi(&d.jump, jump);
   P.addf(&d.body_pos, m.body_pos); P.addf(&d.body_quat, m.body_quat); P.addf(&d.body_ipos, m.body_ipos);
   P.addf(&d.body_iquat, m.body_iquat); P.addf(&d.body_mass, m.body_mass);
   P.addf(&d.body_subtreemass, m.body_subtreemass); P.addf(&d.body_inertia, m.body_inertia);

@@ -59,7 +59,7 @@ struct DevModel {
   LdsLayout L;
   ScratchLayout S;
   // sizes
-  int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth;
+  int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth, njump;
   int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other;
   // options
   int integrator, iterations, disableflags;
@@ -68,6 +68,7 @@ struct DevModel {
   double timestep_d;  // time is accumulated in fp64 like mjData.time
   // bodies
   CPtr<int> body_parentid, body_rootid, body_jntnum, body_jntadr, body_dofnum, body_dofadr, body_subtree_end, level_adr, level_num, level_body;
+  CPtr<int> jump;  // [njump][nbody]: ancestor at distance 2^r (-1 when that is the world or beyond)
   CPtr<float> body_pos, body_quat, body_ipos, body_iquat, body_mass, body_subtreemass, body_inertia, body_gravcomp, body_invweight0;
   // joints / dofs
   CPtr<int> jnt_type, jnt_qposadr, jnt_dofadr, jnt_bodyid, jnt_actfrclimited;

@@ -636,95 +636,163 @@ __device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, cons
   }
 }
 
-// mj_kinematics + rotational part of cinert; bodies of one depth level per pass
+// pose of body b from its parent's frame (P, Q): body offset, then its joints in order (mj_kinematics
+// per body).  With kJoints the world anchors/axes of the joints are written (P, Q must be the
+// parent's world frame then).  A free joint gives the world pose directly (its parent is the world).
+template <bool kJoints>
+__device__ __forceinline__ void body_pose(const DevModel& m, lfloat* s, int b, const float P[3], const float Q[4],
+                                          float pos[3], float q[4]) {
+  const LdsLayout& L = m.L;
+  const int ja = m.body_jntadr[b], nj = m.body_jntnum[b];
+  if (nj > 0 && m.jnt_type[ja] == MRS_JNT_FREE) {
+    const lfloat* qp = s + L.qpos + m.jnt_qposadr[ja];
+    pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
+    q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+    quat_normalize(q);
+    if (kJoints) {
+      lfloat* anc = s + L.xanchor + 3 * ja;
+      lfloat* ax = s + L.xaxis + 3 * ja;
+      for (int i = 0; i < 3; ++i) { anc[i] = pos[i]; ax[i] = 0; }
+    }
+    return;
+  }
+  const float bpos[3] = {m.body_pos[3 * b], m.body_pos[3 * b + 1], m.body_pos[3 * b + 2]};
+  const float bq[4] = {m.body_quat[4 * b], m.body_quat[4 * b + 1], m.body_quat[4 * b + 2], m.body_quat[4 * b + 3]};
+  float r[3];
+  rot_quat(r, bpos, Q);
+  for (int i = 0; i < 3; ++i) pos[i] = P[i] + r[i];
+  quat_mul(q, Q, bq);
+  #pragma unroll 1
+  for (int k2 = 0; k2 < nj; ++k2) {
+    const int j = ja + k2, qa = m.jnt_qposadr[j];
+    const float jp[3] = {m.jnt_pos[3 * j], m.jnt_pos[3 * j + 1], m.jnt_pos[3 * j + 2]};
+    const float ja3[3] = {m.jnt_axis[3 * j], m.jnt_axis[3 * j + 1], m.jnt_axis[3 * j + 2]};
+    float anc[3], ax[3];
+    rot_quat(anc, jp, q);
+    for (int i = 0; i < 3; ++i) anc[i] += pos[i];
+    rot_quat(ax, ja3, q);
+    if (kJoints)
+      for (int i = 0; i < 3; ++i) { s[L.xanchor + 3 * j + i] = anc[i]; s[L.xaxis + 3 * j + i] = ax[i]; }
+    const int jt = m.jnt_type[j];
+    if (jt == MRS_JNT_SLIDE) {
+      const float dq = s[L.qpos + qa] - m.qpos0[qa];
+      for (int i = 0; i < 3; ++i) pos[i] += ax[i] * dq;
+    } else {
+      float ql[4];
+      if (jt == MRS_JNT_BALL) {
+        for (int i = 0; i < 4; ++i) ql[i] = s[L.qpos + qa + i];
+        quat_normalize(ql);
+      } else {
+        axis_angle_quat(ql, ja3, s[L.qpos + qa] - m.qpos0[qa]);
+      }
+      quat_mul(q, q, ql);
+      float v[3];
+      rot_quat(v, jp, q);
+      for (int i = 0; i < 3; ++i) pos[i] = anc[i] - v[i];
+    }
+  }
+}
+
+// body frame outputs: xpos, xquat, xmat, inertial frame and the rotational part of cinert
+__device__ __forceinline__ void body_frame_out(const DevModel& m, lfloat* s, int b, const float pos[3], float q[4]) {
+  const LdsLayout& L = m.L;
+  quat_normalize(q);
+  float xm[9];
+  quat2mat(xm, q);
+  for (int i = 0; i < 3; ++i) s[L.xpos + 3 * b + i] = pos[i];
+  for (int i = 0; i < 4; ++i) s[L.xquat + 4 * b + i] = q[i];
+  for (int i = 0; i < 9; ++i) s[L.xmat + 9 * b + i] = xm[i];
+  // inertial frame; world-frame rotational inertia about the body com goes to cinert[0..5]
+  const float ip[3] = {m.body_ipos[3 * b], m.body_ipos[3 * b + 1], m.body_ipos[3 * b + 2]};
+  const float iq[4] = {m.body_iquat[4 * b], m.body_iquat[4 * b + 1], m.body_iquat[4 * b + 2], m.body_iquat[4 * b + 3]};
+  float r[3], qi[4], R[9];
+  mat_vec(r, xm, ip);
+  for (int i = 0; i < 3; ++i) s[L.xipos + 3 * b + i] = pos[i] + r[i];
+  quat_mul(qi, q, iq);
+  quat2mat(R, qi);
+  const float I0 = m.body_inertia[3 * b], I1 = m.body_inertia[3 * b + 1], I2 = m.body_inertia[3 * b + 2];
+  lfloat* ci = s + L.cinert + 10 * b;
+  ci[0] = R[0] * I0 * R[0] + R[1] * I1 * R[1] + R[2] * I2 * R[2];
+  ci[1] = R[3] * I0 * R[3] + R[4] * I1 * R[4] + R[5] * I2 * R[5];
+  ci[2] = R[6] * I0 * R[6] + R[7] * I1 * R[7] + R[8] * I2 * R[8];
+  ci[3] = R[0] * I0 * R[3] + R[1] * I1 * R[4] + R[2] * I2 * R[5];
+  ci[4] = R[0] * I0 * R[6] + R[1] * I1 * R[7] + R[2] * I2 * R[8];
+  ci[5] = R[3] * I0 * R[6] + R[4] * I1 * R[7] + R[5] * I2 * R[8];
+}
+
+// mj_kinematics + rotational part of cinert.  With one lane per body (nbody <= G) the tree is
+// composed by pointer jumping: every body's pose relative to its parent in parallel, then
+// ceil(log2(max_depth)) rounds T(b) <- T(ancestor at 2^r) o T(b), then every body again from its
+// parent's world pose (joint anchors/axes, frames, inertia).  Otherwise bodies of one depth level
+// per pass.
 template <int G>
 __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   ENV_UNPACK;
-  if (lane == 0) {
-    lfloat* x = s + L.xpos; x[0] = x[1] = x[2] = 0;
-    lfloat* q = s + L.xquat; q[0] = 1; q[1] = q[2] = q[3] = 0;
-    lfloat* mm = s + L.xmat;
-    for (int i = 0; i < 9; ++i) mm[i] = (i % 4 == 0) ? 1.0f : 0.0f;
-    lfloat* xi = s + L.xipos; xi[0] = xi[1] = xi[2] = 0;
-  }
-  wsync();
-  for (int lev = 1; lev <= m.max_depth; ++lev) {
-    const int a0 = m.level_adr[lev], nl = m.level_num[lev];
-    #pragma unroll 1
-    for (int k = lane; k < nl; k += G) {
-      const int b = m.level_body[a0 + k];
-      const int p = m.body_parentid[b];
-      float pos[3], q[4];
-      const int ja = m.body_jntadr[b], nj = m.body_jntnum[b];
-      if (nj > 0 && m.jnt_type[ja] == MRS_JNT_FREE) {
-        const lfloat* qp = s + L.qpos + m.jnt_qposadr[ja];
-        pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
-        q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
-        quat_normalize(q);
-        lfloat* anc = s + L.xanchor + 3 * ja;
-        lfloat* ax = s + L.xaxis + 3 * ja;
-        for (int i = 0; i < 3; ++i) { anc[i] = pos[i]; ax[i] = 0; }
-      } else {
-        float pq[4] = {s[L.xquat + 4 * p], s[L.xquat + 4 * p + 1], s[L.xquat + 4 * p + 2], s[L.xquat + 4 * p + 3]};
-        float bpos[3] = {m.body_pos[3 * b], m.body_pos[3 * b + 1], m.body_pos[3 * b + 2]};
-        float bq[4] = {m.body_quat[4 * b], m.body_quat[4 * b + 1], m.body_quat[4 * b + 2], m.body_quat[4 * b + 3]};
-        float r[3];
-        rot_quat(r, bpos, pq);
-        for (int i = 0; i < 3; ++i) pos[i] = s[L.xpos + 3 * p + i] + r[i];
-        quat_mul(q, pq, bq);
-        #pragma unroll 1
-        for (int k2 = 0; k2 < nj; ++k2) {
-          const int j = ja + k2, qa = m.jnt_qposadr[j];
-          float jp[3] = {m.jnt_pos[3 * j], m.jnt_pos[3 * j + 1], m.jnt_pos[3 * j + 2]};
-          float ja3[3] = {m.jnt_axis[3 * j], m.jnt_axis[3 * j + 1], m.jnt_axis[3 * j + 2]};
-          float anc[3], ax[3];
-          rot_quat(anc, jp, q);
-          for (int i = 0; i < 3; ++i) anc[i] += pos[i];
-          rot_quat(ax, ja3, q);
-          for (int i = 0; i < 3; ++i) { s[L.xanchor + 3 * j + i] = anc[i]; s[L.xaxis + 3 * j + i] = ax[i]; }
-          const int jt = m.jnt_type[j];
-          if (jt == MRS_JNT_SLIDE) {
-            float dq = s[L.qpos + qa] - m.qpos0[qa];
-            for (int i = 0; i < 3; ++i) pos[i] += ax[i] * dq;
-          } else {
-            float ql[4];
-            if (jt == MRS_JNT_BALL) {
-              for (int i = 0; i < 4; ++i) ql[i] = s[L.qpos + qa + i];
-              quat_normalize(ql);
-            } else {
-              axis_angle_quat(ql, ja3, s[L.qpos + qa] - m.qpos0[qa]);
-            }
-            quat_mul(q, q, ql);
-            float v[3];
-            rot_quat(v, jp, q);
-            for (int i = 0; i < 3; ++i) pos[i] = anc[i] - v[i];
-          }
-        }
-      }
-      quat_normalize(q);
-      float xm[9];
-      quat2mat(xm, q);
+  const float P0[3] = {0, 0, 0}, Q0[4] = {1, 0, 0, 0};
+  if (m.nbody <= G) {
+    const int b = lane;
+    float pos[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0};
+    if (b >= 1 && b < m.nbody) body_pose<false>(m, s, b, P0, Q0, pos, q);
+    if (b < m.nbody) {
       for (int i = 0; i < 3; ++i) s[L.xpos + 3 * b + i] = pos[i];
       for (int i = 0; i < 4; ++i) s[L.xquat + 4 * b + i] = q[i];
-      for (int i = 0; i < 9; ++i) s[L.xmat + 9 * b + i] = xm[i];
-      // inertial frame; world-frame rotational inertia about the body com goes to cinert[0..5]
-      float ip[3] = {m.body_ipos[3 * b], m.body_ipos[3 * b + 1], m.body_ipos[3 * b + 2]};
-      float iq[4] = {m.body_iquat[4 * b], m.body_iquat[4 * b + 1], m.body_iquat[4 * b + 2], m.body_iquat[4 * b + 3]};
-      float r[3], qi[4], R[9];
-      mat_vec(r, xm, ip);
-      for (int i = 0; i < 3; ++i) s[L.xipos + 3 * b + i] = pos[i] + r[i];
-      quat_mul(qi, q, iq);
-      quat2mat(R, qi);
-      const float I0 = m.body_inertia[3 * b], I1 = m.body_inertia[3 * b + 1], I2 = m.body_inertia[3 * b + 2];
-      lfloat* ci = s + L.cinert + 10 * b;
-      ci[0] = R[0] * I0 * R[0] + R[1] * I1 * R[1] + R[2] * I2 * R[2];
-      ci[1] = R[3] * I0 * R[3] + R[4] * I1 * R[4] + R[5] * I2 * R[5];
-      ci[2] = R[6] * I0 * R[6] + R[7] * I1 * R[7] + R[8] * I2 * R[8];
-      ci[3] = R[0] * I0 * R[3] + R[1] * I1 * R[4] + R[2] * I2 * R[5];
-      ci[4] = R[0] * I0 * R[6] + R[1] * I1 * R[7] + R[2] * I2 * R[8];
-      ci[5] = R[3] * I0 * R[6] + R[4] * I1 * R[7] + R[5] * I2 * R[8];
     }
     wsync();
+    #pragma unroll 1
+    for (int r = 0; r < m.njump; ++r) {
+      const int a = (b >= 1 && b < m.nbody) ? m.jump[r * m.nbody + b] : -1;
+      float ap[3], aq[4];
+      if (a >= 0) {
+        for (int i = 0; i < 3; ++i) ap[i] = s[L.xpos + 3 * a + i];
+        for (int i = 0; i < 4; ++i) aq[i] = s[L.xquat + 4 * a + i];
+      }
+      wsync();
+      if (a >= 0) {
+        float rr[3];
+        rot_quat(rr, pos, aq);
+        for (int i = 0; i < 3; ++i) pos[i] = ap[i] + rr[i];
+        quat_mul(q, aq, q);
+        for (int i = 0; i < 3; ++i) s[L.xpos + 3 * b + i] = pos[i];
+        for (int i = 0; i < 4; ++i) s[L.xquat + 4 * b + i] = q[i];
+      }
+      wsync();
+    }
+    // every body from its parent's world pose (same values up to rounding, plus joint frames)
+    float P[3] = {0, 0, 0}, Q[4] = {1, 0, 0, 0};
+    if (b >= 1 && b < m.nbody) {
+      const int p = m.body_parentid[b];
+      for (int i = 0; i < 3; ++i) P[i] = s[L.xpos + 3 * p + i];
+      for (int i = 0; i < 4; ++i) Q[i] = s[L.xquat + 4 * p + i];
+    }
+    wsync();
+    if (b >= 1 && b < m.nbody) {
+      body_pose<true>(m, s, b, P, Q, pos, q);
+      body_frame_out(m, s, b, pos, q);
+    } else if (b == 0) {
+      float q1[4] = {1, 0, 0, 0};
+      body_frame_out(m, s, 0, P0, q1);
+    }
+    wsync();
+  } else {
+    if (lane == 0) {
+      float q1[4] = {1, 0, 0, 0};
+      body_frame_out(m, s, 0, P0, q1);
+    }
+    wsync();
+    for (int lev = 1; lev <= m.max_depth; ++lev) {
+      const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+      #pragma unroll 1
+      for (int k = lane; k < nl; k += G) {
+        const int b = m.level_body[a0 + k];
+        const int p = m.body_parentid[b];
+        const float P[3] = {s[L.xpos + 3 * p], s[L.xpos + 3 * p + 1], s[L.xpos + 3 * p + 2]};
+        const float Q[4] = {s[L.xquat + 4 * p], s[L.xquat + 4 * p + 1], s[L.xquat + 4 * p + 2], s[L.xquat + 4 * p + 3]};
+        float pos[3], q[4];
+        body_pose<true>(m, s, b, P, Q, pos, q);
+        body_frame_out(m, s, b, pos, q);
+      }
+      wsync();
+    }
   }
   // geoms
   #pragma unroll 1
@@ -843,10 +911,89 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
   wsync();
 }
 
-// mj_comVel: level by level
+// prefix sums of a 6-vector down the tree by pointer jumping (one lane per body, nbody <= G):
+// on entry lane b holds its own term v, on exit the sum over b and its ancestors (world excluded);
+// buf (6 per body) is the exchange buffer and holds the result
+template <int G>
+__device__ __forceinline__ void tree_prefix6(const DevModel& m, lfloat* buf, int b, float v[6]) {
+  if (b < m.nbody)
+    for (int i = 0; i < 6; ++i) buf[6 * b + i] = v[i];
+  wsync();
+  #pragma unroll 1
+  for (int r = 0; r < m.njump; ++r) {
+    const int a = (b >= 1 && b < m.nbody) ? m.jump[r * m.nbody + b] : -1;
+    float av[6];
+    if (a >= 0)
+      for (int i = 0; i < 6; ++i) av[i] = buf[6 * a + i];
+    wsync();
+    if (a >= 0) {
+      for (int i = 0; i < 6; ++i) v[i] += av[i];
+      for (int i = 0; i < 6; ++i) buf[6 * b + i] = v[i];
+    }
+    wsync();
+  }
+}
+
+// cdof_dot of body b's dofs from the velocity of its parent (mj_comVel per body); returns cvel[b]
+__device__ __forceinline__ void body_comvel(const DevModel& m, lfloat* s, int b, float cv[6]) {
+  const LdsLayout& L = m.L;
+  const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+  #pragma unroll 1
+  for (int k2 = 0; k2 < nd; ++k2) {
+    const int j = da + k2;
+    const int jid = m.dof_jntid[j], jt = m.jnt_type[jid];
+    if (jt == MRS_JNT_FREE && j == m.jnt_dofadr[jid]) {
+      for (int t = 0; t < 3; ++t) {
+        const float qv = s[L.qvel + j + t];
+        for (int i = 0; i < 6; ++i) {
+          s[L.cdofdot + 6 * (j + t) + i] = 0;
+          cv[i] += s[L.cdof + 6 * (j + t) + i] * qv;
+        }
+      }
+      k2 += 2;
+      continue;
+    }
+    if (jt == MRS_JNT_BALL || jt == MRS_JNT_FREE) {
+      for (int t = 0; t < 3; ++t) cross_motion(s + L.cdofdot + 6 * (j + t), cv, s + L.cdof + 6 * (j + t));
+      for (int t = 0; t < 3; ++t) {
+        const float qv = s[L.qvel + j + t];
+        for (int i = 0; i < 6; ++i) cv[i] += s[L.cdof + 6 * (j + t) + i] * qv;
+      }
+      k2 += 2;
+      continue;
+    }
+    cross_motion(s + L.cdofdot + 6 * j, cv, s + L.cdof + 6 * j);
+    const float qv = s[L.qvel + j];
+    for (int i = 0; i < 6; ++i) cv[i] += s[L.cdof + 6 * j + i] * qv;
+  }
+}
+
+// mj_comVel: pointer jumping (cvel[b] = sum over b and its ancestors of cdof qvel) when nbody <= G,
+// then cdof_dot per body from the parent's velocity; level by level otherwise
 template <int G>
 __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
   ENV_UNPACK;
+  if (m.nbody <= G) {
+    const int b = lane;
+    float v[6] = {0, 0, 0, 0, 0, 0};
+    if (b >= 1 && b < m.nbody) {
+      const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      #pragma unroll 1
+      for (int j = da; j < da + nd; ++j) {
+        const float qv = s[L.qvel + j];
+        for (int i = 0; i < 6; ++i) v[i] += s[L.cdof + 6 * j + i] * qv;
+      }
+    }
+    tree_prefix6<G>(m, s + L.cvel, b, v);
+    if (b >= 1 && b < m.nbody) {
+      const int p = m.body_parentid[b];
+      float cv[6];
+      for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
+      body_comvel(m, s, b, cv);
+    }
+    wsync();
+    return;
+  }
   if (lane < 6) s[L.cvel + lane] = 0;
   wsync();
   for (int lev = 1; lev <= m.max_depth; ++lev) {
@@ -857,74 +1004,73 @@ __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
       const int p = m.body_parentid[b];
       float cv[6];
       for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
-      const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
-      #pragma unroll 1
-      for (int k2 = 0; k2 < nd; ++k2) {
-        const int j = da + k2;
-        const int jid = m.dof_jntid[j], jt = m.jnt_type[jid];
-        if (jt == MRS_JNT_FREE && j == m.jnt_dofadr[jid]) {
-          for (int t = 0; t < 3; ++t) {
-            const float qv = s[L.qvel + j + t];
-            for (int i = 0; i < 6; ++i) {
-              s[L.cdofdot + 6 * (j + t) + i] = 0;
-              cv[i] += s[L.cdof + 6 * (j + t) + i] * qv;
-            }
-          }
-          k2 += 2;
-          continue;
-        }
-        if (jt == MRS_JNT_BALL || jt == MRS_JNT_FREE) {
-          for (int t = 0; t < 3; ++t) cross_motion(s + L.cdofdot + 6 * (j + t), cv, s + L.cdof + 6 * (j + t));
-          for (int t = 0; t < 3; ++t) {
-            const float qv = s[L.qvel + j + t];
-            for (int i = 0; i < 6; ++i) cv[i] += s[L.cdof + 6 * (j + t) + i] * qv;
-          }
-          k2 += 2;
-          continue;
-        }
-        cross_motion(s + L.cdofdot + 6 * j, cv, s + L.cdof + 6 * j);
-        const float qv = s[L.qvel + j];
-        for (int i = 0; i < 6; ++i) cv[i] += s[L.cdof + 6 * j + i] * qv;
-      }
+      body_comvel(m, s, b, cv);
       for (int i = 0; i < 6; ++i) s[L.cvel + 6 * b + i] = cv[i];
     }
     wsync();
   }
 }
 
-// mj_rne (no acceleration term): qfrc_bias
+// mj_rne (no acceleration term): qfrc_bias.  cacc[b] = -gravity + sum over b and its ancestors of
+// cdof_dot qvel (pointer jumping when nbody <= G, else level by level); body forces in parallel;
+// subtree sums by DFS ranges
 template <int G>
 __device__ MRS_PHASE void rne(ENV_PARAMS) {
   ENV_UNPACK;
-  if (lane < 6) {
-    const float gx = m.gravity[0], gy = m.gravity[1], gz = m.gravity[2];
-    float g = lane == 3 ? -gx : (lane == 4 ? -gy : (lane == 5 ? -gz : 0.0f));
-    if (m.disableflags & MRS_DSBL_GRAVITY) g = 0;
-    s[L.cacc + lane] = g;
-  }
-  wsync();
-  for (int lev = 1; lev <= m.max_depth; ++lev) {
-    const int a0 = m.level_adr[lev], nl = m.level_num[lev];
-    #pragma unroll 1
-    for (int k = lane; k < nl; k += G) {
-      const int b = m.level_body[a0 + k];
-      float ca[6];
-      for (int i = 0; i < 6; ++i) ca[i] = s[L.cacc + 6 * m.body_parentid[b] + i];
+  float g0[6] = {0, 0, 0, 0, 0, 0};
+  if (!(m.disableflags & MRS_DSBL_GRAVITY)) { g0[3] = -m.gravity[0]; g0[4] = -m.gravity[1]; g0[5] = -m.gravity[2]; }
+  if (m.nbody <= G) {
+    const int b = lane;
+    float v[6] = {0, 0, 0, 0, 0, 0};
+    if (b >= 1 && b < m.nbody) {
       const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
       #pragma unroll 1
-      for (int k2 = 0; k2 < nd; ++k2) {
-        const float qv = s[L.qvel + da + k2];
-        for (int i = 0; i < 6; ++i) ca[i] += s[L.cdofdot + 6 * (da + k2) + i] * qv;
+      for (int j = da; j < da + nd; ++j) {
+        const float qv = s[L.qvel + j];
+        for (int i = 0; i < 6; ++i) v[i] += s[L.cdofdot + 6 * j + i] * qv;
       }
+    }
+    tree_prefix6<G>(m, s + L.cacc, b, v);
+    if (b < m.nbody) {
+      float ca[6];
+      for (int i = 0; i < 6; ++i) ca[i] = v[i] + g0[i];
       for (int i = 0; i < 6; ++i) s[L.cacc + 6 * b + i] = ca[i];
-      float f1[6], t[6], f2[6], cv[6];
-      for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * b + i];
-      mul_inert_vec(f1, s + L.cinert + 10 * b, ca);
-      mul_inert_vec(t, s + L.cinert + 10 * b, cv);
-      cross_force(f2, cv, t);
-      for (int i = 0; i < 6; ++i) s[L.cfrc + 6 * b + i] = f1[i] + f2[i];
+      if (b >= 1) {
+        float f1[6], t[6], f2[6], cv[6];
+        for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * b + i];
+        mul_inert_vec(f1, s + L.cinert + 10 * b, ca);
+        mul_inert_vec(t, s + L.cinert + 10 * b, cv);
+        cross_force(f2, cv, t);
+        for (int i = 0; i < 6; ++i) s[L.cfrc + 6 * b + i] = f1[i] + f2[i];
+      }
     }
     wsync();
+  } else {
+    if (lane < 6) s[L.cacc + lane] = g0[lane];
+    wsync();
+    for (int lev = 1; lev <= m.max_depth; ++lev) {
+      const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+      #pragma unroll 1
+      for (int k = lane; k < nl; k += G) {
+        const int b = m.level_body[a0 + k];
+        float ca[6];
+        for (int i = 0; i < 6; ++i) ca[i] = s[L.cacc + 6 * m.body_parentid[b] + i];
+        const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+        #pragma unroll 1
+        for (int k2 = 0; k2 < nd; ++k2) {
+          const float qv = s[L.qvel + da + k2];
+          for (int i = 0; i < 6; ++i) ca[i] += s[L.cdofdot + 6 * (da + k2) + i] * qv;
+        }
+        for (int i = 0; i < 6; ++i) s[L.cacc + 6 * b + i] = ca[i];
+        float f1[6], t[6], f2[6], cv[6];
+        for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * b + i];
+        mul_inert_vec(f1, s + L.cinert + 10 * b, ca);
+        mul_inert_vec(t, s + L.cinert + 10 * b, cv);
+        cross_force(f2, cv, t);
+        for (int i = 0; i < 6; ++i) s[L.cfrc + 6 * b + i] = f1[i] + f2[i];
+      }
+      wsync();
+    }
   }
   // subtree sums of body forces into crb storage (crb no longer needed)
   #pragma unroll 1
