@@ -29,14 +29,26 @@ typedef __attribute__((address_space(3))) float lfloat;
 // accesses, which also hold the LDS counter and so stall LDS waits behind memory latency).
 typedef __attribute__((address_space(1))) float gfloat;
 
-// Phase functions are out of line by default: each gets its own register allocation under the
-// 64-VGPR budget of 8 waves/SIMD.  Measured on C3 (8192 envs): out-of-line 2.19 ms per 10-step
-// launch vs 2.39 (inlined, 8 waves), 2.64 (inlined, 4 waves), 3.04 (inlined, 6 waves).
-// -DMRS_PHASE_INLINE builds the inlined variant.
-#ifdef MRS_PHASE_INLINE
-#define MRS_PHASE __forceinline__
+// Phase inlining follows the register budget of the group width: with G <= 16 (2 waves/SIMD, 256
+// VGPRs) every phase is inlined into the kernel (measured C3: 0.829 ms per launch vs 0.889 out of
+// line, and 157 vs 384 MB of writes per launch without the callee-saved spills); with G >= 32 (4-8
+// waves/SIMD, 64-128 VGPRs) phases stay out of line so each gets its own register allocation.
+// Call sites use clang's statement attributes; -DMRS_PHASE_INLINE / -DMRS_PHASE_OUTLINE force one
+// policy for A/B builds.
+#define MRS_PHASE
+#if defined(MRS_PHASE_INLINE)
+#define MRS_CALL(G, stmt) do { [[clang::always_inline]] stmt; } while (0)
+#elif defined(MRS_PHASE_OUTLINE)
+#define MRS_CALL(G, stmt) do { [[clang::noinline]] stmt; } while (0)
 #else
-#define MRS_PHASE __noinline__
+#define MRS_CALL(G, stmt)                          \
+  do {                                             \
+    if constexpr ((G) <= 16) {                     \
+      [[clang::always_inline]] stmt;               \
+    } else {                                       \
+      [[clang::noinline]] stmt;                    \
+    }                                              \
+  } while (0)
 #endif
 
 __device__ __forceinline__ void wsync() {
@@ -1166,7 +1178,8 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
     qfs = pas - s[L.qfrc_bias + j] + s[L.qfrc_applied + j] + qa;
     s[L.qfrc_smooth + j] = qfs;
   }
-  float qacc_s = chol_solve_lanes<G>(mp, s + L.L, qfs, lane);
+  float qacc_s;
+  MRS_CALL(G, qacc_s = chol_solve_lanes<G>(mp, s + L.L, qfs, lane));
   if (lane < nv) s[L.qacc_smooth + lane] = qacc_s;
   wsync();
   return qacc_s;
@@ -1927,25 +1940,28 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   PH_BEGIN();
-  kinematics<G>(ENV_ARGS);
+  MRS_CALL(G, kinematics<G>(ENV_ARGS));
   PH_END(ph_acc, PH_KIN);
-  com_pos<G>(ENV_ARGS);
+  MRS_CALL(G, com_pos<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COMPOS);
-  make_M<G>(ENV_ARGS);
+  MRS_CALL(G, make_M<G>(ENV_ARGS));
   PH_END(ph_acc, PH_MAKEM);
-  cholesky<G>(mp, s + L.M, s + L.L, lane);
+  MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
   PH_END(ph_acc, PH_CHOL);
-  com_vel<G>(ENV_ARGS);
+  MRS_CALL(G, com_vel<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COMVEL);
-  rne<G>(ENV_ARGS);
+  MRS_CALL(G, rne<G>(ENV_ARGS));
   PH_END(ph_acc, PH_RNE);
-  const float qacc_s = smooth_forces<G>(ENV_ARGS);
+  float qacc_s;
+  MRS_CALL(G, qacc_s = smooth_forces<G>(ENV_ARGS));
   PH_END(ph_acc, PH_SMOOTH);
-  const int ncon = (m.diag_skip & 2) ? 0 : collision<G>(ENV_ARGS);
+  int ncon = 0;
+  if (!(m.diag_skip & 2)) MRS_CALL(G, ncon = collision<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COLL);
-  const float qacc = (m.diag_skip & 4) ? qacc_s : constraints<G>(ENV_ARGS, ncon, qacc_s);
+  float qacc = qacc_s;
+  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = constraints<G>(ENV_ARGS, ncon, qacc_s));
   PH_END(ph_acc, PH_CONSTR);
-  if (!(m.diag_skip & 1)) sensors<G>(ENV_ARGS, sensordata);
+  if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
   PH_END(ph_acc, PH_SENS);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
@@ -1990,9 +2006,9 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
     // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
     if (lane < nv) s[L.M + lane * nv + lane] += h * dg;
     wsync();
-    cholesky<G>(mp, s + L.M, s + L.L, lane);
+    MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
     float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
-    qacc_int = chol_solve_lanes<G>(mp, s + L.L, rhs, lane);
+    MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + L.L, rhs, lane));
   }
   if (lane < nv) {
     s[L.qacc_ws + lane] = qacc;
@@ -2066,30 +2082,30 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
     if (!kForwardOnly) {
       if (any_bad<G>(ENV_ARGS, L.qpos, m.nq)) {
         ++w_pos;
-        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env<G>(ENV_ARGS); time = 0; }
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { [[clang::noinline]] reset_env<G>(ENV_ARGS); time = 0; }
       }
       if (any_bad<G>(ENV_ARGS, L.qvel, m.nv)) {
         ++w_vel;
-        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { reset_env<G>(ENV_ARGS); time = 0; }
+        if (!(m.disableflags & MRS_DSBL_AUTORESET)) { [[clang::noinline]] reset_env<G>(ENV_ARGS); time = 0; }
       }
     }
-    ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG);
+    MRS_CALL(G, ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG));
     if (kForwardOnly) break;
     bool redo = false;
     if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
       ++w_acc;
       if (!(m.disableflags & MRS_DSBL_AUTORESET)) {
-        reset_env<G>(ENV_ARGS);
+        [[clang::noinline]] reset_env<G>(ENV_ARGS);
         time = 0;
         redo = true;
       }
     }
     // forward() is entered by the whole wave; for envs that were not reset it recomputes the
     // same outputs from the same state
-    if (__any(redo)) ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG);
+    if (__any(redo)) { [[clang::noinline]] ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG); }  // rare
     {
       PH_BEGIN();
-      integrate<G>(ENV_ARGS);
+      MRS_CALL(G, integrate<G>(ENV_ARGS));
       PH_END(ph_acc, PH_INTEG);
     }
     time += m.timestep_d;

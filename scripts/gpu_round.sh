@@ -8,11 +8,9 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
-if [ "${AB:-}" != "" ]; then
-  for v in $AB; do
-    echo "== $v" >> gpurun_out/ab.log
-    MRS_LIB=$PWD/mujoco_ros2_simulation_amd/$v timeout -k 10 120 python bench.py --steps 30 --warmup 3 --no-cpu-baseline >> gpurun_out/ab.log 2>&1 || exit $?
-  done
-fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rocprof -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/rocprof.log 2>&1 || exit $?
+if [ "${PMC:-1}" = "1" ]; then
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || exit $?
+fi
 tail -3 gpurun_out/pytest_gpu.log
