@@ -66,6 +66,19 @@ def cpu_baseline(model, period: int, target_s: float):
                       f"(oracle/oracle.c), {cores} pthreads, {secs:.1f} s"}
 
 
+def measured_traffic(scene: str, envs: int, period: int):
+    """HBM bytes per launch of the step kernel from the committed rocprofv3 PMC summary of this same
+    bench command (scripts/gpu_round.sh -> scripts/pmc_summary.py -> profiles/<round>/pmc_c3.json);
+    None when no summary exists for this workload."""
+    if Path(scene).stem != "arm7_lidar" or envs != 8192 or period != 10:
+        return None, None
+    found = sorted(ROOT.glob("profiles/r*/pmc_c3.json"))
+    if not found:
+        return None, None
+    rec = json.loads(found[-1].read_text())
+    return rec["traffic_bytes_per_launch"], str(found[-1].relative_to(ROOT))
+
+
 def main():
     args = parse()
     import torch
@@ -139,6 +152,7 @@ def main():
     flops, survey_bytes = roofline.SURVEY_PER_ENV_STEP.get(Path(args.scene).stem, (detailed_flops, None))
     bytes_ = roofline.bytes_per_env_step(model, args.period)
     achieved_tf = n * args.period * flops / (kern_ms * 1e-3) / 1e12
+    traffic, traffic_src = measured_traffic(args.scene, n, args.period)
     result = {
         "metric": METRIC,
         "value": value,
@@ -166,7 +180,10 @@ def main():
             "peak": roofline.PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tf / roofline.PEAK_FP32_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": n * args.period * roofline.bytes_per_env_step(model, args.period),
             "kernel": "step_kernel<false> (fused 10-step launch)",
             "kernel_ms": kern_ms,
             "flops_per_env_step": flops,
