@@ -597,6 +597,35 @@ __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat
   }
   lane = __lane_id() & (G - 1);
   const int nv = load_model(mp).nv;
+  if constexpr (G == 16) {
+    // lane i keeps row i of A and then of L in registers; column k needs L[k][p] for p < k, which
+    // is lane k's register p: one DPP row broadcast each, no LDS round trip in the chain
+    float row[16];
+    unroll<16>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      row[p] = (p < nv && lane < nv) ? A[lane * nv + p] : 0.0f;
+    });
+    unroll<16>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if (k < nv) {
+        float t = row[k];
+        unroll<k>([&](auto pc) {
+          constexpr int p = decltype(pc)::value;
+          t -= row[p] * rowb<k>(row[p]);
+        });
+        const float dk = rowb<k>(t);
+        const float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
+        row[k] = lane == k ? lkk : (lane > k ? t / lkk : row[k]);
+      }
+    });
+    if (lane < nv)
+      unroll<16>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        if (p < nv) Lf[lane * nv + p] = p <= lane ? row[p] : 0.0f;
+      });
+    wsync();
+    return;
+  }
   #pragma unroll 1
   for (int k = 0; k < nv; ++k) {
     float t = 0;
@@ -619,6 +648,32 @@ __device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, con
   lane = __lane_id() & (G - 1);
   const int nv = load_model(mp).nv;
   float x = lane < nv ? b : 0.0f;
+  if constexpr (G == 16) {
+    // lane j prefetches row j of L (forward) and column j (backward); the substitution chains are
+    // DPP broadcasts and FMAs
+    float lrow[16], lcol[16], inv[16];
+    unroll<16>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      lrow[i] = (i < nv && lane < nv) ? Lf[lane * nv + i] : 0.0f;
+      lcol[i] = (i < nv && lane < nv) ? Lf[i * nv + lane] : 0.0f;
+      inv[i] = i < nv ? 1.0f / Lf[i * nv + i] : 0.0f;
+    });
+    unroll<16>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if (i < nv) {
+        const float xi = rowb<i>(x) * inv[i];
+        x = lane == i ? xi : (lane > i ? x - lrow[i] * xi : x);
+      }
+    });
+    unroll<16>([&](auto ic) {
+      constexpr int i = 15 - decltype(ic)::value;
+      if (i < nv) {
+        const float xi = rowb<i>(x) * inv[i];
+        x = lane == i ? xi : (lane < i ? x - lcol[i] * xi : x);
+      }
+    });
+    return lane < nv ? x : 0.0f;
+  }
   #pragma unroll 1
   for (int i = 0; i < nv; ++i) {
     float xi = gbcast<G>(x, i) / Lf[i * nv + i];
@@ -832,7 +887,7 @@ __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
     if (b != 0 && m.body_parentid[b] != 0) continue;
     float c[3] = {0, 0, 0};
     const int e = m.body_subtree_end[b];
-    #pragma unroll 1
+    #pragma unroll 4
     for (int k = b; k < e; ++k) {
       const float mk = m.body_mass[k];
       for (int i = 0; i < 3; ++i) c[i] += mk * s[L.xipos + 3 * k + i];
@@ -899,7 +954,7 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (b != 0) {
       const int e = m.body_subtree_end[b];
-      #pragma unroll 1
+      #pragma unroll 4
       for (int k = b; k < e; ++k)
         for (int i = 0; i < 10; ++i) acc[i] += s[L.cinert + 10 * k + i];
     }
@@ -1090,7 +1145,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
     float acc[6] = {0, 0, 0, 0, 0, 0};
     if (b != 0) {
       const int e = m.body_subtree_end[b];
-      #pragma unroll 1
+      #pragma unroll 4
       for (int k = b; k < e; ++k)
         for (int i = 0; i < 6; ++i) acc[i] += s[L.cfrc + 6 * k + i];
     }
@@ -1519,7 +1574,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     }
     float vel = 0, jqs = 0;
     const gfloat* Jr = J + r * nv;
-    #pragma unroll 1
+    #pragma unroll 4
     for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
     const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
     if (small) {
