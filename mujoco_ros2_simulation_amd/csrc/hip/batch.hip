@@ -405,7 +405,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // frame: unit axis a, in-plane direction b and normal c (the least-spread direction of the rays),
   // in-plane half-angle theta around a and out-of-plane slope eps = max |d.c| (a planar lidar fan
   // has eps ~ 0).  Blocks without a common origin, or wider than +-80 degrees, test every geom.
-  std::vector<float> rfblk;
+  std::vector<float> rfblk, rfblk_eps;
   d.nrfblk = 0;
   if (d.nrgeom <= 32 && d.nrf > 0) {
     d.nrfblk = (d.nrf + kRayBlock - 1) / kRayBlock;
@@ -483,8 +483,19 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
                                  static_cast<float>(axis[0]), static_cast<float>(axis[1]), static_cast<float>(axis[2]),
                                  static_cast<float>(bv[0]), static_cast<float>(bv[1]), static_cast<float>(bv[2]),
                                  static_cast<float>(c[0]), static_cast<float>(c[1]), static_cast<float>(c[2]),
-                                 static_cast<float>(theta + 1e-4), static_cast<float>(eps + 1e-6)});
+                                 static_cast<float>(std::cos(theta + 1e-4)), static_cast<float>(std::sin(theta + 1e-4))});
+      rfblk_eps.push_back(static_cast<float>(eps + 1e-6));
     }
+  }
+  // record: body, flag, origin[3], a[3], b[3], c[3], cos(theta), sin(theta); then eps per block
+  rfblk.insert(rfblk.end(), rfblk_eps.begin(), rfblk_eps.end());
+  // every ray of the lidar(s) from one point of one body: the pass loop reuses one frame
+  d.rf_common = d.nrfblk > 0 ? 1 : 0;
+  for (int blk = 0; blk < d.nrfblk && d.rf_common; ++blk) {
+    const float* r0 = &rfblk[0];
+    const float* ri = &rfblk[16 * blk];
+    int f; std::memcpy(&f, &ri[1], 4);
+    if (!f || std::memcmp(&ri[0], &r0[0], 4) != 0 || ri[2] != r0[2] || ri[3] != r0[3] || ri[4] != r0[4]) d.rf_common = 0;
   }
   P.addf(&d.rfblk, rfblk);
   // per-ray records: unit direction (z column of the site rotation) and sensordata address first

@@ -60,7 +60,7 @@ struct DevModel {
   ScratchLayout S;
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth, njump;
-  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other;
+  int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other, rf_common;
   // options
   int integrator, iterations, disableflags;
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
@@ -99,7 +99,9 @@ struct DevModel {
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;
   // ray blocks of kRayBlock consecutive rangefinders, 16 floats each: body, fan flag (int bits),
-  // origin[3], axis a[3], in-plane b[3], normal c[3] in the body frame, half-angle, out-of-plane eps
+  // origin[3], axis a[3], in-plane b[3], normal c[3] in the body frame, cos and sin of the in-plane
+  // half-angle; followed by nrfblk out-of-plane slopes eps.  rf_common: all blocks are fans from
+  // one point of one body
   CPtr<float> rfblk;
   // per rangefinder, 8 floats: unit direction[3], sensordata address (int bits), body (int bits),
   // origin[3], in the body frame

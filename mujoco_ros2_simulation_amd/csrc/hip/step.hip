@@ -1823,7 +1823,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       quat2mat(bmat, bq);
       const float ol[3] = {br[2], br[3], br[4]}, al[3] = {br[5], br[6], br[7]};
       const float bl[3] = {br[8], br[9], br[10]}, cl[3] = {br[11], br[12], br[13]};
-      const float theta = br[14], eps = br[15];
+      const float cth = br[14], sth = br[15], eps = m.rfblk[16 * m.nrfblk + blk];
       float o[3], a[3], bb[3], c[3];
       mat_vec(o, bmat, ol);
       for (int i = 0; i < 3; ++i) o[i] += s[L.xpos + 3 * b + i];
@@ -1854,9 +1854,13 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
               const float lv = sqrtf(l2);
               const float rr = rb + eps * (lv + rb);  // sphere radius plus out-of-plane drift
               const float wa = dot3(v, a), wb = dot3(v, bb), h = dot3(v, c);
-              const float wn = sqrtf(wa * wa + wb * wb);
+              const float wn2 = wa * wa + wb * wb;
+              // in-plane: angle(w, a) <= theta + asin(rb/|w|)  <=>  cos of it >= cos(theta + asin(rb/|w|)),
+              // i.e. wa >= cos(theta) sqrt(|w|^2 - rb^2) - sin(theta) rb (theta + asin <= pi here);
+              // rb is inflated by 0.1% + 1e-4 for rounding
+              const float rbi = rb * 1.001f + 1e-4f;
               cand = fabsf(h) <= rr &&
-                     (wn <= rb || fabsf(atan2f(wb, wa)) <= theta + asinf(fminf(1.0f, rb / wn)) + 1e-3f);
+                     (wn2 <= rbi * rbi || wa >= cth * sqrtf(wn2 - rbi * rbi) - sth * rbi);
             }
           }
         }
@@ -1894,7 +1898,10 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
     // shared body and origin for the whole pass when all its blocks are fans from one point
     int common_body = -1;
     float common_o[3] = {0, 0, 0};
-    if (m.nrfblk > 0) {
+    if (m.rf_common) {
+      common_body = __float_as_int(m.rfblk[0]);
+      common_o[0] = m.rfblk[2]; common_o[1] = m.rfblk[3]; common_o[2] = m.rfblk[4];
+    } else if (m.nrfblk > 0) {
       const int b0 = base / kRayBlock, b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
       const CPtr<float> r0 = m.rfblk + 16 * b0;
       bool same = __float_as_int(r0[1]) != 0;
