@@ -1747,6 +1747,9 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
   SUB_ADD(PH_SENS_SETUP, t_setup);
   unsigned long long t_geoms = SUB_T();
   // geoms some group of the wave still needs (union of the groups' level-1 masks), in order
+#if defined(MRS_DIAG_RAYS) && MRS_DIAG_RAYS == 1
+  gmask = 0;  // diagnostic build: setup and stores only
+#endif
   unsigned wmask = gmask;
   if constexpr (G < 64) {
 #pragma unroll
@@ -1812,6 +1815,9 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
   // of the geom; planes by the direction range of the fan), one bitmask per block; lanes over geoms
   const unsigned all = m.nrgeom >= 32 ? 0xffffffffu : ((1u << m.nrgeom) - 1u);
   unsigned long long t_l1 = SUB_T();
+#if defined(MRS_DIAG_RAYS) && MRS_DIAG_RAYS == 2
+  if (false)  // diagnostic build: no level-1 test (all geoms)
+#endif
   #pragma unroll 1
   for (int blk = 0; blk < m.nrfblk; ++blk) {
     const CPtr<float> br = m.rfblk + 16 * blk;
@@ -1876,7 +1882,11 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
   #pragma unroll 1
   for (int base = 0; base < m.nrf; base += G * R) {
     unsigned gmask = all;
+#if defined(MRS_DIAG_RAYS) && MRS_DIAG_RAYS == 2
+    if (false) {
+#else
     if (m.nrfblk > 0) {
+#endif
       gmask = 0;
       const int b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
       for (int blk = base / kRayBlock; blk < b1; ++blk) gmask |= static_cast<unsigned>(__float_as_int(s[L.rfmask + blk]));
