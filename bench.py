@@ -83,14 +83,9 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    from mujoco_ros2_simulation_amd import build, roofline, sim, synth
+    from mujoco_ros2_simulation_amd import build, roofline, shard, sim, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world, local = shard.init("nccl")   # RCCL over xGMI; only barrier and max-time reduce
     torch.cuda.set_device(local)
     if not sim.LIB_PATH.exists():
         if rank == 0:
@@ -100,7 +95,7 @@ def main():
 
     model = sim.Model.load(args.scene)
     n = args.envs
-    env_ids = rank * n + np.arange(n)
+    env_ids = shard.env_ids(rank, n)
     P = args.warmup + args.steps
     table = synth.ctrl_table(model, env_ids, P, args.period).astype(np.float32)   # [P, n, nu]
     qpos0 = synth.initial_qpos(model, env_ids)
@@ -137,10 +132,7 @@ def main():
         t1 = time.perf_counter()
     elapsed = t1 - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device=f"cuda:{local}")
 
     # sanity: states finite after the run (a diverged run would be invalid)
     q = batch.get(sim.FIELD_QPOS, 0, min(n, 64))

@@ -1,0 +1,54 @@
+"""Environment sharding across ranks: one process per GPU, each owning a contiguous
+range of global env ids; the synthetic inputs (synth.py) are keyed by global env id, so results do not
+depend on the rank count.  There is no collective in the data path: torch.distributed (RCCL over xGMI
+on GPUs, gloo on CPU) only times the job (barrier + max over ranks) and gathers the observations the
+host consumes to rank 0."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def env_ids(rank: int, envs_per_rank: int) -> np.ndarray:
+    """global env ids owned by `rank` (weak scaling: every rank owns envs_per_rank envs)"""
+    return rank * envs_per_rank + np.arange(envs_per_rank)
+
+
+def init(backend: str | None = None):
+    """(rank, world, local_rank) from the torchrun environment; joins the process group when world > 1
+    (backend 'nccl' = RCCL when GPUs are used, 'gloo' on CPU)"""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not dist.is_initialized():
+            be = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            kw = {"device_id": torch.device("cuda", local)} if be == "nccl" else {}
+            dist.init_process_group(be, **kw)
+    return rank, world, local
+
+
+def max_over_ranks(values, device="cpu"):
+    """element-wise max of a list of floats over all ranks (the job time is the slowest rank's)"""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu()]
+
+
+def gather_rows(t, dst: int = 0):
+    """concatenate every rank's [n_local, ...] tensor on rank `dst` in rank order (None elsewhere);
+    equal n_local on every rank"""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())] if dist.get_rank() == dst else None
+    dist.gather(t, parts, dst=dst)
+    return torch.cat(parts) if parts is not None else None
