@@ -228,8 +228,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   if (m.nv > 64) throw UnsupportedError("nv > 64 is not supported by the one-wave-per-env kernel");
   for (int s = 0; s < m.nsensor; ++s) {
     int t = m.sensor_type[s];
-    if (t == MRS_SENS_ACCELEROMETER || t == MRS_SENS_FORCE || t == MRS_SENS_TORQUE)
-      throw UnsupportedError("accelerometer/force/torque sensors are not implemented on the GPU path yet");
+    if (t == MRS_SENS_ACCELEROMETER) d.acc_sens |= 1;
+    if (t == MRS_SENS_FORCE || t == MRS_SENS_TORQUE) d.acc_sens |= 3;
   }
   d.nq = m.nq; d.nv = m.nv; d.nu = m.nu; d.nbody = m.nbody; d.njnt = m.njnt; d.ngeom = m.ngeom;
   d.nsite = m.nsite; d.ncam = m.ncam; d.nsensor = m.nsensor; d.nsensordata = m.nsensordata;

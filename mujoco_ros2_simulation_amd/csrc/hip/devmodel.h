@@ -63,6 +63,7 @@ struct DevModel {
   int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other, rf_common;
   // options
   int integrator, iterations, disableflags;
+  int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
   float timestep, tolerance, pgs_scale, gravity[3];
   double timestep_d;  // time is accumulated in fp64 like mjData.time

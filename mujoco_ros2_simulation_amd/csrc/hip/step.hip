@@ -1299,7 +1299,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
 // in lane r, row r's R, aref, b and friction-loss bound (0 for unilateral rows).  Returns qacc of
 // lane j's dof and writes qfrc_constraint.  Rows past the group's nefc (up to the wave's maximum)
 // are zero rows with R = 1, which never move.
-__device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, int nefc, int rmax,
+__device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
                                              float myR, float myaref, float myb, float myfl, float qacc_s,
                                              int lane) {
   const LdsLayout& L = m.L;
@@ -1403,6 +1403,13 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     if (r < rmax) qc += Jt[r] * f[r];
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
+  if (m.acc_sens & 2) {
+    // row forces for the contact forces of force/torque sensors (mj_rnePostConstraint)
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (lane == r && r < nefc) ff[r] = f[r];
+    });
+  }
   return qa;
 }
 
@@ -1488,11 +1495,13 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   // --- contact rows: lane per dof, loop over contacts
   #pragma unroll 1
   for (int c = 0; c < ncon; ++c) {
-    const gfloat* rec = scr + S.con + kConRec * c;
+    gfloat* rec = scr + S.con + kConRec * c;
     const int p = __float_as_int(rec[0]);
     const int dim = m.pair_dim[p];
     const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
     float cp[3] = {rec[2], rec[3], rec[4]};
+    // first efc row of this contact (rec[14]; -1 if the row cap cut its rows), for cfrc_ext
+    if (lane == 0) rec[14] = __int_as_float(nefc + (dim == 1 ? 1 : 4) <= m.max_efc ? nefc : -1);
     float jc[3] = {0, 0, 0};
     if (lane < nv) {
       float c1[3], c2[3];
@@ -1604,7 +1613,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     for (int bit = 16; bit >= 1; bit >>= 1)
       if (__ballot(mine >= rmax + bit) != 0) rmax += bit;
     if (small) {
-      const float qa = pgs_small16(m, s, J, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      const float qa = pgs_small16(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
       wsync();
       return qa;
     }
@@ -1687,6 +1696,102 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   }
   wsync();
   return qa;
+}
+
+// mj_rnePostConstraint (models with accelerometer / force / torque sensors only): cacc including qacc
+// (world: -gravity) into L.cacc; cfrc_ext from the contact forces (pyramid rows decoded to one world
+// force per row, applied at the contact point, moved to the subtree com; body2 +, body1 -);
+// cfrc_int = cinert cacc + cvel x* (cinert cvel) - cfrc_ext into L.cfrc, summed over subtrees into
+// L.crb.  Needs L.qacc and the row forces (efc_f) of this step.
+template <int G>
+__device__ MRS_PHASE void rne_post(ENV_PARAMS, int ncon) {
+  ENV_UNPACK;
+  float g0[6] = {0, 0, 0, 0, 0, 0};
+  if (!(m.disableflags & MRS_DSBL_GRAVITY)) { g0[3] = -m.gravity[0]; g0[4] = -m.gravity[1]; g0[5] = -m.gravity[2]; }
+  auto own = [&](int b, float v[6]) {
+    const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+    for (int j = da; j < da + nd; ++j) {
+      const float qv = s[L.qvel + j], qa = s[L.qacc + j];
+      for (int i = 0; i < 6; ++i) v[i] += s[L.cdofdot + 6 * j + i] * qv + s[L.cdof + 6 * j + i] * qa;
+    }
+  };
+  if (m.nbody <= G) {
+    const int b = lane;
+    float v[6] = {0, 0, 0, 0, 0, 0};
+    if (b >= 1 && b < m.nbody) own(b, v);
+    tree_prefix6<G>(m, s + L.cacc, b, v);
+    if (b < m.nbody)
+      for (int i = 0; i < 6; ++i) s[L.cacc + 6 * b + i] = v[i] + g0[i];
+    wsync();
+  } else {
+    if (lane < 6) s[L.cacc + lane] = g0[lane];
+    wsync();
+    for (int lev = 1; lev <= m.max_depth; ++lev) {
+      const int a0 = m.level_adr[lev], nl = m.level_num[lev];
+      #pragma unroll 1
+      for (int k = lane; k < nl; k += G) {
+        const int b = m.level_body[a0 + k];
+        float v[6];
+        for (int i = 0; i < 6; ++i) v[i] = s[L.cacc + 6 * m.body_parentid[b] + i];
+        own(b, v);
+        for (int i = 0; i < 6; ++i) s[L.cacc + 6 * b + i] = v[i];
+      }
+      wsync();
+    }
+  }
+  const gfloat* ff = scr + S.efc_f;
+  #pragma unroll 1
+  for (int b = lane; b < m.nbody; b += G) {
+    float fi[6] = {0, 0, 0, 0, 0, 0};
+    if (b != 0) {
+      float ca[6], cv[6], f1[6], t[6], f2[6];
+      for (int i = 0; i < 6; ++i) { ca[i] = s[L.cacc + 6 * b + i]; cv[i] = s[L.cvel + 6 * b + i]; }
+      mul_inert_vec(f1, s + L.cinert + 10 * b, ca);
+      mul_inert_vec(t, s + L.cinert + 10 * b, cv);
+      cross_force(f2, cv, t);
+      for (int i = 0; i < 6; ++i) fi[i] = f1[i] + f2[i];
+      const int rt = m.body_rootid[b];
+      const float c3[3] = {s[L.scom + 3 * rt], s[L.scom + 3 * rt + 1], s[L.scom + 3 * rt + 2]};
+      #pragma unroll 1
+      for (int c = 0; c < ncon; ++c) {
+        const gfloat* rec = scr + S.con + kConRec * c;
+        const int p = __float_as_int(rec[0]);
+        const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+        const int r0 = __float_as_int(rec[14]);
+        if ((b != b1 && b != b2) || r0 < 0) continue;
+        // contact-frame force (mju_decodePyramid), then world: frame' lfrc
+        float lf[3] = {0, 0, 0};
+        if (m.pair_dim[p] == 1) {
+          lf[0] = ff[r0];
+        } else {
+          for (int k = 0; k < 2; ++k) {
+            const float fp = ff[r0 + 2 * k], fm = ff[r0 + 2 * k + 1];
+            lf[0] += fp + fm;
+            lf[k + 1] = (fp - fm) * m.pair_friction[3 * p + k];
+          }
+        }
+        float F[3];
+        for (int i = 0; i < 3; ++i) F[i] = rec[5 + i] * lf[0] + rec[8 + i] * lf[1] + rec[11 + i] * lf[2];
+        const float d[3] = {rec[2] - c3[0], rec[3] - c3[1], rec[4] - c3[2]};
+        float tq[3];
+        cross3(tq, d, F);  // torque about the subtree com: (pos - com) x F
+        const float sg = b == b2 ? -1.0f : 1.0f;  // cfrc_int subtracts cfrc_ext (+ for body2)
+        for (int i = 0; i < 3; ++i) { fi[i] += sg * tq[i]; fi[3 + i] += sg * F[i]; }
+      }
+    }
+    for (int i = 0; i < 6; ++i) s[L.cfrc + 6 * b + i] = fi[i];
+  }
+  wsync();
+  #pragma unroll 1
+  for (int b = lane; b < m.nbody; b += G) {
+    float acc[6] = {0, 0, 0, 0, 0, 0};
+    const int e = b == 0 ? m.nbody : m.body_subtree_end[b];  // the world's subtree is everything
+    #pragma unroll 4
+    for (int k = b; k < e; ++k)
+      for (int i = 0; i < 6; ++i) acc[i] += s[L.cfrc + 6 * k + i];
+    for (int i = 0; i < 6; ++i) s[L.crb + 6 * b + i] = acc[i];
+  }
+  wsync();
 }
 
 // rays per lane per pass over the geoms: 4 with lane groups (measured C3: 1.59 ms per launch vs
@@ -1939,6 +2044,47 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       case MRS_SENS_JOINTPOS: out[0] = s[L.qpos + m.jnt_qposadr[id]]; break;
       case MRS_SENS_JOINTVEL: out[0] = s[L.qvel + m.jnt_dofadr[id]]; break;
       case MRS_SENS_ACTUATORFRC: out[0] = s[L.act_force + id]; break;
+      case MRS_SENS_ACCELEROMETER:
+      case MRS_SENS_FORCE:
+      case MRS_SENS_TORQUE: {
+        // mj_sensorAcc: com-based quantities moved to the site (mju_transformSpatial), site frame
+        const int b = m.site_bodyid[id], rt = m.body_rootid[b];
+        float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+        float sp[3] = {m.site_pos[3 * id], m.site_pos[3 * id + 1], m.site_pos[3 * id + 2]};
+        float sq[4] = {m.site_quat[4 * id], m.site_quat[4 * id + 1], m.site_quat[4 * id + 2], m.site_quat[4 * id + 3]};
+        float r[3], q[4], sm[9], d[3], o3[3];
+        rot_quat(r, sp, bq);
+        for (int i = 0; i < 3; ++i) d[i] = s[L.xpos + 3 * b + i] + r[i] - s[L.scom + 3 * rt + i];
+        quat_mul(q, bq, sq);
+        quat2mat(sm, q);
+        if (t == MRS_SENS_ACCELEROMETER) {
+          // a_lin - d x a_ang + w x (v_lin - d x w), then into the site frame
+          float w3[3], v3[3], a3[3], dw[3], da[3], acc[3];
+          for (int i = 0; i < 3; ++i) {
+            w3[i] = s[L.cvel + 6 * b + i];
+            v3[i] = s[L.cvel + 6 * b + 3 + i];
+            a3[i] = s[L.cacc + 6 * b + i];
+          }
+          cross3(dw, d, w3);
+          cross3(da, d, a3);
+          for (int i = 0; i < 3; ++i) v3[i] -= dw[i];
+          cross3(acc, w3, v3);
+          for (int i = 0; i < 3; ++i) acc[i] += s[L.cacc + 6 * b + 3 + i] - da[i];
+          matT_vec(o3, sm, acc);
+        } else {
+          float tq[3], f3[3], df[3];
+          for (int i = 0; i < 3; ++i) { tq[i] = s[L.crb + 6 * b + i]; f3[i] = s[L.crb + 6 * b + 3 + i]; }
+          if (t == MRS_SENS_FORCE) {
+            matT_vec(o3, sm, f3);
+          } else {
+            cross3(df, d, f3);
+            for (int i = 0; i < 3; ++i) tq[i] -= df[i];
+            matT_vec(o3, sm, tq);
+          }
+        }
+        for (int i = 0; i < 3; ++i) out[i] = o3[i];
+        break;
+      }
       case MRS_SENS_FRAMEPOS:
       case MRS_SENS_FRAMEQUAT:
       case MRS_SENS_GYRO: {
@@ -2033,10 +2179,11 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   float qacc = qacc_s;
   if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = constraints<G>(ENV_ARGS, ncon, qacc_s));
   PH_END(ph_acc, PH_CONSTR);
-  if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
-  PH_END(ph_acc, PH_SENS);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
+  if (m.acc_sens && !(m.disableflags & MRS_DSBL_SENSOR)) MRS_CALL(G, rne_post<G>(ENV_ARGS, ncon));
+  if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
+  PH_END(ph_acc, PH_SENS);
   return ncon;
 }
 

@@ -31,6 +31,8 @@ typedef struct {
   /* kinematics */
   double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis, *geom_xpos, *geom_xmat;
   double *subtree_com, *cinert, *cdof, *crb, *cvel, *cdof_dot, *cacc, *cfrc;
+  double *cacc_full, *cfrc_ext, *cfrc_int; /* mj_rnePostConstraint outputs */
+  int efc_con_first[MAXCON];              /* first efc row of each contact */
   /* dynamics */
   double *M, *L, *qfrc_bias, *qfrc_passive, *qfrc_smooth, *qacc_smooth, *qfrc_constraint,
       *actuator_force, *tmp, *tmp2, *Mi, *Li;
@@ -150,6 +152,7 @@ orc_data* orc_make_data(const mrs_model_view* m) {
   w->subtree_com = dalloc(3 * nb); w->cinert = dalloc(10 * nb); w->cdof = dalloc(6 * nv);
   w->crb = dalloc(10 * nb); w->cvel = dalloc(6 * nb); w->cdof_dot = dalloc(6 * nv);
   w->cacc = dalloc(6 * nb); w->cfrc = dalloc(6 * nb);
+  w->cacc_full = dalloc(6 * nb); w->cfrc_ext = dalloc(6 * nb); w->cfrc_int = dalloc(6 * nb);
   w->M = dalloc(nv * nv); w->L = dalloc(nv * nv); w->Mi = dalloc(nv * nv); w->Li = dalloc(nv * nv);
   w->qfrc_bias = dalloc(nv); w->qfrc_passive = dalloc(nv); w->qfrc_smooth = dalloc(nv);
   w->qacc_smooth = dalloc(nv); w->qfrc_constraint = dalloc(nv); w->actuator_force = dalloc(m->nu);
@@ -169,7 +172,7 @@ void orc_free_data(orc_data* d) {
                     w->cvel, w->cdof_dot, w->cacc, w->cfrc, w->M, w->L, w->Mi, w->Li,
                     w->qfrc_bias, w->qfrc_passive, w->qfrc_smooth, w->qacc_smooth,
                     w->qfrc_constraint, w->actuator_force, w->tmp, w->tmp2, w->efc_J,
-                    w->efc_MinvJT, w->AR};
+                    w->efc_MinvJT, w->AR, w->cacc_full, w->cfrc_ext, w->cfrc_int};
   for (size_t i = 0; i < sizeof arrs / sizeof arrs[0]; ++i) free(arrs[i]);
   free(w);
   free(d->qpos); free(d->qvel); free(d->ctrl); free(d->qfrc_applied); free(d->qacc_warmstart);
@@ -872,6 +875,7 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
       double dc[3] = {col2[0] - col1[0], col2[1] - col1[1], col2[2] - col1[2]};
       for (int r = 0; r < 3; ++r) Jc[r * nv + j] = dot3(con->frame + 3 * r, dc);
     }
+    w->efc_con_first[c] = w->nefc;
     if (con->dim == 1) {
       add_row(w, nv, EFC_CONTACT, c, Jc, con->dist, con->includemargin, 0, tran, con->solref, con->solimp);
     } else {
@@ -1118,9 +1122,109 @@ double orc_ray(const mrs_model_view* m, orc_data* d, const double pnt[3], const 
 
 /* ------------------------------------------------------------------------ sensors
  * mj_sensorPos/Vel [upstream engine_sensor.c] for the implemented types */
+/* mju_transformSpatial [upstream engine_util_spatial.c]: move a com-based motion (flg_force 0) or
+ * force (flg_force 1) vector [rot(3), lin(3)] from oldpos to newpos, then express it in the frame
+ * rot (if given) */
+static void transform_spatial(double res[6], const double vec[6], int flg_force, const double newpos[3],
+                              const double oldpos[3], const double* rot) {
+  double dif[3] = {newpos[0] - oldpos[0], newpos[1] - oldpos[1], newpos[2] - oldpos[2]}, cr[3], tran[6];
+  memcpy(tran, vec, sizeof tran);
+  if (flg_force) {
+    cross3(cr, dif, vec + 3);
+    for (int i = 0; i < 3; ++i) tran[i] = vec[i] - cr[i];
+  } else {
+    cross3(cr, dif, vec);
+    for (int i = 0; i < 3; ++i) tran[3 + i] = vec[3 + i] - cr[i];
+  }
+  if (rot) {
+    matT_vec(res, rot, tran);
+    matT_vec(res + 3, rot, tran + 3);
+  } else {
+    memcpy(res, tran, sizeof tran);
+  }
+}
+
+/* mj_rnePostConstraint [upstream engine_core_smooth.c]: cacc including qacc (world: -gravity);
+ * cfrc_ext from the contact forces (mj_contactForce: pyramidal forces decoded to the contact frame,
+ * rotated to world, moved to the subtree com; body2 +, body1 -); cfrc_int = cinert cacc +
+ * cvel x* (cinert cvel) - cfrc_ext, summed from the leaves to the roots */
+static void rne_post_constraint(const mrs_model_view* m, orc_data* d) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nb = m->nbody;
+  memset(w->cacc_full, 0, 6 * sizeof(double));
+  if (!(m->disableflags & MRS_DSBL_GRAVITY))
+    for (int i = 0; i < 3; ++i) w->cacc_full[3 + i] = -m->gravity[i];
+  memset(w->cfrc_ext, 0, 6 * (size_t)nb * sizeof(double));
+  for (int c = 0; c < w->ncon; ++c) {
+    const orc_contact* con = &w->con[c];
+    const double* f = w->efc_force + w->efc_con_first[c];
+    double lfrc[3] = {0, 0, 0};
+    if (con->dim == 1) {
+      lfrc[0] = f[0];
+    } else {
+      for (int i = 0; i < con->dim - 1; ++i) {
+        lfrc[0] += f[2 * i] + f[2 * i + 1];
+        lfrc[i + 1] = (f[2 * i] - f[2 * i + 1]) * con->friction[i];
+      }
+    }
+    double cfrc[6] = {0, 0, 0, 0, 0, 0}, com6[6];
+    matT_vec(cfrc + 3, con->frame, lfrc); /* world force; no torsional/rolling part at condim <= 3 */
+    for (int side = 0; side < 2; ++side) {
+      int k = m->geom_bodyid[con->geom[side]];
+      if (!k) continue;
+      transform_spatial(com6, cfrc, 1, w->subtree_com + 3 * m->body_rootid[k], con->pos, NULL);
+      for (int i = 0; i < 6; ++i) w->cfrc_ext[6 * k + i] += side ? com6[i] : -com6[i];
+    }
+  }
+  memset(w->cfrc_int, 0, 6 * sizeof(double));
+  for (int b = 1; b < nb; ++b) {
+    double* ca = w->cacc_full + 6 * b;
+    memcpy(ca, w->cacc_full + 6 * m->body_parentid[b], 6 * sizeof(double));
+    int da = m->body_dofadr[b];
+    for (int k = 0; k < m->body_dofnum[b]; ++k)
+      for (int i = 0; i < 6; ++i)
+        ca[i] += w->cdof_dot[6 * (da + k) + i] * d->qvel[da + k] + w->cdof[6 * (da + k) + i] * d->qacc[da + k];
+    double f1[6], t[6], f2[6];
+    mul_inert_vec(f1, w->cinert + 10 * b, ca);
+    mul_inert_vec(t, w->cinert + 10 * b, w->cvel + 6 * b);
+    cross_force(f2, w->cvel + 6 * b, t);
+    for (int i = 0; i < 6; ++i) w->cfrc_int[6 * b + i] = f1[i] + f2[i] - w->cfrc_ext[6 * b + i];
+  }
+  for (int b = nb - 1; b > 0; --b)
+    for (int i = 0; i < 6; ++i) w->cfrc_int[6 * m->body_parentid[b] + i] += w->cfrc_int[6 * b + i];
+}
+
+/* mj_sensorAcc for a site [upstream engine_sensor.c]: accelerometer = linear acceleration at the site
+ * in the site frame (mj_objectAcceleration, local: com-based cacc/cvel moved to the site, plus
+ * w x v); force / torque = cfrc_int of the site's body moved to the site, in the site frame */
+static void acc_sensor(const mrs_model_view* m, orc_data* d, int type, int site, double out[3]) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int b = m->site_bodyid[site];
+  double pos[3], mat[9], v6[6], a6[6];
+  site_pose(m, w, site, pos, mat);
+  const double* com = w->subtree_com + 3 * m->body_rootid[b];
+  if (type == MRS_SENS_ACCELEROMETER) {
+    transform_spatial(v6, w->cvel + 6 * b, 0, pos, com, mat);
+    transform_spatial(a6, w->cacc_full + 6 * b, 0, pos, com, mat);
+    double cr[3];
+    cross3(cr, v6, v6 + 3);
+    for (int i = 0; i < 3; ++i) out[i] = a6[3 + i] + cr[i];
+  } else {
+    transform_spatial(a6, w->cfrc_int + 6 * b, 1, pos, com, mat);
+    memcpy(out, type == MRS_SENS_FORCE ? a6 + 3 : a6, 3 * sizeof(double));
+  }
+}
+
 static void sensors(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   if (m->disableflags & MRS_DSBL_SENSOR) return;
+  for (int s = 0; s < m->nsensor; ++s) {
+    int t = m->sensor_type[s];
+    if (t == MRS_SENS_ACCELEROMETER || t == MRS_SENS_FORCE || t == MRS_SENS_TORQUE) {
+      rne_post_constraint(m, d);
+      break;
+    }
+  }
   for (int s = 0; s < m->nsensor; ++s) {
     double* out = d->sensordata + m->sensor_adr[s];
     int id = m->sensor_objid[s];
@@ -1163,6 +1267,9 @@ static void sensors(const mrs_model_view* m, orc_data* d) {
         matT_vec(out, mat, w->cvel + 6 * m->site_bodyid[id]);
         break;
       }
+      case MRS_SENS_ACCELEROMETER:
+      case MRS_SENS_FORCE:
+      case MRS_SENS_TORQUE: acc_sensor(m, d, m->sensor_type[s], id, out); break;
       default: memset(out, 0, m->sensor_dim[s] * sizeof(double));
     }
     if (m->sensor_cutoff[s] > 0 && m->sensor_type[s] != MRS_SENS_RANGEFINDER &&

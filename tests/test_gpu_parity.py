@@ -188,3 +188,31 @@ def test_autoreset_on_nan():
     w = b.get(sim.FIELD_WARNING)
     assert w[1, 0] == 1 and w[0, 0] == 0 and w[2, 0] == 0
     assert np.all(np.isfinite(b.get(sim.FIELD_QPOS)))
+
+
+IMU_FT = ARM7.parent / "imu_ft.xml"
+
+
+def test_imu_ft_sensor_parity():
+    """row f2: framequat/gyro/accelerometer/force/torque (mj_rnePostConstraint + mj_sensorAcc) on the
+    GPU against the oracle over a seeded rollout with motor torques and a box landing on the floor
+    (contact forces enter cfrc_ext).  Acceleration-level outputs tolerate 1e-3 of their scale: they
+    difference nearly balanced fp32 forces."""
+    model = sim.Model.load(IMU_FT)
+    n, steps, period = 16, 400, 10
+    envs = np.arange(n)
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    checkpoints = [1, 50, 200, steps]
+    ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
+    got = _gpu_rollout(model, qpos0, table, period, checkpoints)
+    for c in checkpoints:
+        q_ref, v_ref, s_ref = ref[c]
+        q, v, s = got[c]
+        assert np.max(np.abs(q - q_ref) / _scale(q_ref)) <= 1e-4, c
+        for i in range(model.nsensor):
+            a, dim = model.sensor_adr[i], model.sensor_dim[i]
+            sr, sg = s_ref[:, a:a + dim], s[:, a:a + dim]
+            scale = max(1.0, float(np.max(np.abs(sr))))
+            err = float(np.max(np.abs(sg - sr))) / scale
+            assert err <= 1e-3, (c, model.id2name(sim.OBJ_SENSOR, i), err)

@@ -2,6 +2,8 @@
 closed-form known answers and the reference's behavioural pin
 (test/src/robot_launch_test.py:112-132).  MuJoCo itself is not available anywhere in this pipeline
 (SURVEY.md §8c), so beyond these pins the oracle is 'parity unpinned' against upstream mj_step."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -142,3 +144,54 @@ def test_contact_sphere_on_plane():
     g, dist, pos, frame = d.contacts()
     assert list(g[0]) == [0, 1]
     np.testing.assert_allclose(frame[0, :3], [0, 0, 1], atol=1e-12)
+
+
+# ---------------------------------------------------------------- IMU / force-torque (row f2)
+IMU_FT = Path(__file__).resolve().parents[1] / "scenes" / "imu_ft.xml"
+
+
+def _sens(m, d, name):
+    from mujoco_ros2_simulation_amd import sim
+    i = m.name2id(sim.OBJ_SENSOR, name)
+    a = m.sensor_adr[i]
+    return d.sensordata[a:a + m.sensor_dim[i]].copy()
+
+
+def _quat2mat(q):
+    w, x, y, z = q
+    return np.array([[w * w + x * x - y * y - z * z, 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), w * w - x * x + y * y - z * z, 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), w * w - x * x - y * y + z * z]])
+
+
+def test_acc_sensors_welded_body_at_rest():
+    """a body welded to the world: accelerometer = R' (0,0,g); force = m R' (0,0,g) (the support);
+    torque about the site = R' ((c - p) x f)  (mj_sensorAcc conventions)"""
+    from mujoco_ros2_simulation_amd import sim
+    m = sim.Model.load(IMU_FT)
+    d = binding.OracleData(m)
+    d.forward()
+    Rb = _quat2mat([0.9238795, 0, 0.3826834, 0])
+    Rs = _quat2mat([0.7071068, 0.7071068, 0, 0])
+    R = Rb @ Rs
+    g = np.array([0, 0, 9.81])
+    f = 2.0 * g
+    c = np.array([0.5, 0.5, 1.0])
+    p = c + Rb @ np.array([0.1, 0, 0.05])
+    np.testing.assert_allclose(_sens(m, d, "fixed_accel"), R.T @ g, atol=1e-5)
+    np.testing.assert_allclose(_sens(m, d, "fixed_force"), R.T @ f, atol=1e-5)
+    np.testing.assert_allclose(_sens(m, d, "fixed_torque"), R.T @ np.cross(c - p, f), atol=1e-5)
+
+
+def test_acc_sensors_free_fall_and_rest_on_floor():
+    """free fall reads zero specific force; resting on the floor the accelerometer reads +g and the
+    free body's interaction force is ~0 (gravity balanced by the contact: cfrc_ext sign)"""
+    from mujoco_ros2_simulation_amd import sim
+    m = sim.Model.load(IMU_FT)
+    d = binding.OracleData(m)
+    d.forward()
+    np.testing.assert_allclose(_sens(m, d, "box_accel"), 0, atol=1e-9)
+    np.testing.assert_allclose(_sens(m, d, "box_force"), 0, atol=1e-9)
+    d.step(2000)
+    np.testing.assert_allclose(_sens(m, d, "box_accel"), [0, 0, 9.81], atol=2e-3)
+    assert np.linalg.norm(_sens(m, d, "box_force")) < 1e-3 * 1.5 * 9.81
