@@ -352,3 +352,35 @@ def test_physics_thread_tracks_wall_clock(pkg_dir):
     _, n = s.clock()
     assert n > 10
     s.close()
+
+
+@pytest.mark.gpu
+def test_imu_ft_read_mapping():
+    """read() maps IMU sensordata in (w, x, y, z) order and negates force/torque
+    (reference src/mujoco_system_interface.cpp:1069-1095)"""
+    import ctypes
+    from mujoco_ros2_simulation_amd import plugin, sim
+    s = plugin.System(ROOT / "tests" / "fixtures" / "imu_ft.urdf", {}, {"mrs_tests": str(ROOT)})
+    s.set_param("physics_thread", "false")
+    assert s.on_init() == plugin.SUCCESS
+    assert len(s.state_names) == 6 + 10 + 6
+    s.set_command("j1/effort", 0.3)
+    s.set_command("j2/effort", -0.2)
+    for _ in range(25):
+        s.cycle(0.02, 10)
+    m = sim.Model.load(ROOT / "scenes" / "imu_ft.xml")
+    sd = np.zeros(m.nsensordata)
+    rc = sim.lib().mrs_batch_get_field(s.batch_handle(), sim.FIELD_SENSORDATA, sd.ctypes.data_as(ctypes.c_void_p), 0, 1)
+    assert rc == 0
+
+    def val(name):
+        i = m.name2id(sim.OBJ_SENSOR, name)
+        return sd[m.sensor_adr[i]:m.sensor_adr[i] + m.sensor_dim[i]]
+
+    q = val("imu_quat")
+    assert [s.state(f"imu/orientation.{c}") for c in "wxyz"] == pytest.approx(list(q), abs=1e-12)
+    assert [s.state(f"imu/angular_velocity.{c}") for c in "xyz"] == pytest.approx(list(val("imu_gyro")), abs=1e-12)
+    assert [s.state(f"imu/linear_acceleration.{c}") for c in "xyz"] == pytest.approx(list(val("imu_accel")), abs=1e-12)
+    assert [s.state(f"ft/force.{c}") for c in "xyz"] == pytest.approx(list(-val("ft_force")), abs=1e-12)
+    assert [s.state(f"ft/torque.{c}") for c in "xyz"] == pytest.approx(list(-val("ft_torque")), abs=1e-12)
+    assert abs(np.linalg.norm(q) - 1) < 1e-5 and np.linalg.norm(val("imu_gyro")) > 0.1
