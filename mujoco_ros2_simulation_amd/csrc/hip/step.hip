@@ -1523,7 +1523,9 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       for (int k = 1; k < 3; ++k)
         for (int sg = 1; sg >= -1; sg -= 2) {
           if (nefc >= m.max_efc) continue;
-          const float mu = m.pair_friction[3 * p + k - 1];
+          // both tangent directions use the sliding coefficient (contact friction is
+          // (slide, slide, spin, roll, roll) from the geoms' (slide, spin, roll), mj_setContact)
+          const float mu = m.pair_friction[3 * p];
           if (lane < nv) J[nefc * nv + lane] = jc[0] + sg * mu * jc[k];
           if (lane == 0) {
             type[nefc] = __int_as_float(EFC_CONTACT * 65536 + c);
@@ -1558,11 +1560,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
       diag = tran;
       if (m.pair_dim[p] == 3) {
-        // edge k of this row: rows of a contact are laid out k=1:(+,-), k=2:(+,-)
-        int first = r;
-        while (first > 0 && __float_as_int(type[first - 1]) == code) --first;
-        const int k = 1 + (r - first) / 2;
-        const float mu = m.pair_friction[3 * p + k - 1];
+        const float mu = m.pair_friction[3 * p];  // sliding, for both tangent directions
         diag = tran * (1 + mu * mu);
       }
     }
@@ -1767,7 +1765,7 @@ __device__ MRS_PHASE void rne_post(ENV_PARAMS, int ncon) {
           for (int k = 0; k < 2; ++k) {
             const float fp = ff[r0 + 2 * k], fm = ff[r0 + 2 * k + 1];
             lf[0] += fp + fm;
-            lf[k + 1] = (fp - fm) * m.pair_friction[3 * p + k];
+            lf[k + 1] = (fp - fm) * m.pair_friction[3 * p];
           }
         }
         float F[3];

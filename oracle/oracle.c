@@ -881,9 +881,11 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
     } else {
       for (int k = 1; k < 3; ++k)
         for (int s = 1; s >= -1; s -= 2) {
-          for (int j = 0; j < nv; ++j) J[j] = Jc[j] + s * con->friction[k - 1] * Jc[k * nv + j];
+          /* both tangent directions use the sliding coefficient: a contact's friction is
+           * (slide, slide, spin, roll, roll) from the geoms' (slide, spin, roll) [upstream mj_setContact] */
+          for (int j = 0; j < nv; ++j) J[j] = Jc[j] + s * con->friction[0] * Jc[k * nv + j];
           add_row(w, nv, EFC_CONTACT, c, J, con->dist, con->includemargin, 0,
-                  tran * (1 + con->friction[k - 1] * con->friction[k - 1]), con->solref, con->solimp);
+                  tran * (1 + con->friction[0] * con->friction[0]), con->solref, con->solimp);
         }
     }
     free(Jc);
@@ -1164,7 +1166,7 @@ static void rne_post_constraint(const mrs_model_view* m, orc_data* d) {
     } else {
       for (int i = 0; i < con->dim - 1; ++i) {
         lfrc[0] += f[2 * i] + f[2 * i + 1];
-        lfrc[i + 1] = (f[2 * i] - f[2 * i + 1]) * con->friction[i];
+        lfrc[i + 1] = (f[2 * i] - f[2 * i + 1]) * con->friction[0];  /* tangent mu = sliding */
       }
     }
     double cfrc[6] = {0, 0, 0, 0, 0, 0}, com6[6];
@@ -1426,6 +1428,19 @@ void orc_kinematics(const mrs_model_view* m, orc_data* d, double* xpos, double* 
   if (xquat) memcpy(xquat, w->xquat, 4 * m->nbody * sizeof(double));
   if (geom_xpos) memcpy(geom_xpos, w->geom_xpos, 3 * m->ngeom * sizeof(double));
   if (geom_xmat) memcpy(geom_xmat, w->geom_xmat, 9 * m->ngeom * sizeof(double));
+}
+
+/* debugging / tests: constraint rows of the last forward (type, force, aref, R, pos, J) */
+int orc_efc(orc_data* d, int nv, int max, int* type, double* force, double* aref, double* R, double* pos,
+            double* J) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int n = w->nefc < max ? w->nefc : max;
+  for (int r = 0; r < n; ++r) {
+    type[r] = w->efc_type[r]; force[r] = w->efc_force[r]; aref[r] = w->efc_aref[r];
+    R[r] = w->efc_R[r]; pos[r] = w->efc_pos[r];
+    memcpy(J + (size_t)r * nv, w->efc_J + (size_t)r * nv, nv * sizeof(double));
+  }
+  return w->nefc;
 }
 
 int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, double* frame) {

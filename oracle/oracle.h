@@ -51,6 +51,8 @@ double orc_ray(const mrs_model_view* m, orc_data* d, const double pnt[3], const 
 /* depth image (H*W floats, ROS row order, eye-space z, `far` on miss) of camera `cam` */
 void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out);
 /* contacts of the last forward: up to `max` records of {geom1, geom2, dist, pos[3], frame[9]} */
+int orc_efc(orc_data* d, int nv, int max, int* type, double* force, double* aref, double* R, double* pos,
+            double* J);
 int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, double* frame);
 
 /* CPU baseline: step `n_envs` independent copies `n_steps` times with ctrl held per period of

@@ -195,3 +195,34 @@ def test_acc_sensors_free_fall_and_rest_on_floor():
     d.step(2000)
     np.testing.assert_allclose(_sens(m, d, "box_accel"), [0, 0, 9.81], atol=2e-3)
     assert np.linalg.norm(_sens(m, d, "box_force")) < 1e-3 * 1.5 * 9.81
+
+
+# ---------------------------------------------------------------- friction (pyramidal, condim 3)
+_SLIDE = """<mujoco><option timestep="0.002"/><worldbody><geom type="plane" size="0 0 1"/>
+<body pos="0 0 0.1"><freejoint/><geom type="{g}" size="{s}" mass="1"/></body></worldbody></mujoco>"""
+
+
+def test_friction_box_stops_at_mu_g():
+    """a box launched at 1 m/s on mu = 1 stops after ~v0^2 / (2 mu g) = 5.1 cm along either tangent
+    direction (both pyramid edges use the sliding coefficient; the impulsive start makes the
+    pyramidal contact hop, so the bounds are loose)"""
+    for axis in (0, 1):
+        m = sim.Model.from_string(_SLIDE.format(g="box", s="0.1 0.1 0.1"))
+        d = binding.OracleData(m)
+        d.step(200)
+        x0 = d.qpos[axis]
+        d.qvel[axis] = 1.0
+        d.step(150)  # 0.3 s
+        assert abs(d.qvel[axis]) < 0.01
+        assert 0.03 < d.qpos[axis] - x0 < 0.1
+
+
+def test_friction_sphere_rolls_at_five_sevenths():
+    """a solid sphere launched sliding settles into rolling without slip at v = 5/7 v0"""
+    m = sim.Model.from_string(_SLIDE.format(g="sphere", s="0.1"))
+    d = binding.OracleData(m)
+    d.step(200)
+    d.qvel[0] = 1.0
+    d.step(500)
+    assert abs(d.qvel[0] - 5 / 7) < 0.01
+    assert abs(d.qvel[4] * 0.1 - d.qvel[0]) < 0.01   # rolling: omega r = v
