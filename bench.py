@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--scene", default=str(ROOT / "scenes" / "arm7_lidar.xml"))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    p.add_argument("--config", choices=["c3", "c4"], default="c3",
+                   help="c3: the BASELINE metric (default); c4: mobile base + lidar + 640x480 depth camera")
+    p.add_argument("--render-every", type=int, default=100, help="C4: physics steps between depth frames")
     return p.parse_args()
 
 
@@ -79,8 +82,89 @@ def measured_traffic(scene: str, envs: int, period: int):
     return rec["traffic_bytes_per_launch"], str(found[-1].relative_to(ROOT))
 
 
+def run_c4(args):
+    """Config C4: scenes/mobile_base.xml, 2048 envs per GPU (16384 over 8), one bench
+    step = one 10-step controller period; every --render-every physics steps (100: the reference's
+    5 Hz camera rate at 500 Hz physics) a 640x480 depth frame of every env into HBM.  The roofline is
+    the depth kernel's (HBM-bound: 1,228,800 B written per env-frame)."""
+    import torch
+    from mujoco_ros2_simulation_amd import shard, sim, synth
+    rank, world, local = shard.init("nccl")
+    torch.cuda.set_device(local)
+    scene = ROOT / "scenes" / "mobile_base.xml"
+    model = sim.Model.load(scene)
+    n = args.envs if args.envs != 8192 else 2048
+    ids = shard.env_ids(rank, n)
+    P = args.warmup + args.steps
+    d_table = torch.from_numpy(synth.ctrl_table(model, ids, P, args.period).astype(np.float32)).to(f"cuda:{local}")
+    stream = torch.cuda.Stream(device=local)
+    batch = sim.Batch(model, n, device=local)
+    batch.set_stream(stream.cuda_stream)
+    batch.set(sim.FIELD_QPOS, synth.initial_qpos(model, ids))
+    W, H = int(model.cam_resolution[0, 0]), int(model.cam_resolution[0, 1])
+    frames = torch.empty((n, H, W), dtype=torch.float32, device=f"cuda:{local}")
+    every = max(1, args.render_every // args.period)
+    torch.cuda.synchronize()
+    step_ev, rend_ev = [], []
+
+    def period(p, timed):
+        batch.set_ctrl_device(d_table[p].data_ptr())
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+        if e: e[0].record(stream)
+        batch.step(args.period)
+        if e: e[1].record(stream); step_ev.append(e)
+        if (p + 1) % every == 0:
+            r = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+            if r: r[0].record(stream)
+            batch.render_depth_device(0, 0, n, frames.data_ptr())
+            if r: r[1].record(stream); rend_ev.append(r)
+
+    with torch.cuda.stream(stream):
+        for p in range(args.warmup):
+            period(p, False)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            period(args.warmup + k, True)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in step_ev]))
+    rend_ms = float(np.mean([a.elapsed_time(b) for a, b in rend_ev])) if rend_ev else float("nan")
+    elapsed, step_ms, rend_ms = shard.max_over_ranks([t1 - t0, step_ms, rend_ms], device=f"cuda:{local}")
+    assert torch.isfinite(frames).all(), "non-finite depth"
+    bytes_frame = n * W * H * 4
+    achieved = bytes_frame / (rend_ms * 1e-3) / 1e9
+    result = {
+        "metric": "env-steps/sec (whole node), mobile base + 32-beam lidar + 640x480 depth camera (C4)",
+        "value": world * n * args.steps * args.period / elapsed,
+        "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (Philox4x32-10 seeded wheel-speed commands and initial states; SURVEY.md §8d)",
+        "config": {"workload": "mobile_base (C4: free base + 2 wheels, 32-ray lidar, 640x480 depth)",
+                   "envs_per_gpu": n, "global_envs": world * n, "physics_steps_per_bench_step": args.period,
+                   "depth_every_physics_steps": every * args.period, "parallelism": f"env-sharded x{world}"},
+        "depth_frames_per_s": world * n * len(rend_ev) / elapsed,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                     "frac": achieved / 8000.0, "traffic": None,
+                     "kernel": "depth_kernel (one 640x480 frame of every env)", "kernel_ms": rend_ms,
+                     "algorithmic_bytes_per_launch": bytes_frame, "step_kernel_ms": step_ms},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    batch.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config == "c4":
+        return run_c4(args)
     import torch
     import torch.distributed as dist
     from mujoco_ros2_simulation_amd import build, roofline, shard, sim, synth
