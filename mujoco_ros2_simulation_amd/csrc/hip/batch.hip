@@ -118,6 +118,11 @@ __device__ float ray_prim(int type, const float* s, const float lp[3], const flo
 }
 
 
+// One workgroup renders a 16x16-pixel tile of one env.  The tile's pixel rays lie inside a cone
+// (apex at the camera, axis through the tile centre, half-angle to the widest corner ray); a geom
+// whose bounding sphere misses that cone, or a plane no ray of the cone can reach, is skipped by the
+// whole tile, and the pixels test only the remaining candidates.  Culling only removes geoms no pixel
+// ray can hit, so every pixel keeps the nearest hit over all geoms.
 __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const int* geom_group,
                                                     const float* geom_size, const float* geom_rbound,
                                                     const float* geom_rgba, int ngeom, const float* geom_xpos,
@@ -127,31 +132,82 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
   __shared__ float gp[kMaxRenderGeoms * 3];
   __shared__ float gm[kMaxRenderGeoms * 9];
   __shared__ float cpos[3], cmat[9];
+  __shared__ int cand[kMaxRenderGeoms];
+  __shared__ int ncand;
   const int env = env0 + blockIdx.y;
   const size_t eo = (size_t)env;
   for (int i = threadIdx.x; i < 3 * ngeom; i += blockDim.x) gp[i] = geom_xpos[eo * 3 * ngeom + i];
   for (int i = threadIdx.x; i < 9 * ngeom; i += blockDim.x) gm[i] = geom_xmat[eo * 9 * ngeom + i];
   if (threadIdx.x < 3) cpos[threadIdx.x] = cam_xpos[(eo * ncam + cam) * 3 + threadIdx.x];
   if (threadIdx.x < 9) cmat[threadIdx.x] = cam_xmat[(eo * ncam + cam) * 9 + threadIdx.x];
+  if (threadIdx.x == 0) ncand = 0;
+  const int tiles_x = (W + 15) / 16;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
   __syncthreads();
-  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pix >= W * H) return;
-  const int row = pix / W, col = pix - row * W;
+  if (threadIdx.x < ngeom) {
+    const int g = threadIdx.x;
+    const int grp = geom_group[g];
+    bool keep = !(grp < 0 || grp > 2 || geom_rgba[4 * g + 3] == 0);
+    if (keep) {
+      // tile cone in the camera frame, then world: axis through the tile centre, cos of the widest
+      // corner angle (pixel centres of the tile's extreme rows/columns)
+      const float c0 = tx * 16 + 0.5f, c1 = fminf(tx * 16 + 15.0f, W - 1.0f) + 0.5f;
+      const float r0 = ty * 16 + 0.5f, r1 = fminf(ty * 16 + 15.0f, H - 1.0f) + 0.5f;
+      float ac[3] = {(0.5f * (c0 + c1) - 0.5f * W) / f, (0.5f * H - 0.5f * (r0 + r1)) / f, -1.0f};
+      const float an = sqrtf(ac[0] * ac[0] + ac[1] * ac[1] + 1.0f);
+      ac[0] /= an; ac[1] /= an; ac[2] /= an;
+      float cth = 1.0f;
+      for (int k = 0; k < 4; ++k) {
+        const float cc = (k & 1) ? c1 : c0, rr = (k & 2) ? r1 : r0;
+        const float dx = (cc - 0.5f * W) / f, dy = (0.5f * H - rr) / f;
+        const float dn = sqrtf(dx * dx + dy * dy + 1.0f);
+        cth = fminf(cth, (dx * ac[0] + dy * ac[1] - ac[2]) / dn);
+      }
+      cth = fmaxf(-1.0f, cth - 1e-4f);
+      const float sth = sqrtf(fmaxf(0.0f, 1.0f - cth * cth));
+      const float a[3] = {cmat[0] * ac[0] + cmat[1] * ac[1] + cmat[2] * ac[2],
+                          cmat[3] * ac[0] + cmat[4] * ac[1] + cmat[5] * ac[2],
+                          cmat[6] * ac[0] + cmat[7] * ac[1] + cmat[8] * ac[2]};
+      const float v[3] = {gp[3 * g] - cpos[0], gp[3 * g + 1] - cpos[1], gp[3 * g + 2] - cpos[2]};
+      if (geom_type[g] == MRS_GEOM_PLANE) {
+        // origin in front of the plane and some direction of the cone with d.n < 0:
+        // min over the cone of d.n = cos(angle(a, n) + theta)
+        const float n[3] = {gm[9 * g + 2], gm[9 * g + 5], gm[9 * g + 8]};
+        const float an2 = a[0] * n[0] + a[1] * n[1] + a[2] * n[2];
+        const float mind = an2 * cth - sqrtf(fmaxf(0.0f, 1.0f - an2 * an2)) * sth;
+        keep = -(v[0] * n[0] + v[1] * n[1] + v[2] * n[2]) > 0 && mind < 1e-6f;
+      } else {
+        const float rb = geom_rbound[g] * 1.001f + 1e-4f;
+        const float l2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+        if (l2 > rb * rb) {
+          // angle(v, a) <= theta + asin(rb/|v|)  <=>  v.a >= |v| cos(theta) cos(beta) - rb sin(theta)
+          const float l = sqrtf(l2);
+          const float va = v[0] * a[0] + v[1] * a[1] + v[2] * a[2];
+          keep = va >= cth * sqrtf(l2 - rb * rb) - sth * rb - 1e-6f * l;
+        }
+      }
+    }
+    if (keep) cand[atomicAdd(&ncand, 1)] = g;
+  }
+  __syncthreads();
+  const int row = ty * 16 + threadIdx.x / 16, col = tx * 16 + threadIdx.x % 16;
+  if (row >= H || col >= W) return;
+  const int pix = row * W + col;
   const float dc[3] = {(col + 0.5f - 0.5f * W) / f, (0.5f * H - row - 0.5f) / f, -1.0f};
   const float vec[3] = {cmat[0] * dc[0] + cmat[1] * dc[1] + cmat[2] * dc[2],
                         cmat[3] * dc[0] + cmat[4] * dc[1] + cmat[5] * dc[2],
                         cmat[6] * dc[0] + cmat[7] * dc[1] + cmat[8] * dc[2]};
+  const float vv = vec[0] * vec[0] + vec[1] * vec[1] + vec[2] * vec[2];
   float best = -1;
-  for (int g = 0; g < ngeom; ++g) {
-    const int grp = geom_group[g];
-    if (grp < 0 || grp > 2 || geom_rgba[4 * g + 3] == 0) continue;
+  const int nc = ncand;
+  for (int i = 0; i < nc; ++i) {
+    const int g = cand[i];
     const float* p = gp + 3 * g;
     const float* mm = gm + 9 * g;
     const float dv[3] = {cpos[0] - p[0], cpos[1] - p[1], cpos[2] - p[2]};
     const int t = geom_type[g];
     if (t != MRS_GEOM_PLANE) {
       // bounding-sphere reject: closest approach of the ray to the geom centre
-      const float vv = vec[0] * vec[0] + vec[1] * vec[1] + vec[2] * vec[2];
       const float dvv = dv[0] * vec[0] + dv[1] * vec[1] + dv[2] * vec[2];
       const float dd = dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2];
       const float rb = geom_rbound[g];
@@ -542,9 +598,16 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
   auto lds_bytes = [&](int g) { return static_cast<size_t>(L.total) * sizeof(float) * kWavesPerBlock * (64 / g); };
+  // and, among those, the narrowest that still gives the chip two workgroups per CU (a small batch
+  // uses wider groups so every CU has work: 2048 envs -> G = 64, 8192 -> G = 16 on 256 CUs)
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, b.device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
   b.group = 64;
-  for (int g : {32, 16})
-    if (m.nv <= g && lds_bytes(g) <= 80 * 1024) b.group = g;
+  for (int g : {32, 16}) {
+    const long wgs = (static_cast<long>(b.n) + kWavesPerBlock * (64 / g) - 1) / (kWavesPerBlock * (64 / g));
+    if (m.nv <= g && lds_bytes(g) <= 80 * 1024 && wgs >= 2L * cus) b.group = g;
+  }
   if (const char* e = std::getenv("MRS_GROUP")) {
     const int g = std::atoi(e);
     if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
@@ -782,7 +845,7 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
   const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
   const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
   const DevModel& d = b->dm;
-  dim3 grid((W * H + 255) / 256, n);
+  dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
   HIP_CHECK(hipEventRecord(b->ev0[1], b->stream));
   hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
                      d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,

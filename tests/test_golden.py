@@ -45,8 +45,10 @@ def gpu_rollout(scene, ids, steps, cps, period=10):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("group", [16, 64])
 @pytest.mark.parametrize("name", ["s2", "arm7"])
-def test_hip_matches_golden(name, built):
+def test_hip_matches_golden(name, group, built, monkeypatch):
+    monkeypatch.setenv("MRS_GROUP", str(group))
     import make_golden
     from mujoco_ros2_simulation_amd import sim
     scene, ids, steps, cps = make_golden.CASES[name]

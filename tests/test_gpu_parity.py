@@ -61,8 +61,13 @@ def _scale(x):
     return np.maximum(np.abs(x), 1.0)
 
 
+GROUPS = [16, 32, 64]   # lanes per env; the batch picks one from nv and the env count, tests force each
+
+
+@pytest.mark.parametrize("group", GROUPS)
 @pytest.mark.parametrize("scene, n_envs, steps", [(REF_SCENE, 64, 1000), (ARM7, 16, 1000)])
-def test_rollout_parity(scene, n_envs, steps):
+def test_rollout_parity(scene, n_envs, steps, group, monkeypatch):
+    monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(scene)
     envs = np.arange(n_envs)
     period = 10
@@ -90,7 +95,9 @@ def test_rollout_parity(scene, n_envs, steps):
         assert np.median(err) < 1e-6
 
 
-def test_forward_lidar_closed_form():
+@pytest.mark.parametrize("group", [16, 64])
+def test_forward_lidar_closed_form(group, monkeypatch):
+    monkeypatch.setenv("MRS_GROUP", str(group))
     """GPU rangefinders of the reference scene at qpos=0 equal 1.95/cos(0.3 - 0.025 i)."""
     model = sim.Model.load(REF_SCENE)
     b = sim.Batch(model, 8)
@@ -162,7 +169,9 @@ CONTACT_SCENE = """<mujoco><compiler angle="radian"/><option timestep="0.002" so
 </worldbody></mujoco>"""
 
 
-def test_contact_parity_short_horizon():
+@pytest.mark.parametrize("group", [16, 64])
+def test_contact_parity_short_horizon(group, monkeypatch):
+    monkeypatch.setenv("MRS_GROUP", str(group))
     """Contact generation and PGS with free bodies: contact counts bit-exact, state within tolerance
     over a short horizon (contact dynamics diverge chaotically in fp32 vs fp64 over long ones)."""
     model = sim.Model.from_string(CONTACT_SCENE)
@@ -178,7 +187,9 @@ def test_contact_parity_short_horizon():
     assert d.ncon >= 3  # sphere on floor, capsule on ledge, box on floor (up to 4 corners)
 
 
-def test_autoreset_on_nan():
+@pytest.mark.parametrize("group", [16, 64])
+def test_autoreset_on_nan(group, monkeypatch):
+    monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(REF_SCENE)
     b = sim.Batch(model, 3)
     q = np.zeros((3, 2))
@@ -193,11 +204,13 @@ def test_autoreset_on_nan():
 IMU_FT = ARM7.parent / "imu_ft.xml"
 
 
-def test_imu_ft_sensor_parity():
+@pytest.mark.parametrize("group", [16, 64])
+def test_imu_ft_sensor_parity(group, monkeypatch):
     """row f2: framequat/gyro/accelerometer/force/torque (mj_rnePostConstraint + mj_sensorAcc) on the
     GPU against the oracle over a seeded rollout with motor torques and a box landing on the floor
     (contact forces enter cfrc_ext).  Acceleration-level outputs tolerate 1e-3 of their scale: they
     difference nearly balanced fp32 forces."""
+    monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(IMU_FT)
     n, steps, period = 16, 400, 10
     envs = np.arange(n)
@@ -221,10 +234,12 @@ def test_imu_ft_sensor_parity():
 MOBILE = ARM7.parent / "mobile_base.xml"
 
 
-def test_mobile_base_parity():
+@pytest.mark.parametrize("group", [16, 64])
+def test_mobile_base_parity(group, monkeypatch):
     """config C4: free-joint base driven by two sphere wheels (velocity actuators, pyramidal friction
     contacts), 32-beam lidar and a 640x480 depth frame, GPU vs oracle over a seeded rollout.
     Contact-driven dynamics amplify fp32 rounding; measured 3e-7 relative after 500 steps, bound 1e-5."""
+    monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(MOBILE)
     n, steps, period = 8, 500, 10
     envs = np.arange(n)
