@@ -120,7 +120,7 @@ mrs_batch* mrs_batch_create(const mrs_model* m, int n_envs, int device) {
   int rc = guarded([&] {
     if (!m) throw std::invalid_argument("null model");
     b->model = m;
-    b->impl = mrs::batch_create(&m->m, n_envs, device, 32);
+    b->impl = mrs::batch_create(&m->m, n_envs, device, 0);  // contact capacity from the model
   });
   return rc == MRS_OK ? b.release() : nullptr;
 }

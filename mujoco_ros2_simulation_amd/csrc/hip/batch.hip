@@ -355,7 +355,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
         int ta = m.geom_type[ga], tb = m.geom_type[gb];
         bool ok = (ta == MRS_GEOM_PLANE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
                   (ta == MRS_GEOM_SPHERE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
-                  (ta == MRS_GEOM_CAPSULE && (tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX));
+                  (ta == MRS_GEOM_CAPSULE && (tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
+                  (ta == MRS_GEOM_BOX && tb == MRS_GEOM_BOX);
         if (!ok)
           throw UnsupportedError("collision pair of geom types " + std::to_string(ta) + "/" + std::to_string(tb) +
                                  " is not implemented (geoms " + std::to_string(g1) + "," + std::to_string(g2) + ")");
@@ -389,7 +390,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nfric = static_cast<int>(fric.size());
   d.nlim = static_cast<int>(lim.size());
   d.nrf = static_cast<int>(rf.size());
-  d.max_con = d.npair == 0 ? 0 : std::min(4 * d.npair, max_con_req);
+  // contact capacity per env: requested, or (<= 0) four per candidate pair clamped to [32, 128]
+  const int cap = max_con_req > 0 ? max_con_req : std::min(128, std::max(32, 4 * d.npair));
+  d.max_con = d.npair == 0 ? 0 : std::min(4 * d.npair, cap);
   d.max_efc = d.nfric + 2 * d.nlim + 4 * d.max_con;
   // actuators
   std::vector<int> act_dof, act_qadr;

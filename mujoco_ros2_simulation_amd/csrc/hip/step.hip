@@ -451,6 +451,150 @@ __device__ int capsule_box(const float a[3], const float b[3], float r, const fl
 __device__ __forceinline__ void capsule_ends(const float* pos, const float* mat, float hl, float a[3], float b[3]) {
   for (int i = 0; i < 3; ++i) { a[i] = pos[i] - mat[3 * i + 2] * hl; b[i] = pos[i] + mat[3 * i + 2] * hl; }
 }
+// box-box: the oracle's col_box_box (oracle/oracle.c) in fp32 -- separating-axis test over 15 axes
+// (edge axes only when clearly better than the best face axis), face case by clipping the most
+// anti-parallel face of the other box against the reference face's side planes, four deepest clipped
+// vertices kept; edge case: one contact between the support edges.  Out of line: rare, and its
+// private arrays stay out of the hot path's registers.
+__device__ __forceinline__ void box_axis(const float* R, int i, float a[3]) { a[0] = R[i]; a[1] = R[3 + i]; a[2] = R[6 + i]; }
+
+// templated on the group width only so each kernel instantiation gets its own copy, compiled under
+// that kernel's register budget (a shared callee is allocated for the widest caller)
+template <int G>
+__device__ __noinline__ int box_box(const float* p1, const float* R1, const float* h1, const float* p2,
+                                    const float* R2, const float* h2, float margin, gCon* out) {
+  float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  float A[3][3], B[3][3];
+  for (int i = 0; i < 3; ++i) { box_axis(R1, i, A[i]); box_axis(R2, i, B[i]); }
+  float best_face = -1e30f, best_edge = -1e30f, nf[3] = {0, 0, 0}, ne[3] = {0, 0, 0};
+  int face_axis = -1, edge_i = -1, edge_j = -1;
+  #pragma unroll 1
+  for (int k = 0; k < 15; ++k) {
+    float L[3];
+    if (k < 3) { L[0] = A[k][0]; L[1] = A[k][1]; L[2] = A[k][2]; }
+    else if (k < 6) { L[0] = B[k - 3][0]; L[1] = B[k - 3][1]; L[2] = B[k - 3][2]; }
+    else cross3(L, A[(k - 6) / 3], B[(k - 6) % 3]);
+    const float ln = sqrtf(dot3(L, L));
+    if (ln < 1e-6f) continue;
+    for (int c = 0; c < 3; ++c) L[c] /= ln;
+    float ra = 0, rb = 0;
+    for (int i = 0; i < 3; ++i) { ra += h1[i] * fabsf(dot3(A[i], L)); rb += h2[i] * fabsf(dot3(B[i], L)); }
+    const float sv = dot3(d, L);
+    const float sep = fabsf(sv) - ra - rb;
+    if (sep > margin) return 0;
+    const float sg = sv >= 0 ? 1.0f : -1.0f;
+    if (k < 6) {
+      if (sep > best_face) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
+    } else if (sep > best_edge) {
+      best_edge = sep; edge_i = (k - 6) / 3; edge_j = (k - 6) % 3;
+      for (int c = 0; c < 3; ++c) ne[c] = sg * L[c];
+    }
+  }
+  if (face_axis < 0) return 0;
+  if (edge_i >= 0 && best_edge > best_face + 0.05f * fabsf(best_face) + 1e-6f) {
+    float a0[3], a1[3], b0[3], b1[3], c1[3], c2[3];
+    for (int c = 0; c < 3; ++c) { a0[c] = p1[c]; b0[c] = p2[c]; }
+    for (int i = 0; i < 3; ++i) {
+      if (i != edge_i) {
+        const float sg = dot3(A[i], ne) >= 0 ? 1.0f : -1.0f;
+        for (int c = 0; c < 3; ++c) a0[c] += sg * h1[i] * A[i][c];
+      }
+      if (i != edge_j) {
+        const float sg = dot3(B[i], ne) >= 0 ? -1.0f : 1.0f;
+        for (int c = 0; c < 3; ++c) b0[c] += sg * h2[i] * B[i][c];
+      }
+    }
+    for (int c = 0; c < 3; ++c) {
+      a1[c] = a0[c] + h1[edge_i] * A[edge_i][c]; a0[c] -= h1[edge_i] * A[edge_i][c];
+      b1[c] = b0[c] + h2[edge_j] * B[edge_j][c]; b0[c] -= h2[edge_j] * B[edge_j][c];
+    }
+    seg_seg_closest(a0, a1, b0, b1, c1, c2);
+    gCon& o = out[0];
+    for (int c = 0; c < 3; ++c) { o.pos[c] = 0.5f * (c1[c] + c2[c]); o.nrm[c] = ne[c]; }
+    o.dist = best_edge;
+    return 1;
+  }
+  // face case: reference box r (normal nr pointing at the other box), incident box i
+  const bool refA = face_axis < 3;
+  const int ir = refA ? face_axis : face_axis - 3;
+  const float* pr = refA ? p1 : p2;
+  const float* pi = refA ? p2 : p1;
+  const float* hr = refA ? h1 : h2;
+  const float* hi = refA ? h2 : h1;
+  float nr[3];
+  for (int c = 0; c < 3; ++c) nr[c] = refA ? nf[c] : -nf[c];
+  float (*Rr)[3] = refA ? A : B;
+  float (*Ri)[3] = refA ? B : A;
+  int j = 0;
+  float bestc = -1;
+  for (int k = 0; k < 3; ++k) {
+    const float cc = fabsf(dot3(Ri[k], nr));
+    if (cc > bestc) { bestc = cc; j = k; }
+  }
+  const int k1 = (j + 1) % 3, k2 = (j + 2) % 3;
+  const float sgn = dot3(Ri[j], nr) > 0 ? -1.0f : 1.0f;
+  // polygon buffers stay in private memory (volatile: not promoted to registers, which would set
+  // the register budget of every kernel that calls this rare path)
+  volatile float poly[8][3], tmp[8][3];
+  int np = 4;
+  for (int v = 0; v < 4; ++v) {
+    const float su = (v == 0 || v == 3) ? 1.0f : -1.0f, sv = (v < 2) ? 1.0f : -1.0f;
+    for (int c = 0; c < 3; ++c)
+      poly[v][c] = pi[c] + sgn * hi[j] * Ri[j][c] + su * hi[k1] * Ri[k1][c] + sv * hi[k2] * Ri[k2][c];
+  }
+  const int r1 = (ir + 1) % 3, r2 = (ir + 2) % 3;
+  float cr[3];
+  for (int c = 0; c < 3; ++c) cr[c] = pr[c] + hr[ir] * nr[c];
+  #pragma unroll 1
+  for (int side = 0; side < 4; ++side) {
+    const float* ax2 = (side < 2) ? Rr[r1] : Rr[r2];
+    const float lim = (side < 2) ? hr[r1] : hr[r2];
+    const float sg = (side & 1) ? -1.0f : 1.0f;
+    int nn = 0;
+    #pragma unroll 1
+    for (int v = 0; v < np; ++v) {
+      const int vb = (v + 1) % np;
+      const float a[3] = {poly[v][0], poly[v][1], poly[v][2]}, b[3] = {poly[vb][0], poly[vb][1], poly[vb][2]};
+      const float da[3] = {a[0] - cr[0], a[1] - cr[1], a[2] - cr[2]}, db[3] = {b[0] - cr[0], b[1] - cr[1], b[2] - cr[2]};
+      const float fa = sg * dot3(da, ax2) - lim, fb = sg * dot3(db, ax2) - lim;
+      if (fa <= 0) { for (int c = 0; c < 3; ++c) tmp[nn][c] = a[c]; ++nn; }
+      if ((fa < 0 && fb > 0) || (fa > 0 && fb < 0)) {
+        const float t = fa / (fa - fb);
+        for (int c = 0; c < 3; ++c) tmp[nn][c] = a[c] + t * (b[c] - a[c]);
+        ++nn;
+      }
+    }
+    np = nn;
+    for (int v = 0; v < np; ++v)
+      for (int c = 0; c < 3; ++c) poly[v][c] = tmp[v][c];
+    if (np == 0) return 0;
+  }
+  volatile float seps[8];
+  volatile int keep[8];
+  int nk = 0;
+  for (int v = 0; v < np; ++v) {
+    const float dv[3] = {poly[v][0] - cr[0], poly[v][1] - cr[1], poly[v][2] - cr[2]};
+    const float sep = dot3(dv, nr);
+    if (sep > margin) continue;
+    seps[nk] = sep;
+    keep[nk++] = v;
+  }
+  volatile bool used[8] = {false, false, false, false, false, false, false, false};
+  int n = 0;
+  #pragma unroll 1
+  for (int k = 0; k < 4 && k < nk; ++k) {
+    int bi = -1;
+    for (int v = 0; v < nk; ++v)
+      if (!used[v] && (bi < 0 || seps[v] < seps[bi])) bi = v;
+    used[bi] = true;
+    gCon& o = out[n++];
+    for (int c = 0; c < 3; ++c) { o.pos[c] = poly[keep[bi]][c] - nr[c] * seps[bi] / 2; o.nrm[c] = nf[c]; }
+    o.dist = seps[bi];
+  }
+  return n;
+}
+
+template <int G>
 __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
                            const float* m2, const float* s2, float margin, gCon* out) {
   float a1[3], b1[3], a2[3], b2[3], c1[3], c2[3];
@@ -482,6 +626,8 @@ __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, con
       capsule_ends(p1, m1, s1[1], a1, b1);
       return capsule_box(a1, b1, s1[0], p2, m2, s2, margin, out, 0);
     }
+  } else if (t1 == MRS_GEOM_BOX && t2 == MRS_GEOM_BOX) {
+    return box_box<G>(p1, m1, s1, p2, m2, s2, margin, out);
   }
   return 0;
 }
@@ -1267,7 +1413,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
         for (int i = 0; i < 9; ++i) { m1[i] = s[L.gxmat + 9 * g1 + i]; m2[i] = s[L.gxmat + 9 * g2 + i]; }
         float s1[3] = {m.geom_size[3 * g1], m.geom_size[3 * g1 + 1], m.geom_size[3 * g1 + 2]};
         float s2[3] = {m.geom_size[3 * g2], m.geom_size[3 * g2 + 1], m.geom_size[3 * g2 + 2]};
-        n = narrowphase(t1, t2, p1, m1, s1, p2, m2, s2, margin, c);
+        n = narrowphase<G>(t1, t2, p1, m1, s1, p2, m2, s2, margin, c);
       }
     }
     int total;

@@ -715,6 +715,151 @@ static int col_capsule_box(const double a[3], const double b[3], double r, const
   return col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
 }
 
+/* box-box: separating-axis test over the 15 axes (3 + 3 face normals, 9 edge cross products);
+ * the least-penetrating axis wins, an edge axis only if it separates clearly more than the best face
+ * axis (sep_edge > sep_face + 0.05 |sep_face| + 1e-6).  Face axis: the most anti-parallel face of the
+ * other box is clipped against the reference face's four side planes (Sutherland-Hodgman); clipped
+ * vertices within margin become contacts at the midpoint to the reference face, the four deepest
+ * kept.  Edge axis: one contact between the closest points of the two support edges.  Normal from
+ * box 1 to box 2.  Same algorithm as the kernel's box_box (csrc/hip/step.hip). */
+static void box_axis(const double* R, int i, double a[3]) { a[0] = R[i]; a[1] = R[3 + i]; a[2] = R[6 + i]; }
+
+static int box_face_clip(const double* pr, const double* Rr, const double* hr, int ir, const double nr[3],
+                         const double* pi, const double* Ri, const double* hi, double margin,
+                         double pts[8][3], double seps[8]) {
+  /* incident face of box i: most anti-parallel to nr */
+  int j = 0;
+  double best = -1, ax[3];
+  for (int k = 0; k < 3; ++k) {
+    box_axis(Ri, k, ax);
+    double c = fabs(dot3(ax, nr));
+    if (c > best) { best = c; j = k; }
+  }
+  double bj[3], bk[3], bl[3];
+  box_axis(Ri, j, bj);
+  int k1 = (j + 1) % 3, k2 = (j + 2) % 3;
+  box_axis(Ri, k1, bk);
+  box_axis(Ri, k2, bl);
+  double sgn = dot3(bj, nr) > 0 ? -1.0 : 1.0;  /* outward normal of the incident face faces -nr */
+  double poly[8][3], tmp[8][3];
+  int np = 4;
+  for (int v = 0; v < 4; ++v) {
+    double su = (v == 0 || v == 3) ? 1.0 : -1.0, sv = (v < 2) ? 1.0 : -1.0;
+    for (int c = 0; c < 3; ++c)
+      poly[v][c] = pi[c] + sgn * hi[j] * bj[c] + su * hi[k1] * bk[c] + sv * hi[k2] * bl[c];
+  }
+  /* reference face: centre and its two in-plane axes */
+  double cr[3], ua[3], va[3];
+  int r1 = (ir + 1) % 3, r2 = (ir + 2) % 3;
+  box_axis(Rr, r1, ua);
+  box_axis(Rr, r2, va);
+  for (int c = 0; c < 3; ++c) cr[c] = pr[c] + hr[ir] * nr[c];
+  for (int side = 0; side < 4; ++side) {
+    const double* ax2 = (side < 2) ? ua : va;
+    double lim = (side < 2) ? hr[r1] : hr[r2];
+    double sg = (side & 1) ? -1.0 : 1.0;  /* keep sg * (x - cr).ax2 <= lim */
+    int nn = 0;
+    for (int v = 0; v < np; ++v) {
+      const double* a = poly[v];
+      const double* b = poly[(v + 1) % np];
+      double da[3] = {a[0] - cr[0], a[1] - cr[1], a[2] - cr[2]}, db[3] = {b[0] - cr[0], b[1] - cr[1], b[2] - cr[2]};
+      double fa = sg * dot3(da, ax2) - lim, fb = sg * dot3(db, ax2) - lim;
+      if (fa <= 0) memcpy(tmp[nn++], a, sizeof tmp[0]);
+      if ((fa < 0 && fb > 0) || (fa > 0 && fb < 0)) {
+        double t = fa / (fa - fb);
+        for (int c = 0; c < 3; ++c) tmp[nn][c] = a[c] + t * (b[c] - a[c]);
+        ++nn;
+      }
+    }
+    np = nn;
+    memcpy(poly, tmp, sizeof poly);
+    if (np == 0) return 0;
+  }
+  int n = 0;
+  for (int v = 0; v < np; ++v) {
+    double dv[3] = {poly[v][0] - cr[0], poly[v][1] - cr[1], poly[v][2] - cr[2]};
+    double sep = dot3(dv, nr);
+    if (sep > margin) continue;
+    memcpy(pts[n], poly[v], sizeof pts[0]);
+    seps[n++] = sep;
+  }
+  return n;
+}
+
+static int col_box_box(const double* p1, const double* R1, const double* h1, const double* p2, const double* R2,
+                       const double* h2, double margin, orc_contact* out, int n) {
+  double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  double A[3][3], B[3][3];
+  for (int i = 0; i < 3; ++i) { box_axis(R1, i, A[i]); box_axis(R2, i, B[i]); }
+  double best_face = -1e30, best_edge = -1e30, nf[3] = {0, 0, 0}, ne[3] = {0, 0, 0};
+  int face_axis = -1, edge_i = -1, edge_j = -1;
+  for (int k = 0; k < 15; ++k) {
+    double L[3];
+    if (k < 3) memcpy(L, A[k], sizeof L);
+    else if (k < 6) memcpy(L, B[k - 3], sizeof L);
+    else cross3(L, A[(k - 6) / 3], B[(k - 6) % 3]);
+    double ln = norm3(L);
+    if (ln < 1e-6) continue;  /* parallel edges: covered by the face axes */
+    for (int c = 0; c < 3; ++c) L[c] /= ln;
+    double ra = 0, rb = 0;
+    for (int i = 0; i < 3; ++i) { ra += h1[i] * fabs(dot3(A[i], L)); rb += h2[i] * fabs(dot3(B[i], L)); }
+    double s = dot3(d, L);
+    double sep = fabs(s) - ra - rb;
+    if (sep > margin) return n;
+    double sg = s >= 0 ? 1.0 : -1.0;
+    if (k < 6) {
+      if (sep > best_face) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
+    } else if (sep > best_edge) {
+      best_edge = sep; edge_i = (k - 6) / 3; edge_j = (k - 6) % 3;
+      for (int c = 0; c < 3; ++c) ne[c] = sg * L[c];
+    }
+  }
+  if (face_axis < 0) return n;
+  if (edge_i >= 0 && best_edge > best_face + 0.05 * fabs(best_face) + 1e-6) {
+    /* support edges: box 1 towards +ne, box 2 towards -ne, free along A[edge_i] / B[edge_j] */
+    double a0[3], a1[3], b0[3], b1[3], c1[3], c2[3];
+    for (int c = 0; c < 3; ++c) { a0[c] = p1[c]; b0[c] = p2[c]; }
+    for (int i = 0; i < 3; ++i) {
+      if (i != edge_i) {
+        double sg = dot3(A[i], ne) >= 0 ? 1.0 : -1.0;
+        for (int c = 0; c < 3; ++c) a0[c] += sg * h1[i] * A[i][c];
+      }
+      if (i != edge_j) {
+        double sg = dot3(B[i], ne) >= 0 ? -1.0 : 1.0;
+        for (int c = 0; c < 3; ++c) b0[c] += sg * h2[i] * B[i][c];
+      }
+    }
+    for (int c = 0; c < 3; ++c) {
+      a1[c] = a0[c] + h1[edge_i] * A[edge_i][c]; a0[c] -= h1[edge_i] * A[edge_i][c];
+      b1[c] = b0[c] + h2[edge_j] * B[edge_j][c]; b0[c] -= h2[edge_j] * B[edge_j][c];
+    }
+    segment_segment_closest(a0, a1, b0, b1, c1, c2);
+    double pos[3] = {0.5 * (c1[0] + c2[0]), 0.5 * (c1[1] + c2[1]), 0.5 * (c1[2] + c2[2])};
+    return add_contact(out, n, best_edge, pos, ne);
+  }
+  double pts[8][3], seps[8], nr[3];
+  int np;
+  if (face_axis < 3) {
+    np = box_face_clip(p1, R1, h1, face_axis, nf, p2, R2, h2, margin, pts, seps);
+    memcpy(nr, nf, sizeof nr);
+  } else {
+    for (int c = 0; c < 3; ++c) nr[c] = -nf[c];
+    np = box_face_clip(p2, R2, h2, face_axis - 3, nr, p1, R1, h1, margin, pts, seps);
+  }
+  /* keep the four deepest (stable order: deepest first, ties by clip order) */
+  int used[8] = {0};
+  for (int k = 0; k < 4 && k < np; ++k) {
+    int bi = -1;
+    for (int v = 0; v < np; ++v)
+      if (!used[v] && (bi < 0 || seps[v] < seps[bi])) bi = v;
+    used[bi] = 1;
+    double pos[3];
+    for (int c = 0; c < 3; ++c) pos[c] = pts[bi][c] - nr[c] * seps[bi] / 2;
+    n = add_contact(out, n, seps[bi], pos, nf);
+  }
+  return n;
+}
+
 static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, double margin, orc_contact* out) {
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const double *p1 = w->geom_xpos + 3 * g1, *p2 = w->geom_xpos + 3 * g2;
@@ -751,6 +896,8 @@ static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, doubl
         capsule_ends(p1, m1, s1[1], a1, b1);
         return col_capsule_box(a1, b1, s1[0], p2, m2, s2, margin, out, 0);
     }
+  } else if (t1 == MRS_GEOM_BOX && t2 == MRS_GEOM_BOX) {
+    return col_box_box(p1, m1, s1, p2, m2, s2, margin, out, 0);
   }
   return -1; /* unsupported pair */
 }

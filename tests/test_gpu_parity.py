@@ -268,3 +268,55 @@ def test_mobile_base_parity(group, monkeypatch):
     close = np.isclose(depth, want, rtol=1e-5, atol=1e-5)
     assert depth.shape == (480, 640) and close.mean() >= 0.999
     b.close()
+
+
+ARM_BOXES = ARM7.parent / "arm_boxes.xml"
+
+
+@pytest.mark.parametrize("group", [64])
+def test_contact_rich_parity(group, monkeypatch):
+    """config C5: 7-DoF arm, floor and 8 free boxes (two stacked pairs): nv = 55, 32 contacts
+    (plane-box and box-box, pyramidal friction), ~135 PGS rows at the 50-iteration cap.  Contact
+    counts must match exactly; states within 1e-3 of scale after 200 steps (the unconverged PGS
+    amplifies fp32 rounding)."""
+    monkeypatch.setenv("MRS_GROUP", str(group))
+    model = sim.Model.load(ARM_BOXES)
+    n, steps, period = 4, 200, 10
+    envs = np.arange(n)
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    checkpoints = [1, 20, steps]
+    ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
+    got = _gpu_rollout(model, qpos0, table, period, checkpoints)
+    for c in checkpoints:
+        err = np.max(np.abs(got[c][0] - ref[c][0]) / _scale(ref[c][0]))
+        print(f"arm_boxes step {c}: qpos rel err {err:.2e}")
+        assert err <= 1e-3, (c, err)
+    b = sim.Batch(model, 1)
+    b.set(sim.FIELD_QPOS, qpos0[:1])
+    b.forward()
+    ncon = int(b.get(sim.FIELD_NCON)[0, 0])
+    d = binding.OracleData(model)
+    d.qpos[:] = qpos0[0]
+    d.forward()
+    assert ncon == d.ncon == 32
+    b.close()
+
+
+def test_box_stack_rests(monkeypatch):
+    """box-box: a rotated box resting on a box resting on the floor stays stacked on the GPU"""
+    xml = """<mujoco><option timestep="0.002"/><worldbody><geom type="plane" size="0 0 1"/>
+    <body pos="0 0 0.1"><freejoint/><geom type="box" size="0.1 0.1 0.1" mass="1"/></body>
+    <body pos="0.03 0.02 0.32" euler="0 0 0.4"><freejoint/><geom type="box" size="0.1 0.1 0.1" mass="1"/></body>
+    </worldbody></mujoco>"""
+    model = sim.Model.from_string(xml)
+    b = sim.Batch(model, 4)
+    b.step(1000)
+    q = b.get(sim.FIELD_QPOS)
+    np.testing.assert_allclose(q[:, 2], 0.1, atol=5e-4)
+    np.testing.assert_allclose(q[:, 9], 0.3, atol=1e-3)
+    assert np.all(b.get(sim.FIELD_NCON)[:, 0] == 8)
+    d = binding.OracleData(model)
+    d.step(1000)
+    np.testing.assert_allclose(q[0], d.qpos, atol=1e-4)
+    b.close()
