@@ -456,16 +456,21 @@ __device__ __forceinline__ void capsule_ends(const float* pos, const float* mat,
 // anti-parallel face of the other box against the reference face's side planes, four deepest clipped
 // vertices kept; edge case: one contact between the support edges.  Out of line: rare, and its
 // private arrays stay out of the hot path's registers.
-__device__ __forceinline__ void box_axis(const float* R, int i, float a[3]) { a[0] = R[i]; a[1] = R[3 + i]; a[2] = R[6 + i]; }
-
-// templated on the group width only so each kernel instantiation gets its own copy, compiled under
+// Templated on the group width only so each kernel instantiation gets its own copy, compiled under
 // that kernel's register budget (a shared callee is allocated for the widest caller)
+// The poses are read from the env's LDS and the sizes from the model here, not passed as arrays: a
+// caller array whose address escapes into a call lives in scratch, and the caller's pair loop would
+// store every pair's pose there whether or not it reaches this function.
 template <int G>
-__device__ __noinline__ int box_box(const float* p1, const float* R1, const float* h1, const float* p2,
-                                    const float* R2, const float* h2, float margin, gCon* out) {
+__device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CPtr<float> gsize, int g1, int g2,
+                                    float margin, gCon* out) {
+  float p1[3], p2[3], h1[3], h2[3], A[3][3], B[3][3];
+  for (int i = 0; i < 3; ++i) {
+    p1[i] = gxpos[3 * g1 + i]; p2[i] = gxpos[3 * g2 + i];
+    h1[i] = gsize[3 * g1 + i]; h2[i] = gsize[3 * g2 + i];
+    for (int c = 0; c < 3; ++c) { A[i][c] = gxmat[9 * g1 + 3 * c + i]; B[i][c] = gxmat[9 * g2 + 3 * c + i]; }
+  }
   float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-  float A[3][3], B[3][3];
-  for (int i = 0; i < 3; ++i) { box_axis(R1, i, A[i]); box_axis(R2, i, B[i]); }
   float best_face = -1e30f, best_edge = -1e30f, nf[3] = {0, 0, 0}, ne[3] = {0, 0, 0};
   int face_axis = -1, edge_i = -1, edge_j = -1;
   #pragma unroll 1
@@ -596,7 +601,8 @@ __device__ __noinline__ int box_box(const float* p1, const float* R1, const floa
 
 template <int G>
 __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
-                           const float* m2, const float* s2, float margin, gCon* out) {
+                           const float* m2, const float* s2, float margin, gCon* out, const lfloat* gxpos,
+                           const lfloat* gxmat, CPtr<float> gsize, int g1, int g2) {
   float a1[3], b1[3], a2[3], b2[3], c1[3], c2[3];
   int n = 0;
   if (t1 == MRS_GEOM_PLANE) {
@@ -627,7 +633,7 @@ __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, con
       return capsule_box(a1, b1, s1[0], p2, m2, s2, margin, out, 0);
     }
   } else if (t1 == MRS_GEOM_BOX && t2 == MRS_GEOM_BOX) {
-    return box_box<G>(p1, m1, s1, p2, m2, s2, margin, out);
+    return box_box<G>(gxpos, gxmat, gsize, g1, g2, margin, out);
   }
   return 0;
 }
@@ -1413,7 +1419,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
         for (int i = 0; i < 9; ++i) { m1[i] = s[L.gxmat + 9 * g1 + i]; m2[i] = s[L.gxmat + 9 * g2 + i]; }
         float s1[3] = {m.geom_size[3 * g1], m.geom_size[3 * g1 + 1], m.geom_size[3 * g1 + 2]};
         float s2[3] = {m.geom_size[3 * g2], m.geom_size[3 * g2 + 1], m.geom_size[3 * g2 + 2]};
-        n = narrowphase<G>(t1, t2, p1, m1, s1, p2, m2, s2, margin, c);
+        n = narrowphase<G>(t1, t2, p1, m1, s1, p2, m2, s2, margin, c, s + L.gxpos, s + L.gxmat, m.geom_size, g1, g2);
       }
     }
     int total;

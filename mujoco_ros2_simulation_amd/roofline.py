@@ -77,6 +77,7 @@ def _ancestors(m, i):
 SURVEY_PER_ENV_STEP = {
     "scene": (2.0e3, 72.0),          # C2: reference 2-DoF scene, dynamics only
     "arm7_lidar": (1.9e5, 1692.0),   # C3: 7-DoF arm + 360-ray lidar
+    "arm_boxes": (3.3e6, 1852.0),    # C5: arm + 8 free boxes, PGS 50 iterations
 }
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
