@@ -377,6 +377,50 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       }
   }
   d.npair = static_cast<int>(pg1.size());
+  // kinematic trees (bodies sharing a root child of the world) that own dofs: their dofs are one
+  // contiguous range, M is block diagonal over them, and constraint rows touch at most two of them
+  // (mj_island's trees).  Blocked mode stores M / its factor per tree and solves the constraint rows
+  // sparsely over the trees they touch (csrc/hip/step.hip constraints_sparse).
+  std::vector<int> body_tree(m.nbody, -1), dof_tree(std::max(1, m.nv), -1), tree_dofadr, tree_dofnum, tree_Moff;
+  {
+    std::vector<int> root_tree(m.nbody, -1);
+    for (int bI = 1; bI < m.nbody; ++bI) {
+      if (m.body_dofnum[bI] == 0) continue;
+      const int r = m.body_rootid[bI];
+      if (root_tree[r] < 0) {
+        root_tree[r] = static_cast<int>(tree_dofadr.size());
+        tree_dofadr.push_back(m.body_dofadr[bI]);
+        tree_dofnum.push_back(0);
+      }
+    }
+    for (int bI = 1; bI < m.nbody; ++bI) body_tree[bI] = root_tree[m.body_rootid[bI]];
+    for (int j = 0; j < m.nv; ++j) {
+      const int t = body_tree[m.dof_bodyid[j]];
+      if (t < 0 || j != tree_dofadr[t] + tree_dofnum[t])
+        throw UnsupportedError("dofs of a kinematic tree are not contiguous");
+      dof_tree[j] = t;
+      ++tree_dofnum[t];
+    }
+    int off = 0;
+    d.tree_nmax = 0;
+    for (size_t t = 0; t < tree_dofadr.size(); ++t) {
+      tree_Moff.push_back(off);
+      off += tree_dofnum[t] * tree_dofnum[t];
+      d.tree_nmax = std::max(d.tree_nmax, tree_dofnum[t]);
+    }
+    d.ntree = static_cast<int>(tree_dofadr.size());
+    d.nMblk = off;
+    // pipe width of the sparse solver: dof slots of the widest row (two trees for a contact)
+    int widest = 1;
+    for (int j = 0; j < m.nv; ++j) widest = std::max(widest, tree_dofnum[dof_tree[j]]);
+    for (size_t p = 0; p < pg1.size(); ++p) {
+      const int t1 = body_tree[m.geom_bodyid[pg1[p]]], t2 = body_tree[m.geom_bodyid[pg2[p]]];
+      int w = (t1 >= 0 ? tree_dofnum[t1] : 0) + (t2 >= 0 && t2 != t1 ? tree_dofnum[t2] : 0);
+      widest = std::max(widest, w);
+    }
+    d.pipe_w = 8;
+    while (d.pipe_w < widest) d.pipe_w *= 2;
+  }
   std::vector<int> fric, lim, rf;
   for (int j = 0; j < m.nv; ++j) if (m.dof_frictionloss[j] > 0) fric.push_back(j);
   for (int j = 0; j < m.njnt; ++j)
@@ -431,6 +475,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addf(&d.dof_solimp, m.dof_solimp); P.addf(&d.dof_invweight0, m.dof_invweight0);
   P.addf(&d.qpos0, m.qpos0); P.addf(&d.qpos_spring, m.qpos_spring);
   P.addi(&d.Mpair, Mpair);
+  P.addi(&d.body_tree, body_tree); P.addi(&d.dof_tree, dof_tree); P.addi(&d.tree_dofadr, tree_dofadr);
+  P.addi(&d.tree_dofnum, tree_dofnum); P.addi(&d.tree_Moff, tree_Moff);
   P.addi(&d.geom_type, m.geom_type); P.addi(&d.geom_bodyid, m.geom_bodyid); P.addi(&d.geom_group, m.geom_group);
   P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
   P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
@@ -582,21 +628,30 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   for (auto& kv : P.iptr) kv.first->p = static_cast<const int*>(b.dblock_i) + kv.second;
   HIP_CHECK(hipStreamSynchronize(b.stream));
 
-  // --- LDS layout (floats)
+  // --- LDS layout (floats).  Dense mode: M and its factor as nv x nv.  Blocked mode (one env per
+  // wave, G = 64): M and its factor per kinematic tree, row forces and the island scratch of the
+  // sparse constraint solver.
   LdsLayout& L = b.dm.L;
   int off = 0;
   auto take = [&](int n) { int o = off; off += n; off = (off + 3) & ~3; return o; };
   const int nb = m.nbody, nj = std::max(1, m.njnt), nv = std::max(1, m.nv), ng = std::max(1, m.ngeom);
-  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
-  L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.gxpos = take(3 * ng); L.gxmat = take(9 * ng);
-  L.scom = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb); L.cdof = take(6 * nv);
-  L.cdofdot = take(6 * nv); L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.cfrc = take(6 * nb);
-  L.M = take(nv * nv); L.L = take(nv * nv); L.qpos = take(std::max(1, m.nq)); L.qvel = take(nv);
-  L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);
-  L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
-  L.qacc = take(nv); L.qfrc_con = take(nv); L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
-  L.rfmask = take(std::max(1, d.nrfblk));
-  L.total = off;
+  auto lds_layout = [&](bool blocked) {
+    off = 0;
+    L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+    L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.gxpos = take(3 * ng); L.gxmat = take(9 * ng);
+    L.scom = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb); L.cdof = take(6 * nv);
+    L.cdofdot = take(6 * nv); L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.cfrc = take(6 * nb);
+    const int msize = blocked ? std::max(1, d.nMblk) : nv * nv;
+    L.M = take(msize); L.L = take(msize); L.qpos = take(std::max(1, m.nq)); L.qvel = take(nv);
+    L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);
+    L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
+    L.qacc = take(nv); L.qfrc_con = take(nv); L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
+    L.rfmask = take(std::max(1, d.nrfblk));
+    L.efc_f = blocked ? take(std::max(1, d.max_efc)) : 0;
+    L.island = blocked ? take(2 * 64) : 0;  // per tree: 64-bit adjacency / component masks
+    L.total = off;
+  };
+  lds_layout(false);
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
@@ -610,15 +665,21 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     const int g = std::atoi(e);
     if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
   }
+  d.blocked = b.group == 64 ? 1 : 0;
+  if (d.blocked) lds_layout(true);
   if (lds_bytes(b.group) > 160 * 1024)
     throw UnsupportedError("model too large for the per-environment LDS working set");
-  // --- scratch layout (floats)
+  // --- scratch layout (floats).  Dense mode: rows J and M^-1 J' as nefc x nv plus per-row scalars;
+  // blocked mode: one record per row in solver order (J, M^-1 J' and dof per pipe slot, scalars)
   ScratchLayout& S = b.dm.S;
   off = 0;
   const int ne = std::max(1, d.max_efc);
-  S.efc_J = take(ne * nv); S.efc_MJ = take(ne * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
-  S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(ne); S.efc_aref = take(ne);
-  S.efc_b = take(ne); S.efc_f = take(ne); S.efc_ARii = take(ne); S.con = take(kConRec * std::max(1, d.max_con));
+  const int dn = d.blocked ? 0 : ne;
+  S.efc_J = take(dn * nv); S.efc_MJ = take(dn * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
+  S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(dn); S.efc_aref = take(dn);
+  S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));
+  S.efc_rec = take(d.blocked ? ne * (3 * d.pipe_w + 8) : 0);
+  S.efc_rowof = take(d.blocked ? ne : 0);
   S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);  // <= 64 lanes x 4 contacts x 7 floats
   S.sens = take(std::max(1, m.nsensordata));
   S.total = off;

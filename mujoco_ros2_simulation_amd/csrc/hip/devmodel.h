@@ -39,7 +39,9 @@ struct LdsLayout {
   int xpos, xquat, xmat, xipos, xanchor, xaxis, gxpos, gxmat, scom, cinert, crb, cdof, cdofdot,
       cvel, cacc, cfrc, M, L, qpos, qvel, ctrl, qfrc_applied, qacc_ws, qfrc_bias, qfrc_passive,
       qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force, Dg,
-      rfmask;  // per ray block: bitmask of candidate ray geoms (int bits)
+      rfmask,  // per ray block: bitmask of candidate ray geoms (int bits)
+      efc_f,   // blocked mode: row forces (by row index)
+      island;  // blocked mode: per-tree 64-bit component masks
   int total;  // floats per env (multiple of 4)
 };
 
@@ -48,6 +50,8 @@ struct LdsLayout {
 struct ScratchLayout {
   int efc_J, efc_MJ, efc_type, efc_pos, efc_margin, efc_floss, efc_R, efc_aref, efc_b, efc_f,
       efc_ARii, con, stage,  // contact records (kConRec floats each); per-lane narrow-phase staging
+      efc_rec,               // blocked mode: row records in solver order (3 * pipe_w + 8 floats each)
+      efc_rowof,             // blocked mode: row index of each record (int bits)
       sens;                  // sensordata sink of idle lane groups (envs past n_envs)
   int total;
 };
@@ -61,6 +65,9 @@ struct DevModel {
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth, njump;
   int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other, rf_common;
+  // kinematic trees with dofs; blocked: M per tree + sparse constraint rows (set when G = 64);
+  // pipe_w: dof slots per constraint row in the sparse solver (64 / pipe_w rows in flight per wave)
+  int ntree, tree_nmax, nMblk, blocked, pipe_w;
   // options
   int integrator, iterations, disableflags;
   int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)
@@ -77,6 +84,7 @@ struct DevModel {
   CPtr<int> dof_bodyid, dof_jntid;
   CPtr<float> dof_armature, dof_damping, dof_frictionloss, dof_solref, dof_solimp, dof_invweight0, qpos0, qpos_spring;
   CPtr<int> Mpair;  // [nMpair][2] (i, j) with j = i or an ancestor dof of i
+  CPtr<int> body_tree, dof_tree, tree_dofadr, tree_dofnum, tree_Moff;  // tree -1: world / no dofs
   // geoms
   CPtr<int> geom_type, geom_bodyid, geom_group;
   CPtr<float> geom_size, geom_pos, geom_quat, geom_rbound, geom_rgba;

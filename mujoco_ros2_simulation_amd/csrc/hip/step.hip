@@ -739,7 +739,20 @@ __device__ __forceinline__ DevModel load_model(const DevModel* mp) {
   const ScratchLayout& S = m.S;     \
   (void)L; (void)S; (void)scr; (void)lane
 
+// Index of M(i, j) (i, j in one kinematic tree) in the LDS storage of M and its factor: dense
+// nv x nv rows, or (blocked mode, one env per wave) the row-major block of the dofs' tree.
+template <int G>
+__device__ __forceinline__ int midx(const DevModel& m, int i, int j) {
+  if constexpr (G == 64) {
+    const int t = m.dof_tree[i], a = m.tree_dofadr[t], n = m.tree_dofnum[t];
+    return m.tree_Moff[t] + (i - a) * n + (j - a);
+  } else {
+    return i * m.nv + j;
+  }
+}
+
 // Cholesky of the dense nv x nv matrix A (LDS) into Lf (LDS), column by column; lanes over rows.
+// Blocked mode (G = 64): every tree's block at once, columns up to the largest tree's size.
 template <int G>
 __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
   mp = uniform_ptr(mp);
@@ -776,6 +789,29 @@ __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat
         if (p < nv) Lf[lane * nv + p] = p <= lane ? row[p] : 0.0f;
       });
     wsync();
+    return;
+  }
+  if constexpr (G == 64) {
+    const DevModel m = load_model(mp);
+    const int tr = lane < nv ? m.dof_tree[lane] : 0;
+    const int a = m.tree_dofadr[tr], n = lane < nv ? m.tree_dofnum[tr] : 0, li = lane - a;
+    const lfloat* Ab = A + m.tree_Moff[tr];
+    lfloat* Lb = Lf + m.tree_Moff[tr];
+    #pragma unroll 1
+    for (int k = 0; k < m.tree_nmax; ++k) {
+      float t = 0;
+      if (li >= k && k < n) {
+        t = Ab[li * n + k];
+        for (int p = 0; p < k; ++p) t -= Lb[li * n + p] * Lb[k * n + p];
+      }
+      const float dk = __shfl(t, a + k);  // pivot lane of this lane's tree (unused when k >= n)
+      const float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
+      if (k < n) {
+        if (li == k) Lb[k * n + k] = lkk;
+        else if (li > k) Lb[li * n + k] = t / lkk;
+      }
+      wsync();
+    }
     return;
   }
   #pragma unroll 1
@@ -824,6 +860,32 @@ __device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, con
         x = lane == i ? xi : (lane < i ? x - lcol[i] * xi : x);
       }
     });
+    return lane < nv ? x : 0.0f;
+  }
+  if constexpr (G == 64) {
+    // per tree block: lane of local index k is the pivot of step k
+    const DevModel m = load_model(mp);
+    const int tr = lane < nv ? m.dof_tree[lane] : 0;
+    const int a = m.tree_dofadr[tr], n = lane < nv ? m.tree_dofnum[tr] : 0, li = lane - a;
+    const lfloat* Lb = Lf + m.tree_Moff[tr];
+    #pragma unroll 1
+    for (int k = 0; k < m.tree_nmax; ++k) {
+      const float xs = __shfl(x, a + k);
+      if (k < n) {
+        const float xk = xs / Lb[k * n + k];
+        if (li == k) x = xk;
+        else if (li > k) x -= Lb[li * n + k] * xk;
+      }
+    }
+    #pragma unroll 1
+    for (int k = m.tree_nmax - 1; k >= 0; --k) {
+      const float xs = __shfl(x, a + k);
+      if (k < n) {
+        const float xk = xs / Lb[k * n + k];
+        if (li == k) x = xk;
+        else if (li < k) x -= Lb[k * n + li] * xk;
+      }
+    }
     return lane < nv ? x : 0.0f;
   }
   #pragma unroll 1
@@ -1112,8 +1174,9 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
     }
     for (int i = 0; i < 10; ++i) s[L.crb + 10 * b + i] = acc[i];
   }
+  const int msize = G == 64 ? m.nMblk : nv * nv;
   #pragma unroll 1
-  for (int i = lane; i < nv * nv; i += G) s[L.M + i] = 0;
+  for (int i = lane; i < msize; i += G) s[L.M + i] = 0;
   wsync();
   #pragma unroll 1
   for (int p = lane; p < m.nMpair; p += G) {
@@ -1124,8 +1187,8 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
     float v = 0;
     for (int k = 0; k < 6; ++k) v += s[L.cdof + 6 * j + k] * buf[k];
     if (i == j) v += m.dof_armature[i];
-    s[L.M + i * nv + j] = v;
-    s[L.M + j * nv + i] = v;
+    s[L.M + midx<G>(m, i, j)] = v;
+    s[L.M + midx<G>(m, j, i)] = v;
   }
   wsync();
 }
@@ -1565,9 +1628,462 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   return qa;
 }
 
+// ---------------------------------------------------------------- blocked mode: sparse rows
+// One env per wave (G = 64).  M is block diagonal over kinematic trees and a constraint row touches
+// at most two trees, so each row is stored over the dof slots of its trees only: P = pipe_w slots,
+// 64 / P rows in flight per wave ("pipes").  Rows are grouped into islands (trees connected through
+// contacts, as mj_island); rows of different islands share no dof, so the Gauss-Seidel sweeps of
+// different islands commute and each pipe sweeps its own islands in row order -- the same PGS
+// iterates as the row-serial solver (mj_solPGS), 64 / P rows per step instead of one.  Islands go to
+// pipes by longest-processing-time.  Records (J, M^-1 J' and dof per slot, row scalars) sit in the
+// env's scratch in solver order, pipe p's rows at [start_p, start_p + n_p); each level k of a sweep
+// is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
+typedef float v4f __attribute__((ext_vector_type(4)));
+constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, pad x3
+
+__device__ __forceinline__ int slot_dof(const DevModel& m, int t1, int t2, int slot) {
+  if (t1 < 0) return -1;
+  const int n1 = m.tree_dofnum[t1];
+  if (slot < n1) return m.tree_dofadr[t1] + slot;
+  if (t2 < 0) return -1;
+  const int l2 = slot - n1;
+  return l2 < m.tree_dofnum[t2] ? m.tree_dofadr[t2] + l2 : -1;
+}
+// trees of a row from its descriptor: t1 >= 0 unless the row touches no dof; t2 = -1 for one tree
+__device__ __forceinline__ void row_trees(const DevModel& m, const gfloat* scr, int code, int& t1, int& t2) {
+  const int t = code >> 16, id = code & 0xffff;
+  t2 = -1;
+  if (t == EFC_FRICTION) {
+    t1 = m.dof_tree[id];
+  } else if (t == EFC_LIMIT) {
+    t1 = m.dof_tree[m.jnt_dofadr[id]];
+  } else {
+    const int p = __float_as_int(scr[m.S.con + kConRec * id]);
+    int a = m.body_tree[m.geom_bodyid[m.pair_g1[p]]], b = m.body_tree[m.geom_bodyid[m.pair_g2[p]]];
+    if (a < 0) { a = b; b = -1; }
+    if (b == a) b = -1;
+    t1 = a;
+    t2 = b;
+  }
+}
+// x = M^-1 v restricted to the row's trees; the P slot lanes of one pipe hold v.  Block-wise forward
+// and back substitution; the pivot of step k of a tree segment is the segment's lane k.
+__device__ __forceinline__ float pipe_msolve(const DevModel& m, const lfloat* Lf, int t1, int t2, int slot, int pbase,
+                                             float v) {
+  int tr = -1, li = 0, sb = 0;
+  const int n1 = t1 >= 0 ? m.tree_dofnum[t1] : 0;
+  if (t1 >= 0 && slot < n1) { tr = t1; li = slot; }
+  else if (t2 >= 0 && slot - n1 < m.tree_dofnum[t2]) { tr = t2; li = slot - n1; sb = n1; }
+  const int n = tr >= 0 ? m.tree_dofnum[tr] : 0;
+  const lfloat* Lb = Lf + (tr >= 0 ? m.tree_Moff[tr] : 0);
+  float x = tr >= 0 ? v : 0.0f;
+  const int src = pbase + sb;
+  #pragma unroll 1
+  for (int k = 0; k < m.tree_nmax; ++k) {
+    const float xs = __shfl(x, src + k);
+    if (k < n) {
+      const float xk = xs / Lb[k * n + k];
+      if (li == k) x = xk;
+      else if (li > k) x -= Lb[li * n + k] * xk;
+    }
+  }
+  #pragma unroll 1
+  for (int k = m.tree_nmax - 1; k >= 0; --k) {
+    const float xs = __shfl(x, src + k);
+    if (k < n) {
+      const float xk = xs / Lb[k * n + k];
+      if (li == k) x = xk;
+      else if (li < k) x -= Lb[k * n + li] * xk;
+    }
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_max(int v) {
+  #pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mask), 0));
+}
+// one record as the sweeps read it
+template <int P>
+struct RowRec {
+  float J, MJ, aref, R, a, bound;
+  int d;
+};
+template <int P>
+__device__ __forceinline__ RowRec<P> load_rec(const gfloat* rec, int q, int slot) {
+  constexpr int RF = 3 * P + kRecScal;
+  const gfloat* r = rec + q * RF;
+  RowRec<P> o;
+  o.J = r[slot];
+  o.MJ = r[P + slot];
+  o.d = __float_as_int(r[2 * P + slot]);
+  const v4f sc = *(const __attribute__((address_space(1))) v4f*)(r + 3 * P);
+  o.aref = sc.x; o.R = sc.y; o.a = sc.z; o.bound = sc.w;
+  return o;
+}
+
+template <int P>
+__device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
+  constexpr int G = 64;
+  ENV_UNPACK;
+  ncon = uniform_int(ncon);
+  constexpr int NP = 64 / P;
+  constexpr int RF = 3 * P + kRecScal;
+  const int pipe = lane / P, slot = lane % P, pbase = pipe * P;
+  const int nv = m.nv, ME = m.max_efc;
+  gfloat* type = scr + S.efc_type;
+  gfloat* pos = scr + S.efc_pos;
+  gfloat* marg = scr + S.efc_margin;
+  gfloat* floss = scr + S.efc_floss;
+  gfloat* rec = scr + S.efc_rec;
+  gfloat* rowof = scr + S.efc_rowof;
+  gfloat* ffg = scr + S.efc_f;
+  lfloat* fl = s + L.efc_f;     // row forces by record position
+  lfloat* qa = s + L.qacc;      // qacc during the solve (lane per dof)
+  lfloat* tmp = s + L.qfrc_con; // warm-start M^-1 J' f, then qfrc_constraint
+  if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) tmp[lane] = 0; wsync(); return qacc_s; }
+
+  // --- 1. row descriptors in the row-serial solver's order: friction loss, limits, contacts
+  int nefc = 0;
+  if (!(m.disableflags & MRS_DSBL_FRICTIONLOSS)) {
+    #pragma unroll 1
+    for (int r = lane; r < m.nfric; r += 64) {
+      const int j = m.fric_dof[r];
+      type[r] = __int_as_float(EFC_FRICTION * 65536 + j);
+      pos[r] = 0; marg[r] = 0; floss[r] = m.dof_frictionloss[j];
+    }
+    nefc = m.nfric;
+  }
+  if (!(m.disableflags & MRS_DSBL_LIMIT)) {
+    #pragma unroll 1
+    for (int base = 0; base < m.nlim; base += 64) {
+      const int k = base + lane;
+      float dist[2] = {0, 0};
+      int jid = -1;
+      bool act[2] = {false, false};
+      if (k < m.nlim) {
+        jid = m.lim_jnt[k];
+        const float q = s[L.qpos + m.jnt_qposadr[jid]], mg = m.jnt_margin[jid];
+        dist[0] = q - m.jnt_range[2 * jid];
+        dist[1] = m.jnt_range[2 * jid + 1] - q;
+        act[0] = dist[0] < mg;
+        act[1] = dist[1] < mg;
+      }
+      int total;
+      int r = nefc + gscan_excl<64>((int)act[0] + (int)act[1], lane, total);
+      for (int sd = 0; sd < 2; ++sd) {
+        if (!act[sd]) continue;
+        type[r] = __int_as_float(EFC_LIMIT * 65536 + jid);
+        pos[r] = dist[sd];
+        marg[r] = m.jnt_margin[jid];
+        floss[r] = sd == 0 ? 1.0f : -1.0f;  // J sign
+        ++r;
+      }
+      nefc += total;
+    }
+  }
+  #pragma unroll 1
+  for (int base = 0; base < ncon; base += 64) {
+    const int c = base + lane;
+    gfloat* crec = scr + S.con + kConRec * (c < ncon ? c : 0);
+    int nr = 0, p = 0;
+    if (c < ncon) { p = __float_as_int(crec[0]); nr = m.pair_dim[p] == 1 ? 1 : 4; }
+    int total;
+    const int r0 = nefc + gscan_excl<64>(nr, lane, total);
+    if (c < ncon) {
+      crec[14] = __int_as_float(r0 + nr <= ME ? r0 : -1);
+      for (int j = 0; j < nr; ++j) {
+        const int r = r0 + j;
+        if (r >= ME) break;
+        type[r] = __int_as_float(EFC_CONTACT * 65536 + c);
+        pos[r] = crec[1]; marg[r] = m.pair_margin[p] - m.pair_gap[p]; floss[r] = (float)j;
+      }
+    }
+    nefc += total;
+  }
+  nefc = min(nefc, ME);
+  wsync();
+  if (nefc == 0) {
+    if (lane < nv) tmp[lane] = 0;
+    wsync();
+    return qacc_s;
+  }
+
+  // --- 2. islands: lane t holds the smallest tree id of its component (contacts merge components)
+  int lbl = lane;
+  #pragma unroll 1
+  for (int base = 0; base < ncon; base += 64) {
+    const int c = base + lane;
+    int a = -1, b = -1;
+    if (c < ncon) {
+      const int p = __float_as_int(scr[S.con + kConRec * c]);
+      a = m.body_tree[m.geom_bodyid[m.pair_g1[p]]];
+      b = m.body_tree[m.geom_bodyid[m.pair_g2[p]]];
+    }
+    const int nc = min(64, ncon - base);
+    #pragma unroll 1
+    for (int k = 0; k < nc; ++k) {
+      const int ak = __builtin_amdgcn_readlane(a, k), bk = __builtin_amdgcn_readlane(b, k);
+      if (ak < 0 || bk < 0 || ak == bk) continue;
+      const int la = __builtin_amdgcn_readlane(lbl, ak), lb = __builtin_amdgcn_readlane(lbl, bk);
+      const int lo = min(la, lb), hi = max(la, lb);
+      if (lbl == hi) lbl = lo;
+    }
+  }
+  // rows per island (lane i: island whose smallest tree is i), rows without dofs go to pipe 0
+  int cnt = 0, nodof = 0;
+  #pragma unroll 1
+  for (int base = 0; base < nefc; base += 64) {
+    const int r = base + lane;
+    int t1 = -1, t2;
+    if (r < nefc) row_trees(m, scr, __float_as_int(type[r]), t1, t2);
+    const int il = __shfl(lbl, t1 < 0 ? 0 : t1);
+    nodof += __popcll(__ballot(r < nefc && t1 < 0));
+    #pragma unroll 1
+    for (int i = 0; i < m.ntree; ++i) {
+      const int ci = __popcll(__ballot(r < nefc && t1 >= 0 && il == i));
+      if (lane == i) cnt += ci;
+    }
+  }
+  // longest-processing-time: largest island first onto the least loaded pipe
+  int load[NP];
+  unroll<NP>([&](auto pc) { load[decltype(pc)::value] = 0; });
+  load[0] = nodof;
+  int mypipe = 0;  // lane i: pipe of island i
+  #pragma unroll 1
+  for (;;) {
+    const int key = wave_max(cnt > 0 ? (cnt << 8) | (255 - lane) : -1);
+    if (key < 0) break;
+    const int win = 255 - (key & 255), c = key >> 8;
+    int best = 0, bl = load[0];
+    unroll<NP>([&](auto pc) {
+      constexpr int q = decltype(pc)::value;
+      if (load[q] < bl) { bl = load[q]; best = q; }
+    });
+    if (lane == win) { mypipe = best; cnt = 0; }
+    unroll<NP>([&](auto pc) {
+      constexpr int q = decltype(pc)::value;
+      if (q == best) load[q] += c;
+    });
+  }
+  // solver order: pipe p's rows in row order at records [start_p, start_p + n_p)
+  int start[NP], fill[NP], nlev = 0, my_n = 0, my_start = 0;
+  {
+    int acc = 0;
+    unroll<NP>([&](auto pc) {
+      constexpr int q = decltype(pc)::value;
+      start[q] = acc; fill[q] = acc; acc += load[q];
+      nlev = max(nlev, load[q]);
+      if (pipe == q) { my_n = load[q]; my_start = start[q]; }
+    });
+  }
+  #pragma unroll 1
+  for (int base = 0; base < nefc; base += 64) {
+    const int r = base + lane;
+    int t1 = -1, t2;
+    if (r < nefc) row_trees(m, scr, __float_as_int(type[r]), t1, t2);
+    const int il = __shfl(lbl, t1 < 0 ? 0 : t1);
+    const int pr = __shfl(mypipe, il);
+    const int rp = t1 < 0 ? 0 : pr;
+    unroll<NP>([&](auto pc) {
+      constexpr int q = decltype(pc)::value;
+      const unsigned long long mk = __ballot(r < nefc && rp == q);
+      if (r < nefc && rp == q) rowof[fill[q] + lanes_below(mk)] = __int_as_float(r);
+      fill[q] += __popcll(mk);
+    });
+  }
+  wsync();
+
+  // --- 3. records: at level k every pipe builds its k-th row
+  #pragma unroll 1
+  for (int k = 0; k < nlev; ++k) {
+    const bool act = k < my_n;
+    const int q = act ? my_start + k : 0;
+    const int r = __float_as_int(rowof[q]);
+    const int code = __float_as_int(type[r]);
+    const int t = code >> 16, id = code & 0xffff;
+    int t1, t2;
+    row_trees(m, scr, code, t1, t2);
+    const int d = slot_dof(m, t1, t2, slot);
+    float J = 0, diag;
+    CPtr<float> sr, si;
+    if (t == EFC_FRICTION) {
+      J = d == id ? 1.0f : 0.0f;
+      sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id];
+    } else if (t == EFC_LIMIT) {
+      const int dof = m.jnt_dofadr[id];
+      J = d == dof ? floss[r] : 0.0f;
+      sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[dof];
+    } else {
+      const gfloat* crec = scr + S.con + kConRec * id;
+      const int p = __float_as_int(crec[0]);
+      const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+      const float mu = m.pair_friction[3 * p];  // sliding, for both tangent directions
+      sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
+      const float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      diag = m.pair_dim[p] == 3 ? tran * (1 + mu * mu) : tran;
+      if (d >= 0) {
+        const float cp[3] = {crec[2], crec[3], crec[4]};
+        float c1[3], c2[3], jc[3];
+        jac_col(m, s, b1, cp, d, c1);
+        jac_col(m, s, b2, cp, d, c2);
+        const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+        for (int i = 0; i < 3; ++i) jc[i] = crec[5 + 3 * i] * dc[0] + crec[6 + 3 * i] * dc[1] + crec[7 + 3 * i] * dc[2];
+        if (m.pair_dim[p] == 1) {
+          J = jc[0];
+        } else {
+          const int j = (int)floss[r];
+          const float sg = (j & 1) ? -1.0f : 1.0f;
+          J = jc[0] + sg * mu * (j < 2 ? jc[1] : jc[2]);
+        }
+      }
+    }
+    const float MJ = pipe_msolve(m, s + L.L, t1, t2, slot, pbase, J);
+    const float vel = gsum<P>(d >= 0 ? J * s[L.qvel + d] : 0.0f);
+    const float jqs = gsum<P>(d >= 0 ? J * s[L.qacc_smooth + d] : 0.0f);
+    const float jmj = gsum<P>(J * MJ);
+    const float imp = impedance(si, pos[r], marg[r]);
+    float R = (1 - imp) * diag / imp;
+    R = R > kMinVal ? R : kMinVal;
+    const float dmax = clampf(si[1], 0.0001f, 0.9999f);
+    float K, B;
+    if (sr[0] > 0) {
+      float tc = sr[0], dr = sr[1];
+      if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -sr[0] / (dmax * dmax);
+      B = -sr[1] / dmax;
+    }
+    const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
+    const float aref = -B * vel - pterm;
+    if (act) {
+      gfloat* o = rec + q * RF;
+      o[slot] = J;
+      o[P + slot] = MJ;
+      o[2 * P + slot] = __int_as_float(d);
+      if (slot == 0) {
+        o[3 * P + 0] = aref;
+        o[3 * P + 1] = R;
+        o[3 * P + 2] = jmj + R;
+        o[3 * P + 3] = t == EFC_FRICTION ? floss[r] : -1.0f;
+        o[3 * P + 4] = jqs - aref;
+      }
+    }
+  }
+  wsync();
+
+  // --- 4. warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost < 0
+  if (lane < nv) qa[lane] = qacc_s;
+  const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+  #pragma unroll 1
+  for (int k = 0; k < nlev; ++k) {
+    const bool act = k < my_n;
+    const int q = act ? my_start + k : 0;
+    const RowRec<P> w = load_rec<P>(rec, q, slot);
+    float f = 0;
+    if (warm) {
+      const float jar = gsum<P>(act && w.d >= 0 ? w.J * s[L.qacc_ws + w.d] : 0.0f) - w.aref;
+      const float D = 1.0f / w.R;
+      if (w.bound >= 0) f = jar <= -w.R * w.bound ? w.bound : (jar >= w.R * w.bound ? -w.bound : -D * jar);
+      else f = jar < 0 ? -D * jar : 0.0f;
+    }
+    if (act && slot == 0) fl[q] = f;
+  }
+  wsync();
+  if (warm) {
+    if (lane < nv) tmp[lane] = 0;
+    wsync();
+    #pragma unroll 1
+    for (int k = 0; k < nlev; ++k) {
+      const bool act = k < my_n;
+      const int q = act ? my_start + k : 0;
+      const RowRec<P> w = load_rec<P>(rec, q, slot);
+      if (act && w.d >= 0) tmp[w.d] += w.MJ * fl[q];
+    }
+    wsync();
+    float cost = 0;
+    #pragma unroll 1
+    for (int k = 0; k < nlev; ++k) {
+      const bool act = k < my_n;
+      const int q = act ? my_start + k : 0;
+      const RowRec<P> w = load_rec<P>(rec, q, slot);
+      const float jv = gsum<P>(act && w.d >= 0 ? w.J * tmp[w.d] : 0.0f);
+      const float f = fl[q];
+      const float b = rec[q * RF + 3 * P + 4];
+      if (act && slot == 0) cost += f * (0.5f * (jv + w.R * f) + b);
+    }
+    cost = gsum<64>(cost);
+    if (cost > 0) {
+      #pragma unroll 1
+      for (int q = lane; q < nefc; q += 64) fl[q] = 0;
+    } else if (lane < nv) {
+      qa[lane] += tmp[lane];
+    }
+    wsync();
+  }
+
+  // --- 5. PGS sweeps: level k = the k-th row of every pipe; next level's record prefetched
+  #pragma unroll 1
+  for (int it = 0; it < m.iterations; ++it) {
+    float improvement = 0;
+    RowRec<P> nxt = load_rec<P>(rec, my_n > 0 ? my_start : 0, slot);
+    #pragma unroll 1
+    for (int k = 0; k < nlev; ++k) {
+      const RowRec<P> w = nxt;
+      const bool act = k < my_n;
+      if (k + 1 < nlev) nxt = load_rec<P>(rec, k + 1 < my_n ? my_start + k + 1 : 0, slot);
+      const int q = act ? my_start + k : 0;
+      const bool mine = act && w.d >= 0;
+      const float qd = mine ? qa[w.d] : 0.0f;
+      const float f0 = fl[q];
+      const float jq = gsum<P>(mine ? w.J * qd : 0.0f);
+      const float res = jq - w.aref + w.R * f0;
+      float nf = f0 - res / w.a;
+      if (w.bound >= 0) nf = clampf(nf, -w.bound, w.bound);
+      else if (nf < 0) nf = 0;
+      const float delta = nf - f0;
+      if (mine && delta != 0) qa[w.d] = qd + w.MJ * delta;
+      if (act && slot == 0) fl[q] = nf;
+      if (act) improvement -= delta * res + 0.5f * delta * delta * w.a;
+    }
+    improvement = gsum<64>(slot == 0 ? improvement : 0.0f);
+    if (improvement * m.pgs_scale < m.tolerance) break;
+  }
+  wsync();
+
+  // --- 6. qfrc_constraint = J' f (per dof in row order: a dof's rows are in one pipe); forces out
+  if (lane < nv) tmp[lane] = 0;
+  wsync();
+  #pragma unroll 1
+  for (int k = 0; k < nlev; ++k) {
+    const bool act = k < my_n;
+    const int q = act ? my_start + k : 0;
+    const RowRec<P> w = load_rec<P>(rec, q, slot);
+    if (act && w.d >= 0) tmp[w.d] += w.J * fl[q];
+  }
+  #pragma unroll 1
+  for (int q = lane; q < nefc; q += 64) ffg[__float_as_int(rowof[q])] = fl[q];
+  wsync();
+  return lane < nv ? qa[lane] : 0.0f;
+}
+
 template <int G>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
+  if constexpr (G == 64) {
+    switch (m.pipe_w) {
+      case 8: return constraints_sparse<8>(ENV_ARGS, ncon, qacc_s);
+      case 16: return constraints_sparse<16>(ENV_ARGS, ncon, qacc_s);
+      case 32: return constraints_sparse<32>(ENV_ARGS, ncon, qacc_s);
+      default: return constraints_sparse<64>(ENV_ARGS, ncon, qacc_s);
+    }
+  }
   if constexpr (G == 64) ncon = uniform_int(ncon);
   const int nv = m.nv;
   gfloat* J = scr + S.efc_J;
@@ -2373,7 +2889,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   float qacc_int = qacc;
   if (need_solve) {
     // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
-    if (lane < nv) s[L.M + lane * nv + lane] += h * dg;
+    if (lane < nv) s[L.M + midx<G>(m, lane, lane)] += h * dg;
     wsync();
     MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
     float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;

@@ -1,5 +1,6 @@
-"""Per-phase cycle breakdown of the C3 step kernel with a profiling build (MRS_LIB pointing at a
-library built with -DMRS_PHASE_TIMING, e.g. scripts/build_variant.sh timing -DMRS_PHASE_TIMING)."""
+"""Per-phase cycle breakdown of the step kernel with a profiling build (MRS_LIB pointing at a
+library built with -DMRS_PHASE_TIMING, e.g. scripts/build_variant.sh timing -DMRS_PHASE_TIMING).
+Usage: phase_profile.py [scene.xml] [n_envs] [launches]  (default: C3, 8192 envs, 20 launches)"""
 import json
 import sys
 from pathlib import Path
@@ -12,8 +13,11 @@ import torch  # noqa: E402
 
 from mujoco_ros2_simulation_amd import sim, synth  # noqa: E402
 
-n, period, launches = 8192, 10, 20
-model = sim.Model.load(ROOT / "scenes" / "arm7_lidar.xml")
+scene = sys.argv[1] if len(sys.argv) > 1 else str(ROOT / "scenes" / "arm7_lidar.xml")
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+launches = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+period = 10
+model = sim.Model.load(scene)
 b = sim.Batch(model, n)
 b.set(sim.FIELD_QPOS, synth.initial_qpos(model, np.arange(n)))
 table = torch.from_numpy(synth.ctrl_table(model, np.arange(n), launches + 2, period).astype(np.float32)).cuda()
@@ -25,4 +29,5 @@ for p in range(launches):
 b.sync()
 pc = sim.phase_cycles()
 tot = sum(v for k, v in pc.items() if "." not in k)
-print(json.dumps({k: round(v / tot, 4) for k, v in pc.items()}))
+print(json.dumps({"scene": Path(scene).stem, "n": n, "cycles_per_env_step": tot / (n * launches * period),
+                  **{k: round(v / tot, 4) for k, v in pc.items()}}))
