@@ -645,7 +645,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.M = take(msize); L.L = take(msize); L.qpos = take(std::max(1, m.nq)); L.qvel = take(nv);
     L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);
     L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
-    L.qacc = take(nv); L.qfrc_con = take(nv); L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
+    L.qacc = take(nv + 1); L.qfrc_con = take(nv + 1);  // + a dummy word (blocked-mode solver)
+    L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
     L.rfmask = take(std::max(1, d.nrfblk));
     L.efc_f = blocked ? take(std::max(1, d.max_efc)) : 0;
     L.island = blocked ? take(2 * 64) : 0;  // per tree: 64-bit adjacency / component masks

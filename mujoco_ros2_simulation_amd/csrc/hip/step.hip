@@ -668,7 +668,8 @@ enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 // Per-phase cycle accounting, built only with -DMRS_PHASE_TIMING (profiling variant): s_memtime
 // around each phase, summed per wave and added to a device table at the end of the kernel.
 enum { PH_KIN, PH_COMPOS, PH_MAKEM, PH_CHOL, PH_COMVEL, PH_RNE, PH_SMOOTH, PH_COLL, PH_CONSTR, PH_SENS,
-       PH_INTEG, PH_CHECK, PH_SENS_L1, PH_SENS_SETUP, PH_SENS_GEOMS, PH_COUNT };
+       PH_INTEG, PH_CHECK, PH_SENS_L1, PH_SENS_SETUP, PH_SENS_GEOMS, PH_CON_ROWS, PH_CON_REC, PH_CON_WARM,
+       PH_CON_PGS, PH_COUNT };
 #ifdef MRS_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[PH_COUNT];
 #define SUB_T() __builtin_amdgcn_s_memtime()
@@ -1640,6 +1641,7 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
 // is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
 typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, pad x3
+constexpr int kRegLevels = 64;  // rows per pipe of the register-resident solve
 
 __device__ __forceinline__ int slot_dof(const DevModel& m, int t1, int t2, int slot) {
   if (t1 < 0) return -1;
@@ -1746,6 +1748,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   lfloat* qa = s + L.qacc;      // qacc during the solve (lane per dof)
   lfloat* tmp = s + L.qfrc_con; // warm-start M^-1 J' f, then qfrc_constraint
   if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) tmp[lane] = 0; wsync(); return qacc_s; }
+  unsigned long long t_sub = SUB_T();
 
   // --- 1. row descriptors in the row-serial solver's order: friction loss, limits, contacts
   int nefc = 0;
@@ -1880,6 +1883,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       nlev = max(nlev, load[q]);
       if (pipe == q) { my_n = load[q]; my_start = start[q]; }
     });
+    nlev = uniform_int(nlev);
   }
   #pragma unroll 1
   for (int base = 0; base < nefc; base += 64) {
@@ -1897,6 +1901,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     });
   }
   wsync();
+  SUB_ADD(PH_CON_ROWS, t_sub);
+  t_sub = SUB_T();
 
   // --- 3. records: at level k every pipe builds its k-th row
   #pragma unroll 1
@@ -1977,10 +1983,158 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     }
   }
   wsync();
-
-  // --- 4. warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost < 0
+  SUB_ADD(PH_CON_REC, t_sub);
+  t_sub = SUB_T();
   if (lane < nv) qa[lane] = qacc_s;
   const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+
+  // --- register-resident solve: P = 16 and at most kRegLevels rows per pipe.  Lane (pipe, slot)
+  // keeps J, M^-1 J' and the dof of its slot for every level (slots outside the row's trees point at
+  // a dummy LDS word after qacc, with J = M^-1 J' = 0); the row scalars and the force of level k live
+  // in slot k % 16 and reach the pipe by one DPP row broadcast each.  A level is branch-free: pipes
+  // with fewer rows run neutral rows (J = 0, R = a = 1, bounds [0, inf)), whose force stays 0.
+  // Sweeps touch LDS only for qacc.
+  if constexpr (P == 16) {
+    if (nlev <= kRegLevels) {
+      constexpr int NL = kRegLevels, NB = NL / 16;
+      float Jr[NL], MJr[NL], sa[NB], sR[NB], sA[NB], sLo[NB], sHi[NB], fr[NB];
+      unsigned dpk[NL / 4];
+      const unsigned dummy = static_cast<unsigned>(nv);
+      if (lane == 0) { qa[nv] = 0; tmp[nv] = 0; }
+      unroll<NL / 4>([&](auto ic) { dpk[decltype(ic)::value] = dummy * 0x01010101u; });
+      unroll<NB>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sa[i] = 0; sR[i] = 1; sA[i] = 1; sLo[i] = 0; sHi[i] = 3.0e38f; fr[i] = 0;
+      });
+      unroll<NL>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        Jr[k] = 0; MJr[k] = 0;
+        if (k < nlev) {
+          const bool act = k < my_n;
+          const gfloat* o = rec + (act ? my_start + k : 0) * RF;
+          const int d = __float_as_int(o[2 * P + slot]);
+          if (act) {
+            Jr[k] = o[slot];
+            MJr[k] = o[P + slot];
+            const unsigned di = d >= 0 ? static_cast<unsigned>(d) : dummy;
+            dpk[k / 4] = (dpk[k / 4] & ~(0xffu << (8 * (k % 4)))) | (di << (8 * (k % 4)));
+          }
+          if (act && slot == k % 16) {
+            const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
+            sa[k / 16] = sc.x; sR[k / 16] = sc.y; sA[k / 16] = sc.z;
+            sLo[k / 16] = sc.w >= 0 ? -sc.w : 0.0f;     // friction: [-frictionloss, frictionloss]
+            sHi[k / 16] = sc.w >= 0 ? sc.w : 3.0e38f;   // others: [0, inf)
+          }
+        }
+      });
+      wsync();
+      auto dof_of = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        return static_cast<int>(__builtin_amdgcn_ubfe(dpk[k / 4], 8 * (k % 4), 8));
+      };
+      // warm start
+      unroll<NL>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k < nlev) {
+          const int d = dof_of(kc);
+          float f = 0;
+          if (warm) {
+            const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+            const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
+            const float jar = gsum<16>(Jr[k] * s[L.qacc_ws + d]) - aref;
+            const float D = 1.0f / R;
+            if (lo < 0) f = jar <= -R * hi ? hi : (jar >= R * hi ? -hi : -D * jar);
+            else f = jar < 0 ? -D * jar : 0.0f;
+          }
+          if (slot == k % 16 && k < my_n) fr[k / 16] = f;
+        }
+      });
+      if (warm) {
+        if (lane < nv) tmp[lane] = 0;
+        wsync();
+        unroll<NL>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if (k < nlev) {
+            const int d = dof_of(kc);
+            tmp[d] += MJr[k] * rowb<k % 16>(fr[k / 16]);
+          }
+        });
+        wsync();
+        float cost = 0;
+        unroll<NL>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if (k < nlev) {
+            const int d = dof_of(kc);
+            const float jv = gsum<16>(Jr[k] * tmp[d]);
+            const float f = rowb<k % 16>(fr[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+            const float b = rec[(k < my_n ? my_start + k : 0) * RF + 3 * P + 4];
+            if (k < my_n) cost += f * (0.5f * (jv + R * f) + b);
+          }
+        });
+        cost = gsum<64>(slot == 0 ? cost : 0.0f);
+        if (cost > 0) {
+          unroll<NB>([&](auto ic) { fr[decltype(ic)::value] = 0; });
+        } else if (lane < nv) {
+          qa[lane] += tmp[lane];
+        }
+        wsync();
+      }
+      SUB_ADD(PH_CON_WARM, t_sub);
+      t_sub = SUB_T();
+      // PGS sweeps
+      int slot_v = slot;
+      #pragma unroll 1
+      for (int it = 0; it < m.iterations; ++it) {
+        // opaque per sweep: keeps the per-level dof indices and lane masks from being hoisted out
+        // of the sweep loop (they would not fit the register budget next to J and M^-1 J')
+#pragma unroll
+        for (int i = 0; i < NL / 4; ++i) asm volatile("" : "+v"(dpk[i]));
+        asm volatile("" : "+v"(slot_v));
+        float improvement = 0;
+        unroll<NL>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if (k < nlev) {
+            const int d = dof_of(kc);
+            const float qd = qa[d];
+            const float f0 = rowb<k % 16>(fr[k / 16]);
+            const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+            const float a = rowb<k % 16>(sA[k / 16]);
+            const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
+            const float jq = gsum<16>(Jr[k] * qd);
+            const float res = jq - aref + R * f0;
+            const float nf = __builtin_amdgcn_fmed3f(f0 - res * __builtin_amdgcn_rcpf(a), lo, hi);
+            const float delta = nf - f0;
+            qa[d] = qd + MJr[k] * delta;
+            fr[k / 16] = slot_v == k % 16 ? nf : fr[k / 16];
+            improvement -= delta * res + 0.5f * delta * delta * a;
+          }
+        });
+        improvement = gsum<64>(slot_v == 0 ? improvement : 0.0f);
+        if (improvement * m.pgs_scale < m.tolerance) break;
+      }
+      wsync();
+      SUB_ADD(PH_CON_PGS, t_sub);
+      // qfrc_constraint = J' f and the forces out (by row index, for mj_rnePostConstraint)
+      if (lane < nv) tmp[lane] = 0;
+      wsync();
+      unroll<NL>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k < nlev) {
+          const int d = dof_of(kc);
+          tmp[d] += Jr[k] * rowb<k % 16>(fr[k / 16]);
+        }
+      });
+      unroll<NB>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const int k = i * 16 + slot;
+        if (k < my_n) ffg[__float_as_int(rowof[my_start + k])] = fr[i];
+      });
+      wsync();
+      return lane < nv ? qa[lane] : 0.0f;
+    }
+  }
+
+  // --- 4. warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost < 0
   #pragma unroll 1
   for (int k = 0; k < nlev; ++k) {
     const bool act = k < my_n;
@@ -2924,11 +3078,13 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   wsync();
 }
 
-// waves per SIMD the register budget is sized for: 8 waves at one env per wave (64 VGPRs); with
-// G < 64 the LDS of 4*64/G envs per workgroup bounds residency instead (e.g. G = 16: 16 envs x 4.5 KB
-// per workgroup -> 2 workgroups per CU -> 2 waves per SIMD, 256 VGPRs)
+// waves per SIMD the register budget is sized for.  One env per wave (G = 64, blocked mode): 2 waves
+// (256 VGPRs) -- the register-resident sparse PGS holds up to 64 rows per pipe, and the per-env LDS of
+// the multi-tree scenes that pick G = 64 (C5: ~13 KB) allows ~2 waves per SIMD anyway.  With G < 64
+// the LDS of 4*64/G envs per workgroup bounds residency instead (e.g. G = 16: 16 envs x 4.5 KB per
+// workgroup -> 2 workgroups per CU -> 2 waves per SIMD, 256 VGPRs)
 template <int G>
-struct Occupancy { static constexpr int waves = G == 64 ? 8 : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
+struct Occupancy { static constexpr int waves = G == 64 ? 2 : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
 template <int G, bool kForwardOnly>
 __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step_kernel(
