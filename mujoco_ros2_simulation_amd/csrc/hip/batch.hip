@@ -649,7 +649,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
     L.rfmask = take(std::max(1, d.nrfblk));
     L.efc_f = blocked ? take(std::max(1, d.max_efc)) : 0;
-    L.island = blocked ? take(2 * 64) : 0;  // per tree: 64-bit adjacency / component masks
+    L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
     L.total = off;
   };
   lds_layout(false);
@@ -681,6 +681,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));
   S.efc_rec = take(d.blocked ? ne * (3 * d.pipe_w + 8) : 0);
   S.efc_rowof = take(d.blocked ? ne : 0);
+  S.efc_item = take(d.blocked ? ne : 0);
+  S.efc_hdr = take(d.blocked ? 8 * ne : 0);
   S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);  // <= 64 lanes x 4 contacts x 7 floats
   S.sens = take(std::max(1, m.nsensordata));
   S.total = off;

@@ -41,7 +41,7 @@ struct LdsLayout {
       qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force, Dg,
       rfmask,  // per ray block: bitmask of candidate ray geoms (int bits)
       efc_f,   // blocked mode: row forces (by row index)
-      island;  // blocked mode: per-tree 64-bit component masks
+      trees;   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
   int total;  // floats per env (multiple of 4)
 };
 
@@ -52,10 +52,12 @@ struct ScratchLayout {
       efc_ARii, con, stage,  // contact records (kConRec floats each); per-lane narrow-phase staging
       efc_rec,               // blocked mode: row records in solver order (3 * pipe_w + 8 floats each)
       efc_rowof,             // blocked mode: row index of each record (int bits)
+      efc_item,              // blocked mode: first row of the item starting at a record (int bits)
+      efc_hdr,               // blocked mode: 8-float header of the item starting at a record
       sens;                  // sensordata sink of idle lane groups (envs past n_envs)
   int total;
 };
-constexpr int kConRec = 16;  // pair id (int bits), dist, pos[3], frame[9], pad[2]
+constexpr int kConRec = 16;  // pair id (int bits), dist, pos[3], frame[9], first efc row (-1 if cut), first row (blocked mode)
 
 // Everything the step kernel reads about the model.  Lives in device memory; the kernel receives
 // one pointer to it.

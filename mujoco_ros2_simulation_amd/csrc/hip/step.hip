@@ -1651,6 +1651,21 @@ __device__ __forceinline__ int slot_dof(const DevModel& m, int t1, int t2, int s
   const int l2 = slot - n1;
   return l2 < m.tree_dofnum[t2] ? m.tree_dofadr[t2] + l2 : -1;
 }
+// a tree's (dofadr, dofnum, M block offset) from the env's LDS copy of the tree table
+struct TreeInfo { int adr, num, off; };
+__device__ __forceinline__ TreeInfo tree_lds(const lfloat* s, const LdsLayout& L, int t) {
+  const v4f v = *(const __attribute__((address_space(3))) v4f*)(s + L.trees + 4 * (t < 0 ? 0 : t));
+  return TreeInfo{__float_as_int(v.x), t < 0 ? 0 : __float_as_int(v.y), __float_as_int(v.z)};
+}
+// slot -> (dof, tree segment) of a row over trees t1, t2 (LDS tree table)
+struct SlotMap { int d, li, n, off, sb; };
+__device__ __forceinline__ SlotMap slot_map(const lfloat* s, const LdsLayout& L, int t1, int t2, int slot) {
+  const TreeInfo a = tree_lds(s, L, t1), b = tree_lds(s, L, t2);
+  SlotMap r{-1, 0, 0, 0, 0};
+  if (t1 >= 0 && slot < a.num) { r.d = a.adr + slot; r.li = slot; r.n = a.num; r.off = a.off; }
+  else if (t1 >= 0 && t2 >= 0 && slot - a.num < b.num) { r.d = b.adr + slot - a.num; r.li = slot - a.num; r.n = b.num; r.off = b.off; r.sb = a.num; }
+  return r;
+}
 // trees of a row from its descriptor: t1 >= 0 unless the row touches no dof; t2 = -1 for one tree
 __device__ __forceinline__ void row_trees(const DevModel& m, const gfloat* scr, int code, int& t1, int& t2) {
   const int t = code >> 16, id = code & 0xffff;
@@ -1699,6 +1714,41 @@ __device__ __forceinline__ float pipe_msolve(const DevModel& m, const lfloat* Lf
     }
   }
   return x;
+}
+// three right-hand sides at once (a contact's normal and tangent Jacobian rows): the substitution
+// chains interleave and share the pivot reciprocal
+__device__ __forceinline__ void pipe_msolve3(const DevModel& m, const lfloat* Lf, const SlotMap& sm, int pbase,
+                                             const float v[3], float x[3]) {
+  const int li = sm.li, n = sm.n;
+  const lfloat* Lb = Lf + sm.off;
+  for (int i = 0; i < 3; ++i) x[i] = sm.d >= 0 ? v[i] : 0.0f;
+  const int src = pbase + sm.sb;
+  #pragma unroll 1
+  for (int k = 0; k < m.tree_nmax; ++k) {
+    float xs[3];
+    for (int i = 0; i < 3; ++i) xs[i] = __shfl(x[i], src + k);
+    if (k < n) {
+      const float inv = 1.0f / Lb[k * n + k];
+      const float lik = li > k ? Lb[li * n + k] : 0.0f;
+      for (int i = 0; i < 3; ++i) {
+        const float xk = xs[i] * inv;
+        x[i] = li == k ? xk : (li > k ? x[i] - lik * xk : x[i]);
+      }
+    }
+  }
+  #pragma unroll 1
+  for (int k = m.tree_nmax - 1; k >= 0; --k) {
+    float xs[3];
+    for (int i = 0; i < 3; ++i) xs[i] = __shfl(x[i], src + k);
+    if (k < n) {
+      const float inv = 1.0f / Lb[k * n + k];
+      const float lki = li < k ? Lb[k * n + li] : 0.0f;
+      for (int i = 0; i < 3; ++i) {
+        const float xk = xs[i] * inv;
+        x[i] = li == k ? xk : (li < k ? x[i] - lki * xk : x[i]);
+      }
+    }
+  }
 }
 __device__ __forceinline__ int wave_max(int v) {
   #pragma unroll
@@ -1789,6 +1839,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       nefc += total;
     }
   }
+  const int nsingle = nefc;  // friction-loss and limit rows: one item each
   #pragma unroll 1
   for (int base = 0; base < ncon; base += 64) {
     const int c = base + lane;
@@ -1799,6 +1850,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     const int r0 = nefc + gscan_excl<64>(nr, lane, total);
     if (c < ncon) {
       crec[14] = __int_as_float(r0 + nr <= ME ? r0 : -1);
+      crec[15] = __int_as_float(r0);
       for (int j = 0; j < nr; ++j) {
         const int r = r0 + j;
         if (r >= ME) break;
@@ -1837,19 +1889,38 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       if (lbl == hi) lbl = lo;
     }
   }
-  // rows per island (lane i: island whose smallest tree is i), rows without dofs go to pipe 0
+  // items: a friction-loss or limit row, or the consecutive 1 or 4 rows of one contact (rows past
+  // max_efc are cut).  Rows per island (lane i: the island whose smallest tree is i); rows without
+  // dofs go to pipe 0.
+  const int nitem = nsingle + ncon;
+  auto item_info = [&](int i, int& r0, int& nr) {
+    if (i < nsingle) {
+      r0 = i;
+      nr = 1;
+    } else {
+      const gfloat* crec = scr + S.con + kConRec * (i - nsingle);
+      r0 = __float_as_int(crec[15]);
+      nr = max(0, min(m.pair_dim[__float_as_int(crec[0])] == 1 ? 1 : 4, ME - r0));
+    }
+  };
+  auto wave_sum_int = [](int v) {
+    #pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  };
   int cnt = 0, nodof = 0;
   #pragma unroll 1
-  for (int base = 0; base < nefc; base += 64) {
-    const int r = base + lane;
-    int t1 = -1, t2;
-    if (r < nefc) row_trees(m, scr, __float_as_int(type[r]), t1, t2);
+  for (int base = 0; base < nitem; base += 64) {
+    const int i = base + lane;
+    int r0 = 0, nr = 0, t1 = -1, t2;
+    if (i < nitem) item_info(i, r0, nr);
+    if (nr > 0) row_trees(m, scr, __float_as_int(type[r0]), t1, t2);
     const int il = __shfl(lbl, t1 < 0 ? 0 : t1);
-    nodof += __popcll(__ballot(r < nefc && t1 < 0));
+    nodof += wave_sum_int(t1 < 0 ? nr : 0);
     #pragma unroll 1
-    for (int i = 0; i < m.ntree; ++i) {
-      const int ci = __popcll(__ballot(r < nefc && t1 >= 0 && il == i));
-      if (lane == i) cnt += ci;
+    for (int k = 0; k < m.ntree; ++k) {
+      const int ck = wave_sum_int(t1 >= 0 && il == k ? nr : 0);
+      if (lane == k) cnt += ck;
     }
   }
   // longest-processing-time: largest island first onto the least loaded pipe
@@ -1873,7 +1944,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       if (q == best) load[q] += c;
     });
   }
-  // solver order: pipe p's rows in row order at records [start_p, start_p + n_p)
+  // solver order: pipe p's rows in row order at records [start_p, start_p + n_p); the first record
+  // of every item holds the item's first row index (itemat)
   int start[NP], fill[NP], nlev = 0, my_n = 0, my_start = 0;
   {
     int acc = 0;
@@ -1885,101 +1957,142 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     });
     nlev = uniform_int(nlev);
   }
+  gfloat* itemat = scr + S.efc_item;
+  gfloat* hdr = scr + S.efc_hdr;
   #pragma unroll 1
-  for (int base = 0; base < nefc; base += 64) {
-    const int r = base + lane;
-    int t1 = -1, t2;
-    if (r < nefc) row_trees(m, scr, __float_as_int(type[r]), t1, t2);
+  for (int base = 0; base < nitem; base += 64) {
+    const int i = base + lane;
+    int r0 = 0, nr = 0, t1 = -1, t2;
+    if (i < nitem) item_info(i, r0, nr);
+    if (nr > 0) row_trees(m, scr, __float_as_int(type[r0]), t1, t2);
     const int il = __shfl(lbl, t1 < 0 ? 0 : t1);
-    const int pr = __shfl(mypipe, il);
-    const int rp = t1 < 0 ? 0 : pr;
+    const int pr = t1 < 0 ? 0 : __shfl(mypipe, il);
+    int q0 = 0;
     unroll<NP>([&](auto pc) {
       constexpr int q = decltype(pc)::value;
-      const unsigned long long mk = __ballot(r < nefc && rp == q);
-      if (r < nefc && rp == q) rowof[fill[q] + lanes_below(mk)] = __int_as_float(r);
-      fill[q] += __popcll(mk);
+      int tot;
+      const int ex = gscan_excl<64>(pr == q ? nr : 0, lane, tot);
+      if (pr == q) q0 = fill[q] + ex;
+      fill[q] += tot;
     });
+    if (nr > 0) {
+      // item header: everything that does not depend on the dof slot, computed here for 64 items
+      // at once (the per-pipe build below then waits on one header load instead of a chain)
+      const int code = __float_as_int(type[r0]);
+      const int t = code >> 16, id = code & 0xffff;
+      CPtr<float> sr, si;
+      float diag, mu = 0, bound = -1;
+      int dim = 1;
+      if (t == EFC_FRICTION) {
+        sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id];
+        bound = floss[r0];
+      } else if (t == EFC_LIMIT) {
+        sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]];
+      } else {
+        const int p = __float_as_int(scr[S.con + kConRec * id]);
+        dim = m.pair_dim[p];
+        mu = m.pair_friction[3 * p];  // sliding, for both tangent directions
+        sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
+        const float tran = m.body_invweight0[2 * m.geom_bodyid[m.pair_g1[p]]] + m.body_invweight0[2 * m.geom_bodyid[m.pair_g2[p]]];
+        diag = dim == 3 ? tran * (1 + mu * mu) : tran;
+      }
+      const float ps = pos[r0], mg = marg[r0];
+      const float imp = impedance(si, ps, mg);
+      float R = (1 - imp) * diag / imp;
+      R = R > kMinVal ? R : kMinVal;
+      const float dmax = clampf(si[1], 0.0001f, 0.9999f);
+      float K, B;
+      if (sr[0] > 0) {
+        float tc = sr[0], dr = sr[1];
+        if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
+        K = 1 / (dmax * dmax * tc * tc * dr * dr);
+        B = 2 / (dmax * tc);
+      } else {
+        K = -sr[0] / (dmax * dmax);
+        B = -sr[1] / dmax;
+      }
+      const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (ps - mg);
+      const float jval = t == EFC_FRICTION ? 1.0f : (t == EFC_LIMIT ? floss[r0] : 0.0f);
+      gfloat* h = hdr + 8 * q0;
+      h[0] = __int_as_float(r0);
+      h[1] = __int_as_float(code);
+      h[2] = __int_as_float((t1 + 1) | ((t2 + 1) << 8) | (nr << 16) | (dim << 20));
+      h[3] = mu;
+      h[4] = R; h[5] = B; h[6] = pterm; h[7] = bound;
+      itemat[q0] = jval;  // J value of a friction / limit row at its dof
+    }
   }
   wsync();
   SUB_ADD(PH_CON_ROWS, t_sub);
   t_sub = SUB_T();
 
-  // --- 3. records: at level k every pipe builds its k-th row
-  #pragma unroll 1
-  for (int k = 0; k < nlev; ++k) {
-    const bool act = k < my_n;
-    const int q = act ? my_start + k : 0;
-    const int r = __float_as_int(rowof[q]);
-    const int code = __float_as_int(type[r]);
-    const int t = code >> 16, id = code & 0xffff;
-    int t1, t2;
-    row_trees(m, scr, code, t1, t2);
-    const int d = slot_dof(m, t1, t2, slot);
-    float J = 0, diag;
-    CPtr<float> sr, si;
-    if (t == EFC_FRICTION) {
-      J = d == id ? 1.0f : 0.0f;
-      sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id];
-    } else if (t == EFC_LIMIT) {
-      const int dof = m.jnt_dofadr[id];
-      J = d == dof ? floss[r] : 0.0f;
-      sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[dof];
-    } else {
-      const gfloat* crec = scr + S.con + kConRec * id;
-      const int p = __float_as_int(crec[0]);
-      const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
-      const float mu = m.pair_friction[3 * p];  // sliding, for both tangent directions
-      sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
-      const float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-      diag = m.pair_dim[p] == 3 ? tran * (1 + mu * mu) : tran;
-      if (d >= 0) {
-        const float cp[3] = {crec[2], crec[3], crec[4]};
-        float c1[3], c2[3], jc[3];
-        jac_col(m, s, b1, cp, d, c1);
-        jac_col(m, s, b2, cp, d, c2);
-        const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
-        for (int i = 0; i < 3; ++i) jc[i] = crec[5 + 3 * i] * dc[0] + crec[6 + 3 * i] * dc[1] + crec[7 + 3 * i] * dc[2];
-        if (m.pair_dim[p] == 1) {
-          J = jc[0];
-        } else {
-          const int j = (int)floss[r];
-          const float sg = (j & 1) ? -1.0f : 1.0f;
-          J = jc[0] + sg * mu * (j < 2 ? jc[1] : jc[2]);
+  // --- 3. records, one item per pipe per level: J of the item's rows from the contact Jacobian
+  // (jc: normal and two tangent rows, pyramid edges jc0 +- mu jck), M^-1 of the three jc vectors in
+  // one interleaved block solve, impedance once per item
+  {
+    const int my_end = my_start + my_n;
+    int qc = my_start;
+    #pragma unroll 1
+    for (;;) {
+      const bool act = qc < my_end;
+      if (!__any(act)) break;
+      const int q0 = act ? qc : 0;  // record 0 always starts an item
+      const gfloat* h = hdr + 8 * q0;
+      const v4f h0 = *(const __attribute__((address_space(1))) v4f*)h;
+      const v4f h1 = *(const __attribute__((address_space(1))) v4f*)(h + 4);
+      const int r0 = __float_as_int(h0.x), code = __float_as_int(h0.y), pk = __float_as_int(h0.z);
+      const float mu = h0.w, R = h1.x, B = h1.y, pterm = h1.z, bound = h1.w;
+      const int t = code >> 16, id = code & 0xffff;
+      const int t1 = (pk & 0xff) - 1, t2 = ((pk >> 8) & 0xff) - 1, nr = (pk >> 16) & 0xf, dim = pk >> 20;
+      const SlotMap sm = slot_map(s, L, t1, t2, slot);
+      const int d = sm.d;
+      float jc[3] = {0, 0, 0};
+      if (t == EFC_CONTACT) {
+        if (d >= 0) {
+          const gfloat* crec = scr + S.con + kConRec * id;
+          const int p = __float_as_int(crec[0]);
+          const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+          const float cp[3] = {crec[2], crec[3], crec[4]};
+          float c1[3], c2[3];
+          jac_col(m, s, b1, cp, d, c1);
+          jac_col(m, s, b2, cp, d, c2);
+          const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+          for (int i = 0; i < 3; ++i) jc[i] = crec[5 + 3 * i] * dc[0] + crec[6 + 3 * i] * dc[1] + crec[7 + 3 * i] * dc[2];
         }
+      } else {
+        // friction loss: e_dof; limit: +-e_dof (value kept in itemat)
+        const int dof = t == EFC_FRICTION ? id : m.jnt_dofadr[id];
+        jc[0] = d == dof ? itemat[q0] : 0.0f;
       }
-    }
-    const float MJ = pipe_msolve(m, s + L.L, t1, t2, slot, pbase, J);
-    const float vel = gsum<P>(d >= 0 ? J * s[L.qvel + d] : 0.0f);
-    const float jqs = gsum<P>(d >= 0 ? J * s[L.qacc_smooth + d] : 0.0f);
-    const float jmj = gsum<P>(J * MJ);
-    const float imp = impedance(si, pos[r], marg[r]);
-    float R = (1 - imp) * diag / imp;
-    R = R > kMinVal ? R : kMinVal;
-    const float dmax = clampf(si[1], 0.0001f, 0.9999f);
-    float K, B;
-    if (sr[0] > 0) {
-      float tc = sr[0], dr = sr[1];
-      if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
-      K = 1 / (dmax * dmax * tc * tc * dr * dr);
-      B = 2 / (dmax * tc);
-    } else {
-      K = -sr[0] / (dmax * dmax);
-      B = -sr[1] / dmax;
-    }
-    const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
-    const float aref = -B * vel - pterm;
-    if (act) {
-      gfloat* o = rec + q * RF;
-      o[slot] = J;
-      o[P + slot] = MJ;
-      o[2 * P + slot] = __int_as_float(d);
-      if (slot == 0) {
-        o[3 * P + 0] = aref;
-        o[3 * P + 1] = R;
-        o[3 * P + 2] = jmj + R;
-        o[3 * P + 3] = t == EFC_FRICTION ? floss[r] : -1.0f;
-        o[3 * P + 4] = jqs - aref;
-      }
+      float mjc[3];
+      pipe_msolve3(m, s + L.L, sm, pbase, jc, mjc);
+      const float qv = d >= 0 ? s[L.qvel + d] : 0.0f, qs = d >= 0 ? s[L.qacc_smooth + d] : 0.0f;
+      unroll<4>([&](auto jcst) {
+        constexpr int j = decltype(jcst)::value;
+        constexpr int k = 1 + (j >> 1);
+        constexpr float sg = (j & 1) ? -1.0f : 1.0f;
+        const float J = dim == 1 ? jc[0] : jc[0] + sg * mu * jc[k];
+        const float MJ = dim == 1 ? mjc[0] : mjc[0] + sg * mu * mjc[k];
+        if (j == 0 || __any(act && j < nr)) {
+          const float vel = gsum<P>(J * qv), jqs = gsum<P>(J * qs), jmj = gsum<P>(J * MJ);
+          const float aref = -B * vel - pterm;
+          if (act && j < nr) {
+            gfloat* o = rec + (q0 + j) * RF;
+            o[slot] = J;
+            o[P + slot] = MJ;
+            o[2 * P + slot] = __int_as_float(d);
+            if (slot == 0) {
+              o[3 * P + 0] = aref;
+              o[3 * P + 1] = R;
+              o[3 * P + 2] = jmj + R;
+              o[3 * P + 3] = bound;
+              o[3 * P + 4] = jqs - aref;
+              rowof[q0 + j] = __int_as_float(r0 + j);
+            }
+          }
+        }
+      });
+      qc += act ? nr : 0;
     }
   }
   wsync();
@@ -3111,6 +3224,15 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
   }
   #pragma unroll 1
   for (int i = lane; i < m.nu; i += G) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
+  if constexpr (G == 64) {
+    #pragma unroll 1
+    for (int t = lane; t < m.ntree; t += G) {
+      s[L.trees + 4 * t] = __int_as_float(m.tree_dofadr[t]);
+      s[L.trees + 4 * t + 1] = __int_as_float(m.tree_dofnum[t]);
+      s[L.trees + 4 * t + 2] = __int_as_float(m.tree_Moff[t]);
+      s[L.trees + 4 * t + 3] = 0;
+    }
+  }
   double time = st.time[e];
   gfloat* sensordata = valid ? (gfloat*)(st.sensordata + e * m.nsensordata) : scr + m.S.sens;
   wsync();
