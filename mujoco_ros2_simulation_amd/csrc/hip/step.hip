@@ -455,7 +455,7 @@ __device__ __forceinline__ void capsule_ends(const float* pos, const float* mat,
 // (edge axes only when clearly better than the best face axis), face case by clipping the most
 // anti-parallel face of the other box against the reference face's side planes, four deepest clipped
 // vertices kept; edge case: one contact between the support edges.  Out of line: rare, and its
-// private arrays stay out of the hot path's registers.
+// clipping slots stay out of the hot path's registers.
 // Templated on the group width only so each kernel instantiation gets its own copy, compiled under
 // that kernel's register budget (a shared callee is allocated for the widest caller)
 // The poses are read from the env's LDS and the sizes from the model here, not passed as arrays: a
@@ -538,63 +538,86 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
   }
   const int k1 = (j + 1) % 3, k2 = (j + 2) % 3;
   const float sgn = dot3(Ri[j], nr) > 0 ? -1.0f : 1.0f;
-  // polygon buffers stay in private memory (volatile: not promoted to registers, which would set
-  // the register budget of every kernel that calls this rare path)
-  volatile float poly[8][3], tmp[8][3];
-  int np = 4;
-  for (int v = 0; v < 4; ++v) {
-    const float su = (v == 0 || v == 3) ? 1.0f : -1.0f, sv = (v < 2) ? 1.0f : -1.0f;
-    for (int c = 0; c < 3; ++c)
-      poly[v][c] = pi[c] + sgn * hi[j] * Ri[j][c] + su * hi[k1] * Ri[k1][c] + sv * hi[k2] * Ri[k2][c];
-  }
+  // Clipping in the reference face's frame: u, v along its in-plane axes Rr[r1], Rr[r2] and w along
+  // nr, measured from the face centre cr, so the four side planes are |u| <= hr[r1], |v| <= hr[r2]
+  // and a vertex's separation is w.  Sutherland-Hodgman with the polygon in 8 static register slots:
+  // each side emits, in input order, every vertex inside and every edge crossing, and output slot o
+  // takes the candidate whose running count is o (no private-memory arrays: a scratch round trip per
+  // vertex made this the slowest part of the contact-rich step).
   const int r1 = (ir + 1) % 3, r2 = (ir + 2) % 3;
   float cr[3];
   for (int c = 0; c < 3; ++c) cr[c] = pr[c] + hr[ir] * nr[c];
-  #pragma unroll 1
+  float pu[8], pv[8], pw[8];
+  for (int vtx = 0; vtx < 4; ++vtx) {
+    const float su = (vtx == 0 || vtx == 3) ? 1.0f : -1.0f, sv = (vtx < 2) ? 1.0f : -1.0f;
+    float q[3];
+    for (int c = 0; c < 3; ++c)
+      q[c] = pi[c] + sgn * hi[j] * Ri[j][c] + su * hi[k1] * Ri[k1][c] + sv * hi[k2] * Ri[k2][c] - cr[c];
+    pu[vtx] = dot3(q, Rr[r1]); pv[vtx] = dot3(q, Rr[r2]); pw[vtx] = dot3(q, nr);
+  }
+  for (int vtx = 4; vtx < 8; ++vtx) { pu[vtx] = 0; pv[vtx] = 0; pw[vtx] = 0; }
+  int np = 4;
+#pragma unroll
   for (int side = 0; side < 4; ++side) {
-    const float* ax2 = (side < 2) ? Rr[r1] : Rr[r2];
     const float lim = (side < 2) ? hr[r1] : hr[r2];
     const float sg = (side & 1) ? -1.0f : 1.0f;
-    int nn = 0;
-    #pragma unroll 1
-    for (int v = 0; v < np; ++v) {
-      const int vb = (v + 1) % np;
-      const float a[3] = {poly[v][0], poly[v][1], poly[v][2]}, b[3] = {poly[vb][0], poly[vb][1], poly[vb][2]};
-      const float da[3] = {a[0] - cr[0], a[1] - cr[1], a[2] - cr[2]}, db[3] = {b[0] - cr[0], b[1] - cr[1], b[2] - cr[2]};
-      const float fa = sg * dot3(da, ax2) - lim, fb = sg * dot3(db, ax2) - lim;
-      if (fa <= 0) { for (int c = 0; c < 3; ++c) tmp[nn][c] = a[c]; ++nn; }
-      if ((fa < 0 && fb > 0) || (fa > 0 && fb < 0)) {
-        const float t = fa / (fa - fb);
-        for (int c = 0; c < 3; ++c) tmp[nn][c] = a[c] + t * (b[c] - a[c]);
-        ++nn;
+    float f[8];
+#pragma unroll
+    for (int vtx = 0; vtx < 8; ++vtx) f[vtx] = sg * (side < 2 ? pu[vtx] : pv[vtx]) - lim;
+    float qu[8], qv[8], qw[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) { qu[o] = 0; qv[o] = 0; qw[o] = 0; }
+    int cnt = 0;
+#pragma unroll
+    for (int vtx = 0; vtx < 8; ++vtx) {
+      const bool in = vtx < np;
+      const bool wrap = vtx + 1 >= np;
+      const int nx = vtx + 1 < 8 ? vtx + 1 : 0;
+      const float fa = f[vtx], fb = wrap ? f[0] : f[nx];
+      const float bu = wrap ? pu[0] : pu[nx], bv = wrap ? pv[0] : pv[nx], bw = wrap ? pw[0] : pw[nx];
+      const bool ea = in && fa <= 0;
+      const bool ei = in && ((fa < 0 && fb > 0) || (fa > 0 && fb < 0));
+      const float t = ei ? fa / (fa - fb) : 0.0f;
+      const float iu = pu[vtx] + t * (bu - pu[vtx]), iv = pv[vtx] + t * (bv - pv[vtx]), iw = pw[vtx] + t * (bw - pw[vtx]);
+      const int pa = cnt, pb = cnt + (ea ? 1 : 0);
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        if (ea && pa == o) { qu[o] = pu[vtx]; qv[o] = pv[vtx]; qw[o] = pw[vtx]; }
+        if (ei && pb == o) { qu[o] = iu; qv[o] = iv; qw[o] = iw; }
       }
+      cnt = pb + (ei ? 1 : 0);
     }
-    np = nn;
-    for (int v = 0; v < np; ++v)
-      for (int c = 0; c < 3; ++c) poly[v][c] = tmp[v][c];
+    np = cnt < 8 ? cnt : 8;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) { pu[o] = qu[o]; pv[o] = qv[o]; pw[o] = qw[o]; }
     if (np == 0) return 0;
   }
-  volatile float seps[8];
-  volatile int keep[8];
-  int nk = 0;
-  for (int v = 0; v < np; ++v) {
-    const float dv[3] = {poly[v][0] - cr[0], poly[v][1] - cr[1], poly[v][2] - cr[2]};
-    const float sep = dot3(dv, nr);
-    if (sep > margin) continue;
-    seps[nk] = sep;
-    keep[nk++] = v;
-  }
-  volatile bool used[8] = {false, false, false, false, false, false, false, false};
+  // the (up to) four deepest clipped vertices within the margin, shallower ties to the earlier vertex
+  unsigned avail = 0;
+#pragma unroll
+  for (int vtx = 0; vtx < 8; ++vtx)
+    if (vtx < np && pw[vtx] <= margin) avail |= 1u << vtx;
   int n = 0;
-  #pragma unroll 1
-  for (int k = 0; k < 4 && k < nk; ++k) {
+#pragma unroll 1
+  for (int k = 0; k < 4 && avail; ++k) {
     int bi = -1;
-    for (int v = 0; v < nk; ++v)
-      if (!used[v] && (bi < 0 || seps[v] < seps[bi])) bi = v;
-    used[bi] = true;
+    float bs = 0;
+#pragma unroll
+    for (int vtx = 0; vtx < 8; ++vtx)
+      if ((avail >> vtx) & 1u)
+        if (bi < 0 || pw[vtx] < bs) { bi = vtx; bs = pw[vtx]; }
+    avail &= ~(1u << bi);
+    float bu = 0, bv = 0;
+#pragma unroll
+    for (int vtx = 0; vtx < 8; ++vtx)
+      if (vtx == bi) { bu = pu[vtx]; bv = pv[vtx]; }
     gCon& o = out[n++];
-    for (int c = 0; c < 3; ++c) { o.pos[c] = poly[keep[bi]][c] - nr[c] * seps[bi] / 2; o.nrm[c] = nf[c]; }
-    o.dist = seps[bi];
+    for (int c = 0; c < 3; ++c) {
+      const float pt = cr[c] + bu * Rr[r1][c] + bv * Rr[r2][c] + bs * nr[c];
+      o.pos[c] = pt - nr[c] * bs / 2;
+      o.nrm[c] = nf[c];
+    }
+    o.dist = bs;
   }
   return n;
 }
@@ -633,6 +656,9 @@ __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, con
       return capsule_box(a1, b1, s1[0], p2, m2, s2, margin, out, 0);
     }
   } else if (t1 == MRS_GEOM_BOX && t2 == MRS_GEOM_BOX) {
+#ifdef MRS_DIAG_NOBB
+    return 0;  // diagnostic build only: no box-box contacts
+#endif
     return box_box<G>(gxpos, gxmat, gsize, g1, g2, margin, out);
   }
   return 0;
@@ -669,7 +695,7 @@ enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 // around each phase, summed per wave and added to a device table at the end of the kernel.
 enum { PH_KIN, PH_COMPOS, PH_MAKEM, PH_CHOL, PH_COMVEL, PH_RNE, PH_SMOOTH, PH_COLL, PH_CONSTR, PH_SENS,
        PH_INTEG, PH_CHECK, PH_SENS_L1, PH_SENS_SETUP, PH_SENS_GEOMS, PH_CON_ROWS, PH_CON_REC, PH_CON_WARM,
-       PH_CON_PGS, PH_COUNT };
+       PH_CON_PGS, PH_COLL_NARROW, PH_COLL_OUT, PH_COUNT };
 #ifdef MRS_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[PH_COUNT];
 #define SUB_T() __builtin_amdgcn_s_memtime()
@@ -1479,13 +1505,16 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
         float rb = m.geom_rbound[g1] + m.geom_rbound[g2] + margin;
         cand = dot3(dv, dv) <= rb * rb;
       }
+      unsigned long long t_np = SUB_T();
       if (cand) {
         for (int i = 0; i < 9; ++i) { m1[i] = s[L.gxmat + 9 * g1 + i]; m2[i] = s[L.gxmat + 9 * g2 + i]; }
         float s1[3] = {m.geom_size[3 * g1], m.geom_size[3 * g1 + 1], m.geom_size[3 * g1 + 2]};
         float s2[3] = {m.geom_size[3 * g2], m.geom_size[3 * g2 + 1], m.geom_size[3 * g2 + 2]};
         n = narrowphase<G>(t1, t2, p1, m1, s1, p2, m2, s2, margin, c, s + L.gxpos, s + L.gxmat, m.geom_size, g1, g2);
       }
+      SUB_ADD(PH_COLL_NARROW, t_np);
     }
+    unsigned long long t_out = SUB_T();
     int total;
     int off = gscan_excl<G>(n, lane, total);
     #pragma unroll 1
@@ -1501,6 +1530,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
       for (int i = 0; i < 9; ++i) rec[5 + i] = fr[i];
     }
     ncon += total;
+    SUB_ADD(PH_COLL_OUT, t_out);
   }
   if (ncon > m.max_con) ncon = m.max_con;
   wsync();

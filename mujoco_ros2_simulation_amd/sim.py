@@ -144,7 +144,8 @@ def lib() -> C.CDLL:
 
 PHASES = ["kinematics", "com_pos", "make_M", "cholesky", "com_vel", "rne", "smooth_forces", "collision",
           "constraints", "sensors", "integrate", "checks", "sensors.level1", "sensors.setup", "sensors.geoms",
-          "constraints.rows", "constraints.records", "constraints.warmstart", "constraints.pgs"]
+          "constraints.rows", "constraints.records", "constraints.warmstart", "constraints.pgs",
+          "collision.narrow", "collision.out"]
 
 
 def phase_cycles(reset: bool = False) -> dict | None:
