@@ -118,6 +118,11 @@ double mrs_batch_last_kernel_ms(mrs_batch* b, int kind);
  * collision, constraints, sensors, integrate, checks.  Only a library built with
  * -DMRS_PHASE_TIMING records them; returns the number of phases written (0 otherwise, <0 on error). */
 int mrs_debug_phase_cycles(double* out, int n, int reset);
+/* diagnostics: the batch's kernel configuration -- out[0] lanes per env (group width), [1] LDS floats
+ * per env, [2] scratch floats per env, [3] blocked mode (tree-blocked M + sparse constraint rows),
+ * [4] dof slots per constraint row (pipe width), [5] constraint-row capacity, [6] contact capacity,
+ * [7] kinematic trees with dofs.  Returns the number of values written. */
+int mrs_debug_batch_layout(const mrs_batch* b, int* out, int n);
 
 #ifdef __cplusplus
 }

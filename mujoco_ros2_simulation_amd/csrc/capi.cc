@@ -222,4 +222,9 @@ int mrs_debug_phase_cycles(double* out, int n, int reset) {
   return mrs::phase_cycles(out, n, reset != 0);
 }
 
+int mrs_debug_batch_layout(const mrs_batch* b, int* out, int n) {
+  if (!b || !out || n < 0) return MRS_ERR_INVALID;
+  return mrs::batch_layout(b->impl, out, n);
+}
+
 }  // extern "C"

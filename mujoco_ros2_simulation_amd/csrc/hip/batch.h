@@ -15,6 +15,7 @@ struct UnsupportedError : std::runtime_error { using std::runtime_error::runtime
 BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_contacts);
 void batch_free(BatchImpl* b);
 int batch_num_envs(const BatchImpl* b);
+int batch_layout(const BatchImpl* b, int* out, int n);  // diagnostics: kernel configuration
 void batch_set_stream(BatchImpl* b, void* stream);
 void batch_reset(BatchImpl* b, int key, int env0, int n);
 void batch_set(BatchImpl* b, int field, const double* host, int env0, int n);

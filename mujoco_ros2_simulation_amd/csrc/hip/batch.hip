@@ -646,9 +646,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);
     L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
     L.qacc = take(nv + 1); L.qfrc_con = take(nv + 1);  // + a dummy word (blocked-mode solver)
-    L.act_force = take(std::max(1, m.nu)); L.Dg = take(nv);
+    L.act_force = take(std::max(1, m.nu));
     L.rfmask = take(std::max(1, d.nrfblk));
-    L.efc_f = blocked ? take(std::max(1, d.max_efc)) : 0;
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
     L.total = off;
   };
@@ -656,7 +655,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
-  auto lds_bytes = [&](int g) { return static_cast<size_t>(L.total) * sizeof(float) * kWavesPerBlock * (64 / g); };
+  auto lds_bytes = [&](int g) { return static_cast<size_t>(L.total) * sizeof(float) * 4 * (64 / g); };  // 4 waves
   // (narrow groups win even when they leave CUs idle: C4's 2048 envs run a 10-step launch in
   // 1.33 ms at G = 16 on 128 workgroups vs 4.0 ms at G = 64 on 512)
   b.group = 64;
@@ -668,7 +667,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.blocked = b.group == 64 ? 1 : 0;
   if (d.blocked) lds_layout(true);
-  if (lds_bytes(b.group) > 160 * 1024)
+  if (static_cast<size_t>(L.total) * sizeof(float) * (b.group == 64 ? 1 : 4 * 64 / b.group) > 160 * 1024)
     throw UnsupportedError("model too large for the per-environment LDS working set");
   // --- scratch layout (floats).  Dense mode: rows J and M^-1 J' as nefc x nv plus per-row scalars;
   // blocked mode: one record per row in solver order (J, M^-1 J' and dof per pipe slot, scalars)
@@ -682,6 +681,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_rec = take(d.blocked ? ne * (3 * d.pipe_w + 8) : 0);
   S.efc_rowof = take(d.blocked ? ne : 0);
   S.efc_item = take(d.blocked ? ne : 0);
+  S.efc_fq = take(d.blocked ? ne : 0);
   S.efc_hdr = take(d.blocked ? 8 * ne : 0);
   S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);  // <= 64 lanes x 4 contacts x 7 floats
   S.sens = take(std::max(1, m.nsensordata));
@@ -782,6 +782,14 @@ void batch_free(BatchImpl* b) {
 }
 
 int batch_num_envs(const BatchImpl* b) { return b->n; }
+
+int batch_layout(const BatchImpl* b, int* out, int n) {
+  const int v[8] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
+                    b->dm.max_con, b->dm.ntree};
+  int k = 0;
+  for (; k < n && k < 8; ++k) out[k] = v[k];
+  return k;
+}
 
 void batch_set_stream(BatchImpl* b, void* stream) {
   b->stream = stream ? static_cast<hipStream_t>(stream) : b->own_stream;

@@ -38,9 +38,8 @@ struct CPtr {
 struct LdsLayout {
   int xpos, xquat, xmat, xipos, xanchor, xaxis, gxpos, gxmat, scom, cinert, crb, cdof, cdofdot,
       cvel, cacc, cfrc, M, L, qpos, qvel, ctrl, qfrc_applied, qacc_ws, qfrc_bias, qfrc_passive,
-      qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force, Dg,
+      qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force,
       rfmask,  // per ray block: bitmask of candidate ray geoms (int bits)
-      efc_f,   // blocked mode: row forces (by row index)
       trees;   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
   int total;  // floats per env (multiple of 4)
 };
@@ -53,6 +52,7 @@ struct ScratchLayout {
       efc_rec,               // blocked mode: row records in solver order (3 * pipe_w + 8 floats each)
       efc_rowof,             // blocked mode: row index of each record (int bits)
       efc_item,              // blocked mode: first row of the item starting at a record (int bits)
+      efc_fq,                // blocked mode: row forces by record (global-record fallback path)
       efc_hdr,               // blocked mode: 8-float header of the item starting at a record
       sens;                  // sensordata sink of idle lane groups (envs past n_envs)
   int total;
@@ -120,7 +120,11 @@ struct DevModel {
 };
 constexpr int kRayBlock = 64;
 
-constexpr int kWavesPerBlock = 4;  // 256-thread workgroups; 64/G environments per wavefront
+// waves per workgroup: 256-thread workgroups with lane groups (G < 64); one wave (one env) per
+// workgroup at G = 64, so LDS is granted per env (the C5 working set of ~13.5 KB fits 11 envs per
+// CU instead of 2 workgroups of 4)
+template <int G>
+struct WavesPerBlock { static constexpr int value = G == 64 ? 1 : 4; };
 
 // device state of a batch (all [n_envs][dim], fp32 unless noted)
 struct DevState {

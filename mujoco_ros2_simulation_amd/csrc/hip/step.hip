@@ -63,9 +63,11 @@ __device__ __forceinline__ float bcast(float v, int src) {
 // ---- lane groups: G consecutive lanes own one environment (64/G environments per wavefront).
 // Group-local reductions, scans, broadcasts and votes; for G = 64 they are the wave-wide forms.
 // DPP move within rows of 16 lanes (no LDS traffic, unlike ds_bpermute-based shuffles)
+// (bound_ctrl set: every control used here reads an in-row lane, and it lets the backend fold the
+// move into the consuming VALU op as a DPP source operand)
 template <int kCtrl>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xf, 0xf, true));
 }
 constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
 constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
@@ -1671,7 +1673,10 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
 // is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
 typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, pad x3
-constexpr int kRegLevels = 64;  // rows per pipe of the register-resident solve
+#ifndef MRS_REG_LEVELS
+#define MRS_REG_LEVELS 48
+#endif
+constexpr int kRegLevels = MRS_REG_LEVELS;  // rows per pipe of the register-resident solve
 
 __device__ __forceinline__ int slot_dof(const DevModel& m, int t1, int t2, int slot) {
   if (t1 < 0) return -1;
@@ -1824,7 +1829,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   gfloat* rec = scr + S.efc_rec;
   gfloat* rowof = scr + S.efc_rowof;
   gfloat* ffg = scr + S.efc_f;
-  lfloat* fl = s + L.efc_f;     // row forces by record position
+  gfloat* fl = scr + S.efc_fq;  // row forces by record position (global-record fallback path)
   lfloat* qa = s + L.qacc;      // qacc during the solve (lane per dof)
   lfloat* tmp = s + L.qfrc_con; // warm-start M^-1 J' f, then qfrc_constraint
   if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) tmp[lane] = 0; wsync(); return qacc_s; }
@@ -2350,6 +2355,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       if (act) improvement -= delta * res + 0.5f * delta * delta * w.a;
     }
     improvement = gsum<64>(slot == 0 ? improvement : 0.0f);
+    wsync();
     if (improvement * m.pgs_scale < m.tolerance) break;
   }
   wsync();
@@ -3227,13 +3233,16 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
 // the LDS of 4*64/G envs per workgroup bounds residency instead (e.g. G = 16: 16 envs x 4.5 KB per
 // workgroup -> 2 workgroups per CU -> 2 waves per SIMD, 256 VGPRs)
 template <int G>
-struct Occupancy { static constexpr int waves = G == 64 ? 2 : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
+#ifndef MRS_G64_WAVES
+#define MRS_G64_WAVES 3
+#endif
+struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
 template <int G, bool kForwardOnly>
-__global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step_kernel(
+__global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int kEnvsPerBlock = kWavesPerBlock * 64 / G;
+  constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
   const DevModel& m = *mp;
   const LdsLayout& L = m.L;
   const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
@@ -3352,13 +3361,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, Occupancy<G>::waves) void step
 template <int G>
 static void launch_g(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
                      bool forward_only, hipStream_t stream) {
-  constexpr int kEnvsPerBlock = kWavesPerBlock * 64 / G;
+  constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * (size_t)lds_floats * kEnvsPerBlock;
   if (forward_only)
-    hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * kWavesPerBlock), lds, stream, d_model, st, n_envs, 1);
+    hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs, 1);
   else
-    hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * kWavesPerBlock), lds, stream, d_model, st, n_envs,
+    hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs,
                        n_steps);
 }
 

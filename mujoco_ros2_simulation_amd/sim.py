@@ -138,6 +138,7 @@ def lib() -> C.CDLL:
         L.mrs_batch_last_kernel_ms.restype = C.c_double
         L.mrs_batch_last_kernel_ms.argtypes = [C.c_void_p, C.c_int]
         L.mrs_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.mrs_debug_batch_layout.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -260,6 +261,14 @@ class Batch:
 
     def reset(self, key: int = -1, env0: int = 0, n: int | None = None) -> None:
         _check(lib().mrs_batch_reset(self._h, key, env0, self.n - env0 if n is None else n))
+
+    def layout(self) -> dict:
+        """kernel configuration of this batch (diagnostics): group width, LDS and scratch floats per
+        env, blocked mode, pipe width, row and contact capacity, kinematic trees"""
+        out = np.zeros(8, dtype=np.int32)
+        k = lib().mrs_debug_batch_layout(self._h, out.ctypes.data, 8)
+        keys = ["group", "lds_floats", "scratch_floats", "blocked", "pipe_w", "max_efc", "max_con", "ntree"]
+        return dict(zip(keys[:k], out[:k].tolist()))
 
     def step(self, n_steps: int = 1) -> None:
         _check(lib().mrs_batch_step(self._h, n_steps))
