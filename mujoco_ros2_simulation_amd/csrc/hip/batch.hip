@@ -224,6 +224,150 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
   out[(size_t)blockIdx.y * W * H + pix] = (best < 0 || best > zfar) ? zfar : best;
 }
 
+// ---- depth kernel v2 (ngeom <= 64): one workgroup renders a whole frame of one env.  The
+// workgroup stages, once per frame, each visible geom's data in LDS: the camera origin in the geom
+// frame lp = R'(c - p) and A = R' C (C: camera rotation), so the geom-frame direction of the pixel
+// ray (x, y, -1) is lv = A (x, y, -1) -- three FMAs per component per pixel -- and, for the cull,
+// the geom's centre and axes in the camera frame with the half extents of an oriented box around it.
+// Each wave walks tiles of 64 x 4 pixels: lane = column (every store is 256 contiguous bytes), 4 rows
+// per lane.  Per tile, lane g tests geom g against the tile's pyramid of rays (four planes through
+// the camera): an oriented box wholly outside one plane, or a plane no corner ray descends onto, is
+// skipped; one ballot gives the candidates and the pixel loop visits only those (wave-uniform geom,
+// so the primitive test does not diverge by type).  Boxes use the slab test: the same face
+// parameters (+-s - lp) / lv as the face-by-face test, nearest non-negative crossing.
+constexpr int kDepthTileW = 64, kDepthTileH = 4, kDepthGeoms = 64;
+struct DepthGeom {  // 24 floats in LDS
+  float lp[3], A[9], size[3];  // row i of A = R'C is also the geom's axis i in the camera frame
+  float cc[3], ext[3];         // cull: centre in the camera frame, oriented-box half extents
+  int type, vis;
+};
+__device__ __forceinline__ float ray_box_slab(const float* s, const float lp[3], const float lv[3]) {
+  float tmin = -3.0e38f, tmax = 3.0e38f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float inv = __builtin_amdgcn_rcpf(lv[i]);
+    const bool par = fabsf(lv[i]) <= 1e-15f;
+    const float t1 = (-s[i] - lp[i]) * inv, t2 = (s[i] - lp[i]) * inv;
+    // a ray parallel to a slab is inside it for all t or for none
+    const bool inside = fabsf(lp[i]) <= s[i];
+    const float lo = par ? (inside ? -3.0e38f : 3.0e38f) : fminf(t1, t2);
+    const float hi = par ? (inside ? 3.0e38f : -3.0e38f) : fmaxf(t1, t2);
+    tmin = fmaxf(tmin, lo);
+    tmax = fminf(tmax, hi);
+  }
+  if (tmax < tmin || tmax < 0) return -1;
+  return tmin >= 0 ? tmin : tmax;
+}
+__global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, const int* geom_group,
+                                                       const float* geom_size, const float* geom_rgba, int ngeom,
+                                                       const float* geom_xpos, const float* geom_xmat,
+                                                       const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
+                                                       int env0, int W, int H, float f, float znear, float zfar,
+                                                       float* out) {
+  __shared__ DepthGeom G[kDepthGeoms];
+  const int env = env0 + blockIdx.x;
+  const size_t eo = static_cast<size_t>(env);
+  const float* cp = cam_xpos + (eo * ncam + cam) * 3;
+  const float* cm = cam_xmat + (eo * ncam + cam) * 9;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < ngeom) {
+    const int g = threadIdx.x;
+    const float cpos[3] = {cp[0], cp[1], cp[2]};
+    float C[9];
+    for (int i = 0; i < 9; ++i) C[i] = cm[i];
+    DepthGeom& o = G[g];
+    const int grp = geom_group[g];
+    o.vis = !(grp < 0 || grp > 2 || geom_rgba[4 * g + 3] == 0);
+    const float* p = geom_xpos + eo * 3 * ngeom + 3 * g;
+    const float* R = geom_xmat + eo * 9 * ngeom + 9 * g;
+    const float d[3] = {cpos[0] - p[0], cpos[1] - p[1], cpos[2] - p[2]};
+    for (int i = 0; i < 3; ++i) o.lp[i] = R[i] * d[0] + R[3 + i] * d[1] + R[6 + i] * d[2];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) o.A[3 * i + j] = R[i] * C[j] + R[3 + i] * C[3 + j] + R[6 + i] * C[6 + j];
+    for (int i = 0; i < 3; ++i) {
+      o.size[i] = geom_size[3 * g + i];
+      o.cc[i] = -(C[i] * d[0] + C[3 + i] * d[1] + C[6 + i] * d[2]);
+    }
+    o.type = geom_type[g];
+    const float s0 = o.size[0], s1 = o.size[1], s2 = o.size[2];
+    float e[3] = {s0, s0, s0};
+    switch (o.type) {
+      case MRS_GEOM_BOX: case MRS_GEOM_ELLIPSOID: e[0] = s0; e[1] = s1; e[2] = s2; break;
+      case MRS_GEOM_CAPSULE: e[2] = s1 + s0; break;
+      case MRS_GEOM_CYLINDER: e[2] = s1; break;
+      default: break;
+    }
+    for (int i = 0; i < 3; ++i) o.ext[i] = e[i] * 1.001f + 1e-4f;
+    if (o.type == MRS_GEOM_PLANE && !(o.lp[2] > 0)) o.vis = 0;  // camera behind the plane
+  }
+  __syncthreads();
+  const int tiles_x = (W + kDepthTileW - 1) / kDepthTileW, tiles_y = (H + kDepthTileH - 1) / kDepthTileH;
+  float* img = out + static_cast<size_t>(blockIdx.x) * W * H;
+  for (int tile = wave; tile < tiles_x * tiles_y; tile += 4) {
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    // extreme pixel-centre ray slopes of the tile (camera frame: x right, y up, -z forward)
+    const float x0 = (tx * kDepthTileW + 0.5f - 0.5f * W) / f;
+    const float x1 = (fminf(tx * kDepthTileW + kDepthTileW - 1.0f, W - 1.0f) + 0.5f - 0.5f * W) / f;
+    const float y1 = (0.5f * H - ty * kDepthTileH - 0.5f) / f;
+    const float y0 = (0.5f * H - fminf(ty * kDepthTileH + kDepthTileH - 1.0f, H - 1.0f) - 0.5f) / f;
+    bool keep = false;
+    if (lane < ngeom && G[lane].vis) {
+      const DepthGeom& o = G[lane];
+      if (o.type == MRS_GEOM_PLANE) {
+        // some corner ray (the minimum of the linear d.n over the tile) must descend onto the plane
+        const float n[3] = {o.A[6], o.A[7], o.A[8]};
+        const float bx = fminf(x0 * n[0], x1 * n[0]), by = fminf(y0 * n[1], y1 * n[1]);
+        keep = bx + by - n[2] < 1e-6f;
+      } else {
+        // oriented box vs the four side planes n.p >= 0 of the tile pyramid (unnormalised normals:
+        // left (1, 0, x0), right (-1, 0, -x1), bottom (0, 1, y0), top (0, -1, -y1))
+        auto outside = [&](float nx, float ny, float nz) {
+          const float c = nx * o.cc[0] + ny * o.cc[1] + nz * o.cc[2];
+          float r = 0;
+          for (int i = 0; i < 3; ++i)
+            r += o.ext[i] * fabsf(nx * o.A[3 * i] + ny * o.A[3 * i + 1] + nz * o.A[3 * i + 2]);
+          return c + r < -1e-5f * (fabsf(c) + r);
+        };
+        keep = !(outside(1, 0, x0) || outside(-1, 0, -x1) || outside(0, 1, y0) || outside(0, -1, -y1));
+      }
+    }
+    unsigned long long cand = __ballot(keep);
+    const int col = tx * kDepthTileW + lane;
+    const float dx = (col + 0.5f - 0.5f * W) / f;
+    float best[kDepthTileH], dy[kDepthTileH];
+#pragma unroll
+    for (int k = 0; k < kDepthTileH; ++k) {
+      best[k] = -1;
+      dy[k] = (0.5f * H - (ty * kDepthTileH + k) - 0.5f) / f;
+    }
+    while (cand) {
+      const int g = __builtin_ctzll(cand);
+      cand &= cand - 1;
+      const DepthGeom& o = G[g];
+      const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]}, sz[3] = {o.size[0], o.size[1], o.size[2]};
+      float A[9];
+      for (int i = 0; i < 9; ++i) A[i] = o.A[i];
+      const int type = o.type;
+#pragma unroll
+      for (int k = 0; k < kDepthTileH; ++k) {
+        const float lv[3] = {A[0] * dx + A[1] * dy[k] - A[2], A[3] * dx + A[4] * dy[k] - A[5],
+                             A[6] * dx + A[7] * dy[k] - A[8]};
+        float t;
+        if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
+        else t = ray_prim(type, sz, lp, lv);
+        if (t >= znear && (best[k] < 0 || t < best[k])) best[k] = t;
+      }
+    }
+    if (col < W) {
+#pragma unroll
+      for (int k = 0; k < kDepthTileH; ++k) {
+        const int row = ty * kDepthTileH + k;
+        if (row < H) img[static_cast<size_t>(row) * W + col] = (best[k] < 0 || best[k] > zfar) ? zfar : best[k];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ packing helpers
 struct Packer {
   std::vector<float> f;
@@ -915,11 +1059,17 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
   const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
   const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
   const DevModel& d = b->dm;
-  dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
   HIP_CHECK(hipEventRecord(b->ev0[1], b->stream));
-  hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
-                     d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                     cam, env0, W, H, f, znear, zfar, dout);
+  if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
+    hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
+                       d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
+                       cam, env0, W, H, f, znear, zfar, dout);
+  } else {
+    dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
+    hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
+                       d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
+                       cam, env0, W, H, f, znear, zfar, dout);
+  }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(b->ev1[1], b->stream));
   b->ev_valid[1] = true;

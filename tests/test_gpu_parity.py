@@ -354,3 +354,36 @@ def test_tall_stack_fallback_solver(monkeypatch):
     assert int(ncon[0]) == d.ncon == 20
     np.testing.assert_allclose(q[0], d.qpos, atol=5e-3)
     np.testing.assert_allclose(q[0, 2::7], [0.1 + 0.2 * k for k in range(5)], atol=3e-3)
+
+
+@pytest.mark.parametrize("v1", [False, True])
+def test_depth_all_primitives(v1, monkeypatch):
+    """depth render of every primitive type (plane, sphere, capsule, cylinder, ellipsoid, rotated box,
+    one box enclosing nothing but partly off-screen, one geom behind the camera) against the oracle's
+    render, with the per-frame (v2) and the per-tile (v1) kernel"""
+    if v1:
+        monkeypatch.setenv("MRS_DEPTH_V1", "1")
+    xml = """<mujoco><worldbody>
+      <geom type="plane" size="0 0 1"/>
+      <geom type="sphere" size="0.3" pos="0.6 -0.4 0.3"/>
+      <geom type="capsule" size="0.1 0.3" pos="-0.5 0.2 0.4" euler="23 11 0"/>
+      <geom type="cylinder" size="0.2 0.25" pos="0.1 0.6 0.25"/>
+      <geom type="ellipsoid" size="0.3 0.15 0.2" pos="-0.1 -0.6 0.2" euler="0 0 40"/>
+      <geom type="box" size="0.2 0.1 0.3" pos="0.5 0.5 0.3" euler="17 29 52"/>
+      <geom type="box" size="0.3 0.3 0.3" pos="-1.4 -0.2 0.3"/>
+      <geom type="sphere" size="0.2" pos="0 -3.5 1.5"/>
+      <camera name="cam" pos="0 -2 1.2" euler="63 0 0" fovy="60" resolution="320 240"/>
+    </worldbody></mujoco>"""
+    model = sim.Model.from_string(xml)
+    b = sim.Batch(model, 2)
+    b.forward()
+    img = b.render_depth(0, 0, 2)
+    b.close()
+    d = binding.OracleData(model)
+    d.forward()
+    want = d.render_depth(0)
+    for e in range(2):
+        close = np.isclose(img[e], want, rtol=1e-5, atol=1e-5)
+        assert img[e].shape == (240, 320) and close.mean() >= 0.999, close.mean()
+    # every primitive is visible somewhere in the frame
+    assert len(np.unique(np.round(want, 2))) > 50
