@@ -108,6 +108,16 @@ int mrs_batch_forward(mrs_batch* b);
 int mrs_batch_render_depth(mrs_batch* b, int cam, int env0, int n, float* host_out);
 /* same, into a device buffer [n][H][W] (stays in HBM) */
 int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float* d_out);
+/* mjData.contact of env `env` after its last step / forward (the output of mj_collision, SURVEY.md
+ * §8a row a2.3): up to `max` contacts in mj_collision's order -- geom [max][2] int32 (geom1, geom2,
+ * the lower geom type first), dist [max], pos [max][3], frame [max][9] fp64 (normal = frame[0:3]);
+ * any output pointer may be NULL.  Returns ncon (which may exceed `max`) or a negative error code. */
+int mrs_batch_get_contacts(mrs_batch* b, int env, int max, int* geom, double* dist, double* pos,
+                           double* frame);
+/* fp32 state field rows of envs [env0, env0+n) into a device buffer [n][dim], asynchronous on the
+ * batch stream (observations for the end-of-step gather stay in HBM; no reference counterpart: the
+ * reference copies mjData on the host, src/mujoco_system_interface.cpp:1759) */
+int mrs_batch_get_field_device(mrs_batch* b, int field, float* d_out, int env0, int n);
 /* wait for all queued batch work */
 int mrs_batch_sync(mrs_batch* b);
 /* duration in ms of the last step / render kernel measured with HIP events on the batch stream

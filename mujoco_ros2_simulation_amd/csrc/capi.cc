@@ -201,6 +201,22 @@ int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float*
   });
 }
 
+int mrs_batch_get_contacts(mrs_batch* b, int env, int max, int* geom, double* dist, double* pos, double* frame) {
+  int ncon = 0;
+  const int rc = guarded([&] {
+    if (!b) throw std::invalid_argument("null batch");
+    ncon = mrs::batch_get_contacts(b->impl, env, max, geom, dist, pos, frame);
+  });
+  return rc == MRS_OK ? ncon : rc;
+}
+
+int mrs_batch_get_field_device(mrs_batch* b, int field, float* d_out, int env0, int n) {
+  return guarded([&] {
+    if (!b || !d_out) throw std::invalid_argument("null argument");
+    mrs::batch_get_field_device(b->impl, field, d_out, env0, n);
+  });
+}
+
 int mrs_batch_sync(mrs_batch* b) {
   return guarded([&] {
     if (!b) throw std::invalid_argument("null batch");

@@ -299,6 +299,15 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
     }
     for (int i = 0; i < 3; ++i) o.ext[i] = e[i] * 1.001f + 1e-4f;
     if (o.type == MRS_GEOM_PLANE && !(o.lp[2] > 0)) o.vis = 0;  // camera behind the plane
+    if (o.type != MRS_GEOM_PLANE) {
+      // view-axis extent of the oriented box: a geom wholly nearer than znear (e.g. the robot's own
+      // body behind the camera) or wholly beyond zfar gives no pixel its depth -- hits nearer than
+      // znear are discarded and hits beyond zfar read as zfar -- so it is dropped for the frame
+      float rz = 0;
+      for (int i = 0; i < 3; ++i) rz += o.ext[i] * fabsf(o.A[3 * i + 2]);
+      const float zc = -o.cc[2];  // eye depth of the centre
+      if (zc + rz < znear || zc - rz > zfar) o.vis = 0;
+    }
   }
   __syncthreads();
   const int tiles_x = (W + kDepthTileW - 1) / kDepthTileW, tiles_y = (H + kDepthTileH - 1) / kDepthTileH;
@@ -410,6 +419,7 @@ struct BatchImpl {
   hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
   bool ev_valid[2] = {false, false};
   std::vector<float> staging;
+  std::vector<int> pair_g1, pair_g2;  // host copy of the static collision pairs (contact export)
 };
 
 namespace {
@@ -521,6 +531,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       }
   }
   d.npair = static_cast<int>(pg1.size());
+  b.pair_g1 = pg1;
+  b.pair_g2 = pg2;
   // kinematic trees (bodies sharing a root child of the world) that own dofs: their dofs are one
   // contiguous range, M is block diagonal over them, and constraint rows touch at most two of them
   // (mj_island's trees).  Blocked mode stores M / its factor per tree and solves the constraint rows
@@ -1078,6 +1090,50 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
     HIP_CHECK(hipFreeAsync(tmp, b->stream));
     HIP_CHECK(hipStreamSynchronize(b->stream));
   }
+}
+
+// mjData.contact of the last forward pass of one env (geom1/geom2 as mj_collision orders them: pair
+// order g1 < g2 with the lower geom type first, then the narrow phase's order).  Records are read from
+// the env's contact scratch (step.hip collision(): pair id, dist, pos, frame).  Returns ncon.
+int batch_get_contacts(BatchImpl* b, int env, int max, int* geom, double* dist, double* pos, double* frame) {
+  if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
+  if (max < 0) throw std::invalid_argument("negative capacity");
+  HIP_CHECK(hipSetDevice(b->device));
+  int ncon = 0;
+  HIP_CHECK(hipMemcpyAsync(&ncon, b->st.ncon + env, sizeof(int), hipMemcpyDeviceToHost, b->stream));
+  HIP_CHECK(hipStreamSynchronize(b->stream));
+  const int n = std::min(ncon, max);
+  if (n <= 0) return ncon;
+  std::vector<float> rec(static_cast<size_t>(n) * kConRec);
+  const float* src = b->st.scratch + static_cast<size_t>(env) * b->S.total + b->S.con;
+  HIP_CHECK(hipMemcpyAsync(rec.data(), src, rec.size() * sizeof(float), hipMemcpyDeviceToHost, b->stream));
+  HIP_CHECK(hipStreamSynchronize(b->stream));
+  for (int c = 0; c < n; ++c) {
+    const float* r = &rec[static_cast<size_t>(c) * kConRec];
+    int p;
+    std::memcpy(&p, r, sizeof(int));
+    if (p < 0 || p >= static_cast<int>(b->pair_g1.size())) throw DeviceError("corrupt contact record");
+    if (geom) { geom[2 * c] = b->pair_g1[p]; geom[2 * c + 1] = b->pair_g2[p]; }
+    if (dist) dist[c] = r[1];
+    if (pos) for (int i = 0; i < 3; ++i) pos[3 * c + i] = r[2 + i];
+    if (frame) for (int i = 0; i < 9; ++i) frame[9 * c + i] = r[5 + i];
+  }
+  return ncon;
+}
+
+// fp32 field rows [env0, env0 + n) into a caller device buffer [n][dim], ordered on the batch stream
+// (observation export without a host round trip, e.g. for the end-of-step RCCL gather)
+void batch_get_field_device(BatchImpl* b, int field, float* d_out, int env0, int n) {
+  const Model& m = *b->model;
+  const int dim = field_dim(m, field);
+  if (dim < 0 || field == MRS_FIELD_TIME || field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON)
+    throw std::invalid_argument("not an fp32 state field");
+  if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
+  if (n == 0 || dim == 0) return;
+  HIP_CHECK(hipSetDevice(b->device));
+  const float* src = static_cast<const float*>(field_ptr(*b, field)) + static_cast<size_t>(env0) * dim;
+  HIP_CHECK(hipMemcpyAsync(d_out, src, static_cast<size_t>(n) * dim * sizeof(float), hipMemcpyDeviceToDevice,
+                           b->stream));
 }
 
 void batch_sync(BatchImpl* b) {

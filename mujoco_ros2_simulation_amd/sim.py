@@ -135,6 +135,9 @@ def lib() -> C.CDLL:
         L.mrs_batch_render_depth.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.mrs_batch_render_depth_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.mrs_batch_sync.argtypes = [C.c_void_p]
+        L.mrs_batch_get_contacts.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
+        L.mrs_batch_get_field_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.mrs_batch_last_kernel_ms.restype = C.c_double
         L.mrs_batch_last_kernel_ms.argtypes = [C.c_void_p, C.c_int]
         L.mrs_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int, C.c_int]
@@ -296,6 +299,23 @@ class Batch:
 
     def render_depth_device(self, cam: int, env0: int, n: int, dptr: int) -> None:
         _check(lib().mrs_batch_render_depth_device(self._h, cam, env0, n, C.c_void_p(dptr)))
+
+    def contacts(self, env: int = 0, max_n: int = 256):
+        """mjData.contact of `env` after the last step/forward: (geom [n, 2] int32, dist [n],
+        pos [n, 3], frame [n, 9]) in mj_collision's order"""
+        g = np.zeros((max_n, 2), dtype=np.int32)
+        dist, pos, frame = np.zeros(max_n), np.zeros((max_n, 3)), np.zeros((max_n, 9))
+        n = lib().mrs_batch_get_contacts(self._h, env, max_n, g.ctypes.data, dist.ctypes.data, pos.ctypes.data,
+                                         frame.ctypes.data)
+        if n < 0:
+            _check(n)
+        n = min(n, max_n)
+        return g[:n], dist[:n], pos[:n], frame[:n]
+
+    def get_device(self, field: int, dptr: int, env0: int = 0, n: int | None = None) -> None:
+        """fp32 rows of `field` into a device buffer [n, dim], asynchronous on the batch stream"""
+        n = self.n - env0 if n is None else n
+        _check(lib().mrs_batch_get_field_device(self._h, field, C.c_void_p(dptr), env0, n))
 
     def last_kernel_ms(self, kind: int = 0) -> float:
         return lib().mrs_batch_last_kernel_ms(self._h, kind)

@@ -187,6 +187,76 @@ def test_contact_parity_short_horizon(group, monkeypatch):
     assert d.ncon >= 3  # sphere on floor, capsule on ledge, box on floor (up to 4 corners)
 
 
+def _contact_state(model, steps, n=4):
+    """a state with contacts: seeded start, `steps` GPU steps under seeded actions (fp32 values)"""
+    envs = np.arange(n)
+    b = sim.Batch(model, n)
+    b.set(sim.FIELD_QPOS, synth.initial_qpos(model, envs))
+    if model.nu:
+        b.set(sim.FIELD_CTRL, synth.ctrl_table(model, envs, 1, 10)[0])
+    if steps:
+        b.step(steps)
+    q = b.get(sim.FIELD_QPOS)
+    b.close()
+    return q
+
+
+@pytest.mark.parametrize("scene, group, steps", [("contact", 16, 150), ("contact", 64, 150),
+                                                 ("arm_boxes", 64, 0), ("arm_boxes", 64, 100)])
+def test_contact_list_bit_exact(scene, group, steps, monkeypatch):
+    """mjData.contact (mj_collision's output) after a forward pass from the same
+    state on both sides: the (geom1, geom2) list equals the oracle's element by element (integer
+    output: bit-exact, north_star), dist / pos / frame within 1e-4 (fp32 geometry)"""
+    monkeypatch.setenv("MRS_GROUP", str(group))
+    model = sim.Model.from_string(CONTACT_SCENE) if scene == "contact" else sim.Model.load(ARM_BOXES)
+    qs = _contact_state(model, steps)
+    b = sim.Batch(model, len(qs))
+    b.set(sim.FIELD_QPOS, qs)
+    b.forward()
+    total = 0
+    for e, q in enumerate(qs):
+        g, dist, pos, frame = b.contacts(e)
+        d = binding.OracleData(model)
+        d.qpos[:] = q
+        d.forward()
+        g_ref, dist_ref, pos_ref, frame_ref = d.contacts()
+        assert g.shape == g_ref.shape and np.array_equal(g, g_ref), (e, g.tolist(), g_ref.tolist())
+        np.testing.assert_allclose(dist, dist_ref, atol=1e-4)
+        np.testing.assert_allclose(pos, pos_ref, atol=1e-4)
+        np.testing.assert_allclose(frame, frame_ref, atol=1e-4)
+        total += len(g)
+    b.close()
+    assert total >= 4 * len(qs)
+
+
+def test_full_size_c3_batch_properties():
+    """8192 envs of the C3 arm + 360-ray lidar (BASELINE configs[2] size): envs with equal inputs
+    give bit-identical state and scans wherever they sit in the batch, launches are deterministic,
+    and env 0 matches the oracle after 100 steps"""
+    model = sim.Model.load(ARM7)
+    n, reps = 8192, 8
+    q0 = np.tile(synth.initial_qpos(model, np.arange(reps)), (n // reps, 1))
+    ctrl = np.tile(synth.ctrl_table(model, np.arange(reps), 1, 10)[0], (n // reps, 1))
+    outs = []
+    for _ in range(2):
+        b = sim.Batch(model, n)
+        b.set(sim.FIELD_QPOS, q0)
+        b.set(sim.FIELD_CTRL, ctrl)
+        b.step(100)
+        outs.append((b.get(sim.FIELD_QPOS), b.get(sim.FIELD_SENSORDATA)))
+        b.close()
+    for a, c in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, c)
+    q, s = outs[0]
+    assert np.all(q.reshape(n // reps, reps, -1) == q[:reps][None])
+    assert np.all(s.reshape(n // reps, reps, -1) == s[:reps][None])
+    d = binding.OracleData(model)
+    d.qpos[:] = q0[0]
+    d.ctrl[:] = ctrl[0]
+    d.step(100)
+    np.testing.assert_allclose(q[0], d.qpos, rtol=RTOL, atol=RTOL)
+
+
 @pytest.mark.parametrize("group", [16, 64])
 def test_autoreset_on_nan(group, monkeypatch):
     monkeypatch.setenv("MRS_GROUP", str(group))
