@@ -19,8 +19,8 @@
 
 namespace mrs {
 
-hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
-                       bool forward_only, int group, hipStream_t stream);
+hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
+                       int n_steps, bool forward_only, int group, hipStream_t stream);
 
 namespace {
 
@@ -808,10 +808,16 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.total = off;
   };
   lds_layout(false);
+  // workgroup-shared tables: ray-geom records, and the per-ray direction + address when every ray
+  // starts at one point of one body (DevModel::shr_*)
+  d.shr_rf = d.nrgeom * 8;
+  d.shr_total = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
-  auto lds_bytes = [&](int g) { return static_cast<size_t>(L.total) * sizeof(float) * 4 * (64 / g); };  // 4 waves
+  auto lds_bytes = [&](int g) {  // 4 waves
+    return (static_cast<size_t>(L.total) * 4 * (64 / g) + d.shr_total) * sizeof(float);
+  };
   // (narrow groups win even when they leave CUs idle: C4's 2048 envs run a 10-step launch in
   // 1.33 ms at G = 16 on 128 workgroups vs 4.0 ms at G = 64 on 512)
   b.group = 64;
@@ -823,7 +829,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.blocked = b.group == 64 ? 1 : 0;
   if (d.blocked) lds_layout(true);
-  if (static_cast<size_t>(L.total) * sizeof(float) * (b.group == 64 ? 1 : 4 * 64 / b.group) > 160 * 1024)
+  d.shr_off = L.total * (b.group == 64 ? 1 : 4 * 64 / b.group);
+  if ((static_cast<size_t>(d.shr_off) + d.shr_total) * sizeof(float) > 160 * 1024)
     throw UnsupportedError("model too large for the per-environment LDS working set");
   // --- scratch layout (floats).  Dense mode: rows J and M^-1 J' as nefc x nv plus per-row scalars;
   // blocked mode: one record per row in solver order (J, M^-1 J' and dof per pipe slot, scalars)
@@ -1049,7 +1056,7 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
-  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->st, b->n, n_steps, forward_only, b->group, b->stream));
+  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
 }

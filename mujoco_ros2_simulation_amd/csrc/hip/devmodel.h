@@ -70,6 +70,11 @@ struct DevModel {
   // kinematic trees with dofs; blocked: M per tree + sparse constraint rows (set when G = 64);
   // pipe_w: dof slots per constraint row in the sparse solver (64 / pipe_w rows in flight per wave)
   int ntree, tree_nmax, nMblk, blocked, pipe_w;
+  // workgroup-shared LDS tables (one copy per workgroup, after its envs' working sets; offsets in
+  // floats from the start of the dynamic LDS): the ray-geom records (8 floats each) at shr_off, and
+  // when rf_common the per-ray direction + sensordata address (4 floats each) at shr_off + shr_rf.
+  // Staged once per launch, read by the ray phase every step instead of global loads.
+  int shr_off, shr_rf, shr_total;
   // options
   int integrator, iterations, disableflags;
   int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)

@@ -748,6 +748,10 @@ __device__ __forceinline__ lfloat* uniform_lds(lfloat* p) {
   return (lfloat*)(unsigned long)__builtin_amdgcn_readfirstlane((unsigned)(unsigned long)p);
 }
 __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// the workgroup-shared LDS tables (DevModel::shr_*), staged by step_kernel at launch
+extern __shared__ __attribute__((aligned(16))) float g_dyn_lds[];
+__device__ __forceinline__ const lfloat* shared_lds(const DevModel& m) { return (const lfloat*)(g_dyn_lds + m.shr_off); }
 // by-value copy of the model descriptor read through the constant address space: only the fields a
 // phase uses are loaded (scalar loads), and they stay in SGPRs for the whole phase
 __device__ __forceinline__ DevModel load_model(const DevModel* mp) {
@@ -2767,6 +2771,11 @@ __device__ MRS_PHASE void rne_post(ENV_PARAMS, int ncon) {
 // 1.98 at 1, 1.71 at 2), 2 at one env per wave (64-VGPR budget: 2.15 ms vs 2.38 at 1, 2.95 at 4)
 template <int G>
 struct RayBatch { static constexpr int value = G == 64 ? 2 : 4; };
+#ifdef MRS_DIAG_SENS_LAST
+#define MRS_SD_OK(p) ((p) != nullptr)
+#else
+#define MRS_SD_OK(p) true
+#endif
 
 // R rangefinders per lane in one pass over the geoms (mj_ray per sensor: nearest hit along the
 // site's +z over all visible geoms not on the site's body).  Each geom's pose is read from LDS once
@@ -2791,7 +2800,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     for (int j = 0; j < R; ++j) {
       const int k = k0 + j * stride;
       act[j] = k < m.nrf;
-      const CPtr<float> rr = m.rfray + 8 * (act[j] ? k : 0);
+      const lfloat* rr = shared_lds(m) + m.shr_rf + 4 * (act[j] ? k : 0);
       const float dl[3] = {rr[0], rr[1], rr[2]};
       adr[j] = __float_as_int(rr[3]);
       bod[j] = b;
@@ -2869,7 +2878,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
   }
 #pragma unroll
   for (int j = 0; j < R; ++j)
-    if (act[j]) sd[adr[j]] = dist[j];
+    if (act[j] && MRS_SD_OK(sd)) sd[adr[j]] = dist[j];
   SUB_ADD(PH_SENS_GEOMS, t_geoms);
 }
 
@@ -2916,7 +2925,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
         const int i = c0 + lane;
         bool cand = false;
         if (i < m.nrgeom) {
-          const CPtr<float> rec = m.rgeom + 8 * i;
+          const lfloat* rec = shared_lds(m) + 8 * i;
           const int g = __float_as_int(rec[0]), type = __float_as_int(rec[1]);
           const float v[3] = {s[L.gxpos + 3 * g] - o[0], s[L.gxpos + 3 * g + 1] - o[1], s[L.gxpos + 3 * g + 2] - o[2]};
           if (type == MRS_GEOM_PLANE) {
@@ -2975,7 +2984,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const int k = base + lane + j * G;
-        if (k < m.nrf) sensordata[__float_as_int(m.rfray[8 * k + 3])] = -1.0f;
+        if (k < m.nrf && MRS_SD_OK(sensordata)) sensordata[__float_as_int(m.rfray[8 * k + 3])] = -1.0f;
       }
       continue;
     }
@@ -3001,6 +3010,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
     }
     rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask, common_body, common_o);
   }
+  if (!MRS_SD_OK(sensordata)) return;
   #pragma unroll 1
   for (int ks = lane; ks < m.nsens_other; ks += G) {
     const int sid = m.sens_other[ks];
@@ -3274,6 +3284,15 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
   }
   double time = st.time[e];
   gfloat* sensordata = valid ? (gfloat*)(st.sensordata + e * m.nsensordata) : scr + m.S.sens;
+  {
+    // workgroup-shared tables (DevModel::shr_*): ray-geom records and per-ray direction + address
+    float* shr = smem + m.shr_off;
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < m.shr_rf; i += blockDim.x) shr[i] = m.rgeom[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < m.shr_total - m.shr_rf; i += blockDim.x) shr[m.shr_rf + i] = m.rfray[8 * (i >> 2) + (i & 3)];
+  }
+  __syncthreads();
   wsync();
   int ncon = 0;
   int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
@@ -3291,7 +3310,13 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
         if (!(m.disableflags & MRS_DSBL_AUTORESET)) { [[clang::noinline]] reset_env<G>(ENV_ARGS); time = 0; }
       }
     }
-    MRS_CALL(G, ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG));
+#ifdef MRS_DIAG_SENS_LAST
+    // diagnostic build: sensordata stored on the last step of the launch only (rays still computed)
+    gfloat* sd_step = (kForwardOnly || step == n_steps - 1) ? sensordata : nullptr;
+#else
+    gfloat* sd_step = sensordata;
+#endif
+    MRS_CALL(G, ncon = forward<G>(ENV_ARGS, sd_step PH_ACC_ARG));
     if (kForwardOnly) break;
     bool redo = false;
     if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
@@ -3304,7 +3329,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     }
     // forward() is entered by the whole wave; for envs that were not reset it recomputes the
     // same outputs from the same state
-    if (__any(redo)) { [[clang::noinline]] ncon = forward<G>(ENV_ARGS, sensordata PH_ACC_ARG); }  // rare
+    if (__any(redo)) { [[clang::noinline]] ncon = forward<G>(ENV_ARGS, sd_step PH_ACC_ARG); }  // rare
     {
       PH_BEGIN();
       MRS_CALL(G, integrate<G>(ENV_ARGS));
@@ -3359,11 +3384,11 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 }  // namespace
 
 template <int G>
-static void launch_g(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
-                     bool forward_only, hipStream_t stream) {
+static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
+                     int n_steps, bool forward_only, hipStream_t stream) {
   constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
-  const size_t lds = sizeof(float) * (size_t)lds_floats * kEnvsPerBlock;
+  const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
   if (forward_only)
     hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs, 1);
   else
@@ -3389,13 +3414,13 @@ int phase_cycles(double* out, int n, bool reset) {
 #endif
 }
 
-hipError_t launch_step(const DevModel* d_model, int lds_floats, const DevState& st, int n_envs, int n_steps,
-                       bool forward_only, int group, hipStream_t stream) {
+hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
+                       int n_steps, bool forward_only, int group, hipStream_t stream) {
   switch (group) {
-    case 8: launch_g<8>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
-    case 16: launch_g<16>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
-    case 32: launch_g<32>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
-    case 64: launch_g<64>(d_model, lds_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
