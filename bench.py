@@ -43,6 +43,9 @@ def parse():
                    help="c3: the BASELINE metric (default); c4: mobile base + lidar + 640x480 depth camera; "
                         "c5: contact-rich arm + 8 free boxes, PGS 50 iterations")
     p.add_argument("--render-every", type=int, default=100, help="C4: physics steps between depth frames")
+    p.add_argument("--gather", action="store_true",
+                   help="N>1: end-of-step observation gather, every period each rank's (qpos, qvel) to rank 0 "
+                        "with grouped RCCL point-to-point ops (SURVEY.md §8e), inside the timed region")
     return p.parse_args()
 
 
@@ -193,6 +196,7 @@ def main():
     batch.set_stream(stream.cuda_stream)
     batch.set(sim.FIELD_QPOS, qpos0)
     d_table = torch.from_numpy(table).to(f"cuda:{local}")
+    gather = shard.ObsGather(n, [model.nq, model.nv], device=f"cuda:{local}") if args.gather and world > 1 else None
     torch.cuda.synchronize()
 
     def period(p: int, ev=None):
@@ -202,6 +206,12 @@ def main():
         batch.step(args.period)
         if ev is not None:
             ev[1].record(stream)
+        if gather is not None:
+            # observations of this period into HBM buffers, then grouped sends to rank 0
+            q, v = gather.start(p)
+            batch.get_device(sim.FIELD_QPOS, q.data_ptr())
+            batch.get_device(sim.FIELD_QVEL, v.data_ptr())
+            gather.launch()
 
     with torch.cuda.stream(stream):
         for p in range(args.warmup):
@@ -255,6 +265,7 @@ def main():
             "physics_steps_per_bench_step": args.period,
             "timestep": model.timestep,
             "parallelism": f"env-sharded x{world}",
+            "obs_gather": "per period (qpos, qvel) of every env to rank 0, RCCL batch_isend_irecv" if gather else None,
         },
         "roofline": {
             "bound": "mfma",

@@ -42,6 +42,50 @@ def max_over_ranks(values, device="cpu"):
     return [float(x) for x in t.cpu()]
 
 
+class ObsGather:
+    """End-of-step observation gather to rank 0: every rank's [n_local, dim] rows of
+    each observation field go to the root with grouped point-to-point ops (`batch_isend_irecv`: on an
+    xGMI node one direct link per peer, not a ring).  Double buffered: `start(k)` returns the buffers
+    of slot k % 2 to be filled (by the producer, on the current stream) and `launch()` posts the
+    transfers; the next `start` of the same slot first makes the current stream wait for that slot's
+    previous transfer, so the producer overlaps the one in flight.  Rank 0's gathered rows of slot k
+    are `gathered(k)[f]` ([world, n_local, dim]; its own rows are filled in place)."""
+
+    def __init__(self, n_local: int, dims: list[int], device="cpu"):
+        import torch
+        import torch.distributed as dist
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self._bufs = [[torch.zeros((self.world, n_local, d), device=device) for d in dims] for _ in range(2)]
+        self._pending = [None, None]
+        self._slot = 0
+
+    def start(self, k: int):
+        self._slot = k % 2
+        for w in self._pending[self._slot] or []:
+            w.wait()
+        self._pending[self._slot] = None
+        return [b[self.rank] for b in self._bufs[self._slot]]
+
+    def launch(self):
+        import torch.distributed as dist
+        if self.world == 1:
+            return
+        ops = []
+        for b in self._bufs[self._slot]:
+            if self.rank == 0:
+                ops += [dist.P2POp(dist.irecv, b[r], r) for r in range(1, self.world)]
+            else:
+                ops.append(dist.P2POp(dist.isend, b[self.rank], 0))
+        self._pending[self._slot] = dist.batch_isend_irecv(ops)
+
+    def gathered(self, k: int):
+        for w in self._pending[k % 2] or []:
+            w.wait()
+        self._pending[k % 2] = None
+        return self._bufs[k % 2]
+
+
 def gather_rows(t, dst: int = 0):
     """concatenate every rank's [n_local, ...] tensor on rank `dst` in rank order (None elsewhere);
     equal n_local on every rank"""

@@ -59,6 +59,44 @@ def test_sharded_rollout_matches_single_process(tmp_path, built):
     assert list(got["tmax"]) == [2.0, 0.0]
 
 
+def _gather_worker(rank, port, out_path):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+    from mujoco_ros2_simulation_amd import shard
+    shard.init("gloo")
+    g = shard.ObsGather(PER_RANK, [2, 3])
+    got = []
+    for k in range(4):  # four periods through the two buffer slots
+        q, v = g.start(k)
+        q.copy_(torch.full((PER_RANK, 2), 100.0 * k + rank))
+        v.copy_(torch.arange(PER_RANK * 3, dtype=torch.float32).reshape(PER_RANK, 3) + 10 * rank + 1000 * k)
+        g.launch()
+        if k >= 1 and rank == 0:
+            got.append([b.clone().numpy() for b in g.gathered(k - 1)])
+    if rank == 0:
+        got.append([b.clone().numpy() for b in g.gathered(3)])
+        np.savez(out_path, **{f"p{k}_{f}": got[k][f] for k in range(4) for f in range(2)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_observation_gather_double_buffered(tmp_path, built):
+    """end-of-step observation gather with grouped point-to-point ops, world size 2 on
+    gloo: rank 0 holds every rank's rows of every period, slots reused across periods"""
+    out = tmp_path / "obs.npz"
+    mp.spawn(_gather_worker, args=(_free_port(), str(out)), nprocs=WORLD, join=True)
+    got = np.load(out)
+    for k in range(4):
+        q, v = got[f"p{k}_0"], got[f"p{k}_1"]
+        assert q.shape == (WORLD, PER_RANK, 2) and v.shape == (WORLD, PER_RANK, 3)
+        for r in range(WORLD):
+            assert np.all(q[r] == 100.0 * k + r)
+            assert np.array_equal(v[r], np.arange(PER_RANK * 3).reshape(PER_RANK, 3) + 10 * r + 1000 * k)
+
+
 def test_env_ids_partition():
     from mujoco_ros2_simulation_amd import shard
     ids = np.concatenate([shard.env_ids(r, 5) for r in range(4)])
