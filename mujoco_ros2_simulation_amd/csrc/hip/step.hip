@@ -1551,9 +1551,12 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
 // in lane r, row r's R, aref, b and friction-loss bound (0 for unilateral rows).  Returns qacc of
 // lane j's dof and writes qfrc_constraint.  Rows past the group's nefc (up to the wave's maximum)
 // are zero rows with R = 1, which never move.
+// kUnit: every row's Jacobian is the unit vector of the dof held in lane r's `mydof` (dof friction
+// loss rows), built in registers instead of read from the global rows J
+template <bool kUnit = false>
 __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
                                              float myR, float myaref, float myb, float myfl, float qacc_s,
-                                             int lane) {
+                                             int lane, int mydof = -1) {
   const LdsLayout& L = m.L;
   const int nv = m.nv;
   constexpr int KR = 16;
@@ -1561,7 +1564,10 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   if (lane >= nefc) { myR = 1; myaref = 0; myb = 0; myfl = 0; }
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    Jt[r] = (r < nefc && lane < nv) ? J[r * nv + lane] : 0.0f;
+    if constexpr (kUnit)
+      Jt[r] = (r < nefc && lane == __float_as_int(rowb<r>(__int_as_float(mydof)))) ? 1.0f : 0.0f;
+    else
+      Jt[r] = (r < nefc && lane < nv) ? J[r * nv + lane] : 0.0f;
     MJt[r] = Jt[r];
     Rr[r] = rowb<r>(myR);
     ar[r] = rowb<r>(myaref);
@@ -2406,6 +2412,47 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   gfloat* ARii = scr + S.efc_ARii;
   int nefc = 0;
   if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) s[L.qfrc_con + lane] = 0; wsync(); return qacc_s; }
+  if constexpr (G == 16) {
+    // Friction-loss rows only (no contact, no active joint limit: C3's steady state): every row is
+    // the unit vector of its dof, so lane r builds row r's scalars from the model and the LDS state
+    // and the register-resident PGS builds J itself -- no row goes through the global scratch.
+    const int nf = (m.disableflags & MRS_DSBL_FRICTIONLOSS) ? 0 : m.nfric;
+    bool lim = false;
+    if (!(m.disableflags & MRS_DSBL_LIMIT))
+      #pragma unroll 1
+      for (int k = lane; k < m.nlim; k += G) {
+        const int jid = m.lim_jnt[k];
+        const float q = s[L.qpos + m.jnt_qposadr[jid]], mg = m.jnt_margin[jid];
+        lim |= (q - m.jnt_range[2 * jid] < mg) | (m.jnt_range[2 * jid + 1] - q < mg);
+      }
+    if (ncon == 0 && nf > 0 && nf <= 16 && !gany<G>(lim)) {
+      int mydof = -1;
+      float myR = 1, myaref = 0, myb = 0, myfl = 0;
+      if (lane < nf) {
+        const int j = m.fric_dof[lane];
+        mydof = j;
+        const CPtr<float> sr = m.dof_solref + 2 * j, si = m.dof_solimp + 5 * j;
+        const float imp = impedance(si, 0.0f, 0.0f);
+        const float R = (1 - imp) * m.dof_invweight0[j] / imp;
+        myR = R > kMinVal ? R : kMinVal;
+        const float dmax = clampf(si[1], 0.0001f, 0.9999f);
+        float B;
+        if (sr[0] > 0) {
+          float tc = sr[0];
+          if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
+          B = 2 / (dmax * tc);
+        } else {
+          B = -sr[1] / dmax;
+        }
+        myaref = -B * s[L.qvel + j];  // friction rows have no position term
+        myb = s[L.qacc_smooth + j] - myaref;
+        myfl = m.dof_frictionloss[j];
+      }
+      const float qa = pgs_small16<true>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+      wsync();
+      return qa;
+    }
+  }
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
   // keep ids in a small per-row int array inside the type slot (type*65536 + id)
   // --- friction loss rows
@@ -2865,12 +2912,20 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     float gm[9];
     for (int k = 0; k < 9; ++k) gm[k] = se[L.gxmat + 9 * g + k];
     const CPtr<float> gs = rec + 4;
+    // rays of a pass from one origin: the origin goes into the geom frame once, not once per ray
+    float lp0[3] = {0, 0, 0};
+    if (common_body >= 0) {
+      const float dv[3] = {pnt[0][0] - gp[0], pnt[0][1] - gp[1], pnt[0][2] - gp[2]};
+      matT_vec(lp0, gm, dv);
+    }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       if (!((cmask >> j) & 1)) continue;
-      const float dv[3] = {pnt[j][0] - gp[0], pnt[j][1] - gp[1], pnt[j][2] - gp[2]};
-      float lp[3], lv[3];
-      matT_vec(lp, gm, dv);
+      float lp[3] = {lp0[0], lp0[1], lp0[2]}, lv[3];
+      if (common_body < 0) {
+        const float dv[3] = {pnt[j][0] - gp[0], pnt[j][1] - gp[1], pnt[j][2] - gp[2]};
+        matT_vec(lp, gm, dv);
+      }
       matT_vec(lv, gm, vec[j]);
       const float t = ray_geom_local(type, gs, lp, lv);
       if (t >= 0 && (dist[j] < 0 || t < dist[j])) dist[j] = t;

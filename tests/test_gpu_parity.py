@@ -6,7 +6,8 @@ north_star "qpos/qvel within 1e-5 rel"):
   rangefinder       |gpu - cpu| <= 2e-5 * max(1, range) on >= 99.5% of rays (grazing hits at box
                     edges may switch faces) and identical hit/miss (-1) pattern
   depth image       |gpu - cpu| <= 1e-5 * depth on >= 99.9% of pixels (silhouette edges may flip)
-  contact counts    identical (integer work is bit-exact)
+  contacts          counts and the (geom1, geom2) list identical (integer work is bit-exact);
+                    dist / pos / frame within 1e-4
 """
 import numpy as np
 import pytest
@@ -257,6 +258,29 @@ def test_full_size_c3_batch_properties():
     d.ctrl[:] = ctrl[0]
     d.step(100)
     np.testing.assert_allclose(q[0], d.qpos, rtol=RTOL, atol=RTOL)
+
+
+def test_abi_errors_leave_batch_usable():
+    """error behaviour of the C ABI on a live batch (int status codes, message via
+    mrs_last_error, no exceptions across the ABI): out-of-range env ranges, n_steps < 1, a bad
+    camera index and an out-of-range contact env all fail with MRS_ERR_INVALID, and the batch
+    still steps afterwards"""
+    model = sim.Model.load(REF_SCENE)
+    b = sim.Batch(model, 3)
+    bad = [lambda: b.get(sim.FIELD_QPOS, 2, 2), lambda: b.set(sim.FIELD_QPOS, np.zeros((4, 2))),
+           lambda: b.step(0), lambda: b.contacts(3), lambda: b.reset(-1, 1, 5),
+           lambda: b.get_device(sim.FIELD_TIME, 1)]
+    for call in bad:
+        with pytest.raises(sim.MrsError) as ei:
+            call()
+        assert ei.value.code == -1 and str(ei.value)
+    img = np.zeros((480, 640), dtype=np.float32)
+    assert sim.lib().mrs_batch_render_depth(b._h, 5, 0, 1, img.ctypes.data) == -1  # no camera 5
+    assert b"camera" in sim.lib().mrs_last_error()
+    b.step(5)
+    assert np.all(np.isfinite(b.get(sim.FIELD_QPOS)))
+    assert b.contacts(0)[0].shape == (0, 2)  # the reference scene has no contact pairs
+    b.close()
 
 
 @pytest.mark.parametrize("group", [16, 64])
