@@ -73,13 +73,14 @@ def cpu_baseline(model, period: int, target_s: float):
                       f"(oracle/oracle.c), {cores} pthreads, {secs:.1f} s"}
 
 
-def measured_traffic(scene: str, envs: int, period: int):
-    """HBM bytes per launch of the step kernel from the committed rocprofv3 PMC summary of this same
-    bench command (scripts/gpu_round.sh -> scripts/pmc_summary.py -> profiles/<round>/pmc_c3.json);
-    None when no summary exists for this workload."""
-    if Path(scene).stem != "arm7_lidar" or envs != 8192 or period != 10:
+def measured_traffic(cfg: str, envs: int, period: int):
+    """HBM bytes per launch of the config's dominant kernel from the committed rocprofv3 PMC summary of
+    this same bench command (scripts/gpu_full.sh -> scripts/pmc_summary.py ->
+    profiles/<round>/pmc_<cfg>.json); None when no summary exists for this workload."""
+    default_envs = {"c3": 8192, "c4": 2048, "c5": 8192}
+    if cfg not in default_envs or envs != default_envs[cfg] or period != 10:
         return None, None
-    found = sorted(ROOT.glob("profiles/r*/pmc_c3.json"))
+    found = sorted(ROOT.glob(f"profiles/r*/pmc_{cfg}.json"))
     if not found:
         return None, None
     rec = json.loads(found[-1].read_text())
@@ -142,6 +143,7 @@ def run_c4(args):
     assert torch.isfinite(frames).all(), "non-finite depth"
     bytes_frame = n * W * H * 4
     achieved = bytes_frame / (rend_ms * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic("c4", n, args.period)
     result = {
         "metric": "env-steps/sec (whole node), mobile base + 32-beam lidar + 640x480 depth camera (C4)",
         "value": world * n * args.steps * args.period / elapsed,
@@ -154,7 +156,8 @@ def run_c4(args):
                    "depth_every_physics_steps": every * args.period, "parallelism": f"env-sharded x{world}"},
         "depth_frames_per_s": world * n * len(rend_ev) / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                     "frac": achieved / 8000.0, "traffic": None,
+                     "frac": achieved / 8000.0, "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
                      "kernel": "depth_kernel (one 640x480 frame of every env)", "kernel_ms": rend_ms,
                      "algorithmic_bytes_per_launch": bytes_frame, "step_kernel_ms": step_ms},
     }
@@ -242,7 +245,8 @@ def main():
     flops, survey_bytes = roofline.SURVEY_PER_ENV_STEP.get(Path(args.scene).stem, (detailed_flops, None))
     bytes_ = roofline.bytes_per_env_step(model, args.period)
     achieved_tf = n * args.period * flops / (kern_ms * 1e-3) / 1e12
-    traffic, traffic_src = measured_traffic(args.scene, n, args.period)
+    cfg = {"arm7_lidar": "c3", "arm_boxes": "c5"}.get(Path(args.scene).stem, "")
+    traffic, traffic_src = measured_traffic(cfg, n, args.period)
     result = {
         "metric": METRIC if args.config == "c3" else "env-steps/sec (whole node), contact-rich arm + 8 free boxes (C5)",
         "value": value,
