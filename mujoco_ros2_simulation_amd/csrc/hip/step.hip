@@ -1560,7 +1560,9 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   const LdsLayout& L = m.L;
   const int nv = m.nv;
   constexpr int KR = 16;
-  float Jt[KR], MJt[KR], Rr[KR], ar[KR], bq[KR], fl[KR], iA[KR], Ai[KR], f[KR];
+  // J and M^-1 J' columns per row in registers; row scalars (R, aref, b, bound, diagonal of A, force)
+  // stay in the row's own lane and reach the other lanes by DPP row broadcasts when used
+  float Jt[KR], MJt[KR];
   if (lane >= nefc) { myR = 1; myaref = 0; myb = 0; myfl = 0; }
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
@@ -1569,11 +1571,6 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     else
       Jt[r] = (r < nefc && lane < nv) ? J[r * nv + lane] : 0.0f;
     MJt[r] = Jt[r];
-    Rr[r] = rowb<r>(myR);
-    ar[r] = rowb<r>(myaref);
-    bq[r] = rowb<r>(myb);
-    fl[r] = rowb<r>(myfl);
-    f[r] = 0;
   });
   // M^-1 J' for all rows at once: forward then backward substitution with L (Cholesky of M, LDS)
   unroll<KR>([&](auto ic) {
@@ -1604,11 +1601,12 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       });
     }
   });
+  float myA = 1, myf = 0;  // lane r: A_rr = J_r M^-1 J_r' + R_r and the force of row r
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
     if (r < rmax) {
-      Ai[r] = gsum<16>(Jt[r] * MJt[r]) + Rr[r];
-      iA[r] = 1.0f / Ai[r];
+      const float a = gsum<16>(Jt[r] * MJt[r]) + rowb<r>(myR);
+      if (lane == r) myA = a;
     }
   });
   float qa = lane < nv ? qacc_s : 0.0f;
@@ -1619,20 +1617,24 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
-        const float jar = gsum<16>(Jt[r] * qw) - ar[r];
-        const float D = 1.0f / Rr[r];
-        f[r] = fl[r] > 0 ? (jar <= -Rr[r] * fl[r] ? fl[r] : (jar >= Rr[r] * fl[r] ? -fl[r] : -D * jar))
-                         : (jar < 0 ? -D * jar : 0.0f);
-        v += MJt[r] * f[r];
+        const float R = rowb<r>(myR), fl = rowb<r>(myfl);
+        const float jar = gsum<16>(Jt[r] * qw) - rowb<r>(myaref);
+        const float D = 1.0f / R;
+        const float f = fl > 0 ? (jar <= -R * fl ? fl : (jar >= R * fl ? -fl : -D * jar)) : (jar < 0 ? -D * jar : 0.0f);
+        v += MJt[r] * f;
+        if (lane == r) myf = f;
       }
     });
     float cost = 0;
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
-      if (r < rmax) cost += f[r] * (0.5f * (gsum<16>(Jt[r] * v) + Rr[r] * f[r]) + bq[r]);
+      if (r < rmax) {
+        const float f = rowb<r>(myf);
+        cost += f * (0.5f * (gsum<16>(Jt[r] * v) + rowb<r>(myR) * f) + rowb<r>(myb));
+      }
     });
     if (cost > 0) {
-      unroll<KR>([&](auto rc) { f[decltype(rc)::value] = 0; });
+      myf = 0;
     } else {
       qa += v;
     }
@@ -1644,13 +1646,14 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
-        const float res = gsum<16>(Jt[r] * qa) - ar[r] + Rr[r] * f[r];
-        float nf = f[r] - res * iA[r];
-        nf = fl[r] > 0 ? clampf(nf, -fl[r], fl[r]) : (nf < 0 ? 0.0f : nf);
-        const float delta = nf - f[r];
+        const float f0 = rowb<r>(myf), a = rowb<r>(myA), fl = rowb<r>(myfl);
+        const float res = gsum<16>(Jt[r] * qa) - rowb<r>(myaref) + rowb<r>(myR) * f0;
+        float nf = f0 - res * (1.0f / a);
+        nf = fl > 0 ? clampf(nf, -fl, fl) : (nf < 0 ? 0.0f : nf);
+        const float delta = nf - f0;
         qa += MJt[r] * delta;
-        f[r] = nf;
-        improvement -= delta * res + 0.5f * delta * delta * Ai[r];
+        if (lane == r) myf = nf;
+        improvement -= delta * res + 0.5f * delta * delta * a;
       }
     });
     if (improvement * m.pgs_scale < m.tolerance) break;
@@ -1658,16 +1661,11 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   float qc = 0;
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if (r < rmax) qc += Jt[r] * f[r];
+    if (r < rmax) qc += Jt[r] * rowb<r>(myf);
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
-  if (m.acc_sens & 2) {
-    // row forces for the contact forces of force/torque sensors (mj_rnePostConstraint)
-    unroll<KR>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if (lane == r && r < nefc) ff[r] = f[r];
-    });
-  }
+  // row forces for the contact forces of force/torque sensors (mj_rnePostConstraint)
+  if ((m.acc_sens & 2) && lane < nefc) ff[lane] = myf;
   return qa;
 }
 
@@ -2387,6 +2385,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
 }
 
 template <int G>
+__device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s);
+
+template <int G>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) {
@@ -2397,20 +2398,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       default: return constraints_sparse<64>(ENV_ARGS, ncon, qacc_s);
     }
   }
-  if constexpr (G == 64) ncon = uniform_int(ncon);
   const int nv = m.nv;
-  gfloat* J = scr + S.efc_J;
-  gfloat* MJ = scr + S.efc_MJ;
-  gfloat* type = scr + S.efc_type;
-  gfloat* pos = scr + S.efc_pos;
-  gfloat* marg = scr + S.efc_margin;
-  gfloat* floss = scr + S.efc_floss;
-  gfloat* Rr = scr + S.efc_R;
-  gfloat* aref = scr + S.efc_aref;
-  gfloat* bb = scr + S.efc_b;
-  gfloat* ff = scr + S.efc_f;
-  gfloat* ARii = scr + S.efc_ARii;
-  int nefc = 0;
   if (m.disableflags & MRS_DSBL_CONSTRAINT) { if (lane < nv) s[L.qfrc_con + lane] = 0; wsync(); return qacc_s; }
   if constexpr (G == 16) {
     // Friction-loss rows only (no contact, no active joint limit: C3's steady state): every row is
@@ -2453,6 +2441,32 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       return qa;
     }
   }
+  // rows with contacts or active joint limits: the dense row path, out of line -- cold in C3's
+  // steady state, and keeping it out of the inlined step loop keeps the hot code footprint small
+  float qa;
+  [[clang::noinline]] qa = constraints_dense<G>(ENV_ARGS, ncon, qacc_s);
+  return qa;
+}
+
+// dense constraint rows in the env's global scratch (J, M^-1 J', row scalars), then the
+// register-resident PGS (<= 16 rows on G = 16) or the row-serial PGS with wave reductions
+template <int G>
+__device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
+  ENV_UNPACK;
+  if constexpr (G == 64) ncon = uniform_int(ncon);
+  const int nv = m.nv;
+  gfloat* J = scr + S.efc_J;
+  gfloat* MJ = scr + S.efc_MJ;
+  gfloat* type = scr + S.efc_type;
+  gfloat* pos = scr + S.efc_pos;
+  gfloat* marg = scr + S.efc_margin;
+  gfloat* floss = scr + S.efc_floss;
+  gfloat* Rr = scr + S.efc_R;
+  gfloat* aref = scr + S.efc_aref;
+  gfloat* bb = scr + S.efc_b;
+  gfloat* ff = scr + S.efc_f;
+  gfloat* ARii = scr + S.efc_ARii;
+  int nefc = 0;
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
   // keep ids in a small per-row int array inside the type slot (type*65536 + id)
   // --- friction loss rows
@@ -3215,7 +3229,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
-  if (m.acc_sens && !(m.disableflags & MRS_DSBL_SENSOR)) MRS_CALL(G, rne_post<G>(ENV_ARGS, ncon));
+  if (m.acc_sens && !(m.disableflags & MRS_DSBL_SENSOR)) { [[clang::noinline]] rne_post<G>(ENV_ARGS, ncon); }
   if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
   PH_END(ph_acc, PH_SENS);
   return ncon;
