@@ -1594,13 +1594,12 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
 // are zero rows with R = 1, which never move.
 // kUnit: every row's Jacobian is the unit vector of the dof held in lane r's `mydof` (dof friction
 // loss rows), built in registers instead of read from the global rows J
-template <bool kUnit = false>
+template <bool kUnit = false, int KR = 16>
 __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
                                              float myR, float myaref, float myb, float myfl, float qacc_s,
                                              int lane, int mydof = -1) {
   const LdsLayout& L = m.L;
   const int nv = m.nv;
-  constexpr int KR = 16;
   // J and M^-1 J' columns per row in registers; row scalars (R, aref, b, bound, diagonal of A, force)
   // stay in the row's own lane and reach the other lanes by DPP row broadcasts when used
   float Jt[KR], MJt[KR];
@@ -2477,7 +2476,13 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
         myb = s[L.qacc_smooth + j] - myaref;
         myfl = m.dof_frictionloss[j];
       }
-      const float qa = pgs_small16<true>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+      // rows (and the dofs they touch) unrolled to 8 when the model has at most 8 friction dofs:
+      // a quarter of the substitution code
+      float qa;
+      if (nf <= 8 && m.nv <= 8)
+        qa = pgs_small16<true, 8>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+      else
+        qa = pgs_small16<true, 16>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
       wsync();
       return qa;
     }
