@@ -800,6 +800,36 @@ __device__ __forceinline__ int midx(const DevModel& m, int i, int j) {
 
 // Cholesky of the dense nv x nv matrix A (LDS) into Lf (LDS), column by column; lanes over rows.
 // Blocked mode (G = 64): every tree's block at once, columns up to the largest tree's size.
+// G = 16 dense factor, N = unroll bound >= nv: lane i keeps row i of A and then of L in registers;
+// column k needs L[k][p] for p < k, which is lane k's register p: one DPP row broadcast each, no LDS
+// round trip in the chain
+template <int N>
+__device__ __forceinline__ void chol_rows16(const lfloat* A, lfloat* Lf, int nv, int lane) {
+  float row[N];
+  unroll<N>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    row[p] = (p < nv && lane < nv) ? A[lane * nv + p] : 0.0f;
+  });
+  unroll<N>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if (k < nv) {
+      float t = row[k];
+      unroll<k>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        t -= row[p] * rowb<k>(row[p]);
+      });
+      const float dk = rowb<k>(t);
+      const float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
+      row[k] = lane == k ? lkk : (lane > k ? t / lkk : row[k]);
+    }
+  });
+  if (lane < nv)
+    unroll<N>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      if (p < nv) Lf[lane * nv + p] = p <= lane ? row[p] : 0.0f;
+    });
+}
+
 template <int G>
 __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
   mp = uniform_ptr(mp);
@@ -810,31 +840,9 @@ __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat
   lane = __lane_id() & (G - 1);
   const int nv = load_model(mp).nv;
   if constexpr (G == 16) {
-    // lane i keeps row i of A and then of L in registers; column k needs L[k][p] for p < k, which
-    // is lane k's register p: one DPP row broadcast each, no LDS round trip in the chain
-    float row[16];
-    unroll<16>([&](auto pc) {
-      constexpr int p = decltype(pc)::value;
-      row[p] = (p < nv && lane < nv) ? A[lane * nv + p] : 0.0f;
-    });
-    unroll<16>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      if (k < nv) {
-        float t = row[k];
-        unroll<k>([&](auto pc) {
-          constexpr int p = decltype(pc)::value;
-          t -= row[p] * rowb<k>(row[p]);
-        });
-        const float dk = rowb<k>(t);
-        const float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
-        row[k] = lane == k ? lkk : (lane > k ? t / lkk : row[k]);
-      }
-    });
-    if (lane < nv)
-      unroll<16>([&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        if (p < nv) Lf[lane * nv + p] = p <= lane ? row[p] : 0.0f;
-      });
+    // unrolled to 8 dofs when nv <= 8 (a quarter of the code of the 16-dof form)
+    if (nv <= 8) chol_rows16<8>(A, Lf, nv, lane);
+    else chol_rows16<16>(A, Lf, nv, lane);
     wsync();
     return;
   }
@@ -876,6 +884,34 @@ __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat
   }
 }
 // x = A^-1 b with A = Lf Lf'; lane j holds b_j / returns x_j (lanes >= nv return 0)
+// G = 16 solve, N = unroll bound >= nv: lane j prefetches row j of L (forward) and column j
+// (backward); the substitution chains are DPP broadcasts and FMAs
+template <int N>
+__device__ __forceinline__ float chol_solve_rows16(const lfloat* Lf, float x, int nv, int lane) {
+  float lrow[N], lcol[N], inv[N];
+  unroll<N>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    lrow[i] = (i < nv && lane < nv) ? Lf[lane * nv + i] : 0.0f;
+    lcol[i] = (i < nv && lane < nv) ? Lf[i * nv + lane] : 0.0f;
+    inv[i] = i < nv ? 1.0f / Lf[i * nv + i] : 0.0f;
+  });
+  unroll<N>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i < nv) {
+      const float xi = rowb<i>(x) * inv[i];
+      x = lane == i ? xi : (lane > i ? x - lrow[i] * xi : x);
+    }
+  });
+  unroll<N>([&](auto ic) {
+    constexpr int i = N - 1 - decltype(ic)::value;
+    if (i < nv) {
+      const float xi = rowb<i>(x) * inv[i];
+      x = lane == i ? xi : (lane < i ? x - lcol[i] * xi : x);
+    }
+  });
+  return x;
+}
+
 template <int G>
 __device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, const lfloat* Lf, float b, int lane) {
   mp = uniform_ptr(mp);
@@ -884,29 +920,7 @@ __device__ MRS_PHASE float chol_solve_lanes(const DevModel* __restrict__ mp, con
   const int nv = load_model(mp).nv;
   float x = lane < nv ? b : 0.0f;
   if constexpr (G == 16) {
-    // lane j prefetches row j of L (forward) and column j (backward); the substitution chains are
-    // DPP broadcasts and FMAs
-    float lrow[16], lcol[16], inv[16];
-    unroll<16>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      lrow[i] = (i < nv && lane < nv) ? Lf[lane * nv + i] : 0.0f;
-      lcol[i] = (i < nv && lane < nv) ? Lf[i * nv + lane] : 0.0f;
-      inv[i] = i < nv ? 1.0f / Lf[i * nv + i] : 0.0f;
-    });
-    unroll<16>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      if (i < nv) {
-        const float xi = rowb<i>(x) * inv[i];
-        x = lane == i ? xi : (lane > i ? x - lrow[i] * xi : x);
-      }
-    });
-    unroll<16>([&](auto ic) {
-      constexpr int i = 15 - decltype(ic)::value;
-      if (i < nv) {
-        const float xi = rowb<i>(x) * inv[i];
-        x = lane == i ? xi : (lane < i ? x - lcol[i] * xi : x);
-      }
-    });
+    x = nv <= 8 ? chol_solve_rows16<8>(Lf, x, nv, lane) : chol_solve_rows16<16>(Lf, x, nv, lane);
     return lane < nv ? x : 0.0f;
   }
   if constexpr (G == 64) {
