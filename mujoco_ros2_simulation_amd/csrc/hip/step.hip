@@ -1693,21 +1693,26 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       qa += v;
     }
   }
-  // PGS sweeps
+  // PGS sweeps: row scalars broadcast into every lane once, forces replicated across the sweeps
+  float f[KR], bR[KR], bA[KR], iA[KR], bref[KR], bfl[KR];
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    f[r] = rowb<r>(myf); bR[r] = rowb<r>(myR); bA[r] = rowb<r>(myA); bref[r] = rowb<r>(myaref);
+    bfl[r] = rowb<r>(myfl); iA[r] = 1.0f / bA[r];
+  });
   #pragma unroll 1
   for (int it = 0; it < m.iterations; ++it) {
     float improvement = 0;
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
-        const float f0 = rowb<r>(myf), a = rowb<r>(myA), fl = rowb<r>(myfl);
-        const float res = gsum<16>(Jt[r] * qa) - rowb<r>(myaref) + rowb<r>(myR) * f0;
-        float nf = f0 - res * (1.0f / a);
-        nf = fl > 0 ? clampf(nf, -fl, fl) : (nf < 0 ? 0.0f : nf);
-        const float delta = nf - f0;
+        const float res = gsum<16>(Jt[r] * qa) - bref[r] + bR[r] * f[r];
+        float nf = f[r] - res * iA[r];
+        nf = bfl[r] > 0 ? clampf(nf, -bfl[r], bfl[r]) : (nf < 0 ? 0.0f : nf);
+        const float delta = nf - f[r];
         qa += MJt[r] * delta;
-        if (lane == r) myf = nf;
-        improvement -= delta * res + 0.5f * delta * delta * a;
+        f[r] = nf;
+        improvement -= delta * res + 0.5f * delta * delta * bA[r];
       }
     });
     if (improvement * m.pgs_scale < m.tolerance) break;
@@ -1715,7 +1720,8 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   float qc = 0;
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if (r < rmax) qc += Jt[r] * rowb<r>(myf);
+    if (r < rmax) qc += Jt[r] * f[r];
+    if (lane == r) myf = f[r];
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
   // row forces for the contact forces of force/torque sensors (mj_rnePostConstraint)
