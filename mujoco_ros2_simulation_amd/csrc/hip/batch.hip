@@ -229,13 +229,16 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
 // frame lp = R'(c - p) and A = R' C (C: camera rotation), so the geom-frame direction of the pixel
 // ray (x, y, -1) is lv = A (x, y, -1) -- three FMAs per component per pixel -- and, for the cull,
 // the geom's centre and axes in the camera frame with the half extents of an oriented box around it.
-// Each wave walks tiles of 64 x 4 pixels: lane = column (every store is 256 contiguous bytes), 4 rows
+// Each wave walks tiles of 64 x 16 pixels: lane = column (every store is 256 contiguous bytes), 16 rows
 // per lane.  Per tile, lane g tests geom g against the tile's pyramid of rays (four planes through
 // the camera): an oriented box wholly outside one plane, or a plane no corner ray descends onto, is
 // skipped; one ballot gives the candidates and the pixel loop visits only those (wave-uniform geom,
 // so the primitive test does not diverge by type).  Boxes use the slab test: the same face
 // parameters (+-s - lp) / lv as the face-by-face test, nearest non-negative crossing.
-constexpr int kDepthTileW = 64, kDepthTileH = 4, kDepthGeoms = 64;
+#ifndef MRS_DEPTH_TILE_H
+#define MRS_DEPTH_TILE_H 16  // measured C4 (2048 frames): 4 rows 2.08 ms, 8 rows 1.70, 16 rows 1.68, 32 rows 2.13
+#endif
+constexpr int kDepthTileW = 64, kDepthTileH = MRS_DEPTH_TILE_H, kDepthGeoms = 64;
 struct DepthGeom {  // 24 floats in LDS
   float lp[3], A[9], size[3];  // row i of A = R'C is also the geom's axis i in the camera frame
   float cc[3], ext[3];         // cull: centre in the camera frame, oriented-box half extents
