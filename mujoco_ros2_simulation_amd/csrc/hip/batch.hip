@@ -818,8 +818,16 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
-  auto lds_bytes = [&](int g) {  // 4 waves
-    return (static_cast<size_t>(L.total) * 4 * (64 / g) + d.shr_total) * sizeof(float);
+  auto envs_per_block = [](int g) {
+    switch (g) {
+      case 8: return WavesPerBlock<8>::value * 8;
+      case 16: return WavesPerBlock<16>::value * 4;
+      case 32: return WavesPerBlock<32>::value * 2;
+      default: return WavesPerBlock<64>::value;
+    }
+  };
+  auto lds_bytes = [&](int g) {
+    return (static_cast<size_t>(L.total) * envs_per_block(g) + d.shr_total) * sizeof(float);
   };
   // (narrow groups win even when they leave CUs idle: C4's 2048 envs run a 10-step launch in
   // 1.33 ms at G = 16 on 128 workgroups vs 4.0 ms at G = 64 on 512)
@@ -832,7 +840,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.blocked = b.group == 64 ? 1 : 0;
   if (d.blocked) lds_layout(true);
-  d.shr_off = L.total * (b.group == 64 ? 1 : 4 * 64 / b.group);
+  d.shr_off = L.total * envs_per_block(b.group);
   if ((static_cast<size_t>(d.shr_off) + d.shr_total) * sizeof(float) > 160 * 1024)
     throw UnsupportedError("model too large for the per-environment LDS working set");
   // --- scratch layout (floats).  Dense mode: rows J and M^-1 J' as nefc x nv plus per-row scalars;

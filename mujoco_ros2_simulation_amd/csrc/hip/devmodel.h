@@ -129,7 +129,10 @@ constexpr int kRayBlock = 64;
 // workgroup at G = 64, so LDS is granted per env (the C5 working set of ~13.5 KB fits 11 envs per
 // CU instead of 2 workgroups of 4)
 template <int G>
-struct WavesPerBlock { static constexpr int value = G == 64 ? 1 : 4; };
+#ifndef MRS_G16_WAVES
+#define MRS_G16_WAVES 4
+#endif
+struct WavesPerBlock { static constexpr int value = G == 64 ? 1 : (G == 16 ? MRS_G16_WAVES : 4); };
 
 // device state of a batch (all [n_envs][dim], fp32 unless noted)
 struct DevState {
