@@ -59,8 +59,8 @@ typedef struct mrs_model_view {
   int max_depth;     /* longest root-to-leaf body chain (levels for tree-parallel passes) */
 
   /* options (mjOption subset) */
-  double timestep, gravity[3], tolerance, impratio;
-  int integrator, solver, iterations, disableflags, cone;
+  double timestep, gravity[3], tolerance, impratio, ls_tolerance;
+  int integrator, solver, iterations, disableflags, cone, ls_iterations;
 
   /* statistic / visual (for the depth camera) */
   double stat_extent, stat_center[3], stat_meaninertia, vis_znear, vis_zfar;

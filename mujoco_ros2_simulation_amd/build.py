@@ -81,7 +81,7 @@ def build_plugin(verbose: bool = False) -> Path:
     libmrs.so; host C++ only (no device code), linked with rpath $ORIGIN."""
     lib = build_lib(verbose)
     inc = [f"-I{CSRC / 'plugin' / 'include'}", f"-I{CSRC / 'plugin' / 'ros_shim'}", f"-I{ROOT / 'include'}"]
-    deps = [p for p in (CSRC / "plugin").rglob("*.hpp")] + [ROOT / "include" / "mrs.h",
+    deps = [p for p in (CSRC / "plugin").rglob("*.hpp")] + [ROOT / "include" / "mrs.h", ROOT / "include" / "mrs_model.h",
                                                           ROOT / "include" / "mrs_plugin.h", CSRC / "mjcf" / "xml.h"]
     objs, procs = [], []
     for rel in PLUGIN_SOURCES:

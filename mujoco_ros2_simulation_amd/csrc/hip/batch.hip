@@ -448,6 +448,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nsite = m.nsite; d.ncam = m.ncam; d.nsensor = m.nsensor; d.nsensordata = m.nsensordata;
   d.max_depth = m.max_depth;
   d.integrator = m.integrator; d.iterations = m.iterations; d.disableflags = m.disableflags;
+  d.solver = m.solver; d.ls_iterations = m.ls_iterations;
+  d.impratio = static_cast<float>(m.impratio); d.ls_tolerance = static_cast<float>(m.ls_tolerance);
   // diagnostic phase ablation for profiling only (bit 0 sensors, 1 collision, 2 constraints)
   d.diag_skip = std::getenv("MRS_DIAG_SKIP") ? std::atoi(std::getenv("MRS_DIAG_SKIP")) : 0;
   d.timestep = static_cast<float>(m.timestep);
@@ -808,6 +810,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.act_force = take(std::max(1, m.nu));
     L.rfmask = take(std::max(1, d.nrfblk));
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
+    // primal solvers in blocked mode: H = M + J'DJ couples the trees a contact joins, so it is
+    // stored dense (dense mode builds H in the factor slot L.L instead)
+    L.H = blocked && m.solver != MRS_SOL_PGS ? take(nv * nv) : 0;
     L.total = off;
   };
   lds_layout(false);
@@ -818,14 +823,6 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
-  auto envs_per_block = [](int g) {
-    switch (g) {
-      case 8: return WavesPerBlock<8>::value * 8;
-      case 16: return WavesPerBlock<16>::value * 4;
-      case 32: return WavesPerBlock<32>::value * 2;
-      default: return WavesPerBlock<64>::value;
-    }
-  };
   auto lds_bytes = [&](int g) {
     return (static_cast<size_t>(L.total) * envs_per_block(g) + d.shr_total) * sizeof(float);
   };
@@ -839,6 +836,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
   }
   d.blocked = b.group == 64 ? 1 : 0;
+
   if (d.blocked) lds_layout(true);
   d.shr_off = L.total * envs_per_block(b.group);
   if ((static_cast<size_t>(d.shr_off) + d.shr_total) * sizeof(float) > 160 * 1024)
@@ -848,7 +846,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   ScratchLayout& S = b.dm.S;
   off = 0;
   const int ne = std::max(1, d.max_efc);
-  const int dn = d.blocked ? 0 : ne;
+  // dense rows: dense mode, and blocked mode with a primal solver (the sparse records are PGS's)
+  const int dn = d.blocked && m.solver == MRS_SOL_PGS ? 0 : ne;
   S.efc_J = take(dn * nv); S.efc_MJ = take(dn * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(dn); S.efc_aref = take(dn);
   S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));
@@ -925,8 +924,9 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     b->st.time = static_cast<double*>(dalloc(*b, n * sizeof(double)));
     b->st.warning = static_cast<int*>(dalloc(*b, n * 4 * sizeof(int)));
     b->st.ncon = static_cast<int*>(dalloc(*b, n * sizeof(int)));
-    // padded to whole workgroups (32 envs at the narrowest group width): idle groups use it
-    const size_t n_pad = (static_cast<size_t>(n) + 31) / 32 * 32;
+    // padded to whole workgroups of the chosen group width: idle groups use it
+    const size_t epb = static_cast<size_t>(envs_per_block(b->group));
+    const size_t n_pad = (static_cast<size_t>(n) + epb - 1) / epb * epb;
     b->st.scratch = static_cast<float*>(dalloc(*b, n_pad * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));
     b->st.geom_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 9 * sizeof(float)));

@@ -40,7 +40,8 @@ struct LdsLayout {
       cvel, cacc, cfrc, M, L, qpos, qvel, ctrl, qfrc_applied, qacc_ws, qfrc_bias, qfrc_passive,
       qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force,
       rfmask,  // per ray block: bitmask of candidate ray geoms (int bits)
-      trees;   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
+      trees,   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
+      H;       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
   int total;  // floats per env (multiple of 4)
 };
 
@@ -76,10 +77,10 @@ struct DevModel {
   // Staged once per launch, read by the ray phase every step instead of global loads.
   int shr_off, shr_rf, shr_total;
   // options
-  int integrator, iterations, disableflags;
+  int integrator, iterations, disableflags, solver, ls_iterations;
   int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
-  float timestep, tolerance, pgs_scale, gravity[3];
+  float timestep, tolerance, pgs_scale, gravity[3], impratio, ls_tolerance;
   double timestep_d;  // time is accumulated in fp64 like mjData.time
   // bodies
   CPtr<int> body_parentid, body_rootid, body_jntnum, body_jntadr, body_dofnum, body_dofadr, body_subtree_end, level_adr, level_num, level_body;
@@ -133,6 +134,15 @@ template <int G>
 #define MRS_G16_WAVES 4
 #endif
 struct WavesPerBlock { static constexpr int value = G == 64 ? 1 : (G == 16 ? MRS_G16_WAVES : 4); };
+// environments per workgroup of the step kernel at group width g (kEnvsPerBlock)
+inline int envs_per_block(int g) {
+  switch (g) {
+    case 8: return WavesPerBlock<8>::value * 8;
+    case 16: return WavesPerBlock<16>::value * 4;
+    case 32: return WavesPerBlock<32>::value * 2;
+    default: return WavesPerBlock<64>::value;
+  }
+}
 
 // device state of a batch (all [n_envs][dim], fp32 unless noted)
 struct DevState {

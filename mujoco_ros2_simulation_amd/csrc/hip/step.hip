@@ -2097,7 +2097,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         mu = m.pair_friction[3 * p];  // sliding, for both tangent directions
         sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
         const float tran = m.body_invweight0[2 * m.geom_bodyid[m.pair_g1[p]]] + m.body_invweight0[2 * m.geom_bodyid[m.pair_g2[p]]];
-        diag = dim == 3 ? tran * (1 + mu * mu) : tran;
+        // pyramid edges: diagApprox tran (1 + mu^2), regulariser scaled by 2 mu^2 / impratio
+        // (mj_makeImpedance; oracle/oracle.c make_constraint)
+        diag = dim == 3 ? tran * (1 + mu * mu) * (2 * mu * mu / m.impratio) : tran;
       }
       const float ps = pos[r0], mg = marg[r0];
       const float imp = impedance(si, ps, mg);
@@ -2444,6 +2446,267 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   return lane < nv ? qa[lane] : 0.0f;
 }
 
+// ---------------------------------------------------------------- primal solvers (Newton, CG)
+// mj_solNewton / mj_solCG [upstream engine_solver.c mj_solPrimal]; the algorithm, its stopping rules
+// and the restatement choices are stated once in oracle/oracle.c (solve_primal).  Dense rows in the
+// env's scratch (J, R, aref, frictionloss); lane j < nv holds dof j of every vector (qacc, M qacc,
+// gradient, search direction, M search); row quantities are lane-strided over rows: jar = J qacc -
+// aref in efc_b, J search in efc_ARii, the row state in efc_MJ, forces in efc_f.  Newton builds
+// H = M + J' diag(D of quadratic rows) J row-per-lane into the LDS factor slot and factors it in
+// place (M's factor is not needed again before integrate() refactors); CG preconditions with M's
+// factor.  The broadcast buffer for matrix-vector products is L.qacc (written by forward() after).
+enum { PST_SAT = 0, PST_QUAD = 1, PST_LINNEG = 2, PST_LINPOS = 3 };
+__device__ __forceinline__ int prow_state(bool fric, float R, float fl, float jar) {
+  if (fric) {
+    const float rf = R * fl;
+    return jar <= -rf ? PST_LINNEG : (jar >= rf ? PST_LINPOS : PST_QUAD);
+  }
+  return jar < 0 ? PST_QUAD : PST_SAT;
+}
+__device__ __forceinline__ float prow_cost(int st, float R, float fl, float jar) {
+  return st == PST_QUAD ? 0.5f * jar * jar / R
+                        : (st == PST_LINNEG ? -fl * jar - 0.5f * R * fl * fl
+                                            : (st == PST_LINPOS ? fl * jar - 0.5f * R * fl * fl : 0.0f));
+}
+__device__ __forceinline__ float prow_slope(int st, float R, float fl, float jar) {
+  return st == PST_QUAD ? jar / R : (st == PST_LINNEG ? -fl : (st == PST_LINPOS ? fl : 0.0f));
+}
+
+// dense in-place Cholesky of an nv x nv LDS matrix (lower triangle read and written), lanes over
+// rows; and the solve with its factor (lane j holds b_j / returns x_j).  Blocked mode's Hessian.
+template <int G>
+__device__ void chol_dense(lfloat* A, int nv, int lane) {
+  #pragma unroll 1
+  for (int k = 0; k < nv; ++k) {
+    float t = 0;
+    if (lane >= k && lane < nv) {
+      t = A[lane * nv + k];
+      for (int p = 0; p < k; ++p) t -= A[lane * nv + p] * A[k * nv + p];
+    }
+    const float dk = gbcast<G>(t, k);
+    const float lkk = sqrtf(dk > kMinVal ? dk : kMinVal);
+    if (lane == k) A[k * nv + k] = lkk;
+    else if (lane > k && lane < nv) A[lane * nv + k] = t / lkk;
+    wsync();
+  }
+}
+template <int G>
+__device__ float chol_solve_dense(const lfloat* Lf, float x, int nv, int lane) {
+  x = lane < nv ? x : 0.0f;
+  #pragma unroll 1
+  for (int i = 0; i < nv; ++i) {
+    const float xi = gbcast<G>(x, i) / Lf[i * nv + i];
+    if (lane == i) x = xi;
+    else if (lane > i && lane < nv) x -= Lf[lane * nv + i] * xi;
+  }
+  #pragma unroll 1
+  for (int i = nv - 1; i >= 0; --i) {
+    const float xi = gbcast<G>(x, i) / Lf[i * nv + i];
+    if (lane == i) x = xi;
+    else if (lane < i) x -= Lf[i * nv + lane] * xi;
+  }
+  return x;
+}
+
+template <int G>
+__device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
+  ENV_UNPACK;
+  const int nv = m.nv;
+  const bool dof = lane < nv;
+  const gfloat* J = scr + S.efc_J;
+  const gfloat* type = scr + S.efc_type;
+  const gfloat* floss = scr + S.efc_floss;
+  const gfloat* Rr = scr + S.efc_R;
+  const gfloat* aref = scr + S.efc_aref;
+  gfloat* jar = scr + S.efc_b;
+  gfloat* jv = scr + S.efc_ARii;
+  gfloat* st = scr + S.efc_MJ;
+  gfloat* ff = scr + S.efc_f;
+  lfloat* xb = s + L.qacc;
+  const float scale = m.pgs_scale;
+  const float qs = dof ? s[L.qacc_smooth + lane] : 0.0f;
+  const float fs = dof ? s[L.qfrc_smooth + lane] : 0.0f;
+  auto is_fric = [&](int r) { return (__float_as_int(type[r]) >> 16) == EFC_FRICTION; };
+  // M[lane][k]: dense, or per kinematic tree in blocked mode (zero across trees)
+  const int mytree = G == 64 && dof ? m.dof_tree[lane] : 0;
+  auto mval = [&](int k) {
+    if constexpr (G == 64) return m.dof_tree[k] == mytree ? (float)s[L.M + midx<G>(m, lane, k)] : 0.0f;
+    else return (float)s[L.M + lane * nv + k];
+  };
+  lfloat* H = G == 64 ? s + L.H : s + L.L;
+  // (M x)_lane
+  auto mmul = [&](float x) {
+    if (dof) xb[lane] = x;
+    wsync();
+    float y = 0;
+    if (dof)
+      #pragma unroll 1
+      for (int k = 0; k < nv; ++k) y += mval(k) * xb[k];
+    wsync();
+    return y;
+  };
+  // out[r] = J_r x - shift * aref_r
+  auto jmul = [&](float x, gfloat* out, float shift) {
+    if (dof) xb[lane] = x;
+    wsync();
+    #pragma unroll 1
+    for (int r = lane; r < nefc; r += G) {
+      float v = -shift * aref[r];
+      const gfloat* Jr = J + r * nv;
+      #pragma unroll 1
+      for (int j = 0; j < nv; ++j) v += Jr[j] * xb[j];
+      out[r] = v;
+    }
+    wsync();
+  };
+  // mj_constraintUpdate at the stored jar: row states and forces; returns (J' f)_lane
+  auto update = [&]() {
+    #pragma unroll 1
+    for (int r = lane; r < nefc; r += G) {
+      const float R = Rr[r], fl = floss[r], ja = jar[r];
+      const int stt = prow_state(is_fric(r), R, fl, ja);
+      st[r] = __int_as_float(stt);
+      ff[r] = -prow_slope(stt, R, fl, ja);
+    }
+    wsync();
+    float q = 0;
+    if (dof)
+      #pragma unroll 1
+      for (int r = 0; r < nefc; ++r) q += J[r * nv + lane] * ff[r];
+    return q;
+  };
+  // total cost at x (warm-start selection); leaves J x - aref in jar
+  auto cost_at = [&](float x) {
+    const float mx = mmul(x);
+    jmul(x, jar, 1.0f);
+    float c = 0;
+    #pragma unroll 1
+    for (int r = lane; r < nefc; r += G) {
+      const float R = Rr[r], fl = floss[r], ja = jar[r];
+      c += prow_cost(prow_state(is_fric(r), R, fl, ja), R, fl, ja);
+    }
+    return gsum<G>((dof ? 0.5f * (mx - fs) * (x - qs) : 0.0f) + c);
+  };
+
+  float qa = qs;
+  if (!(m.disableflags & MRS_DSBL_WARMSTART)) {
+    const float xw = dof ? s[L.qacc_ws + lane] : 0.0f;
+    const float c_ws = cost_at(xw), c_sm = cost_at(qs);
+    if (c_ws <= c_sm) qa = xw;
+  }
+  float Ma = mmul(qa);
+  jmul(qa, jar, 1.0f);
+  float qfrc = update();
+  float p = 0, gold = 0, Mgold = 0;
+  #pragma unroll 1
+  for (int iter = 0;; ++iter) {
+    const float grad = dof ? Ma - fs - qfrc : 0.0f;
+    float Mg;
+    if (newton) {
+      // H row `lane` (dense: into the factor slot L.L; blocked: L.H), then factor in place
+      if (dof)
+        #pragma unroll 1
+        for (int k = 0; k < nv; ++k) {
+          float h = mval(k);
+          #pragma unroll 1
+          for (int r = 0; r < nefc; ++r)
+            if (__float_as_int(st[r]) == PST_QUAD) h += J[r * nv + lane] * J[r * nv + k] / Rr[r];
+          H[lane * nv + k] = h;
+        }
+      wsync();
+      if constexpr (G == 64) {
+        chol_dense<G>(H, nv, lane);
+        Mg = chol_solve_dense<G>(H, grad, nv, lane);
+      } else {
+        MRS_CALL(G, cholesky<G>(mp, H, H, lane));
+        MRS_CALL(G, Mg = chol_solve_lanes<G>(mp, H, grad, lane));
+      }
+    } else {
+      MRS_CALL(G, Mg = chol_solve_lanes<G>(mp, s + L.L, grad, lane));
+    }
+    if (iter == 0 || newton) {
+      p = -Mg;
+    } else {
+      // Polak-Ribiere, reset when negative
+      const float num = gsum<G>(grad * (Mg - Mgold)), den = gsum<G>(gold * Mgold);
+      const float beta = fmaxf(0.0f, num / (den > kMinVal ? den : kMinVal));
+      p = -Mg + beta * p;
+    }
+    if (iter >= m.iterations) break;
+    const float Mv = mmul(p);
+    jmul(p, jv, 0.0f);
+    // exact line search: safeguarded Newton on the 1-D piecewise quadratic
+    const float g1 = gsum<G>(p * (Ma - fs)), g2 = gsum<G>(p * Mv), snorm = sqrtf(gsum<G>(p * p));
+    auto ls_eval = [&](float a, float a0, float& d1, float& d2, bool& ch) {
+      float s1 = 0, s2 = 0;
+      bool c = false;
+      #pragma unroll 1
+      for (int r = lane; r < nefc; r += G) {
+        const float v = jv[r];
+        if (v == 0) continue;
+        const bool fr = is_fric(r);
+        const float R = Rr[r], fl = floss[r], j0 = jar[r], ja = j0 + a * v;
+        const int stt = prow_state(fr, R, fl, ja);
+        c |= stt != prow_state(fr, R, fl, j0 + a0 * v);
+        s1 += v * prow_slope(stt, R, fl, ja);
+        if (stt == PST_QUAD) s2 += v * v / R;
+      }
+      d1 = g1 + a * g2 + gsum<G>(s1);
+      d2 = g2 + gsum<G>(s2);
+      ch = gany<G>(c);
+    };
+    float alpha = 0;
+    if (snorm >= kMinVal && g2 > 0) {
+      const float gtol = m.tolerance * m.ls_tolerance * snorm / scale;
+      float d1, d2;
+      bool ch;
+      ls_eval(0.0f, 0.0f, d1, d2, ch);
+      if (d1 < 0) {
+        float a = 0, lo = 0, hi = -1;
+        #pragma unroll 1
+        for (int it = 0; it < m.ls_iterations; ++it) {
+          float an = a - d1 / d2;
+          bool nstep = true;
+          if (hi >= 0 && (an <= lo || an >= hi)) { an = 0.5f * (lo + hi); nstep = false; }
+          float n1, n2;
+          ls_eval(an, a, n1, n2, ch);
+          a = an; d1 = n1; d2 = n2;
+          if (fabsf(d1) < gtol || (nstep && !ch)) break;
+          if (d1 < 0) lo = a; else hi = a;
+        }
+        alpha = a;
+      }
+    }
+    if (alpha == 0) break;
+    // cost decrease of the step from per-row differences; rows move to the new point
+    float dc = 0;
+    bool changed = false;
+    #pragma unroll 1
+    for (int r = lane; r < nefc; r += G) {
+      const bool fr = is_fric(r);
+      const float R = Rr[r], fl = floss[r], j0 = jar[r], j1 = j0 + alpha * jv[r];
+      const int s0 = __float_as_int(st[r]), s1 = prow_state(fr, R, fl, j1);
+      dc += prow_cost(s1, R, fl, j1) - prow_cost(s0, R, fl, j0);
+      changed |= s0 != s1;
+      jar[r] = j1;
+    }
+    const float dcost = alpha * g1 + 0.5f * alpha * alpha * g2 + gsum<G>(dc);
+    changed = gany<G>(changed);
+    qa += alpha * p;
+    Ma += alpha * Mv;
+    gold = grad;
+    Mgold = Mg;
+    wsync();
+    qfrc = update();
+    const float gn = dof ? Ma - fs - qfrc : 0.0f;
+    const float gnorm = sqrtf(gsum<G>(gn * gn));
+    if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance || (newton && !changed)) break;
+  }
+  if (dof) s[L.qfrc_con + lane] = qfrc;
+  wsync();
+  return dof ? qa : 0.0f;
+}
+
 template <int G>
 __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s);
 
@@ -2451,6 +2714,12 @@ template <int G>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) {
+    if (m.solver != MRS_SOL_PGS) {
+      // Newton / CG in blocked mode: dense rows, dense Hessian (solve_primal)
+      float qa;
+      [[clang::noinline]] qa = constraints_dense<G>(ENV_ARGS, ncon, qacc_s);
+      return qa;
+    }
     switch (m.pipe_w) {
       case 8: return constraints_sparse<8>(ENV_ARGS, ncon, qacc_s);
       case 16: return constraints_sparse<16>(ENV_ARGS, ncon, qacc_s);
@@ -2473,7 +2742,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
         const float q = s[L.qpos + m.jnt_qposadr[jid]], mg = m.jnt_margin[jid];
         lim |= (q - m.jnt_range[2 * jid] < mg) | (m.jnt_range[2 * jid + 1] - q < mg);
       }
-    if (ncon == 0 && nf > 0 && nf <= 16 && !gany<G>(lim)) {
+    if (m.solver == MRS_SOL_PGS && ncon == 0 && nf > 0 && nf <= 16 && !gany<G>(lim)) {
       int mydof = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
       if (lane < nf) {
@@ -2643,8 +2912,9 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     wsync();
     return qacc_s;
   }
-  // --- impedance, R, aref, M^-1 J', ARii, b (lane per row)
-  const bool small = G == 16 && nefc <= 16;
+  // --- impedance, R, aref, M^-1 J', ARii, b (lane per row); the primal solvers need R and aref only
+  const bool primal = m.solver != MRS_SOL_PGS;
+  const bool small = G == 16 && nefc <= 16 && !primal;
   float my_R = 1, my_aref = 0, my_b = 0, my_fl = 0;
   #pragma unroll 1
   for (int r = lane; r < nefc; r += G) {
@@ -2662,8 +2932,10 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
       diag = tran;
       if (m.pair_dim[p] == 3) {
-        const float mu = m.pair_friction[3 * p];  // sliding, for both tangent directions
-        diag = tran * (1 + mu * mu);
+        // pyramid edge: diagApprox tran (1 + mu^2) (mu sliding, for both tangent directions);
+        // mj_makeImpedance scales the edges' regulariser by 2 mu^2 / impratio
+        const float mu = m.pair_friction[3 * p];
+        diag = tran * (1 + mu * mu) * (2 * mu * mu / m.impratio);
       }
     }
     const float imp = impedance(si, pos[r], marg[r]);
@@ -2695,6 +2967,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     }
     aref[r] = -B * vel - pterm;
     bb[r] = jqs - aref[r];
+    if (primal) continue;
     // M^-1 J_r'
     gfloat* MJr = MJ + r * nv;
     chol_solve_serial(s + L.L, nv, Jr, MJr);
@@ -2704,6 +2977,11 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     ARii[r] = d + R;
   }
   wsync();
+  if (primal) {
+    float qa;
+    [[clang::noinline]] qa = solve_primal<G>(ENV_ARGS, nefc, m.solver == MRS_SOL_NEWTON);
+    return qa;
+  }
   if constexpr (G == 16) {
     // rows unrolled up to the largest small system among the wave's active groups (wave-uniform
     // bound; binary search with ballots, which only see active lanes)

@@ -422,7 +422,13 @@ struct Compiler {
     }
     if (auto* s = e->attr("iterations")) m.iterations = static_cast<int>(parse_reals(*s, e, "iterations").at(0));
     if (auto* s = e->attr("tolerance")) m.tolerance = parse_reals(*s, e, "tolerance").at(0);
-    if (auto* s = e->attr("impratio")) m.impratio = parse_reals(*s, e, "impratio").at(0);
+    if (auto* s = e->attr("impratio")) {
+      m.impratio = parse_reals(*s, e, "impratio").at(0);
+      if (!(m.impratio > 0)) fail(e, "impratio must be positive");
+    }
+    if (auto* s = e->attr("ls_tolerance")) m.ls_tolerance = parse_reals(*s, e, "ls_tolerance").at(0);
+    if (auto* s = e->attr("ls_iterations"))
+      m.ls_iterations = static_cast<int>(parse_reals(*s, e, "ls_iterations").at(0));
     if (auto* s = e->attr("cone")) {
       if (*s != "pyramidal") fail(e, "only cone=\"pyramidal\" is supported");
     }
@@ -1520,6 +1526,7 @@ mrs_model_view Model::view() const {
   for (int i = 0; i < 3; ++i) { v.gravity[i] = gravity[i]; v.stat_center[i] = stat_center[i]; }
   v.tolerance = tolerance; v.impratio = impratio; v.integrator = integrator; v.solver = solver;
   v.iterations = iterations; v.disableflags = disableflags; v.cone = cone;
+  v.ls_tolerance = ls_tolerance; v.ls_iterations = ls_iterations;
   v.stat_extent = stat_extent; v.stat_meaninertia = stat_meaninertia;
   v.vis_znear = vis_znear; v.vis_zfar = vis_zfar;
 #define MRS_V(f) v.f = f.empty() ? nullptr : f.data()

@@ -14,9 +14,10 @@ struct Model {
   int nq = 0, nv = 0, nu = 0, na = 0, nbody = 0, njnt = 0, ngeom = 0, nsite = 0, ncam = 0,
       nsensor = 0, nsensordata = 0, nkey = 0, max_depth = 0;
 
-  double timestep = 0.002, gravity[3] = {0, 0, -9.81}, tolerance = 1e-8, impratio = 1;
+  double timestep = 0.002, gravity[3] = {0, 0, -9.81}, tolerance = 1e-8, impratio = 1,
+         ls_tolerance = 0.01;
   int integrator = MRS_INT_EULER, solver = MRS_SOL_NEWTON, iterations = 100, disableflags = 0,
-      cone = 0;
+      cone = 0, ls_iterations = 50;
 
   double stat_extent = 0, stat_center[3] = {0, 0, 0}, stat_meaninertia = 1, vis_znear = 0.01,
          vis_zfar = 50;

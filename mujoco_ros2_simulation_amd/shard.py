@@ -15,6 +15,27 @@ def env_ids(rank: int, envs_per_rank: int) -> np.ndarray:
     return rank * envs_per_rank + np.arange(envs_per_rank)
 
 
+def spawn(nprocs: int, argv: list[str]) -> int:
+    """Start `nprocs` ranks of `argv` (a Python command line) as child processes with the torchrun
+    environment (RANK, LOCAL_RANK = GPU index, WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free port) and
+    wait for them; returns the first non-zero exit code (0 if all succeed).  The caller must not have
+    touched the GPU: each child owns one device."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                   LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def init(backend: str | None = None):
     """(rank, world, local_rank) from the torchrun environment; joins the process group when world > 1
     (backend 'nccl' = RCCL when GPUs are used, 'gloo' on CPU)"""

@@ -90,9 +90,9 @@ _ARRAYS = [
 class ModelView(C.Structure):
     _fields_ = ([(n, C.c_int) for n in _SIZES] +
                 [("timestep", C.c_double), ("gravity", C.c_double * 3), ("tolerance", C.c_double),
-                 ("impratio", C.c_double),
+                 ("impratio", C.c_double), ("ls_tolerance", C.c_double),
                  ("integrator", C.c_int), ("solver", C.c_int), ("iterations", C.c_int), ("disableflags", C.c_int),
-                 ("cone", C.c_int),
+                 ("cone", C.c_int), ("ls_iterations", C.c_int),
                  ("stat_extent", C.c_double), ("stat_center", C.c_double * 3), ("stat_meaninertia", C.c_double),
                  ("vis_znear", C.c_double), ("vis_zfar", C.c_double)] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _ARRAYS])
@@ -176,7 +176,8 @@ class Model:
         v = self.view
         for n in _SIZES:
             setattr(self, n, getattr(v, n))
-        for n in ["timestep", "tolerance", "impratio", "integrator", "solver", "iterations", "disableflags",
+        for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "integrator", "solver",
+                  "iterations", "disableflags",
                   "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
             setattr(self, n, getattr(v, n))
         self.gravity = np.array(v.gravity[:])

@@ -47,6 +47,7 @@ def lib():
         L.orc_ray.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P, C.c_int, C.POINTER(C.c_int)]
         L.orc_render_depth.argtypes = [C.c_void_p, C.POINTER(OrcData), C.c_int, C.POINTER(C.c_float)]
         L.orc_contacts.argtypes = [C.POINTER(OrcData), C.c_int, C.POINTER(C.c_int), P, P, P]
+        L.orc_efc.argtypes = [C.POINTER(OrcData), C.c_int, C.c_int, C.POINTER(C.c_int), P, P, P, P, P]
         L.orc_rollout.restype = C.c_double
         L.orc_rollout.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P, P]
         _lib = L
@@ -138,6 +139,17 @@ class OracleData:
         n = lib().orc_contacts(self._d, max_n, g.ctypes.data_as(C.POINTER(C.c_int)), _dp(dist), _dp(pos), _dp(frame))
         n = min(n, max_n)
         return g[:2 * n].reshape(-1, 2), dist[:n], pos[:3 * n].reshape(-1, 3), frame[:9 * n].reshape(-1, 9)
+
+    def efc(self, max_n: int = 1024):
+        """constraint rows of the last forward: dict of type [n], force, aref, R, pos [n], J [n, nv]"""
+        nv = self.model.nv
+        t = np.zeros(max_n, dtype=np.int32)
+        f, a, R, p = (np.zeros(max_n) for _ in range(4))
+        J = np.zeros(max_n * max(nv, 1))
+        n = lib().orc_efc(self._d, nv, max_n, t.ctypes.data_as(C.POINTER(C.c_int)), _dp(f), _dp(a), _dp(R), _dp(p), _dp(J))
+        n = min(n, max_n)
+        return {"type": t[:n], "force": f[:n], "aref": a[:n], "R": R[:n], "pos": p[:n],
+                "J": J[:n * nv].reshape(n, nv)}
 
     def __del__(self):
         if getattr(self, "_d", None) and _lib is not None:

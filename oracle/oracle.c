@@ -12,6 +12,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -42,7 +43,9 @@ typedef struct {
   double *efc_J, *efc_MinvJT;
   double efc_pos[MAXEFC], efc_margin[MAXEFC], efc_frictionloss[MAXEFC], efc_diag[MAXEFC],
       efc_R[MAXEFC], efc_D[MAXEFC], efc_aref[MAXEFC], efc_b[MAXEFC], efc_force[MAXEFC],
-      efc_vel[MAXEFC], efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5], efc_KBIP[MAXEFC][4];
+      efc_vel[MAXEFC], efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5], efc_KBIP[MAXEFC][4],
+      efc_rscale[MAXEFC], efc_jar[MAXEFC], efc_jv[MAXEFC];
+  int efc_state[MAXEFC];
   double* AR;
   orc_contact con[MAXCON];
 } orc_ws;
@@ -974,6 +977,7 @@ static void add_row(orc_ws* w, int nv, int type, int id, const double* J, double
   w->efc_type[r] = type; w->efc_id[r] = id;
   w->efc_pos[r] = pos; w->efc_margin[r] = margin; w->efc_frictionloss[r] = floss;
   w->efc_diag[r] = diag;
+  w->efc_rscale[r] = 1;
   memcpy(w->efc_solref[r], solref, 2 * sizeof(double));
   memcpy(w->efc_solimp[r], solimp, 5 * sizeof(double));
 }
@@ -1026,13 +1030,20 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
     if (con->dim == 1) {
       add_row(w, nv, EFC_CONTACT, c, Jc, con->dist, con->includemargin, 0, tran, con->solref, con->solimp);
     } else {
+      /* pyramid edges J_n +/- mu J_tk.  diagApprox of an edge is tran (1 + mu^2) [upstream
+       * mj_diagApprox]; mj_makeImpedance then gives every edge of the pyramid the regulariser
+       * R_py = 2 mu^2 R / impratio, which matches the elliptic cone's frictional regulariser
+       * R_t = R_n / impratio on the tangent components (two edges per direction, each carrying half
+       * the normal load): rscale below */
+      const double mu = con->friction[0];
       for (int k = 1; k < 3; ++k)
         for (int s = 1; s >= -1; s -= 2) {
           /* both tangent directions use the sliding coefficient: a contact's friction is
            * (slide, slide, spin, roll, roll) from the geoms' (slide, spin, roll) [upstream mj_setContact] */
-          for (int j = 0; j < nv; ++j) J[j] = Jc[j] + s * con->friction[0] * Jc[k * nv + j];
+          for (int j = 0; j < nv; ++j) J[j] = Jc[j] + s * mu * Jc[k * nv + j];
           add_row(w, nv, EFC_CONTACT, c, J, con->dist, con->includemargin, 0,
-                  tran * (1 + con->friction[0] * con->friction[0]), con->solref, con->solimp);
+                  tran * (1 + mu * mu), con->solref, con->solimp);
+          if (w->nefc > 0) w->efc_rscale[w->nefc - 1] = 2 * mu * mu / m->impratio;
         }
     }
     free(Jc);
@@ -1042,7 +1053,7 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
   for (int r = 0; r < w->nefc; ++r) {
     const double* sr = w->efc_solref[r];
     double imp = impedance(w->efc_solimp[r], w->efc_pos[r], w->efc_margin[r]);
-    double R = (1 - imp) * w->efc_diag[r] / imp;
+    double R = (1 - imp) * w->efc_diag[r] * w->efc_rscale[r] / imp;
     w->efc_R[r] = R > MINVAL ? R : MINVAL;
     w->efc_D[r] = 1 / w->efc_R[r];
     double K, B;
@@ -1078,6 +1089,223 @@ static double row_force(orc_ws* w, int r, double jar) {
   return jar < 0 ? -D * jar : 0;
 }
 
+/* ---- primal solvers: mj_solNewton / mj_solCG [upstream engine_solver.c, mj_solPrimal].
+ * Both minimise over qacc the convex cost
+ *   F(qacc) = 1/2 (qacc - qacc_smooth)' M (qacc - qacc_smooth) + sum_r s_r(J_r qacc - aref_r)
+ * with the soft-constraint row costs of mj_constraintUpdate (s_r on jar = J_r qacc - aref_r):
+ *   limit / contact rows: 1/2 D jar^2 when jar < 0, else 0;
+ *   friction-loss rows:   1/2 D jar^2 inside |jar| < R floss, linear floss |jar| - 1/2 R floss^2 outside.
+ * Newton: search = -H^-1 grad with H = M + J' diag(D of quadratic rows) J (mj_solNewton's Hessian;
+ * upstream updates its factor incrementally, the matrix is the same); CG: Polak-Ribiere with the
+ * M^-1 preconditioner.  Exact line search along the search direction: safeguarded 1-D Newton on
+ * the piecewise-quadratic F(qacc + a p) (upstream PrimalLinesearch brackets with Newton steps to
+ * |dF/da| < tolerance * ls_tolerance * |p| / scale).  Stops on scale * (cost decrease) < tolerance,
+ * scale * |grad| < tolerance, a zero step, `iterations`, or (Newton) a step that left every row's
+ * state unchanged -- the quadratic model was then exact and the point is the minimiser.
+ * Restatement choices: the line search's stopping point, the exact-step stop, and the
+ * cost decrease summed from per-row differences.  At convergence all of these reach the unique
+ * minimiser of F, which is what mj_solNewton returns to within its tolerance. */
+enum { ST_SAT = 0, ST_QUAD = 1, ST_LINNEG = 2, ST_LINPOS = 3 };
+
+static int row_state(const orc_ws* w, int r, double jar) {
+  if (w->efc_type[r] == EFC_FRICTION) {
+    double rf = w->efc_R[r] * w->efc_frictionloss[r];
+    return jar <= -rf ? ST_LINNEG : (jar >= rf ? ST_LINPOS : ST_QUAD);
+  }
+  return jar < 0 ? ST_QUAD : ST_SAT;
+}
+static double row_cost(const orc_ws* w, int r, double jar, int st) {
+  double fl = w->efc_frictionloss[r];
+  switch (st) {
+    case ST_QUAD: return 0.5 * w->efc_D[r] * jar * jar;
+    case ST_LINNEG: return -fl * jar - 0.5 * w->efc_R[r] * fl * fl;
+    case ST_LINPOS: return fl * jar - 0.5 * w->efc_R[r] * fl * fl;
+  }
+  return 0;
+}
+/* d cost / d jar */
+static double row_slope(const orc_ws* w, int r, double jar, int st) {
+  double fl = w->efc_frictionloss[r];
+  return st == ST_QUAD ? w->efc_D[r] * jar : (st == ST_LINNEG ? -fl : (st == ST_LINPOS ? fl : 0));
+}
+
+static void mat_vec_n(double* y, const double* A, const double* x, int n) {
+  for (int i = 0; i < n; ++i) {
+    double v = 0;
+    for (int k = 0; k < n; ++k) v += A[i * n + k] * x[k];
+    y[i] = v;
+  }
+}
+
+/* constraint update at the rows' current jar: states, forces, qfrc_constraint; returns row cost */
+static double primal_update(const mrs_model_view* m, orc_ws* w) {
+  int nv = m->nv, nefc = w->nefc;
+  double cost = 0;
+  for (int r = 0; r < nefc; ++r) {
+    int st = row_state(w, r, w->efc_jar[r]);
+    w->efc_state[r] = st;
+    cost += row_cost(w, r, w->efc_jar[r], st);
+    w->efc_force[r] = -row_slope(w, r, w->efc_jar[r], st);
+  }
+  for (int j = 0; j < nv; ++j) {
+    double v = 0;
+    for (int r = 0; r < nefc; ++r) v += w->efc_J[(size_t)r * nv + j] * w->efc_force[r];
+    w->qfrc_constraint[j] = v;
+  }
+  return cost;
+}
+
+/* total cost at qacc x (warm-start selection) */
+static double primal_cost_at(const mrs_model_view* m, orc_ws* w, const double* x, double* Mx) {
+  int nv = m->nv;
+  mat_vec_n(Mx, w->M, x, nv);
+  double gauss = 0;
+  for (int j = 0; j < nv; ++j) gauss += 0.5 * (Mx[j] - w->qfrc_smooth[j]) * (x[j] - w->qacc_smooth[j]);
+  double c = 0;
+  for (int r = 0; r < w->nefc; ++r) {
+    double jar = -w->efc_aref[r];
+    for (int j = 0; j < nv; ++j) jar += w->efc_J[(size_t)r * nv + j] * x[j];
+    c += row_cost(w, r, jar, row_state(w, r, jar));
+  }
+  return gauss + c;
+}
+
+/* 1-D derivatives of F(qacc + a p) at step a; *changed: some row's state differs from step `a0` */
+static void ls_eval(const orc_ws* w, double g1, double g2, double a, double a0, double* d1, double* d2,
+                    int* changed) {
+  double s1 = g1 + a * g2, s2 = g2;
+  int ch = 0;
+  for (int r = 0; r < w->nefc; ++r) {
+    double jv = w->efc_jv[r];
+    if (jv == 0) continue;
+    double jar = w->efc_jar[r] + a * jv;
+    int st = row_state(w, r, jar);
+    ch |= st != row_state(w, r, w->efc_jar[r] + a0 * jv);
+    s1 += jv * row_slope(w, r, jar, st);
+    if (st == ST_QUAD) s2 += w->efc_D[r] * jv * jv;
+  }
+  *d1 = s1; *d2 = s2; *changed = ch;
+}
+
+static double primal_linesearch(const mrs_model_view* m, const orc_ws* w, const double* p, const double* Mv,
+                                const double* Ma, double scale) {
+  int nv = m->nv;
+  double snorm = 0, g1 = 0, g2 = 0;
+  for (int j = 0; j < nv; ++j) {
+    snorm += p[j] * p[j];
+    g1 += p[j] * (Ma[j] - w->qfrc_smooth[j]);
+    g2 += p[j] * Mv[j];
+  }
+  snorm = sqrt(snorm);
+  if (snorm < MINVAL || g2 <= 0) return 0;
+  double gtol = m->tolerance * m->ls_tolerance * snorm / scale;
+  double a = 0, d1, d2;
+  int ch;
+  ls_eval(w, g1, g2, 0, 0, &d1, &d2, &ch);
+  if (d1 >= 0) return 0; /* not a descent direction */
+  double lo = 0, hi = -1; /* bracket: F'(lo) < 0 < F'(hi) once hi >= 0 */
+  for (int it = 0; it < m->ls_iterations; ++it) {
+    double an = a - d1 / d2;
+    int newton = 1;
+    if (hi >= 0 && (an <= lo || an >= hi)) { an = 0.5 * (lo + hi); newton = 0; }
+    double n1, n2;
+    ls_eval(w, g1, g2, an, a, &n1, &n2, &ch);
+    a = an; d1 = n1; d2 = n2;
+    if (fabs(d1) < gtol || (newton && !ch)) break;
+    if (d1 < 0) lo = a; else hi = a;
+  }
+  return a;
+}
+
+static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
+  orc_ws* w = (orc_ws*)d->ws;
+  int nv = m->nv, nefc = w->nefc;
+  double scale = 1 / (m->stat_meaninertia * (nv > 1 ? nv : 1));
+  size_t vb = (nv ? nv : 1) * sizeof(double);
+  double *Ma = malloc(vb), *grad = malloc(vb), *Mgrad = malloc(vb), *p = malloc(vb), *Mv = malloc(vb),
+         *gold = malloc(vb), *Mgold = malloc(vb), *x2 = malloc(vb);
+  double *H = malloc((size_t)nv * nv * sizeof(double) + 8), *HL = malloc((size_t)nv * nv * sizeof(double) + 8);
+  double* qacc = d->qacc;
+  memcpy(qacc, w->qacc_smooth, vb);
+  if (!(m->disableflags & MRS_DSBL_WARMSTART)) {
+    /* mj_fwdConstraint: start from qacc_warmstart when its cost is not above qacc_smooth's */
+    double c_ws = primal_cost_at(m, w, d->qacc_warmstart, x2);
+    double c_sm = primal_cost_at(m, w, w->qacc_smooth, x2);
+    if (c_ws <= c_sm) memcpy(qacc, d->qacc_warmstart, vb);
+  }
+  mat_vec_n(Ma, w->M, qacc, nv);
+  for (int r = 0; r < nefc; ++r) {
+    double jar = -w->efc_aref[r];
+    for (int j = 0; j < nv; ++j) jar += w->efc_J[(size_t)r * nv + j] * qacc[j];
+    w->efc_jar[r] = jar;
+  }
+  primal_update(m, w);
+  int iter = 0;
+  for (;;) {
+    /* gradient and preconditioned gradient */
+    for (int j = 0; j < nv; ++j) grad[j] = Ma[j] - w->qfrc_smooth[j] - w->qfrc_constraint[j];
+    if (newton) {
+      memcpy(H, w->M, (size_t)nv * nv * sizeof(double));
+      for (int r = 0; r < nefc; ++r) {
+        if (w->efc_state[r] != ST_QUAD) continue;
+        const double* Jr = w->efc_J + (size_t)r * nv;
+        for (int i = 0; i < nv; ++i)
+          for (int k = 0; k < nv; ++k) H[i * nv + k] += w->efc_D[r] * Jr[i] * Jr[k];
+      }
+      cholesky(H, HL, nv);
+      chol_solve(HL, Mgrad, grad, nv);
+    } else {
+      chol_solve(w->L, Mgrad, grad, nv);
+    }
+    if (iter == 0) {
+      for (int j = 0; j < nv; ++j) p[j] = -Mgrad[j];
+    } else if (newton) {
+      for (int j = 0; j < nv; ++j) p[j] = -Mgrad[j];
+    } else {
+      double num = 0, den = 0;
+      for (int j = 0; j < nv; ++j) { num += grad[j] * (Mgrad[j] - Mgold[j]); den += gold[j] * Mgold[j]; }
+      double beta = num / (den > MINVAL ? den : MINVAL);
+      if (beta < 0) beta = 0;
+      for (int j = 0; j < nv; ++j) p[j] = -Mgrad[j] + beta * p[j];
+    }
+    if (iter >= m->iterations) break;
+    /* line search along p */
+    mat_vec_n(Mv, w->M, p, nv);
+    for (int r = 0; r < nefc; ++r) {
+      double v = 0;
+      for (int j = 0; j < nv; ++j) v += w->efc_J[(size_t)r * nv + j] * p[j];
+      w->efc_jv[r] = v;
+    }
+    double alpha = primal_linesearch(m, w, p, Mv, Ma, scale);
+    if (alpha == 0) break;
+    /* cost decrease of the step, summed from per-row differences (exact in the 1-D model) */
+    double g1 = 0, g2 = 0;
+    for (int j = 0; j < nv; ++j) { g1 += p[j] * (Ma[j] - w->qfrc_smooth[j]); g2 += p[j] * Mv[j]; }
+    double dcost = alpha * g1 + 0.5 * alpha * alpha * g2;
+    int changed = 0;
+    for (int r = 0; r < nefc; ++r) {
+      double j0 = w->efc_jar[r], j1 = j0 + alpha * w->efc_jv[r];
+      int s0 = w->efc_state[r], s1 = row_state(w, r, j1);
+      dcost += row_cost(w, r, j1, s1) - row_cost(w, r, j0, s0);
+      changed |= s0 != s1;
+      w->efc_jar[r] = j1;
+    }
+    for (int j = 0; j < nv; ++j) { qacc[j] += alpha * p[j]; Ma[j] += alpha * Mv[j]; }
+    memcpy(gold, grad, vb);
+    memcpy(Mgold, Mgrad, vb);
+    primal_update(m, w);
+    ++iter;
+    double gnorm = 0;
+    for (int j = 0; j < nv; ++j) {
+      double g = Ma[j] - w->qfrc_smooth[j] - w->qfrc_constraint[j];
+      gnorm += g * g;
+    }
+    if (scale * -dcost < m->tolerance || scale * sqrt(gnorm) < m->tolerance || (newton && !changed)) break;
+  }
+  d->solver_niter = iter;
+  free(Ma); free(grad); free(Mgrad); free(p); free(Mv); free(gold); free(Mgold); free(x2); free(H); free(HL);
+}
+
 /* mj_solPGS [upstream engine_solver.c] on the dual problem
  *   min 0.5 f'AR f + f'b,  AR = J M^-1 J' + diag(R),  b = J qacc_smooth - aref,
  * friction rows boxed to [-frictionloss, frictionloss], limit/contact rows f >= 0; warm start from
@@ -1089,6 +1317,10 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
   if (nefc == 0) {
     memcpy(d->qacc, w->qacc_smooth, nv * sizeof(double));
     memset(w->qfrc_constraint, 0, nv * sizeof(double));
+    return;
+  }
+  if (m->solver != MRS_SOL_PGS) {
+    solve_primal(m, d, m->solver == MRS_SOL_NEWTON);
     return;
   }
   /* M^-1 J' */
@@ -1632,7 +1864,7 @@ void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out)
 /* ------------------------------------------------------------------------ CPU baseline */
 typedef struct {
   const mrs_model_view* m;
-  int env0, env1, n_steps, period, n_envs;
+  int env0, env1, n_steps, period, n_envs, cpu;
   const double *ctrl_table, *qpos_init;
   double *qpos_out, *qvel_out;
 } rollout_job;
@@ -1640,6 +1872,12 @@ typedef struct {
 static void* rollout_worker(void* arg) {
   rollout_job* j = (rollout_job*)arg;
   const mrs_model_view* m = j->m;
+  if (j->cpu >= 0) { /* one worker per allowed CPU, pinned */
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(j->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+  }
   orc_data* d = orc_make_data(m);
   for (int e = j->env0; e < j->env1; ++e) {
     orc_reset(m, d, -1);
@@ -1664,10 +1902,18 @@ double orc_rollout(const mrs_model_view* m, int n_envs, int n_steps, int period,
   pthread_t th[256];
   rollout_job jobs[256];
   if (n_threads > 256) n_threads = 256;
+  /* the CPUs this process may run on, in order: worker i is pinned to the i-th of them when there
+   * are at least as many CPUs as workers */
+  int cpus[256], ncpu = 0;
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof allowed, &allowed) == 0)
+    for (int c = 0; c < CPU_SETSIZE && ncpu < 256; ++c)
+      if (CPU_ISSET(c, &allowed)) cpus[ncpu++] = c;
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   for (int i = 0; i < n_threads; ++i) {
     rollout_job* j = &jobs[i];
+    j->cpu = ncpu >= n_threads ? cpus[i] : -1;
     j->m = m; j->n_steps = n_steps; j->period = period > 0 ? period : 1; j->n_envs = n_envs;
     j->ctrl_table = ctrl_table; j->qpos_init = qpos_init; j->qpos_out = qpos_out; j->qvel_out = qvel_out;
     j->env0 = (int)((long)n_envs * i / n_threads);

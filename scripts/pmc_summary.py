@@ -30,7 +30,7 @@ def per_launch(name: str) -> tuple[float, str, int]:
 
 fetch_kib, kname, n1 = per_launch("fetch")
 write_kib, _, n2 = per_launch("write")
-steps = 200 if CFG == "c4" else 5  # C4: the bench line's own command (20 depth frames)
+steps = 200 if CFG == "c4" else 5  # C4: 20 depth frames
 rec = {
     "kernel": kname,
     "config": CFG,

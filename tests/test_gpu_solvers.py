@@ -1,0 +1,139 @@
+"""GPU parity of the constraint solvers (mj_fwdConstraint) and step-wise
+re-seeded parity of the contact configs ("step-wise re-seeding from the oracle for
+config C5").
+
+* Newton (MuJoCo's default solver) and CG: the HIP primal solvers (step.hip solve_primal) against
+  the oracle's (oracle.c solve_primal) on contact scenes, dense lane-group mode and blocked mode.
+* Re-seeded: every step the GPU state is overwritten with the oracle's fp64 state (qpos, qvel,
+  qacc_warmstart, ctrl), one step runs on both, and qpos/qvel are compared at 1e-5 of scale -- a
+  per-step bound that chaotic divergence of long contact rollouts cannot hide.
+Tolerance: |gpu - cpu| <= 1e-5 * max(|cpu|, 1) (north_star).
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import ARM7
+from mujoco_ros2_simulation_amd import sim, synth
+import binding
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+SCENES = ARM7.parent
+MOBILE = SCENES / "mobile_base.xml"
+ARM_BOXES = SCENES / "arm_boxes.xml"
+
+
+def with_solver(path: Path, solver: str, iterations: int = 100) -> "sim.Model":
+    xml = path.read_text().replace('solver="PGS" iterations="50"', f'solver="{solver}" iterations="{iterations}"')
+    assert f'solver="{solver}"' in xml
+    return sim.Model.from_string(xml, str(path.parent))
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1.0)))
+
+
+def _rollout_both(model, n, steps, period=10):
+    envs = np.arange(n)
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    b = sim.Batch(model, n)
+    b.set(sim.FIELD_QPOS, qpos0)
+    for t in range(0, steps, period):
+        b.set(sim.FIELD_CTRL, table[t // period])
+        b.step(period)
+    q, v = b.get(sim.FIELD_QPOS), b.get(sim.FIELD_QVEL)
+    layout = b.layout()
+    b.close()
+    qr, vr, iters = np.zeros_like(q), np.zeros_like(v), []
+    for e in range(n):
+        d = binding.OracleData(model)
+        d.qpos[:] = qpos0[e]
+        for t in range(steps):
+            if t % period == 0:
+                d.ctrl[:] = table[t // period, e]
+            d.step()
+            iters.append(d.solver_niter)
+        qr[e], vr[e] = d.qpos, d.qvel
+    return q, v, qr, vr, layout, iters
+
+
+@pytest.mark.parametrize("solver", ["Newton", "CG"])
+@pytest.mark.parametrize("group", [16, 32, 64])
+def test_primal_solver_mobile_base(solver, group, monkeypatch):
+    """C4's mobile base (wheel-floor contacts, pyramidal friction) under Newton / CG, 300 steps"""
+    monkeypatch.setenv("MRS_GROUP", str(group))
+    model = with_solver(MOBILE, solver)
+    q, v, qr, vr, layout, iters = _rollout_both(model, 8, 300)
+    assert layout["group"] == group and layout["blocked"] == (group == 64)
+    eq, ev = _rel(q, qr), _rel(v, vr)
+    print(f"{solver} G={group}: qpos {eq:.2e} qvel {ev:.2e}, oracle iterations mean {np.mean(iters):.1f}")
+    assert eq <= RTOL and ev <= RTOL
+
+
+def test_newton_contact_rich_blocked(monkeypatch):
+    """C5's arm + 8 free boxes (nv = 55, blocked mode, ~135 rows) under Newton, 100 steps at 1e-5:
+    Newton converges where 50 PGS sweeps do not, so fp32 and fp64 stay together"""
+    model = with_solver(ARM_BOXES, "Newton")
+    q, v, qr, vr, layout, iters = _rollout_both(model, 4, 100)
+    assert layout["blocked"] == 1
+    eq, ev = _rel(q, qr), _rel(v, vr)
+    print(f"arm_boxes Newton: qpos {eq:.2e} qvel {ev:.2e}, oracle iterations mean {np.mean(iters):.1f}")
+    assert eq <= RTOL and ev <= RTOL
+
+
+def test_newton_is_default_and_reference_scene_pin():
+    """no <option solver>: Newton (mjOption default); the reference scene (test_robot.xml, no solver
+    attribute) tracks [0.5, -0.5] within 0.05 rad after 2 s (test/src/robot_launch_test.py:112-132)"""
+    from conftest import REF_SCENE
+    model = sim.Model.load(REF_SCENE)
+    assert model.solver == 2
+    b = sim.Batch(model, 4)
+    b.set(sim.FIELD_CTRL, np.tile([0.5, -0.5], (4, 1)))
+    b.step(1000)
+    q = b.get(sim.FIELD_QPOS)
+    assert np.all(np.abs(q[:, 0] - 0.5) < 0.05) and np.all(np.abs(q[:, 1] + 0.5) < 0.05)
+
+
+def _reseeded(model, n, steps, period=10, group=None):
+    """max per-step relative error of qpos/qvel when every GPU step starts from the oracle's state"""
+    envs = np.arange(n)
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    orc = [binding.OracleData(model) for _ in envs]
+    for e, d in enumerate(orc):
+        d.qpos[:] = qpos0[e]
+    b = sim.Batch(model, n)
+    worst_q = worst_v = 0.0
+    ncon = []
+    for t in range(steps):
+        for e, d in enumerate(orc):
+            if t % period == 0:
+                d.ctrl[:] = table[t // period, e]
+        b.set(sim.FIELD_QPOS, np.array([d.qpos for d in orc]))
+        b.set(sim.FIELD_QVEL, np.array([d.qvel for d in orc]))
+        b.set(sim.FIELD_QACC_WARMSTART, np.array([d.qacc_warmstart for d in orc]))
+        b.set(sim.FIELD_CTRL, np.array([d.ctrl for d in orc]))
+        b.step(1)
+        for d in orc:
+            d.step()
+        q, v = b.get(sim.FIELD_QPOS), b.get(sim.FIELD_QVEL)
+        qr, vr = np.array([d.qpos for d in orc]), np.array([d.qvel for d in orc])
+        worst_q, worst_v = max(worst_q, _rel(q, qr)), max(worst_v, _rel(v, vr))
+        ncon.append([d.ncon for d in orc])
+    b.close()
+    return worst_q, worst_v, np.array(ncon)
+
+
+@pytest.mark.parametrize("scene, n, steps", [("arm_boxes", 64, 200), ("mobile_base", 64, 200)])
+def test_reseeded_step_parity(scene, n, steps):
+    """C5 (arm + 8 boxes, PGS 50 iterations, blocked mode) and C4 (mobile base): 64 envs, every one
+    of 200 steps from the oracle's state, qpos/qvel within 1e-5 of scale"""
+    model = sim.Model.load(SCENES / f"{scene}.xml")
+    wq, wv, ncon = _reseeded(model, n, steps)
+    print(f"{scene}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts per env {ncon.mean():.1f}")
+    assert ncon.max() > 0
+    assert wq <= RTOL and wv <= RTOL

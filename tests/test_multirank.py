@@ -101,3 +101,42 @@ def test_env_ids_partition():
     from mujoco_ros2_simulation_amd import shard
     ids = np.concatenate([shard.env_ids(r, 5) for r in range(4)])
     assert np.array_equal(ids, np.arange(20))
+
+
+def test_spawn_and_obs_gather(tmp_path, built):
+    """the launcher of `bench.py --gpus N` (shard.spawn: N child ranks with the torchrun environment)
+    at world size 2 on gloo, with the per-period observation gather (shard.ObsGather) that bench.py
+    times for N > 1: rank 0 holds every env's (qpos, qvel) of every period, equal to one process
+    stepping all envs"""
+    sys.path.insert(0, str(ROOT / "tests" / "fixtures"))
+    import mr_worker
+    from mujoco_ros2_simulation_amd import shard, sim, synth
+    import binding
+    out = tmp_path / "rows.npy"
+    rc = shard.spawn(2, [str(ROOT / "tests" / "fixtures" / "mr_worker.py"), str(out)])
+    assert rc == 0
+    got = np.load(out)
+    n = 2 * mr_worker.PER_RANK
+    m = sim.Model.load(REF_SCENE)
+    ids = np.arange(n)
+    q0 = synth.initial_qpos(m, ids)
+    tab = synth.ctrl_table(m, ids, mr_worker.PERIODS, mr_worker.PERIOD)
+    envs = [binding.OracleData(m) for _ in ids]
+    for e, d in enumerate(envs):
+        d.qpos[:] = q0[e]
+    assert got.shape[0] == mr_worker.PERIODS
+    for p in range(mr_worker.PERIODS):
+        for e, d in enumerate(envs):
+            d.ctrl[:] = tab[p, e]
+            d.step(mr_worker.PERIOD)
+        want = np.array([np.concatenate([d.qpos, d.qvel]) for d in envs]).astype(np.float32)
+        assert np.array_equal(got[p], want), p
+
+
+def test_bench_rejects_mismatched_world():
+    """bench.py fails loudly when --gpus disagrees with a torchrun WORLD_SIZE"""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "does not match WORLD_SIZE=3" in r.stderr
