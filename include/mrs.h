@@ -44,7 +44,8 @@ enum {
   MRS_FIELD_TIME = 8,          /* 1,   fp64 */
   MRS_FIELD_WARNING = 9,       /* 4,   int32: counts of bad qpos, bad qvel, bad qacc, last info */
   MRS_FIELD_NCON = 10,         /* 1,   int32: contacts found in the last step (output) */
-  MRS_FIELD_COUNT = 11
+  MRS_FIELD_SOLVER_NITER = 11, /* 1,   int32: constraint solver iterations of the last step (mjData.solver_niter) */
+  MRS_FIELD_COUNT = 12
 };
 
 /* last error message of the calling thread ("" if none) */
@@ -114,6 +115,14 @@ int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float*
  * any output pointer may be NULL.  Returns ncon (which may exceed `max`) or a negative error code. */
 int mrs_batch_get_contacts(mrs_batch* b, int env, int max, int* geom, double* dist, double* pos,
                            double* frame);
+/* mjData.efc_* of env `env` after its last step / forward (the rows mj_makeConstraint built and the
+ * solver's forces): up to `max` rows in mj_makeConstraint's order --
+ * type [max] int32 (1 friction loss, 2 joint limit, 3 contact), J [max][nv], R [max], aref [max],
+ * force [max] fp64; any output pointer may be NULL.  Returns nefc (which may exceed `max`), or
+ * MRS_ERR_UNSUPPORTED for the layouts that keep no dense rows (the register friction-loss path of
+ * models without contacts or active limits, and PGS in blocked mode, whose rows are sparse). */
+int mrs_batch_get_efc(mrs_batch* b, int env, int max, int* type, double* J, double* R, double* aref,
+                      double* force);
 /* fp32 state field rows of envs [env0, env0+n) into a device buffer [n][dim], asynchronous on the
  * batch stream (observations for the end-of-step gather stay in HBM; no reference counterpart: the
  * reference copies mjData on the host, src/mujoco_system_interface.cpp:1759) */

@@ -210,6 +210,16 @@ int mrs_batch_get_contacts(mrs_batch* b, int env, int max, int* geom, double* di
   return rc == MRS_OK ? ncon : rc;
 }
 
+int mrs_batch_get_efc(mrs_batch* b, int env, int max, int* type, double* J, double* R, double* aref,
+                      double* force) {
+  int nefc = 0;
+  const int rc = guarded([&] {
+    if (!b) throw std::invalid_argument("null batch");
+    nefc = mrs::batch_get_efc(b->impl, env, max, type, J, R, aref, force);
+  });
+  return rc == MRS_OK ? nefc : rc;
+}
+
 int mrs_batch_get_field_device(mrs_batch* b, int field, float* d_out, int env0, int n) {
   return guarded([&] {
     if (!b || !d_out) throw std::invalid_argument("null argument");

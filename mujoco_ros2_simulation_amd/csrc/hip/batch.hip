@@ -595,9 +595,13 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nfric = static_cast<int>(fric.size());
   d.nlim = static_cast<int>(lim.size());
   d.nrf = static_cast<int>(rf.size());
-  // contact capacity per env: requested, or (<= 0) four per candidate pair clamped to [32, 128]
-  const int cap = max_con_req > 0 ? max_con_req : std::min(128, std::max(32, 4 * d.npair));
-  d.max_con = d.npair == 0 ? 0 : std::min(4 * d.npair, cap);
+  // contact capacity per env: requested, or (<= 0) the pairs' own maxima (8 for box-box, 4 for the
+  // other primitive pairs) clamped to [32, 128]
+  int pair_max = 0;
+  for (size_t p = 0; p < pg1.size(); ++p)
+    pair_max += m.geom_type[pg1[p]] == MRS_GEOM_BOX && m.geom_type[pg2[p]] == MRS_GEOM_BOX ? kMaxPairCon : 4;
+  const int cap = max_con_req > 0 ? max_con_req : std::min(128, std::max(32, pair_max));
+  d.max_con = d.npair == 0 ? 0 : std::min(pair_max, cap);
   d.max_efc = d.nfric + 2 * d.nlim + 4 * d.max_con;
   // actuators
   std::vector<int> act_dof, act_qadr;
@@ -808,6 +812,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
     L.qacc = take(nv + 1); L.qfrc_con = take(nv + 1);  // + a dummy word (blocked-mode solver)
     L.act_force = take(std::max(1, m.nu));
+    L.niter = take(1);
     L.rfmask = take(std::max(1, d.nrfblk));
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
     // primal solvers in blocked mode: H = M + J'DJ couples the trees a contact joins, so it is
@@ -856,7 +861,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_item = take(d.blocked ? ne : 0);
   S.efc_fq = take(d.blocked ? ne : 0);
   S.efc_hdr = take(d.blocked ? 8 * ne : 0);
-  S.stage = take(d.npair > 0 ? 64 * 4 * 7 : 0);  // <= 64 lanes x 4 contacts x 7 floats
+  S.stage = take(d.npair > 0 ? 64 * kMaxPairCon * 7 : 0);  // <= 64 lanes x 8 contacts x 7 floats
+  S.efc_n = take(1);
   S.sens = take(std::max(1, m.nsensordata));
   S.total = off;
   b.d_dm = static_cast<DevModel*>(dalloc(b, sizeof(DevModel)));
@@ -874,6 +880,7 @@ int field_dim(const Model& m, int field) {
     case MRS_FIELD_TIME: return 1;
     case MRS_FIELD_WARNING: return 4;
     case MRS_FIELD_NCON: return 1;
+    case MRS_FIELD_SOLVER_NITER: return 1;
   }
   return -1;
 }
@@ -890,6 +897,7 @@ void* field_ptr(BatchImpl& b, int field) {
     case MRS_FIELD_TIME: return b.st.time;
     case MRS_FIELD_WARNING: return b.st.warning;
     case MRS_FIELD_NCON: return b.st.ncon;
+    case MRS_FIELD_SOLVER_NITER: return b.st.niter;
   }
   return nullptr;
 }
@@ -924,6 +932,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     b->st.time = static_cast<double*>(dalloc(*b, n * sizeof(double)));
     b->st.warning = static_cast<int*>(dalloc(*b, n * 4 * sizeof(int)));
     b->st.ncon = static_cast<int*>(dalloc(*b, n * sizeof(int)));
+    b->st.niter = static_cast<int*>(dalloc(*b, n * sizeof(int)));
     // padded to whole workgroups of the chosen group width: idle groups use it
     const size_t epb = static_cast<size_t>(envs_per_block(b->group));
     const size_t n_pad = (static_cast<size_t>(n) + epb - 1) / epb * epb;
@@ -1008,7 +1017,7 @@ void batch_set(BatchImpl* b, int field, const double* host, int env0, int n) {
   char* dst = static_cast<char*>(field_ptr(*b, field));
   if (field == MRS_FIELD_TIME) {
     HIP_CHECK(hipMemcpyAsync(dst + sizeof(double) * env0, host, cnt * sizeof(double), hipMemcpyHostToDevice, b->stream));
-  } else if (field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON) {
+  } else if (field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON || field == MRS_FIELD_SOLVER_NITER) {
     std::vector<int> tmp(cnt);
     for (size_t i = 0; i < cnt; ++i) tmp[i] = static_cast<int>(host[i]);
     HIP_CHECK(hipMemcpyAsync(dst + sizeof(int) * static_cast<size_t>(env0) * dim, tmp.data(), cnt * sizeof(int),
@@ -1038,7 +1047,7 @@ void batch_get(BatchImpl* b, int field, double* host, int env0, int n) {
   if (field == MRS_FIELD_TIME) {
     HIP_CHECK(hipMemcpyAsync(host, src + sizeof(double) * env0, cnt * sizeof(double), hipMemcpyDeviceToHost, b->stream));
     HIP_CHECK(hipStreamSynchronize(b->stream));
-  } else if (field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON) {
+  } else if (field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON || field == MRS_FIELD_SOLVER_NITER) {
     std::vector<int> tmp(cnt);
     HIP_CHECK(hipMemcpyAsync(tmp.data(), src + sizeof(int) * static_cast<size_t>(env0) * dim, cnt * sizeof(int),
                              hipMemcpyDeviceToHost, b->stream));
@@ -1113,6 +1122,39 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
 // mjData.contact of the last forward pass of one env (geom1/geom2 as mj_collision orders them: pair
 // order g1 < g2 with the lower geom type first, then the narrow phase's order).  Records are read from
 // the env's contact scratch (step.hip collision(): pair id, dist, pos, frame).  Returns ncon.
+int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force) {
+  if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
+  if (max < 0) throw std::invalid_argument("negative capacity");
+  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS)
+    throw UnsupportedError("blocked-mode PGS keeps its constraint rows in sparse records");
+  HIP_CHECK(hipSetDevice(b->device));
+  const ScratchLayout& S = b->S;
+  const float* base = b->st.scratch + static_cast<size_t>(env) * S.total;
+  int nefc = 0;
+  HIP_CHECK(hipMemcpyAsync(&nefc, base + S.efc_n, sizeof(int), hipMemcpyDeviceToHost, b->stream));
+  HIP_CHECK(hipStreamSynchronize(b->stream));
+  if (nefc < 0) throw UnsupportedError("the register friction-loss path keeps no dense rows");
+  const int n = std::min(nefc, max), nv = b->model->nv;
+  if (n <= 0) return nefc;
+  std::vector<float> t(n), j(static_cast<size_t>(n) * nv), r(n), a(n), f(n);
+  auto get = [&](float* dst, int off, size_t count) {
+    HIP_CHECK(hipMemcpyAsync(dst, base + off, count * sizeof(float), hipMemcpyDeviceToHost, b->stream));
+  };
+  get(t.data(), S.efc_type, n); get(j.data(), S.efc_J, j.size()); get(r.data(), S.efc_R, n);
+  get(a.data(), S.efc_aref, n); get(f.data(), S.efc_f, n);
+  HIP_CHECK(hipStreamSynchronize(b->stream));
+  for (int i = 0; i < n; ++i) {
+    int code;
+    std::memcpy(&code, &t[i], sizeof code);
+    if (type) type[i] = code >> 16;
+    if (R) R[i] = r[i];
+    if (aref) aref[i] = a[i];
+    if (force) force[i] = f[i];
+    if (J) for (int k = 0; k < nv; ++k) J[static_cast<size_t>(i) * nv + k] = j[static_cast<size_t>(i) * nv + k];
+  }
+  return nefc;
+}
+
 int batch_get_contacts(BatchImpl* b, int env, int max, int* geom, double* dist, double* pos, double* frame) {
   if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
   if (max < 0) throw std::invalid_argument("negative capacity");
@@ -1144,7 +1186,7 @@ int batch_get_contacts(BatchImpl* b, int env, int max, int* geom, double* dist, 
 void batch_get_field_device(BatchImpl* b, int field, float* d_out, int env0, int n) {
   const Model& m = *b->model;
   const int dim = field_dim(m, field);
-  if (dim < 0 || field == MRS_FIELD_TIME || field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON)
+  if (dim < 0 || field == MRS_FIELD_TIME || field == MRS_FIELD_WARNING || field == MRS_FIELD_NCON || field == MRS_FIELD_SOLVER_NITER)
     throw std::invalid_argument("not an fp32 state field");
   if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
   if (n == 0 || dim == 0) return;

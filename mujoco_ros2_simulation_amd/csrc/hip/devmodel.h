@@ -41,7 +41,8 @@ struct LdsLayout {
       qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force,
       rfmask,  // per ray block: bitmask of candidate ray geoms (int bits)
       trees,   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
-      H;       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
+      H,       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
+      niter;   // constraint solver iterations of the last forward (int bits)
   int total;  // floats per env (multiple of 4)
 };
 
@@ -55,9 +56,11 @@ struct ScratchLayout {
       efc_item,              // blocked mode: first row of the item starting at a record (int bits)
       efc_fq,                // blocked mode: row forces by record (global-record fallback path)
       efc_hdr,               // blocked mode: 8-float header of the item starting at a record
-      sens;                  // sensordata sink of idle lane groups (envs past n_envs)
+      sens,                  // sensordata sink of idle lane groups (envs past n_envs)
+      efc_n;                 // rows of the dense layout of the last forward (int bits; -1: none stored)
   int total;
 };
+constexpr int kMaxPairCon = 8;  // contacts one geom pair can produce (box-box: the clipped face polygon)
 constexpr int kConRec = 16;  // pair id (int bits), dist, pos[3], frame[9], first efc row (-1 if cut), first row (blocked mode)
 
 // Everything the step kernel reads about the model.  Lives in device memory; the kernel receives
@@ -150,6 +153,7 @@ struct DevState {
   double* time;
   int* warning;  // [n_envs][4]
   int* ncon;     // [n_envs]
+  int* niter;    // [n_envs] constraint solver iterations of the last step (mjData.solver_niter)
   float* scratch;
   float* geom_xpos;  // [n_envs][ngeom][3]  kinematics of the last forward (for the depth camera)
   float* geom_xmat;  // [n_envs][ngeom][9]

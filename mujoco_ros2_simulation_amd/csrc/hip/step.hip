@@ -89,7 +89,12 @@ constexpr int kDppHalfMirror = 0x141; // lane i <-> 7-i within each 8
 constexpr int kDppMirror = 0x140;     // lane i <-> 15-i within each 16
 template <int G>
 __device__ __forceinline__ float gsum(float v) {
-  // full sum of each row of 16 in every lane of the row: quads, then halves, then rows
+  // full sum of each row of 16 in every lane of the row: quads, then halves, then rows.  Every lane
+  // must end with the same bits (group-uniform branches and replicated solver state depend on it):
+  // each step adds the same two rounded values in both lanes of a pair, which IEEE addition makes
+  // symmetric -- but only if the compiler cannot contract the caller's product into the first add
+  // (lane i would add its exact product to lane j's rounded one).  The empty asm makes v opaque.
+  asm volatile("" : "+v"(v));
   v += dpp<kDppXor1>(v);
   v += dpp<kDppXor2>(v);
   v += dpp<kDppHalfMirror>(v);
@@ -608,32 +613,21 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
     for (int o = 0; o < 8; ++o) { pu[o] = qu[o]; pv[o] = qv[o]; pw[o] = qw[o]; }
     if (np == 0) return 0;
   }
-  // the (up to) four deepest clipped vertices within the margin, shallower ties to the earlier vertex
-  unsigned avail = 0;
-#pragma unroll
-  for (int vtx = 0; vtx < 8; ++vtx)
-    if (vtx < np && pw[vtx] <= margin) avail |= 1u << vtx;
+  // every clipped vertex within the margin, in clip order (up to 8; oracle.c col_box_box): choosing
+  // the deepest few would decide among the equal depths of two flat-resting faces by rounding
   int n = 0;
-#pragma unroll 1
-  for (int k = 0; k < 4 && avail; ++k) {
-    int bi = -1;
-    float bs = 0;
 #pragma unroll
-    for (int vtx = 0; vtx < 8; ++vtx)
-      if ((avail >> vtx) & 1u)
-        if (bi < 0 || pw[vtx] < bs) { bi = vtx; bs = pw[vtx]; }
-    avail &= ~(1u << bi);
-    float bu = 0, bv = 0;
-#pragma unroll
-    for (int vtx = 0; vtx < 8; ++vtx)
-      if (vtx == bi) { bu = pu[vtx]; bv = pv[vtx]; }
-    gCon& o = out[n++];
-    for (int c = 0; c < 3; ++c) {
-      const float pt = cr[c] + bu * Rr[r1][c] + bv * Rr[r2][c] + bs * nr[c];
-      o.pos[c] = pt - nr[c] * bs / 2;
-      o.nrm[c] = nf[c];
+  for (int vtx = 0; vtx < 8; ++vtx) {
+    if (vtx < np && pw[vtx] <= margin) {
+      const float bu = pu[vtx], bv = pv[vtx], bs = pw[vtx];
+      gCon& o = out[n++];
+      for (int c = 0; c < 3; ++c) {
+        const float pt = cr[c] + bu * Rr[r1][c] + bv * Rr[r2][c] + bs * nr[c];
+        o.pos[c] = pt - nr[c] * bs / 2;
+        o.nrm[c] = nf[c];
+      }
+      o.dist = bs;
     }
-    o.dist = bs;
   }
   return n;
 }
@@ -1552,7 +1546,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
   #pragma unroll 1
   for (int base = 0; base < m.npair; base += G) {
     const int p = base + lane;
-    gCon* c = (gCon*)(scr + S.stage) + 4 * lane;  // per-lane staging in global scratch
+    gCon* c = (gCon*)(scr + S.stage) + kMaxPairCon * lane;  // per-lane staging in global scratch
     int n = 0;
     if (p < m.npair) {
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
@@ -1664,20 +1658,29 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     }
   });
   float qa = lane < nv ? qacc_s : 0.0f;
-  // warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost is negative
+  // warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost is negative.
+  // Lane r owns row r: it alone computes the row's force, which every lane then takes from it by
+  // broadcast, so M^-1 J' f and the sweeps' forces are built from one value per row
   if (!(m.disableflags & MRS_DSBL_WARMSTART)) {
     const float qw = lane < nv ? s[L.qacc_ws + lane] : 0.0f;
-    float v = 0;
+    float myjar = 0;
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
-        const float R = rowb<r>(myR), fl = rowb<r>(myfl);
-        const float jar = gsum<16>(Jt[r] * qw) - rowb<r>(myaref);
-        const float D = 1.0f / R;
-        const float f = fl > 0 ? (jar <= -R * fl ? fl : (jar >= R * fl ? -fl : -D * jar)) : (jar < 0 ? -D * jar : 0.0f);
-        v += MJt[r] * f;
-        if (lane == r) myf = f;
+        const float jr = gsum<16>(Jt[r] * qw);
+        if (lane == r) myjar = jr - myaref;
       }
+    });
+    {
+      const float D = 1.0f / myR;
+      myf = lane >= nefc ? 0.0f
+                         : (myfl > 0 ? (myjar <= -myR * myfl ? myfl : (myjar >= myR * myfl ? -myfl : -D * myjar))
+                                     : (myjar < 0 ? -D * myjar : 0.0f));
+    }
+    float v = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) v += MJt[r] * rowb<r>(myf);
     });
     float cost = 0;
     unroll<KR>([&](auto rc) {
@@ -1700,6 +1703,7 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     f[r] = rowb<r>(myf); bR[r] = rowb<r>(myR); bA[r] = rowb<r>(myA); bref[r] = rowb<r>(myaref);
     bfl[r] = rowb<r>(myfl); iA[r] = 1.0f / bA[r];
   });
+  int nit = 0;  // sweeps done (mjData.solver_niter)
   #pragma unroll 1
   for (int it = 0; it < m.iterations; ++it) {
     float improvement = 0;
@@ -1715,8 +1719,10 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
         improvement -= delta * res + 0.5f * delta * delta * bA[r];
       }
     });
+    nit = it + 1;
     if (improvement * m.pgs_scale < m.tolerance) break;
   }
+  if (lane == 0) s[L.niter] = __int_as_float(nit);
   float qc = 0;
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
@@ -1724,8 +1730,9 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     if (lane == r) myf = f[r];
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
-  // row forces for the contact forces of force/torque sensors (mj_rnePostConstraint)
-  if ((m.acc_sens & 2) && lane < nefc) ff[lane] = myf;
+  // row forces (mj_rnePostConstraint's contact forces, mrs_batch_get_efc)
+  // (the friction-loss fast path stores them only when force/torque sensors read them)
+  if (ff && (!kUnit || (m.acc_sens & 2)) && lane < nefc) ff[lane] = myf;
   return qa;
 }
 
@@ -2301,6 +2308,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       t_sub = SUB_T();
       // PGS sweeps
       int slot_v = slot;
+      int nit = 0;  // sweeps done (mjData.solver_niter)
       #pragma unroll 1
       for (int it = 0; it < m.iterations; ++it) {
         // opaque per sweep: keeps the per-level dof indices and lane masks from being hoisted out
@@ -2328,8 +2336,10 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           }
         });
         improvement = gsum<64>(slot_v == 0 ? improvement : 0.0f);
+        nit = it + 1;
         if (improvement * m.pgs_scale < m.tolerance) break;
       }
+      if (lane == 0) s[L.niter] = __int_as_float(nit);
       wsync();
       SUB_ADD(PH_CON_PGS, t_sub);
       // qfrc_constraint = J' f and the forces out (by row index, for mj_rnePostConstraint)
@@ -2401,6 +2411,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   }
 
   // --- 5. PGS sweeps: level k = the k-th row of every pipe; next level's record prefetched
+  int nit = 0;  // sweeps done (mjData.solver_niter)
   #pragma unroll 1
   for (int it = 0; it < m.iterations; ++it) {
     float improvement = 0;
@@ -2426,8 +2437,10 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     }
     improvement = gsum<64>(slot == 0 ? improvement : 0.0f);
     wsync();
+    nit = it + 1;
     if (improvement * m.pgs_scale < m.tolerance) break;
   }
+  if (lane == 0) s[L.niter] = __int_as_float(nit);
   wsync();
 
   // --- 6. qfrc_constraint = J' f (per dof in row order: a dof's rows are in one pipe); forces out
@@ -2470,6 +2483,13 @@ __device__ __forceinline__ float prow_cost(int st, float R, float fl, float jar)
 }
 __device__ __forceinline__ float prow_slope(int st, float R, float fl, float jar) {
   return st == PST_QUAD ? jar / R : (st == PST_LINNEG ? -fl : (st == PST_LINPOS ? fl : 0.0f));
+}
+// cost change of a row moved from jar j0 (state s0) by dj to state s1, in factored form when the
+// state is kept (no cancellation of two nearly equal costs in fp32)
+__device__ __forceinline__ float prow_dcost(int s0, int s1, float R, float fl, float j0, float dj) {
+  if (s0 != s1) return prow_cost(s1, R, fl, j0 + dj) - prow_cost(s0, R, fl, j0);
+  return s0 == PST_QUAD ? 0.5f * dj * (2.0f * j0 + dj) / R
+                        : (s0 == PST_LINNEG ? -fl * dj : (s0 == PST_LINPOS ? fl * dj : 0.0f));
 }
 
 // dense in-place Cholesky of an nv x nv LDS matrix (lower triangle read and written), lanes over
@@ -2575,9 +2595,10 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
       for (int r = 0; r < nefc; ++r) q += J[r * nv + lane] * ff[r];
     return q;
   };
-  // total cost at x (warm-start selection); leaves J x - aref in jar
+  // total cost at x (warm-start selection); leaves J x - aref in jar.  The Gauss term is
+  // 1/2 (x - qs)' M (x - qs), formed from the difference (fp32: no cancellation of M x - M qs)
   auto cost_at = [&](float x) {
-    const float mx = mmul(x);
+    const float md = mmul(x - qs);
     jmul(x, jar, 1.0f);
     float c = 0;
     #pragma unroll 1
@@ -2585,7 +2606,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
       const float R = Rr[r], fl = floss[r], ja = jar[r];
       c += prow_cost(prow_state(is_fric(r), R, fl, ja), R, fl, ja);
     }
-    return gsum<G>((dof ? 0.5f * (mx - fs) * (x - qs) : 0.0f) + c);
+    return gsum<G>((dof ? 0.5f * md * (x - qs) : 0.0f) + c);
   };
 
   float qa = qs;
@@ -2594,13 +2615,15 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     const float c_ws = cost_at(xw), c_sm = cost_at(qs);
     if (c_ws <= c_sm) qa = xw;
   }
-  float Ma = mmul(qa);
+  // Md = M (qacc - qacc_smooth) = M qacc - qfrc_smooth, carried as a difference
+  float Md = mmul(qa - qs);
   jmul(qa, jar, 1.0f);
   float qfrc = update();
   float p = 0, gold = 0, Mgold = 0;
+  int nit = 0;  // steps taken (mjData.solver_niter)
   #pragma unroll 1
   for (int iter = 0;; ++iter) {
-    const float grad = dof ? Ma - fs - qfrc : 0.0f;
+    const float grad = dof ? Md - qfrc : 0.0f;
     float Mg;
     if (newton) {
       // H row `lane` (dense: into the factor slot L.L; blocked: L.H), then factor in place
@@ -2636,7 +2659,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     const float Mv = mmul(p);
     jmul(p, jv, 0.0f);
     // exact line search: safeguarded Newton on the 1-D piecewise quadratic
-    const float g1 = gsum<G>(p * (Ma - fs)), g2 = gsum<G>(p * Mv), snorm = sqrtf(gsum<G>(p * p));
+    const float g1 = gsum<G>(p * Md), g2 = gsum<G>(p * Mv), snorm = sqrtf(gsum<G>(p * p));
     auto ls_eval = [&](float a, float a0, float& d1, float& d2, bool& ch) {
       float s1 = 0, s2 = 0;
       bool c = false;
@@ -2686,23 +2709,25 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
       const bool fr = is_fric(r);
       const float R = Rr[r], fl = floss[r], j0 = jar[r], j1 = j0 + alpha * jv[r];
       const int s0 = __float_as_int(st[r]), s1 = prow_state(fr, R, fl, j1);
-      dc += prow_cost(s1, R, fl, j1) - prow_cost(s0, R, fl, j0);
+      dc += prow_dcost(s0, s1, R, fl, j0, alpha * jv[r]);
       changed |= s0 != s1;
       jar[r] = j1;
     }
     const float dcost = alpha * g1 + 0.5f * alpha * alpha * g2 + gsum<G>(dc);
     changed = gany<G>(changed);
     qa += alpha * p;
-    Ma += alpha * Mv;
+    Md += alpha * Mv;
     gold = grad;
     Mgold = Mg;
     wsync();
     qfrc = update();
-    const float gn = dof ? Ma - fs - qfrc : 0.0f;
+    ++nit;
+    const float gn = dof ? Md - qfrc : 0.0f;
     const float gnorm = sqrtf(gsum<G>(gn * gn));
     if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance || (newton && !changed)) break;
   }
   if (dof) s[L.qfrc_con + lane] = qfrc;
+  if (lane == 0) s[L.niter] = __int_as_float(nit);
   wsync();
   return dof ? qa : 0.0f;
 }
@@ -2743,6 +2768,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
         lim |= (q - m.jnt_range[2 * jid] < mg) | (m.jnt_range[2 * jid + 1] - q < mg);
       }
     if (m.solver == MRS_SOL_PGS && ncon == 0 && nf > 0 && nf <= 16 && !gany<G>(lim)) {
+      if (lane == 0) scr[S.efc_n] = __int_as_float(-1);  // rows stay in registers
       int mydof = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
       if (lane < nf) {
@@ -2906,6 +2932,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
         }
     }
   }
+  if (lane == 0) scr[S.efc_n] = __int_as_float(nefc);
   wsync();
   if (nefc == 0) {
     if (lane < nv) s[L.qfrc_con + lane] = 0;
@@ -2941,7 +2968,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     const float imp = impedance(si, pos[r], marg[r]);
     float R = (1 - imp) * diag / imp;
     R = R > kMinVal ? R : kMinVal;
-    if (!small) Rr[r] = R;
+    Rr[r] = R;
     const float dmax = clampf(si[1], 0.0001f, 0.9999f);
     float K, B;
     if (sr[0] > 0) {
@@ -2963,6 +2990,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       my_aref = -B * vel - pterm;
       my_b = jqs - my_aref;
       my_fl = t == EFC_FRICTION ? floss[r] : 0.0f;
+      aref[r] = my_aref;
       continue;
     }
     aref[r] = -B * vel - pterm;
@@ -3042,6 +3070,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     }
   }
   // --- PGS sweeps (rows serial, dot products across lanes)
+  int nit = 0;  // sweeps done (mjData.solver_niter)
   #pragma unroll 1
   for (int it = 0; it < m.iterations; ++it) {
     float improvement = 0;
@@ -3063,8 +3092,10 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       improvement -= delta * res + 0.5f * delta * delta * a;
       wsync();
     }
+    nit = it + 1;
     if (improvement * m.pgs_scale < m.tolerance) break;
   }
+  if (lane == 0) s[L.niter] = __int_as_float(nit);
   // --- qfrc_constraint = J' f
   if (lane < nv) {
     float v = 0;
@@ -3569,6 +3600,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   if (!(m.diag_skip & 2)) MRS_CALL(G, ncon = collision<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COLL);
   float qacc = qacc_s;
+  if (lane == 0) s[L.niter] = __int_as_float(0);
   if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = constraints<G>(ENV_ARGS, ncon, qacc_s));
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
@@ -3785,6 +3817,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
   if (lane == 0) {
     st.time[e] = time;
     st.ncon[e] = ncon;
+    st.niter[e] = __float_as_int(s[L.niter]);
     if (w_pos | w_vel | w_acc) {
       st.warning[4 * e + 0] += w_pos;
       st.warning[4 * e + 1] += w_vel;

@@ -30,7 +30,7 @@ SENS_ACCELEROMETER, SENS_GYRO, SENS_FORCE, SENS_TORQUE, SENS_RANGEFINDER = 1, 3,
 SENS_JOINTPOS, SENS_JOINTVEL, SENS_ACTUATORFRC, SENS_FRAMEPOS, SENS_FRAMEQUAT = 9, 10, 15, 25, 26
 BIAS_NONE, BIAS_AFFINE = 0, 1
 (FIELD_QPOS, FIELD_QVEL, FIELD_CTRL, FIELD_QFRC_APPLIED, FIELD_QACC_WARMSTART, FIELD_QACC,
- FIELD_QFRC_ACTUATOR, FIELD_SENSORDATA, FIELD_TIME, FIELD_WARNING, FIELD_NCON) = range(11)
+ FIELD_QFRC_ACTUATOR, FIELD_SENSORDATA, FIELD_TIME, FIELD_WARNING, FIELD_NCON, FIELD_SOLVER_NITER) = range(12)
 # ActuatorType (include/mujoco_ros2_control/data.hpp:43-51 numbering)
 ACT_UNKNOWN, ACT_MOTOR, ACT_POSITION, ACT_VELOCITY, ACT_CUSTOM = range(5)
 
@@ -137,6 +137,8 @@ def lib() -> C.CDLL:
         L.mrs_batch_sync.argtypes = [C.c_void_p]
         L.mrs_batch_get_contacts.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p]
+        L.mrs_batch_get_efc.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]
         L.mrs_batch_get_field_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.mrs_batch_last_kernel_ms.restype = C.c_double
         L.mrs_batch_last_kernel_ms.argtypes = [C.c_void_p, C.c_int]
@@ -234,7 +236,7 @@ class Model:
 _FIELD_DIM = {
     FIELD_QPOS: "nq", FIELD_QVEL: "nv", FIELD_CTRL: "nu", FIELD_QFRC_APPLIED: "nv", FIELD_QACC_WARMSTART: "nv",
     FIELD_QACC: "nv", FIELD_QFRC_ACTUATOR: "nv", FIELD_SENSORDATA: "nsensordata", FIELD_TIME: 1, FIELD_WARNING: 4,
-    FIELD_NCON: 1,
+    FIELD_NCON: 1, FIELD_SOLVER_NITER: 1,
 }
 
 
@@ -312,6 +314,20 @@ class Batch:
             _check(n)
         n = min(n, max_n)
         return g[:n], dist[:n], pos[:n], frame[:n]
+
+    def efc(self, env: int = 0, max_n: int = 1024):
+        """mjData.efc_* of `env` after the last step/forward: dict of type [n] (1 friction loss,
+        2 limit, 3 contact), J [n, nv], R, aref, force [n]"""
+        nv = self.model.nv
+        t = np.zeros(max_n, dtype=np.int32)
+        J = np.zeros((max_n, max(nv, 1)))
+        R, a, f = np.zeros(max_n), np.zeros(max_n), np.zeros(max_n)
+        n = lib().mrs_batch_get_efc(self._h, env, max_n, t.ctypes.data, J.ctypes.data, R.ctypes.data, a.ctypes.data,
+                                    f.ctypes.data)
+        if n < 0:
+            _check(n)
+        n = min(n, max_n)
+        return {"type": t[:n], "J": J[:n, :nv], "R": R[:n], "aref": a[:n], "force": f[:n]}
 
     def get_device(self, field: int, dptr: int, env0: int = 0, n: int | None = None) -> None:
         """fp32 rows of `field` into a device buffer [n, dim], asynchronous on the batch stream"""

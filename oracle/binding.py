@@ -47,6 +47,7 @@ def lib():
         L.orc_ray.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P, C.c_int, C.POINTER(C.c_int)]
         L.orc_render_depth.argtypes = [C.c_void_p, C.POINTER(OrcData), C.c_int, C.POINTER(C.c_float)]
         L.orc_contacts.argtypes = [C.POINTER(OrcData), C.c_int, C.POINTER(C.c_int), P, P, P]
+        L.orc_smooth.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P]
         L.orc_efc.argtypes = [C.POINTER(OrcData), C.c_int, C.c_int, C.POINTER(C.c_int), P, P, P, P, P]
         L.orc_rollout.restype = C.c_double
         L.orc_rollout.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P, P]
@@ -139,6 +140,12 @@ class OracleData:
         n = lib().orc_contacts(self._d, max_n, g.ctypes.data_as(C.POINTER(C.c_int)), _dp(dist), _dp(pos), _dp(frame))
         n = min(n, max_n)
         return g[:2 * n].reshape(-1, 2), dist[:n], pos[:3 * n].reshape(-1, 3), frame[:9 * n].reshape(-1, 9)
+
+    def smooth(self):
+        """(qacc_smooth, qfrc_smooth) of the last forward"""
+        a, f = np.zeros(self.model.nv), np.zeros(self.model.nv)
+        lib().orc_smooth(self._mv, self._d, _dp(a), _dp(f))
+        return a, f
 
     def efc(self, max_n: int = 1024):
         """constraint rows of the last forward: dict of type [n], force, aref, R, pos [n], J [n, nv]"""

