@@ -567,7 +567,7 @@ static void make_frame(double f[9]) {
   cross3(f + 6, f, f + 3);
 }
 static int add_contact(orc_contact* out, int n, double dist, const double pos[3], const double nrm[3]) {
-  if (n >= 4) return n;
+  if (n >= 8) return n; /* a pair gives at most 8 contacts (box-box face polygon) */
   orc_contact* c = out + n;
   c->dist = dist;
   memcpy(c->pos, pos, 3 * sizeof(double));
@@ -925,7 +925,7 @@ static void collision(const mrs_model_view* m, orc_data* d) {
       }
       int ga = g1, gb = g2;
       if (m->geom_type[ga] > m->geom_type[gb]) { ga = g2; gb = g1; }
-      orc_contact tmp[4];
+      orc_contact tmp[8]; /* a pair gives at most 8 contacts (box-box face polygon) */
       int nc = narrowphase(m, w, ga, gb, margin, tmp);
       if (nc < 0) continue; /* unsupported pairs are rejected at batch creation in the product */
       /* contact parameters [upstream mj_contactParam]: max friction/condim, solmix-weighted solref */

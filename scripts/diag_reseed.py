@@ -28,6 +28,8 @@ for t in range(steps):
     for e, d in enumerate(orc):
         if t % 10 == 0:
             d.ctrl[:] = tab[t // 10, e]
+        for a in (d.qpos, d.qvel, d.qacc_warmstart, d.ctrl):
+            a[:] = a.astype(np.float32)
     S = {k: np.array([getattr(d, k) for d in orc]) for k in ("qpos", "qvel", "qacc_warmstart", "ctrl")}
     b.set(sim.FIELD_QPOS, S["qpos"]); b.set(sim.FIELD_QVEL, S["qvel"])
     b.set(sim.FIELD_QACC_WARMSTART, S["qacc_warmstart"]); b.set(sim.FIELD_CTRL, S["ctrl"])
@@ -35,6 +37,9 @@ for t in range(steps):
     for d in orc:
         d.step()
     v, vr = b.get(sim.FIELD_QVEL), np.array([d.qvel for d in orc])
+    nc, nr = b.get(sim.FIELD_NCON)[:, 0].astype(int), np.array([d.ncon for d in orc])
+    if np.any(nc != nr) and t % 10 == 0:
+        print(f"step {t}: {np.sum(nc != nr)} flips; env0 ncon gpu {nc[0]} oracle {nr[0]}; gpu ncon {nc[:8]} oracle {nr[:8]}")
     err = np.abs(v - vr) / np.maximum(np.abs(vr), 1)
     e, j = np.unravel_index(np.argmax(err), err.shape)
     if err[e, j] > worst[0]:
