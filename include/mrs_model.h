@@ -57,6 +57,7 @@ typedef struct mrs_model_view {
   int nq, nv, nu, na, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, nkey;
   int nM;            /* nv*nv (dense joint-space matrices on this path) */
   int max_depth;     /* longest root-to-leaf body chain (levels for tree-parallel passes) */
+  int npair;         /* statically admissible collision pairs (broad-phase filters of mj_collision) */
 
   /* options (mjOption subset) */
   double timestep, gravity[3], tolerance, impratio, ls_tolerance;
@@ -111,6 +112,10 @@ typedef struct mrs_model_view {
 
   /* keyframes */
   const double *key_time, *key_qpos, *key_qvel, *key_ctrl;
+
+  /* candidate collision pairs [npair]: geoms of different weld groups, not parent-child welds,
+   * contype/conaffinity compatible; the lower geom type first */
+  const int *pair_geom1, *pair_geom2;
 } mrs_model_view;
 
 #ifdef __cplusplus

@@ -498,19 +498,11 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // static collision-pair filter (mj_collision broad phase minus the dynamic bounding test)
   std::vector<int> pg1, pg2, pdim;
   std::vector<float> pmargin, pgap, pfric, psolref, psolimp;
-  if (!(m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT))) {
-    for (int g1 = 0; g1 < m.ngeom; ++g1)
-      for (int g2 = g1 + 1; g2 < m.ngeom; ++g2) {
-        int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-        int w1 = m.body_weldid[b1], w2 = m.body_weldid[b2];
-        if (w1 == w2) continue;
-        if (!(m.disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
-            (w1 == m.body_weldid[m.body_parentid[w2]] || w2 == m.body_weldid[m.body_parentid[w1]]))
-          continue;
-        if (!((m.geom_contype[g1] & m.geom_conaffinity[g2]) || (m.geom_contype[g2] & m.geom_conaffinity[g1])))
-          continue;
-        int ga = g1, gb = g2;
-        if (m.geom_type[ga] > m.geom_type[gb]) std::swap(ga, gb);
+  {
+    // the compiler's statically admissible pairs (mrs::Model::pair_geom1/2, lower geom type first)
+    for (size_t q = 0; q < m.pair_geom1.size(); ++q) {
+        const int ga = m.pair_geom1[q], gb = m.pair_geom2[q];
+        const int g1 = std::min(ga, gb), g2 = std::max(ga, gb);
         int ta = m.geom_type[ga], tb = m.geom_type[gb];
         bool ok = (ta == MRS_GEOM_PLANE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
                   (ta == MRS_GEOM_SPHERE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||

@@ -1472,7 +1472,32 @@ struct Compiler {
         if (!c->children.empty()) fail(c.get(), "explicit <contact> pairs/excludes are not supported");
       }
     }
+    candidate_pairs();
     return std::move(m);
+  }
+  // Static part of mj_collision's broad phase [upstream engine_collision_driver.c mj_collideGeoms /
+  // filterBitmask]: geom pairs of different weld groups, not parent-child welds (unless the
+  // filterparent flag is disabled; the world body is never filtered), with contype/conaffinity
+  // compatible in either direction.  The dynamic bounding-sphere test stays per step.  Each pair is
+  // ordered with the lower geom type first (the narrow phase's convention).
+  void candidate_pairs() {
+    m.pair_geom1.clear();
+    m.pair_geom2.clear();
+    if (m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) return;
+    for (int g1 = 0; g1 < m.ngeom; ++g1)
+      for (int g2 = g1 + 1; g2 < m.ngeom; ++g2) {
+        const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+        const int w1 = m.body_weldid[b1], w2 = m.body_weldid[b2];
+        if (w1 == w2) continue;
+        if (!(m.disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
+            (w1 == m.body_weldid[m.body_parentid[w2]] || w2 == m.body_weldid[m.body_parentid[w1]]))
+          continue;
+        if (!((m.geom_contype[g1] & m.geom_conaffinity[g2]) || (m.geom_contype[g2] & m.geom_conaffinity[g1])))
+          continue;
+        const bool swap = m.geom_type[g1] > m.geom_type[g2];
+        m.pair_geom1.push_back(swap ? g2 : g1);
+        m.pair_geom2.push_back(swap ? g1 : g2);
+      }
   }
   // dampratio -> kv for position-like actuators: kv = dampratio * 2 * sqrt(kp * mass) with
   // mass = sum over transmitted dofs of dof_M0 / moment^2  [upstream engine_setconst.c; verify].
@@ -1521,7 +1546,7 @@ mrs_model_view Model::view() const {
   std::memset(&v, 0, sizeof v);
   v.nq = nq; v.nv = nv; v.nu = nu; v.na = na; v.nbody = nbody; v.njnt = njnt; v.ngeom = ngeom;
   v.nsite = nsite; v.ncam = ncam; v.nsensor = nsensor; v.nsensordata = nsensordata; v.nkey = nkey;
-  v.nM = nv * nv; v.max_depth = max_depth;
+  v.nM = nv * nv; v.max_depth = max_depth; v.npair = static_cast<int>(pair_geom1.size());
   v.timestep = timestep;
   for (int i = 0; i < 3; ++i) { v.gravity[i] = gravity[i]; v.stat_center[i] = stat_center[i]; }
   v.tolerance = tolerance; v.impratio = impratio; v.integrator = integrator; v.solver = solver;
@@ -1553,6 +1578,7 @@ mrs_model_view Model::view() const {
   MRS_V(sensor_type); MRS_V(sensor_objtype); MRS_V(sensor_objid); MRS_V(sensor_dim);
   MRS_V(sensor_adr); MRS_V(sensor_cutoff);
   MRS_V(qpos0); MRS_V(qpos_spring); MRS_V(key_time); MRS_V(key_qpos); MRS_V(key_qvel); MRS_V(key_ctrl);
+  MRS_V(pair_geom1); MRS_V(pair_geom2);
 #undef MRS_V
   return v;
 }

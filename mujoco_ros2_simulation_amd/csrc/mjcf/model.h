@@ -56,6 +56,8 @@ struct Model {
 
   std::vector<double> qpos0, qpos_spring;
   std::vector<double> key_time, key_qpos, key_qvel, key_ctrl;
+  // statically admissible collision pairs (mj_collision's broad-phase filters), lower geom type first
+  std::vector<int> pair_geom1, pair_geom2;
 
   // names per object type (MRS_OBJ_*), index = object id
   std::map<int, std::vector<std::string>> names;

@@ -46,7 +46,7 @@ class MrsError(RuntimeError):
 
 # (name, kind, size-expression) in exactly the order of struct mrs_model_view
 _SIZES = ["nq", "nv", "nu", "na", "nbody", "njnt", "ngeom", "nsite", "ncam", "nsensor", "nsensordata", "nkey",
-          "nM", "max_depth"]
+          "nM", "max_depth", "npair"]
 _ARRAYS = [
     ("body_parentid", "i", "nbody", 1), ("body_rootid", "i", "nbody", 1), ("body_weldid", "i", "nbody", 1),
     ("body_jntnum", "i", "nbody", 1), ("body_jntadr", "i", "nbody", 1), ("body_dofnum", "i", "nbody", 1),
@@ -84,6 +84,7 @@ _ARRAYS = [
     ("qpos0", "d", "nq", 1), ("qpos_spring", "d", "nq", 1),
     ("key_time", "d", "nkey", 1), ("key_qpos", "d", "nkey", "nq"), ("key_qvel", "d", "nkey", "nv"),
     ("key_ctrl", "d", "nkey", "nu"),
+    ("pair_geom1", "i", "npair", 1), ("pair_geom2", "i", "npair", 1),
 ]
 
 

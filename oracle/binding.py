@@ -47,6 +47,7 @@ def lib():
         L.orc_ray.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P, C.c_int, C.POINTER(C.c_int)]
         L.orc_render_depth.argtypes = [C.c_void_p, C.POINTER(OrcData), C.c_int, C.POINTER(C.c_float)]
         L.orc_contacts.argtypes = [C.POINTER(OrcData), C.c_int, C.POINTER(C.c_int), P, P, P]
+        L.orc_candidate_pairs.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_smooth.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P]
         L.orc_efc.argtypes = [C.POINTER(OrcData), C.c_int, C.c_int, C.POINTER(C.c_int), P, P, P, P, P]
         L.orc_rollout.restype = C.c_double
@@ -162,6 +163,15 @@ class OracleData:
         if getattr(self, "_d", None) and _lib is not None:
             _lib.orc_free_data(self._d)
             self._d = None
+
+
+def candidate_pairs(model) -> np.ndarray:
+    """[npair, 2] statically admissible collision pairs by the oracle's own broad-phase filter"""
+    cap = max(1, model.ngeom * model.ngeom)
+    g1, g2 = np.zeros(cap, dtype=np.int32), np.zeros(cap, dtype=np.int32)
+    n = lib().orc_candidate_pairs(C.byref(model.view), cap, g1.ctypes.data_as(C.POINTER(C.c_int)),
+                                  g2.ctypes.data_as(C.POINTER(C.c_int)))
+    return np.stack([g1[:n], g2[:n]], axis=1)
 
 
 def rollout(model, qpos_init: np.ndarray, ctrl_table: np.ndarray, n_steps: int, period: int, n_threads: int):

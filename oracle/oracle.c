@@ -902,20 +902,41 @@ static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, doubl
   return -1; /* unsupported pair */
 }
 
+/* static broad-phase filters of mj_collision [upstream mj_collideGeoms / filterBitmask]: different
+ * weld groups, not parent-child welds (world never filtered), contype/conaffinity compatible */
+static int pair_admissible(const mrs_model_view* m, int g1, int g2) {
+  int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+  int w1 = m->body_weldid[b1], w2 = m->body_weldid[b2];
+  if (w1 == w2) return 0;
+  if (!(m->disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
+      (w1 == m->body_weldid[m->body_parentid[w2]] || w2 == m->body_weldid[m->body_parentid[w1]]))
+    return 0;
+  return (m->geom_contype[g1] & m->geom_conaffinity[g2]) || (m->geom_contype[g2] & m->geom_conaffinity[g1]);
+}
+
+int orc_candidate_pairs(const mrs_model_view* m, int max, int* geom1, int* geom2) {
+  int n = 0;
+  if (m->disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) return 0;
+  for (int g1 = 0; g1 < m->ngeom; ++g1)
+    for (int g2 = g1 + 1; g2 < m->ngeom; ++g2) {
+      if (!pair_admissible(m, g1, g2)) continue;
+      if (n < max) {
+        int swap = m->geom_type[g1] > m->geom_type[g2];
+        geom1[n] = swap ? g2 : g1;
+        geom2[n] = swap ? g1 : g2;
+      }
+      ++n;
+    }
+  return n;
+}
+
 static void collision(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   w->ncon = 0;
   if (m->disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) return;
   for (int g1 = 0; g1 < m->ngeom; ++g1)
     for (int g2 = g1 + 1; g2 < m->ngeom; ++g2) {
-      int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
-      int w1 = m->body_weldid[b1], w2 = m->body_weldid[b2];
-      if (w1 == w2) continue;
-      if (!(m->disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
-          (w1 == m->body_weldid[m->body_parentid[w2]] || w2 == m->body_weldid[m->body_parentid[w1]]))
-        continue;
-      if (!((m->geom_contype[g1] & m->geom_conaffinity[g2]) || (m->geom_contype[g2] & m->geom_conaffinity[g1])))
-        continue;
+      if (!pair_admissible(m, g1, g2)) continue;
       double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
       double gap = fmax(m->geom_gap[g1], m->geom_gap[g2]);
       if (m->geom_type[g1] != MRS_GEOM_PLANE && m->geom_type[g2] != MRS_GEOM_PLANE) {

@@ -54,6 +54,9 @@ void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out)
 int orc_efc(orc_data* d, int nv, int max, int* type, double* force, double* aref, double* R, double* pos,
             double* J);
 int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, double* frame);
+/* statically admissible collision pairs by the oracle's own filter (lower geom type first); returns
+ * the count, writes up to `max` */
+int orc_candidate_pairs(const mrs_model_view* m, int max, int* geom1, int* geom2);
 /* qacc_smooth, qfrc_smooth (nv each) of the last forward */
 void orc_smooth(const mrs_model_view* m, orc_data* d, double* qacc_smooth, double* qfrc_smooth);
 
