@@ -62,6 +62,49 @@ def _scale(x):
     return np.maximum(np.abs(x), 1.0)
 
 
+def _quat_rot(q, v):
+    w, x, y, z = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                  [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                  [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+    return R @ v
+
+
+def _grazing(model, qpos, sensor, delta=1e-4):
+    """is rangefinder `sensor`'s ray within `delta` rad of a geom silhouette at `qpos`?  The oracle's
+    mj_ray along the site's z axis is compared with rays tilted by +-delta about two axes normal to it:
+    a ray that grazes an edge flips hit/miss or jumps to another surface (range changes by far more
+    than the smooth delta * range * slope of a face it hits squarely)"""
+    d = binding.OracleData(model)
+    d.qpos[:] = qpos
+    xpos, xquat, _, _ = d.kinematics()
+    site = model.sensor_objid[sensor]
+    b = model.site_bodyid[site]
+    pnt = xpos[b] + _quat_rot(xquat[b], model.site_pos[site])
+    sq = model.site_quat[site]
+    w, x, y, z = sq
+    bq = xquat[b]
+    q = np.array([bq[0] * w - bq[1] * x - bq[2] * y - bq[3] * z, bq[0] * x + bq[1] * w + bq[2] * z - bq[3] * y,
+                  bq[0] * y - bq[1] * z + bq[2] * w + bq[3] * x, bq[0] * z + bq[1] * y - bq[2] * x + bq[3] * w])
+    vec = _quat_rot(q, np.array([0.0, 0.0, 1.0]))
+    far = 50.0  # hits beyond this count as misses: a horizontal lidar ray tilted down by delta
+    #             meets the infinite floor thousands of metres away, which is not a silhouette
+    r0, _ = d.ray(pnt, vec, b)
+    r0 = -1.0 if r0 > far else r0
+    e1 = np.cross(vec, [1.0, 0, 0] if abs(vec[0]) < 0.9 else [0, 1.0, 0])
+    e1 /= np.linalg.norm(e1)
+    e2 = np.cross(vec, e1)
+    for e in (e1, -e1, e2, -e2):
+        v = vec + delta * e
+        r, _ = d.ray(pnt, v / np.linalg.norm(v), b)
+        r = -1.0 if r > far else r
+        if (r < 0) != (r0 < 0):
+            return True
+        if r0 >= 0 and abs(r - r0) > 10 * delta * max(1.0, r0):
+            return True
+    return False
+
+
 def _oracle_rollout_f32_state(model, qpos0, table, period, checkpoints):
     """the oracle's rollout with qpos/qvel rounded to fp32 after every step: how far fp32 storage of
     the state alone moves a trajectory from the fp64 one (the scene's own sensitivity)"""
@@ -106,15 +149,22 @@ def test_rollout_parity(scene, n_envs, steps, group, monkeypatch):
         print(f"{scene.name} step {c}: max rel err qpos {eq:.2e} qvel {ev:.2e}")
         assert eq <= RTOL, f"qpos rel err {eq} at step {c}"
         assert ev <= RTOL, f"qvel rel err {ev} at step {c}"
-        rf = [i for i in range(model.nsensor) if model.sensor_type[i] == sim.SENS_RANGEFINDER]
+        rf = np.array([i for i in range(model.nsensor) if model.sensor_type[i] == sim.SENS_RANGEFINDER])
         adr = model.sensor_adr[rf]
         # grazing rays (tangent to a sphere/capsule within rounding) may flip hit/miss
-        assert np.mean((s[:, adr] < 0) != (s_ref[:, adr] < 0)) <= 0.002
+        flip = (s[:, adr] < 0) != (s_ref[:, adr] < 0)
+        assert np.mean(flip) <= 0.002
         hit = (s_ref[:, adr] >= 0) & (s[:, adr] >= 0)
-        err = np.abs(s[:, adr][hit] - s_ref[:, adr][hit]) / np.maximum(1.0, s_ref[:, adr][hit])
+        err = np.zeros_like(s[:, adr])
+        err[hit] = np.abs(s[:, adr][hit] - s_ref[:, adr][hit]) / np.maximum(1.0, s_ref[:, adr][hit])
         # a ray grazing a box edge may land on the adjacent face under a 1e-7 pose difference
-        assert np.mean(err > 2e-5) <= 0.005, f"rangefinder mismatch fraction {np.mean(err > 2e-5)}"
-        assert np.median(err) < 1e-6
+        assert np.mean(err[hit] > 2e-5) <= 0.005, f"rangefinder mismatch fraction {np.mean(err[hit] > 2e-5)}"
+        assert np.median(err[hit]) < 1e-6
+        # every outlier and every hit/miss flip is a grazing ray: within 1e-4 rad of a silhouette
+        bad = np.argwhere(flip | (err > 2e-5))
+        for e, k in bad:
+            assert _grazing(model, q_ref[e], rf[k]), (c, e, k, s[e, adr[k]], s_ref[e, adr[k]])
+        print(f"  {len(bad)} rangefinder outliers / flips, all grazing a silhouette")
 
 
 @pytest.mark.parametrize("group", [16, 64])
