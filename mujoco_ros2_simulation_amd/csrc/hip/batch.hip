@@ -813,10 +813,26 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.total = off;
   };
   lds_layout(false);
-  // workgroup-shared tables: ray-geom records, and the per-ray direction + address when every ray
-  // starts at one point of one body (DevModel::shr_*)
+  // static ray split: every rangefinder on a world-welded body and some ray geom on one too
+  d.rf_mode = 0;
+  d.rf_static_mask = 0;
+  if (d.nrfblk > 0 && d.nrgeom <= 32) {
+    bool static_rays = true;
+    for (int k = 0; k < d.nrf; ++k)
+      if (m.body_weldid[m.site_bodyid[m.sensor_objid[rf[k]]]] != 0) static_rays = false;
+    for (int i = 0, g = 0; g < m.ngeom; ++g) {
+      if (m.geom_rgba[4 * g + 3] == 0) continue;
+      if (m.body_weldid[m.geom_bodyid[g]] == 0) d.rf_static_mask |= 1u << i;
+      ++i;
+    }
+    if (static_rays && d.rf_static_mask && !std::getenv("MRS_NO_STATIC_RAYS")) d.rf_mode = 2;
+  }
+  d.rf_static = d.rf_mode ? static_cast<float*>(dalloc(b, std::max(1, d.nrf) * sizeof(float))) : nullptr;
+  // workgroup-shared tables: ray-geom records, the per-ray direction + address when every ray
+  // starts at one point of one body, and the rays' static hits (DevModel::shr_*)
   d.shr_rf = d.nrgeom * 8;
-  d.shr_total = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
+  d.shr_rfst = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
+  d.shr_total = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
@@ -934,6 +950,15 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     b->st.cam_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ncam) * 3 * sizeof(float)));
     b->st.cam_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ncam) * 9 * sizeof(float)));
     batch_reset(b, -1, 0, n_envs);
+    if (b->dm.rf_mode == 2) {
+      // static ray hits: one forward-only pass of env 0 with the producer's model copy
+      DevModel prod = b->dm;
+      prod.rf_mode = 1;
+      DevModel* d_prod = static_cast<DevModel*>(dalloc(*b, sizeof(DevModel)));
+      HIP_CHECK(hipMemcpyAsync(d_prod, &prod, sizeof(DevModel), hipMemcpyHostToDevice, b->stream));
+      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, b->stream));
+      HIP_CHECK(hipStreamSynchronize(b->stream));
+    }
     batch_launch(b, 1, true);  // mj_forward after load (src/mujoco_system_interface.cpp:741)
     HIP_CHECK(hipStreamSynchronize(b->stream));
   } catch (...) {

@@ -79,6 +79,14 @@ struct DevModel {
   // when rf_common the per-ray direction + sensordata address (4 floats each) at shr_off + shr_rf.
   // Staged once per launch, read by the ray phase every step instead of global loads.
   int shr_off, shr_rf, shr_total;
+  // static ray split: when every rangefinder sits on a world-welded body, its hits on
+  // world-welded geoms are the same every step and in every env.  rf_mode 1: the one-off producer
+  // pass at batch creation, testing only those static geoms and writing the nearest hit per ray to
+  // rf_static; rf_mode 2: the step kernel starts every ray from rf_static (staged in workgroup LDS
+  // at shr_rfst) and tests only the moving geoms; 0: no split.  rf_static_mask: static ray-geom bits.
+  int rf_mode, shr_rfst;
+  unsigned rf_static_mask;
+  float* rf_static;
   // options
   int integrator, iterations, disableflags, solver, ls_iterations;
   int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)

@@ -3242,7 +3242,8 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       bod[j] = b;
       mat_vec(vec[j], bm, dl);
       for (int i = 0; i < 3; ++i) pnt[j][i] = o[i];
-      dist[j] = -1;
+      // static split: start from the ray's hit on the world-welded geoms (never beaten: -1)
+      dist[j] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + (act[j] ? k : 0)] : -1.0f;
     }
   } else {
 #pragma unroll
@@ -3260,7 +3261,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       mat_vec(pnt[j], bm, ol);
       for (int i = 0; i < 3; ++i) pnt[j][i] += se[L.xpos + 3 * b + i];
       mat_vec(vec[j], bm, dl);
-      dist[j] = -1;
+      dist[j] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + (act[j] ? k : 0)] : -1.0f;
     }
   }
   SUB_ADD(PH_SENS_SETUP, t_setup);
@@ -3321,8 +3322,13 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     }
   }
 #pragma unroll
-  for (int j = 0; j < R; ++j)
-    if (act[j] && MRS_SD_OK(sd)) sd[adr[j]] = dist[j];
+  for (int j = 0; j < R; ++j) {
+    if (m.rf_mode == 1) {
+      if (act[j]) m.rf_static[k0 + j * stride] = dist[j];  // producer pass: the static hits
+    } else if (act[j] && MRS_SD_OK(sd)) {
+      sd[adr[j]] = dist[j];
+    }
+  }
   SUB_ADD(PH_SENS_GEOMS, t_geoms);
 }
 
@@ -3418,6 +3424,9 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       const int b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
       for (int blk = base / kRayBlock; blk < b1; ++blk) gmask |= static_cast<unsigned>(__float_as_int(s[L.rfmask + blk]));
     }
+    // static split: the producer tests the world-welded geoms, the step the moving ones
+    if (m.rf_mode == 1) gmask &= m.rf_static_mask;
+    else if (m.rf_mode == 2) gmask &= ~m.rf_static_mask;
     // no geom reachable from this pass in any group of the wave: every ray misses (-1)
     unsigned wm = gmask;
     if constexpr (G < 64) {
@@ -3425,10 +3434,14 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       for (int i = 0; i < 64 / G; ++i) wm |= __builtin_amdgcn_readlane(gmask, i * G);
     }
     if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+      // (static split: the static hit is the answer)
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const int k = base + lane + j * G;
-        if (k < m.nrf && MRS_SD_OK(sensordata)) sensordata[__float_as_int(m.rfray[8 * k + 3])] = -1.0f;
+        if (k >= m.nrf) continue;
+        if (m.rf_mode == 1) m.rf_static[k] = -1.0f;
+        else if (MRS_SD_OK(sensordata))
+          sensordata[__float_as_int(m.rfray[8 * k + 3])] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + k] : -1.0f;
       }
       continue;
     }
@@ -3735,7 +3748,10 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     #pragma unroll 1
     for (int i = threadIdx.x; i < m.shr_rf; i += blockDim.x) shr[i] = m.rgeom[i];
     #pragma unroll 1
-    for (int i = threadIdx.x; i < m.shr_total - m.shr_rf; i += blockDim.x) shr[m.shr_rf + i] = m.rfray[8 * (i >> 2) + (i & 3)];
+    for (int i = threadIdx.x; i < m.shr_rfst - m.shr_rf; i += blockDim.x) shr[m.shr_rf + i] = m.rfray[8 * (i >> 2) + (i & 3)];
+    if (m.rf_mode == 2)
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < m.nrf; i += blockDim.x) shr[m.shr_rfst + i] = m.rf_static[i];
   }
   __syncthreads();
   wsync();
