@@ -60,6 +60,9 @@ mrs_model* mrs_model_load_xml_string(const char* xml, const char* basedir, char*
                                      int error_len);
 /* replaces mj_deleteModel (src/mujoco_system_interface.cpp:512) */
 void mrs_model_free(mrs_model* m);
+/* deep copy of a compiled model (mj_copyModel behind get_model, src/mujoco_system_interface.cpp:
+ * 1794-1798); NULL on a null argument */
+mrs_model* mrs_model_copy(const mrs_model* m);
 /* read-only view of the compiled arrays (mjModel field access throughout the plugin, e.g.
  * jnt_qposadr at src/mujoco_system_interface.cpp:1224); valid while `m` lives */
 int mrs_model_view_get(const mrs_model* m, mrs_model_view* out);

@@ -58,6 +58,14 @@ int mrsp_write(mrsp_system* s, double period_s);
  * physics_thread=false); returns 0, or 1 if the step reported divergence */
 int mrsp_step(mrsp_system* s, int n_steps);
 double mrsp_sim_time(const mrsp_system* s);
+/* get_model(mjModel*&) (reference src/mujoco_system_interface.cpp:1794-1798) on a fresh pointer:
+ * sizes[4] = nq, nv, nu, nsensordata of the deep copy, *timestep = its opt.timestep */
+int mrsp_get_model(mrsp_system* s, int* sizes, double* timestep);
+/* get_data(mjData*&) (:1800-1808): copies of env 0's qpos[nq], qvel[nv], ctrl[nu],
+ * sensordata[nsensordata] and time (any pointer may be NULL) */
+int mrsp_get_data(mrsp_system* s, double* qpos, double* qvel, double* ctrl, double* sensordata, double* time);
+/* set_data(mjData*) (:1810-1814) with a get_data copy whose qpos / qvel / time are replaced */
+int mrsp_set_data(mrsp_system* s, const double* qpos, const double* qvel, double time);
 /* last /clock message (seconds) and the number published */
 double mrsp_clock(const mrsp_system* s, long* count);
 

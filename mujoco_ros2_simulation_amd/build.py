@@ -73,7 +73,7 @@ def build_lib(verbose: bool = False) -> Path:
 
 PLUGIN_LIB = PKG / "libmrs_plugin.so"
 PLUGIN_SOURCES = ["plugin/src/mujoco_system_interface.cpp", "plugin/src/mujoco_lidar.cpp",
-                  "plugin/src/mujoco_cameras.cpp", "plugin/src/plugin_capi.cc", "mjcf/xml.cc"]
+                  "plugin/src/mujoco_cameras.cpp", "plugin/src/mj_types.cpp", "plugin/src/plugin_capi.cc", "mjcf/xml.cc"]
 
 
 def build_plugin(verbose: bool = False) -> Path:

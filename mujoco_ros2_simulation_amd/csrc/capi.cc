@@ -85,6 +85,15 @@ mrs_model* mrs_model_load_xml_string(const char* xml, const char* basedir, char*
 
 void mrs_model_free(mrs_model* m) { delete m; }
 
+mrs_model* mrs_model_copy(const mrs_model* m) {
+  std::unique_ptr<mrs_model> out;
+  int rc = guarded([&] {
+    if (!m) throw std::invalid_argument("null model");
+    out.reset(new mrs_model{m->m});
+  });
+  return rc == MRS_OK ? out.release() : nullptr;
+}
+
 int mrs_model_view_get(const mrs_model* m, mrs_model_view* out) {
   return guarded([&] {
     if (!m || !out) throw std::invalid_argument("null argument");

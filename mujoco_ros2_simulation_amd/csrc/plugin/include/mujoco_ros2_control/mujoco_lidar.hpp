@@ -13,7 +13,7 @@
 
 #include "hardware_interface/hardware_info.hpp"
 #include "mrs.h"
-#include "mujoco_ros2_control/sim_state.hpp"
+#include "mujoco_ros2_control/mj_types.hpp"
 #include "rclcpp/rclcpp.hpp"
 #include "sensor_msgs/msg/laser_scan.hpp"
 
@@ -39,8 +39,8 @@ std::optional<LidarData> get_lidar_data(const hardware_interface::HardwareInfo& 
 
 class MujocoLidar {
  public:
-  MujocoLidar(rclcpp::Node::SharedPtr& node, std::recursive_mutex* sim_mutex, const SimState* sim_state,
-              const mrs_model* model, double lidar_publish_rate);
+  MujocoLidar(rclcpp::Node::SharedPtr& node, std::recursive_mutex* sim_mutex, mjData* mujoco_data,
+              mjModel* mujoco_model, double lidar_publish_rate);
   ~MujocoLidar() { close(); }
   void init();
   void close();
@@ -52,8 +52,8 @@ class MujocoLidar {
   void update_loop();
   rclcpp::Node::SharedPtr node_;
   std::recursive_mutex* sim_mutex_;
-  const SimState* sim_state_;
-  const mrs_model* model_;
+  mjData* mj_data_;
+  mjModel* mj_model_;
   double lidar_publish_rate_;
   std::vector<double> snapshot_;
   std::vector<LidarData> lidar_sensors_;

@@ -1,9 +1,9 @@
 // mujoco_ros2_control/MujocoSystemInterface backed by the MI355X batch simulator.
 //
 // Public API identical to the reference (include/mujoco_ros2_control/mujoco_system_interface.hpp:
-// 61-100) except get_model/get_data/set_data, whose mjModel/mjData types are replaced by the C-ABI
-// model handle and a SimState copy.  MuJoCo is not linked: the physics is libmrs (include/mrs.h),
-// env 0 of a batch is the ROS-visible robot.
+// 61-100), get_model/get_data/set_data included: mjModel / mjData are this library's own
+// (mujoco_ros2_control/mj_types.hpp, MuJoCo field names).  MuJoCo is not linked: the physics is
+// libmrs (include/mrs.h), env 0 of a batch is the ROS-visible robot.
 #pragma once
 
 #include <atomic>
@@ -22,7 +22,7 @@
 #include "mujoco_ros2_control/data.hpp"
 #include "mujoco_ros2_control/mujoco_cameras.hpp"
 #include "mujoco_ros2_control/mujoco_lidar.hpp"
-#include "mujoco_ros2_control/sim_state.hpp"
+#include "mujoco_ros2_control/mj_types.hpp"
 #include "rclcpp/rclcpp.hpp"
 #include "rclcpp_lifecycle/state.hpp"
 #include "realtime_tools/realtime_publisher.hpp"
@@ -45,10 +45,11 @@ class MujocoSystemInterface : public hardware_interface::SystemInterface {
   hardware_interface::return_type read(const rclcpp::Time& time, const rclcpp::Duration& period) override;
   hardware_interface::return_type write(const rclcpp::Time& time, const rclcpp::Duration& period) override;
 
-  // deep copies under the sim mutex (reference :1794-1814)
-  void get_model(const mrs_model*& dest);
-  void get_data(SimState& dest);
-  void set_data(const SimState& src);
+  // deep copies under the sim mutex (reference :1794-1814); dest == nullptr allocates (the caller
+  // frees with mj_deleteModel / mj_deleteData)
+  void get_model(mjModel*& dest);
+  void get_data(mjData*& dest);
+  void set_data(mjData* mj_data);
 
   // --- additions (not in the reference API) used by the test harness and tools
   rclcpp::Node::SharedPtr node() const { return mujoco_node_; }
@@ -75,11 +76,12 @@ class MujocoSystemInterface : public hardware_interface::SystemInterface {
   void pull_state_locked();
 
   std::string model_path_;
-  mrs_model* model_ = nullptr;
+  mjModel* mj_model_ = nullptr;         // owns the compiled model
+  mrs_model* model_ = nullptr;          // mj_model_->handle
   mrs_batch* batch_ = nullptr;
   mrs_model_view view_{};
-  SimState sim_state_;      // latest state of env 0 ("mj_data_")
-  SimState control_state_;  // buffer read()/write() use ("mj_data_control_")
+  mjData* mj_data_ = nullptr;           // latest state of env 0
+  mjData* mj_data_control_ = nullptr;   // buffer read()/write() use
   rclcpp::Logger logger_ = rclcpp::get_logger("MujocoSystemInterface");
   double sim_speed_factor_ = -1;
   bool run_ = true;

@@ -57,17 +57,16 @@ std::optional<LidarData> get_lidar_data(const hardware_interface::HardwareInfo& 
   return d;
 }
 
-MujocoLidar::MujocoLidar(rclcpp::Node::SharedPtr& node, std::recursive_mutex* sim_mutex, const SimState* sim_state,
-                         const mrs_model* model, double lidar_publish_rate)
-    : node_(node), sim_mutex_(sim_mutex), sim_state_(sim_state), model_(model), lidar_publish_rate_(lidar_publish_rate) {}
+MujocoLidar::MujocoLidar(rclcpp::Node::SharedPtr& node, std::recursive_mutex* sim_mutex, mjData* mujoco_data,
+                         mjModel* mujoco_model, double lidar_publish_rate)
+    : node_(node), sim_mutex_(sim_mutex), mj_data_(mujoco_data), mj_model_(mujoco_model), lidar_publish_rate_(lidar_publish_rate) {}
 
 bool MujocoLidar::register_lidar(const hardware_interface::HardwareInfo& hardware_info) {
   lidar_sensors_.clear();
-  mrs_model_view v{};
-  mrs_model_view_get(model_, &v);
+  const mjModel& v = *mj_model_;
   for (int i = 0; i < v.nsensor; ++i) {
     if (v.sensor_type[i] != MRS_SENS_RANGEFINDER) continue;
-    const char* raw = mrs_id2name(model_, MRS_OBJ_SENSOR, i);
+    const char* raw = mrs_id2name(mj_model_->handle, MRS_OBJ_SENSOR, i);
     if (!raw) {
       RCLCPP_WARN_STREAM(node_->get_logger(), "Cannot find a name for lidar sensor at index: " << i << ", skipping!");
       continue;
@@ -125,7 +124,7 @@ void MujocoLidar::update_loop() {
 void MujocoLidar::update() {
   {
     std::lock_guard<std::recursive_mutex> lock(*sim_mutex_);
-    snapshot_ = sim_state_->sensordata;
+    snapshot_.assign(mj_data_->sensordata, mj_data_->sensordata + mj_data_->nsensordata);
   }
   for (auto& lidar : lidar_sensors_) {
     auto& ranges = lidar.laser_scan_msg.ranges;

@@ -118,7 +118,9 @@ MujocoSystemInterface::~MujocoSystemInterface() {
   exit_request_ = true;
   if (physics_thread_.joinable()) physics_thread_.join();
   if (batch_) mrs_batch_free(batch_);
-  if (model_) mrs_model_free(model_);
+  mj_deleteData(mj_data_);
+  mj_deleteData(mj_data_control_);
+  mj_deleteModel(mj_model_);
 }
 
 hi::CallbackReturn MujocoSystemInterface::on_init(const hi::HardwareComponentInterfaceParams& params) {
@@ -153,32 +155,29 @@ hi::CallbackReturn MujocoSystemInterface::on_init(const hi::HardwareComponentInt
 
   // model: file, else the /mujoco_robot_description string (reference :415, :358-413)
   char err[1024] = "";
+  mrs_model* compiled = nullptr;
   if (!model_path_.empty()) {
-    model_ = mrs_model_load_xml(model_path_.c_str(), err, sizeof err);
+    compiled = mrs_model_load_xml(model_path_.c_str(), err, sizeof err);
   } else if (auto xml = compat::robot_description(mujoco_node_)) {
-    model_ = mrs_model_load_xml_string(xml->c_str(), ".", err, sizeof err);
+    compiled = mrs_model_load_xml_string(xml->c_str(), ".", err, sizeof err);
   } else {
     std::snprintf(err, sizeof err, "no 'mujoco_model' parameter and no /mujoco_robot_description");
   }
-  if (!model_) {
+  if (!compiled) {
     load_error_ = err;
     RCLCPP_FATAL(get_logger(), "Failed to load the model: %s", err);
     return hi::CallbackReturn::ERROR;
   }
-  mrs_model_view_get(model_, &view_);
+  mj_model_ = mj_wrapModel(compiled);
+  model_ = compiled;
+  view_ = *mj_model_;
   batch_ = mrs_batch_create(model_, std::max(1, num_envs), device);
   if (!batch_) {
     RCLCPP_FATAL(get_logger(), "Could not create the simulation batch: %s", mrs_last_error());
     return hi::CallbackReturn::ERROR;
   }
-  for (SimState* st : {&sim_state_, &control_state_}) {
-    st->qpos.assign(view_.nq, 0.0);
-    st->qvel.assign(view_.nv, 0.0);
-    st->ctrl.assign(view_.nu, 0.0);
-    st->qfrc_applied.assign(view_.nv, 0.0);
-    st->qfrc_actuator.assign(view_.nv, 0.0);
-    st->sensordata.assign(view_.nsensordata, 0.0);
-  }
+  mj_data_ = mj_makeData(mj_model_);
+  mj_data_control_ = mj_makeData(mj_model_);
   {
     std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
     pull_state_locked();
@@ -194,7 +193,7 @@ hi::CallbackReturn MujocoSystemInterface::on_init(const hi::HardwareComponentInt
 
   cameras_ = std::make_unique<MujocoCameras>(mujoco_node_, &sim_mutex_, batch_, model_, camera_publish_rate);
   cameras_->register_cameras(get_hardware_info());
-  lidar_sensors_ = std::make_unique<MujocoLidar>(mujoco_node_, &sim_mutex_, &sim_state_, model_, lidar_publish_rate);
+  lidar_sensors_ = std::make_unique<MujocoLidar>(mujoco_node_, &sim_mutex_, mj_data_, mj_model_, lidar_publish_rate);
   if (!lidar_sensors_->register_lidar(get_hardware_info())) {
     RCLCPP_INFO(get_logger(), "Failed to initialize lidar, exiting...");
     return hi::CallbackReturn::FAILURE;
@@ -335,7 +334,7 @@ hi::return_type MujocoSystemInterface::perform_command_mode_switch(const std::ve
 
 hi::return_type MujocoSystemInterface::read(const rclcpp::Time&, const rclcpp::Duration&) {
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
-  const SimState& c = control_state_;
+  const mjData& c = *mj_data_control_;
   for (auto& j : joint_states_) {
     if (j.mj_pos_adr < 0) continue;
     j.position = c.qpos[j.mj_pos_adr];
@@ -373,17 +372,17 @@ hi::return_type MujocoSystemInterface::write(const rclcpp::Time&, const rclcpp::
   for (auto& j : joint_states_) {
     if (j.mj_actuator_id == -1) continue;
     if (j.is_position_control_enabled) {
-      control_state_.ctrl[j.mj_actuator_id] = j.position_command;
+      mj_data_control_->ctrl[j.mj_actuator_id] = j.position_command;
     } else if (j.is_position_pid_control_enabled) {
-      const double error = j.position_command - sim_state_.qpos[j.mj_pos_adr];  // live sim state (:1133)
-      control_state_.qfrc_applied[j.mj_vel_adr] = j.pos_pid->compute_command(error, period);
+      const double error = j.position_command - mj_data_->qpos[j.mj_pos_adr];  // live sim state (:1133)
+      mj_data_control_->qfrc_applied[j.mj_vel_adr] = j.pos_pid->compute_command(error, period);
     } else if (j.is_velocity_control_enabled) {
-      control_state_.ctrl[j.mj_actuator_id] = j.velocity_command;
+      mj_data_control_->ctrl[j.mj_actuator_id] = j.velocity_command;
     } else if (j.is_velocity_pid_control_enabled) {
-      const double error = j.velocity_command - sim_state_.qvel[j.mj_vel_adr];
-      control_state_.qfrc_applied[j.mj_vel_adr] = j.vel_pid->compute_command(error, period);
+      const double error = j.velocity_command - mj_data_->qvel[j.mj_vel_adr];
+      mj_data_control_->qfrc_applied[j.mj_vel_adr] = j.vel_pid->compute_command(error, period);
     } else if (j.is_effort_control_enabled) {
-      control_state_.ctrl[j.mj_actuator_id] = j.effort_command;
+      mj_data_control_->ctrl[j.mj_actuator_id] = j.effort_command;
     }
   }
   return hi::return_type::OK;
@@ -432,8 +431,8 @@ void MujocoSystemInterface::register_joints(const hi::HardwareInfo& info) {
     }
     auto initial = [](const hi::InterfaceInfo& ii) { return ii.initial_value.empty() ? 0.0 : std::stod(ii.initial_value); };
     for (const auto& si : joint.state_interfaces) {
-      if (si.name == hi::HW_IF_POSITION) js.position = override_start ? sim_state_.qpos[js.mj_pos_adr] : initial(si);
-      else if (si.name == hi::HW_IF_VELOCITY) js.velocity = override_start ? sim_state_.qvel[js.mj_vel_adr] : initial(si);
+      if (si.name == hi::HW_IF_POSITION) js.position = override_start ? mj_data_->qpos[js.mj_pos_adr] : initial(si);
+      else if (si.name == hi::HW_IF_VELOCITY) js.velocity = override_start ? mj_data_->qvel[js.mj_vel_adr] : initial(si);
       else if (is_effort_name(si.name)) js.effort = initial(si);
     }
     if (aid == -1) {
@@ -442,7 +441,7 @@ void MujocoSystemInterface::register_joints(const hi::HardwareInfo& info) {
     }
     js.actuator_type = static_cast<ActuatorType>(mrs_actuator_type(model_, aid));
     const bool motor_like = js.actuator_type == ActuatorType::MOTOR || js.actuator_type == ActuatorType::CUSTOM;
-    const double ctrl0 = override_start ? sim_state_.ctrl[aid] : 0.0;
+    const double ctrl0 = override_start ? mj_data_->ctrl[aid] : 0.0;
     auto make_pid = [&](const std::string& kind) {
       auto pid = std::make_shared<control_toolbox::PidROS>(mujoco_node_, "pid_gains." + kind + "." + joint.name, "", false);
       const bool ok = pid->initialize_from_ros_parameters();
@@ -593,47 +592,55 @@ bool MujocoSystemInterface::set_override_start_positions(const std::string& file
     return false;
   }
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
-  sim_state_.qpos = v[0];
-  sim_state_.qvel = v[1];
-  sim_state_.ctrl = v[2];
-  control_state_.ctrl = v[2];
-  mrs_batch_set_field(batch_, MRS_FIELD_QPOS, sim_state_.qpos.data(), 0, 1);
-  mrs_batch_set_field(batch_, MRS_FIELD_QVEL, sim_state_.qvel.data(), 0, 1);
-  mrs_batch_set_field(batch_, MRS_FIELD_CTRL, sim_state_.ctrl.data(), 0, 1);
+  std::copy(v[0].begin(), v[0].end(), mj_data_->qpos);
+  std::copy(v[1].begin(), v[1].end(), mj_data_->qvel);
+  std::copy(v[2].begin(), v[2].end(), mj_data_->ctrl);
+  std::copy(v[2].begin(), v[2].end(), mj_data_control_->ctrl);
+  mrs_batch_set_field(batch_, MRS_FIELD_QPOS, mj_data_->qpos, 0, 1);
+  mrs_batch_set_field(batch_, MRS_FIELD_QVEL, mj_data_->qvel, 0, 1);
+  mrs_batch_set_field(batch_, MRS_FIELD_CTRL, mj_data_->ctrl, 0, 1);
   return true;
 }
 
 void MujocoSystemInterface::set_initial_pose() {
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
   for (const auto& j : joint_states_)
-    if (j.mj_pos_adr >= 0) sim_state_.qpos[j.mj_pos_adr] = j.position;
-  mrs_batch_set_field(batch_, MRS_FIELD_QPOS, sim_state_.qpos.data(), 0, 1);
+    if (j.mj_pos_adr >= 0) mj_data_->qpos[j.mj_pos_adr] = j.position;
+  mrs_batch_set_field(batch_, MRS_FIELD_QPOS, mj_data_->qpos, 0, 1);
   mrs_batch_forward(batch_);
   mrs_batch_sync(batch_);
   pull_state_locked();
 }
 
 void MujocoSystemInterface::pull_state_locked() {
-  mrs_batch_get_field(batch_, MRS_FIELD_QPOS, sim_state_.qpos.data(), 0, 1);
-  mrs_batch_get_field(batch_, MRS_FIELD_QVEL, sim_state_.qvel.data(), 0, 1);
-  mrs_batch_get_field(batch_, MRS_FIELD_QFRC_ACTUATOR, sim_state_.qfrc_actuator.data(), 0, 1);
-  if (view_.nsensordata > 0) mrs_batch_get_field(batch_, MRS_FIELD_SENSORDATA, sim_state_.sensordata.data(), 0, 1);
-  mrs_batch_get_field(batch_, MRS_FIELD_TIME, &sim_state_.time, 0, 1);
+  mrs_batch_get_field(batch_, MRS_FIELD_QPOS, mj_data_->qpos, 0, 1);
+  mrs_batch_get_field(batch_, MRS_FIELD_QVEL, mj_data_->qvel, 0, 1);
+  mrs_batch_get_field(batch_, MRS_FIELD_QFRC_ACTUATOR, mj_data_->qfrc_actuator, 0, 1);
+  if (view_.nsensordata > 0) mrs_batch_get_field(batch_, MRS_FIELD_SENSORDATA, mj_data_->sensordata, 0, 1);
+  if (view_.nv > 0) {
+    mrs_batch_get_field(batch_, MRS_FIELD_QACC, mj_data_->qacc, 0, 1);
+    mrs_batch_get_field(batch_, MRS_FIELD_QACC_WARMSTART, mj_data_->qacc_warmstart, 0, 1);
+  }
+  mrs_batch_get_field(batch_, MRS_FIELD_TIME, &mj_data_->time, 0, 1);
   // sim -> control copy of the outputs (mj_copyData(control <- sim), reference :1759); the control
   // inputs ctrl / qfrc_applied stay what write() put there
-  control_state_.qpos = sim_state_.qpos;
-  control_state_.qvel = sim_state_.qvel;
-  control_state_.qfrc_actuator = sim_state_.qfrc_actuator;
-  control_state_.sensordata = sim_state_.sensordata;
-  control_state_.time = sim_state_.time;
+  const mjData& d = *mj_data_;
+  mjData& c = *mj_data_control_;
+  std::copy(d.qpos, d.qpos + d.nq, c.qpos);
+  std::copy(d.qvel, d.qvel + d.nv, c.qvel);
+  std::copy(d.qacc, d.qacc + d.nv, c.qacc);
+  std::copy(d.qacc_warmstart, d.qacc_warmstart + d.nv, c.qacc_warmstart);
+  std::copy(d.qfrc_actuator, d.qfrc_actuator + d.nv, c.qfrc_actuator);
+  std::copy(d.sensordata, d.sensordata + d.nsensordata, c.sensordata);
+  c.time = d.time;
 }
 
 bool MujocoSystemInterface::advance_locked(int n) {
   // control -> sim (reference :1688-1689, with nv for qfrc_applied)
-  sim_state_.ctrl = control_state_.ctrl;
-  sim_state_.qfrc_applied = control_state_.qfrc_applied;
-  if (view_.nu > 0) mrs_batch_set_field(batch_, MRS_FIELD_CTRL, sim_state_.ctrl.data(), 0, 1);
-  if (view_.nv > 0) mrs_batch_set_field(batch_, MRS_FIELD_QFRC_APPLIED, sim_state_.qfrc_applied.data(), 0, 1);
+  std::copy(mj_data_control_->ctrl, mj_data_control_->ctrl + view_.nu, mj_data_->ctrl);
+  std::copy(mj_data_control_->qfrc_applied, mj_data_control_->qfrc_applied + view_.nv, mj_data_->qfrc_applied);
+  if (view_.nu > 0) mrs_batch_set_field(batch_, MRS_FIELD_CTRL, mj_data_->ctrl, 0, 1);
+  if (view_.nv > 0) mrs_batch_set_field(batch_, MRS_FIELD_QFRC_APPLIED, mj_data_->qfrc_applied, 0, 1);
   double before[4], after[4];
   mrs_batch_get_field(batch_, MRS_FIELD_WARNING, before, 0, 1);
   if (mrs_batch_step(batch_, n) != MRS_OK || mrs_batch_sync(batch_) != MRS_OK) {
@@ -663,14 +670,14 @@ void MujocoSystemInterface::PhysicsLoop() {
       if (run_) {
         const auto start_cpu = Clock::now();
         const double elapsed_cpu = std::chrono::duration<double>(start_cpu - sync_cpu).count();
-        const double elapsed_sim = sim_state_.time - sync_sim;
+        const double elapsed_sim = mj_data_->time - sync_sim;
         const double slowdown = sim_speed_factor_ > 0 ? 1.0 / sim_speed_factor_ : 1.0;  // UI default 100%
         const bool misaligned = std::abs(elapsed_cpu / slowdown - elapsed_sim) > kSyncMisalign;
         int n = 0;
         if (!synced || elapsed_sim < 0 || misaligned) {
           // out of sync: re-sync and take one step (reference :1679-1703)
           sync_cpu = start_cpu;
-          sync_sim = sim_state_.time;
+          sync_sim = mj_data_->time;
           synced = true;
           n = 1;
         } else {
@@ -703,7 +710,7 @@ bool MujocoSystemInterface::step_physics(int n) {
 
 double MujocoSystemInterface::sim_time() const {
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
-  return sim_state_.time;
+  return mj_data_->time;
 }
 
 void MujocoSystemInterface::publish_clock() {
@@ -716,23 +723,33 @@ void MujocoSystemInterface::publish_clock() {
   clock_realtime_publisher_->try_publish(msg);
 }
 
-void MujocoSystemInterface::get_model(const mrs_model*& dest) {
+void MujocoSystemInterface::get_model(mjModel*& dest) {
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
-  dest = model_;
+  dest = mj_copyModel(dest, mj_model_);
 }
 
-void MujocoSystemInterface::get_data(SimState& dest) {
+void MujocoSystemInterface::get_data(mjData*& dest) {
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
-  dest = sim_state_;
+  if (dest == nullptr) dest = mj_makeData(mj_model_);
+  mj_copyData(dest, mj_model_, mj_data_);
 }
 
-void MujocoSystemInterface::set_data(const SimState& src) {
+// mj_copyData(mj_data_ <- mj_data) (reference :1810-1814), then the arrays go to env 0 and a forward
+// pass recomputes the outputs (qacc, qfrc_actuator, sensordata) from the new state
+void MujocoSystemInterface::set_data(mjData* mj_data) {
   std::lock_guard<std::recursive_mutex> lock(sim_mutex_);
-  sim_state_.qpos = src.qpos;
-  sim_state_.qvel = src.qvel;
-  mrs_batch_set_field(batch_, MRS_FIELD_QPOS, sim_state_.qpos.data(), 0, 1);
-  mrs_batch_set_field(batch_, MRS_FIELD_QVEL, sim_state_.qvel.data(), 0, 1);
-  mrs_batch_set_field(batch_, MRS_FIELD_TIME, &src.time, 0, 1);
+  if (!mj_copyData(mj_data_, mj_model_, mj_data)) {
+    RCLCPP_ERROR(get_logger(), "set_data: mjData was made for a different model");
+    return;
+  }
+  mrs_batch_set_field(batch_, MRS_FIELD_QPOS, mj_data_->qpos, 0, 1);
+  if (view_.nv > 0) {
+    mrs_batch_set_field(batch_, MRS_FIELD_QVEL, mj_data_->qvel, 0, 1);
+    mrs_batch_set_field(batch_, MRS_FIELD_QACC_WARMSTART, mj_data_->qacc_warmstart, 0, 1);
+    mrs_batch_set_field(batch_, MRS_FIELD_QFRC_APPLIED, mj_data_->qfrc_applied, 0, 1);
+  }
+  if (view_.nu > 0) mrs_batch_set_field(batch_, MRS_FIELD_CTRL, mj_data_->ctrl, 0, 1);
+  mrs_batch_set_field(batch_, MRS_FIELD_TIME, &mj_data_->time, 0, 1);
   mrs_batch_forward(batch_);
   mrs_batch_sync(batch_);
   pull_state_locked();

@@ -1,5 +1,6 @@
 // C entry points of the plugin host (include/mrs_plugin.h): URDF <ros2_control> parsing with the
 // xacro subset the reference's test robot uses, lifecycle and read/write driving.
+#include <algorithm>
 #include "mrs_plugin.h"
 
 #include <cstring>
@@ -297,6 +298,49 @@ int mrsp_step(mrsp_system* s, int n_steps) {
 }
 
 double mrsp_sim_time(const mrsp_system* s) { return s && s->plugin ? s->plugin->sim_time() : -1.0; }
+
+int mrsp_get_model(mrsp_system* s, int* sizes, double* timestep) {
+  if (!s || !s->plugin) return fail("plugin not initialised");
+  mjModel* m = nullptr;
+  s->plugin->get_model(m);
+  if (!m) return fail("get_model failed");
+  if (sizes) {
+    sizes[0] = m->nq;
+    sizes[1] = m->nv;
+    sizes[2] = m->nu;
+    sizes[3] = m->nsensordata;
+  }
+  if (timestep) *timestep = m->opt.timestep;
+  mj_deleteModel(m);
+  return 0;
+}
+
+int mrsp_get_data(mrsp_system* s, double* qpos, double* qvel, double* ctrl, double* sensordata, double* time) {
+  if (!s || !s->plugin) return fail("plugin not initialised");
+  mjData* d = nullptr;
+  s->plugin->get_data(d);
+  if (!d) return fail("get_data failed");
+  if (qpos) std::copy(d->qpos, d->qpos + d->nq, qpos);
+  if (qvel) std::copy(d->qvel, d->qvel + d->nv, qvel);
+  if (ctrl) std::copy(d->ctrl, d->ctrl + d->nu, ctrl);
+  if (sensordata) std::copy(d->sensordata, d->sensordata + d->nsensordata, sensordata);
+  if (time) *time = d->time;
+  mj_deleteData(d);
+  return 0;
+}
+
+int mrsp_set_data(mrsp_system* s, const double* qpos, const double* qvel, double time) {
+  if (!s || !s->plugin) return fail("plugin not initialised");
+  mjData* d = nullptr;
+  s->plugin->get_data(d);
+  if (!d) return fail("get_data failed");
+  if (qpos) std::copy(qpos, qpos + d->nq, d->qpos);
+  if (qvel) std::copy(qvel, qvel + d->nv, d->qvel);
+  d->time = time;
+  s->plugin->set_data(d);
+  mj_deleteData(d);
+  return 0;
+}
 
 double mrsp_clock(const mrsp_system* s, long* count) {
   if (!s || !s->plugin) return -1.0;

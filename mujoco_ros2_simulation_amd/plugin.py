@@ -51,6 +51,9 @@ def lib() -> C.CDLL:
             "mrsp_step": (I, [P, I]),
             "mrsp_sim_time": (D, [P]),
             "mrsp_clock": (D, [P, C.POINTER(C.c_long)]),
+            "mrsp_get_model": (I, [P, C.POINTER(C.c_int), C.POINTER(C.c_double)]),
+            "mrsp_get_data": (I, [P] + [C.POINTER(C.c_double)] * 5),
+            "mrsp_set_data": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_double), D]),
             "mrsp_lidar_update": (I, [P]),
             "mrsp_last_scan": (I, [P, S, F, I, F]),
             "mrsp_camera_update": (I, [P]),
@@ -190,6 +193,31 @@ class System:
     @property
     def sim_time(self) -> float:
         return lib().mrsp_sim_time(self._h)
+
+    # -- get_model / get_data / set_data (reference src/mujoco_system_interface.cpp:1794-1814)
+    def get_model(self) -> dict:
+        sizes, dt = (C.c_int * 4)(), C.c_double(0)
+        if lib().mrsp_get_model(self._h, sizes, C.byref(dt)) != 0:
+            raise PluginError(_err())
+        return {"nq": sizes[0], "nv": sizes[1], "nu": sizes[2], "nsensordata": sizes[3], "timestep": dt.value}
+
+    def get_data(self) -> dict:
+        m = self.get_model()
+        out = {k: np.zeros(m[n]) for k, n in (("qpos", "nq"), ("qvel", "nv"), ("ctrl", "nu"), ("sensordata", "nsensordata"))}
+        t = C.c_double(0)
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        if lib().mrsp_get_data(self._h, ptr(out["qpos"]), ptr(out["qvel"]), ptr(out["ctrl"]), ptr(out["sensordata"]),
+                               C.byref(t)) != 0:
+            raise PluginError(_err())
+        out["time"] = t.value
+        return out
+
+    def set_data(self, qpos, qvel, time: float) -> None:
+        q = np.ascontiguousarray(qpos, dtype=np.float64)
+        v = np.ascontiguousarray(qvel, dtype=np.float64)
+        ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        if lib().mrsp_set_data(self._h, ptr(q), ptr(v), float(time)) != 0:
+            raise PluginError(_err())
 
     def clock(self) -> tuple[float, int]:
         n = C.c_long(0)

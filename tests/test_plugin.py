@@ -220,6 +220,43 @@ REF_SCENE = GOLD / "ref_scenes" / "scene.xml"
 PID_SCENE = GOLD / "ref_scenes" / "test_pid" / "scene_pid.xml"
 
 
+def test_mj_types_lifecycle(built, tmp_path):
+    """mjModel / mjData behind get_model / get_data / set_data (csrc/plugin/src/mj_types.cpp): deep
+    copies, dest == nullptr allocation, the copy outliving its source, size checks (no GPU)"""
+    import subprocess
+    from mujoco_ros2_simulation_amd import plugin
+    pkg = plugin.LIB_PATH.parent
+    exe = tmp_path / "mj_types_check"
+    subprocess.run(["g++", "-std=c++17", "-O1", str(ROOT / "tests" / "fixtures" / "mj_types_check.cc"),
+                    f"-I{ROOT / 'include'}", f"-I{pkg / 'csrc' / 'plugin' / 'include'}",
+                    f"-L{pkg}", "-lmrs_plugin", "-lmrs", f"-Wl,-rpath,{pkg}", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), str(GOLD / "ref_scenes" / "test_robot.xml")], capture_output=True, text=True)
+    assert out.stdout.strip() == "ok", out.stdout + out.stderr
+
+
+@pytest.mark.gpu
+def test_get_model_get_data_set_data(pkg_dir):
+    """reference-typed accessors (src/mujoco_system_interface.cpp:1794-1814): get_model returns the
+    scene's sizes; get_data reflects the stepped state; set_data moves env 0 and the next read() reports
+    it"""
+    from mujoco_ros2_simulation_amd import plugin
+    s = make_system(pkg_dir, physics_thread="false")
+    assert s.on_init() == plugin.SUCCESS
+    m = s.get_model()
+    assert (m["nq"], m["nv"], m["nu"]) == (2, 2, 2) and m["timestep"] > 0
+    drive(s, [0.3, -0.2], 10, 10)
+    d = s.get_data()
+    assert math.isclose(d["time"], s.sim_time, abs_tol=1e-9)
+    s.read()
+    assert math.isclose(s.state("joint1/position"), d["qpos"][0], abs_tol=1e-6)
+    s.set_data([0.7, -0.4], [0.0, 0.0], 5.0)
+    e = s.get_data()
+    np.testing.assert_allclose(e["qpos"], [0.7, -0.4], atol=1e-6)
+    assert math.isclose(e["time"], 5.0) and math.isclose(s.sim_time, 5.0)
+    s.read()
+    assert math.isclose(s.state("joint1/position"), 0.7, abs_tol=1e-6)
+
+
 @pytest.mark.gpu
 def test_arm_position_mode(pkg_dir):
     """robot_launch_test.py::test_arm: command [0.5, -0.5]; |q - cmd| < 0.05 after 2.0 s of sim time
