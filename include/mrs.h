@@ -112,6 +112,12 @@ int mrs_batch_forward(mrs_batch* b);
 int mrs_batch_render_depth(mrs_batch* b, int cam, int env0, int n, float* host_out);
 /* same, into a device buffer [n][H][W] (stays in HBM) */
 int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float* d_out);
+/* depth and colour in one pass (the RGB8 image of src/mujoco_cameras.cpp:211-240): depth as above,
+ * rgb [n][H][W][3] uint8, ROS row order, flat headlight shading of each pixel's nearest geom
+ * (rgba x (0.3 + 0.7 max(0, -n.d))), black where nothing is hit -- not an OpenGL raster match */
+int mrs_batch_render_rgbd(mrs_batch* b, int cam, int env0, int n, float* host_depth, unsigned char* host_rgb);
+/* same, into device buffers */
+int mrs_batch_render_rgbd_device(mrs_batch* b, int cam, int env0, int n, float* d_depth, unsigned char* d_rgb);
 /* mjData.contact of env `env` after its last step / forward (the output of mj_collision, SURVEY.md
  * §8a row a2.3): up to `max` contacts in mj_collision's order -- geom [max][2] int32 (geom1, geom2,
  * the lower geom type first), dist [max], pos [max][3], frame [max][9] fp64 (normal = frame[0:3]);

@@ -80,6 +80,8 @@ int mrsp_camera_update(mrsp_system* s);
 int mrsp_last_depth(const mrsp_system* s, const char* topic, float* depth, int max, int* wh);
 int mrsp_last_camera_info(const mrsp_system* s, const char* topic, double* k9, double* p12, int* wh);
 int mrsp_last_image(const mrsp_system* s, const char* topic, int* wh_step, char* encoding, int len);
+/* the bytes of the last Image on `topic` (up to max copied); returns the message's byte count */
+int mrsp_last_image_data(const mrsp_system* s, const char* topic, unsigned char* out, int max);
 
 /* host-logic hooks (no GPU needed):
  * parse_lidar_name: "<name>-<digits>" -> index (or -1), name copied to buf (reference

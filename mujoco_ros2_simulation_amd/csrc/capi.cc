@@ -210,6 +210,20 @@ int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float*
   });
 }
 
+int mrs_batch_render_rgbd(mrs_batch* b, int cam, int env0, int n, float* host_depth, unsigned char* host_rgb) {
+  return guarded([&] {
+    if (!b || !host_depth || !host_rgb) throw std::invalid_argument("null argument");
+    mrs::batch_render_depth(b->impl, cam, env0, n, host_depth, false, host_rgb);
+  });
+}
+
+int mrs_batch_render_rgbd_device(mrs_batch* b, int cam, int env0, int n, float* d_depth, unsigned char* d_rgb) {
+  return guarded([&] {
+    if (!b || !d_depth || !d_rgb) throw std::invalid_argument("null argument");
+    mrs::batch_render_depth(b->impl, cam, env0, n, d_depth, true, d_rgb);
+  });
+}
+
 int mrs_batch_get_contacts(mrs_batch* b, int env, int max, int* geom, double* dist, double* pos, double* frame) {
   int ncon = 0;
   const int rc = guarded([&] {

@@ -23,7 +23,8 @@ void batch_get(BatchImpl* b, int field, double* host, int env0, int n);
 void* batch_device_ptr(BatchImpl* b, int field);
 void batch_set_ctrl_device(BatchImpl* b, const float* d_ctrl);
 void batch_launch(BatchImpl* b, int n_steps, bool forward_only);
-void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out);
+// rgb (may be null): n * H * W * 3 bytes, same host/device side as out
+void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out, unsigned char* rgb = nullptr);
 int batch_get_contacts(BatchImpl* b, int env, int max, int* geom, double* dist, double* pos, double* frame);
 int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force);
 void batch_get_field_device(BatchImpl* b, int field, float* d_out, int env0, int n);

@@ -118,6 +118,47 @@ __device__ float ray_prim(int type, const float* s, const float lp[3], const flo
 }
 
 
+// ---- colour: flat headlight shading of the nearest geom (oracle.c orc_render_rgb restates it).
+// The reference renders RGB with OpenGL (mjr_render, src/mujoco_cameras.cpp:211-240); this is not a
+// rasteriser match: colour = rgba * (kAmbient + kDiffuse * max(0, -n.d)) with n the surface normal
+// at the hit and d the unit pixel ray, background black.
+constexpr float kAmbient = 0.3f, kDiffuse = 0.7f;
+__device__ __forceinline__ void local_normal(int type, const float* s, const float p[3], float n[3]) {
+  n[0] = 0; n[1] = 0; n[2] = 1;
+  switch (type) {
+    case MRS_GEOM_SPHERE: n[0] = p[0]; n[1] = p[1]; n[2] = p[2]; break;
+    case MRS_GEOM_CAPSULE: n[0] = p[0]; n[1] = p[1]; n[2] = p[2] - fminf(fmaxf(p[2], -s[1]), s[1]); break;
+    case MRS_GEOM_ELLIPSOID: n[0] = p[0] / (s[0] * s[0]); n[1] = p[1] / (s[1] * s[1]); n[2] = p[2] / (s[2] * s[2]); break;
+    case MRS_GEOM_CYLINDER: {
+      const float rr = sqrtf(p[0] * p[0] + p[1] * p[1]);
+      if (fabsf(p[2]) - s[1] > rr - s[0]) { n[0] = 0; n[1] = 0; n[2] = p[2] >= 0 ? 1.0f : -1.0f; }
+      else { n[0] = p[0]; n[1] = p[1]; n[2] = 0; }
+      break;
+    }
+    case MRS_GEOM_BOX: {
+      int k = 0;
+      float best = fabsf(p[0]) / s[0];
+      for (int i = 1; i < 3; ++i)
+        if (fabsf(p[i]) / s[i] > best) { best = fabsf(p[i]) / s[i]; k = i; }
+      n[0] = 0; n[1] = 0; n[2] = 0;
+      n[k] = p[k] >= 0 ? 1.0f : -1.0f;
+      break;
+    }
+    default: break;
+  }
+}
+// Lambert term max(0, -cos) between the (unnormalised) normal nv and ray v, both in one frame
+__device__ __forceinline__ float lambert(const float nv[3], const float v[3]) {
+  const float nn = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
+  const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const float c = -(nv[0] * v[0] + nv[1] * v[1] + nv[2] * v[2]) * rsqrtf(fmaxf(nn * vv, 1e-30f));
+  return fmaxf(c, 0.0f);
+}
+__device__ __forceinline__ void shade(const float* rgba, float lam, unsigned char* px) {
+  const float k = kAmbient + kDiffuse * lam;
+  for (int c = 0; c < 3; ++c) px[c] = static_cast<unsigned char>(fminf(fmaxf(rgba[c] * k, 0.0f), 1.0f) * 255.0f + 0.5f);
+}
+
 // One workgroup renders a 16x16-pixel tile of one env.  The tile's pixel rays lie inside a cone
 // (apex at the camera, axis through the tile centre, half-angle to the widest corner ray); a geom
 // whose bounding sphere misses that cone, or a plane no ray of the cone can reach, is skipped by the
@@ -128,7 +169,8 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
                                                     const float* geom_rgba, int ngeom, const float* geom_xpos,
                                                     const float* geom_xmat, const float* cam_xpos,
                                                     const float* cam_xmat, int ncam, int cam, int env0, int W,
-                                                    int H, float f, float znear, float zfar, float* out) {
+                                                    int H, float f, float znear, float zfar, float* out,
+                                                    unsigned char* rgb) {
   __shared__ float gp[kMaxRenderGeoms * 3];
   __shared__ float gm[kMaxRenderGeoms * 9];
   __shared__ float cpos[3], cmat[9];
@@ -199,6 +241,7 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
                         cmat[6] * dc[0] + cmat[7] * dc[1] + cmat[8] * dc[2]};
   const float vv = vec[0] * vec[0] + vec[1] * vec[1] + vec[2] * vec[2];
   float best = -1;
+  int bestg = -1;
   const int nc = ncand;
   for (int i = 0; i < nc; ++i) {
     const int g = cand[i];
@@ -219,9 +262,24 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
                          mm[1] * vec[0] + mm[4] * vec[1] + mm[7] * vec[2],
                          mm[2] * vec[0] + mm[5] * vec[1] + mm[8] * vec[2]};
     const float tt = ray_prim(t, geom_size + 3 * g, lp, lv);
-    if (tt >= znear && (best < 0 || tt < best)) best = tt;
+    if (tt >= znear && (best < 0 || tt < best)) { best = tt; bestg = g; }
   }
-  out[(size_t)blockIdx.y * W * H + pix] = (best < 0 || best > zfar) ? zfar : best;
+  const bool hit = !(best < 0 || best > zfar);
+  out[(size_t)blockIdx.y * W * H + pix] = hit ? best : zfar;
+  if (rgb) {
+    unsigned char* px = rgb + ((size_t)blockIdx.y * W * H + pix) * 3;
+    if (!hit) { px[0] = px[1] = px[2] = 0; return; }
+    const float* p = gp + 3 * bestg;
+    const float* mm = gm + 9 * bestg;
+    const float dv[3] = {cpos[0] - p[0], cpos[1] - p[1], cpos[2] - p[2]};
+    float q[3], nl[3], nw[3];
+    for (int i = 0; i < 3; ++i)
+      q[i] = mm[i] * dv[0] + mm[3 + i] * dv[1] + mm[6 + i] * dv[2] +
+             best * (mm[i] * vec[0] + mm[3 + i] * vec[1] + mm[6 + i] * vec[2]);
+    local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
+    for (int i = 0; i < 3; ++i) nw[i] = mm[3 * i] * nl[0] + mm[3 * i + 1] * nl[1] + mm[3 * i + 2] * nl[2];
+    shade(geom_rgba + 4 * bestg, lambert(nw, vec), px);
+  }
 }
 
 // ---- depth kernel v2 (ngeom <= 64): one workgroup renders a whole frame of one env.  The
@@ -239,9 +297,10 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
 #define MRS_DEPTH_TILE_H 16  // measured C4 (2048 frames): 4 rows 2.08 ms, 8 rows 1.70, 16 rows 1.68, 32 rows 2.13
 #endif
 constexpr int kDepthTileW = 64, kDepthTileH = MRS_DEPTH_TILE_H, kDepthGeoms = 64;
-struct DepthGeom {  // 24 floats in LDS
+struct DepthGeom {  // 28 floats in LDS
   float lp[3], A[9], size[3];  // row i of A = R'C is also the geom's axis i in the camera frame
   float cc[3], ext[3];         // cull: centre in the camera frame, oriented-box half extents
+  float rgba[3];               // colour (RGB output)
   int type, vis;
 };
 __device__ __forceinline__ float ray_box_slab(const float* s, const float lp[3], const float lv[3]) {
@@ -266,7 +325,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                                                        const float* geom_xpos, const float* geom_xmat,
                                                        const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
                                                        int env0, int W, int H, float f, float znear, float zfar,
-                                                       float* out) {
+                                                       float* out, unsigned char* rgb) {
   __shared__ DepthGeom G[kDepthGeoms];
   const int env = env0 + blockIdx.x;
   const size_t eo = static_cast<size_t>(env);
@@ -292,6 +351,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       o.cc[i] = -(C[i] * d[0] + C[3 + i] * d[1] + C[6 + i] * d[2]);
     }
     o.type = geom_type[g];
+    for (int c = 0; c < 3; ++c) o.rgba[c] = geom_rgba[4 * g + c];
     const float s0 = o.size[0], s1 = o.size[1], s2 = o.size[2];
     float e[3] = {s0, s0, s0};
     switch (o.type) {
@@ -347,9 +407,11 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
     const int col = tx * kDepthTileW + lane;
     const float dx = (col + 0.5f - 0.5f * W) / f;
     float best[kDepthTileH], dy[kDepthTileH];
+    int bestg[kDepthTileH];
 #pragma unroll
     for (int k = 0; k < kDepthTileH; ++k) {
       best[k] = -1;
+      bestg[k] = 0;
       dy[k] = (0.5f * H - (ty * kDepthTileH + k) - 0.5f) / f;
     }
     while (cand) {
@@ -367,7 +429,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         float t;
         if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
         else t = ray_prim(type, sz, lp, lv);
-        if (t >= znear && (best[k] < 0 || t < best[k])) best[k] = t;
+        if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
     }
     if (col < W) {
@@ -375,6 +437,23 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       for (int k = 0; k < kDepthTileH; ++k) {
         const int row = ty * kDepthTileH + k;
         if (row < H) img[static_cast<size_t>(row) * W + col] = (best[k] < 0 || best[k] > zfar) ? zfar : best[k];
+      }
+      if (rgb) {
+        unsigned char* frame = rgb + static_cast<size_t>(blockIdx.x) * W * H * 3;
+        for (int k = 0; k < kDepthTileH; ++k) {
+          const int row = ty * kDepthTileH + k;
+          if (row >= H) break;
+          unsigned char* px = frame + (static_cast<size_t>(row) * W + col) * 3;
+          if (best[k] < 0 || best[k] > zfar) { px[0] = px[1] = px[2] = 0; continue; }
+          const DepthGeom& o = G[bestg[k]];
+          // hit point in the geom frame lp + t lv; normal back to the camera frame through A's rows
+          const float v[3] = {dx, dy[k], -1.0f};
+          float q[3], nl[3], nc[3];
+          for (int i = 0; i < 3; ++i) q[i] = o.lp[i] + best[k] * (o.A[3 * i] * dx + o.A[3 * i + 1] * dy[k] - o.A[3 * i + 2]);
+          local_normal(o.type, o.size, q, nl);
+          for (int j = 0; j < 3; ++j) nc[j] = nl[0] * o.A[j] + nl[1] * o.A[3 + j] + nl[2] * o.A[6 + j];
+          shade(o.rgba, lambert(nc, v), px);
+        }
       }
     }
   }
@@ -1098,7 +1177,7 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   b->ev_valid[0] = true;
 }
 
-void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out) {
+void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out, unsigned char* rgb_out) {
   const Model& m = *b->model;
   if (cam < 0 || cam >= m.ncam) throw std::invalid_argument("camera index out of range");
   if (env0 < 0 || n < 1 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
@@ -1106,11 +1185,14 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
   HIP_CHECK(hipSetDevice(b->device));
   const int W = m.cam_resolution[2 * cam], H = m.cam_resolution[2 * cam + 1];
   const size_t bytes = static_cast<size_t>(n) * W * H * sizeof(float);
+  const size_t rgb_bytes = rgb_out ? static_cast<size_t>(n) * W * H * 3 : 0;
   float* dout = out;
+  unsigned char* drgb = rgb_out;
   void* tmp = nullptr;
   if (!device_out) {
-    HIP_CHECK(hipMallocAsync(&tmp, bytes, b->stream));
+    HIP_CHECK(hipMallocAsync(&tmp, bytes + rgb_bytes, b->stream));
     dout = static_cast<float*>(tmp);
+    if (rgb_out) drgb = static_cast<unsigned char*>(tmp) + bytes;
   }
   const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
   const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
@@ -1119,18 +1201,19 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
   if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
     hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb);
   } else {
     dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
     hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
                        d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb);
   }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(b->ev1[1], b->stream));
   b->ev_valid[1] = true;
   if (!device_out) {
     HIP_CHECK(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, b->stream));
+    if (rgb_out) HIP_CHECK(hipMemcpyAsync(rgb_out, drgb, rgb_bytes, hipMemcpyDeviceToHost, b->stream));
     HIP_CHECK(hipFreeAsync(tmp, b->stream));
     HIP_CHECK(hipStreamSynchronize(b->stream));
   }

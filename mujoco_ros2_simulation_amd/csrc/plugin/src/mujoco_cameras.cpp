@@ -1,7 +1,7 @@
-// Camera wrapper (behaviour of the reference's src/mujoco_cameras.cpp).  Depth comes from the HIP
-// ray-cast depth kernel (mrs_batch_render_depth, env 0) — already in ROS row order and linear
+// Camera wrapper (behaviour of the reference's src/mujoco_cameras.cpp).  Depth and colour come from
+// the HIP ray-cast kernel (mrs_batch_render_rgbd, env 0) — already in ROS row order, depth in linear
 // eye-space metres, so the reference's OpenGL readback, flip and linearisation loops (:211-250) have
-// no counterpart.  No GL context: init() cannot fail for lack of a display.
+// no counterpart.  Colour is flat headlight shading of geom rgba, not an OpenGL raster match.  No GL context: init() cannot fail for lack of a display.
 #include "mujoco_ros2_control/mujoco_cameras.hpp"
 
 #include <cmath>
@@ -103,8 +103,8 @@ void MujocoCameras::update() {
     // the physics thread from stepping underneath it (mjv_copyData under the lock, reference :199-203)
     std::lock_guard<std::recursive_mutex> lock(*sim_mutex_);
     for (auto& cam : cameras_)
-      if (mrs_batch_render_depth(batch_, cam.cam_id, 0, 1, cam.depth.data()) != MRS_OK)
-        RCLCPP_ERROR(node_->get_logger(), "depth render of camera %s failed: %s", cam.name.c_str(), mrs_last_error());
+      if (mrs_batch_render_rgbd(batch_, cam.cam_id, 0, 1, cam.depth.data(), cam.image.data.data()) != MRS_OK)
+        RCLCPP_ERROR(node_->get_logger(), "render of camera %s failed: %s", cam.name.c_str(), mrs_last_error());
   }
   for (auto& cam : cameras_) {
     std::memcpy(cam.depth_image.data.data(), cam.depth.data(), cam.depth_image.data.size());

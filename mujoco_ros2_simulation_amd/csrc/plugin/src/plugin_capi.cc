@@ -1,8 +1,8 @@
 // C entry points of the plugin host (include/mrs_plugin.h): URDF <ros2_control> parsing with the
 // xacro subset the reference's test robot uses, lifecycle and read/write driving.
-#include <algorithm>
 #include "mrs_plugin.h"
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -412,6 +412,17 @@ int mrsp_last_image(const mrsp_system* s, const char* topic, int* wh_step, char*
   if (wh_step) { wh_step[0] = static_cast<int>(m->width); wh_step[1] = static_cast<int>(m->height); wh_step[2] = static_cast<int>(m->step); }
   copy_out(m->encoding, encoding, len);
   return static_cast<int>(m->data.size());
+}
+
+int mrsp_last_image_data(const mrsp_system* s, const char* topic, unsigned char* out, int max) {
+  NEED_PLUGIN(s);
+  auto pub = s->plugin->node()->find_publisher<sensor_msgs::msg::Image>(topic);
+  if (!pub) return fail(std::string("no publisher on ") + topic);
+  auto m = pub->last();
+  if (!m) return fail(std::string("nothing published on ") + topic);
+  const int n = static_cast<int>(m->data.size());
+  if (out) std::memcpy(out, m->data.data(), static_cast<size_t>(std::min(n, std::max(max, 0))));
+  return n;
 }
 
 int mrsp_parse_lidar_name(const char* sensor_name, char* buf, int len) {

@@ -60,6 +60,7 @@ def lib() -> C.CDLL:
             "mrsp_last_depth": (I, [P, S, F, I, C.POINTER(C.c_int)]),
             "mrsp_last_camera_info": (I, [P, S, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
             "mrsp_last_image": (I, [P, S, C.POINTER(C.c_int), S, I]),
+            "mrsp_last_image_data": (I, [P, S, C.c_void_p, I]),
             "mrsp_batch": (P, [P]),
             "mrsp_parse_lidar_name": (I, [S, S, I]),
             "mrsp_lidar_config": (I, [P, S, C.POINTER(C.c_double), S, I]),
@@ -266,6 +267,14 @@ class System:
         if n < 0:
             raise PluginError(_err())
         return {"width": whs[0], "height": whs[1], "step": whs[2], "encoding": enc.value.decode(), "bytes": n}
+
+    def last_image_data(self, topic: str) -> np.ndarray:
+        """the last Image's bytes on `topic`, as [height, width, channels] uint8"""
+        meta = self.last_image(topic)
+        out = np.zeros(meta["bytes"], dtype=np.uint8)
+        if lib().mrsp_last_image_data(self._h, topic.encode(), out.ctypes.data, out.size) < 0:
+            raise PluginError(_err())
+        return out.reshape(meta["height"], meta["width"], -1)
 
     def batch_handle(self):
         return lib().mrsp_batch(self._h)

@@ -135,6 +135,8 @@ def lib() -> C.CDLL:
         L.mrs_batch_forward.argtypes = [C.c_void_p]
         L.mrs_batch_render_depth.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.mrs_batch_render_depth_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.mrs_batch_render_rgbd.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.mrs_batch_render_rgbd_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.mrs_batch_sync.argtypes = [C.c_void_p]
         L.mrs_batch_get_contacts.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p]
@@ -300,6 +302,17 @@ class Batch:
         out = np.empty((n, H, W), dtype=np.float32)
         _check(lib().mrs_batch_render_depth(self._h, cam, env0, n, out.ctypes.data))
         return out
+
+    def render_rgbd(self, cam: int, env0: int = 0, n: int = 1) -> tuple[np.ndarray, np.ndarray]:
+        """(depth [n, H, W] fp32, rgb [n, H, W, 3] uint8) in one pass"""
+        W, H = self.model.cam_resolution[cam]
+        depth = np.empty((n, H, W), dtype=np.float32)
+        rgb = np.empty((n, H, W, 3), dtype=np.uint8)
+        _check(lib().mrs_batch_render_rgbd(self._h, cam, env0, n, depth.ctypes.data, rgb.ctypes.data))
+        return depth, rgb
+
+    def render_rgbd_device(self, cam: int, env0: int, n: int, depth_ptr: int, rgb_ptr: int) -> None:
+        _check(lib().mrs_batch_render_rgbd_device(self._h, cam, env0, n, C.c_void_p(depth_ptr), C.c_void_p(rgb_ptr)))
 
     def render_depth_device(self, cam: int, env0: int, n: int, dptr: int) -> None:
         _check(lib().mrs_batch_render_depth_device(self._h, cam, env0, n, C.c_void_p(dptr)))

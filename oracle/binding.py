@@ -46,6 +46,7 @@ def lib():
         L.orc_ray.restype = C.c_double
         L.orc_ray.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P, C.c_int, C.POINTER(C.c_int)]
         L.orc_render_depth.argtypes = [C.c_void_p, C.POINTER(OrcData), C.c_int, C.POINTER(C.c_float)]
+        L.orc_render_rgbd.argtypes = [C.c_void_p, C.POINTER(OrcData), C.c_int, C.c_void_p, C.c_void_p]
         L.orc_contacts.argtypes = [C.POINTER(OrcData), C.c_int, C.POINTER(C.c_int), P, P, P]
         L.orc_candidate_pairs.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_smooth.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P]
@@ -134,6 +135,13 @@ class OracleData:
         out = np.zeros((H, W), dtype=np.float32)
         lib().orc_render_depth(self._mv, self._d, cam, out.ctypes.data_as(C.POINTER(C.c_float)))
         return out
+
+    def render_rgbd(self, cam: int) -> tuple[np.ndarray, np.ndarray]:
+        W, H = self.model.cam_resolution[cam]
+        depth = np.zeros((H, W), dtype=np.float32)
+        rgb = np.zeros((H, W, 3), dtype=np.uint8)
+        lib().orc_render_rgbd(self._mv, self._d, cam, depth.ctypes.data, rgb.ctypes.data)
+        return depth, rgb
 
     def contacts(self, max_n: int = 256):
         g = np.zeros(2 * max_n, dtype=np.int32)

@@ -1873,7 +1873,40 @@ int orc_contacts(orc_data* d, int max, int* geom, double* dist, double* pos, dou
  * intrinsics :119-123), eye-space depth = ray parameter along the camera -z axis, geoms of groups
  * 0-2 (mjvOption default), hits nearer than znear*extent ignored, misses -> far = zfar*extent.
  * Row 0 is the top row (the plugin's vertical flip, :229-240, already applied). */
-void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out) {
+/* colour of a hit: flat headlight shading rgba * (0.3 + 0.7 max(0, -n.d)) of the geom's surface
+ * normal n at the hit and the unit pixel ray d (the device's batch.hip local_normal / shade).  Not a
+ * restatement of the reference's OpenGL render (src/mujoco_cameras.cpp:211-240): parity unpinned
+ * against the reference, pinned between device and this oracle. */
+static void local_normal(int type, const double* s, const double p[3], double n[3]) {
+  n[0] = 0; n[1] = 0; n[2] = 1;
+  switch (type) {
+    case MRS_GEOM_SPHERE: n[0] = p[0]; n[1] = p[1]; n[2] = p[2]; break;
+    case MRS_GEOM_CAPSULE: {
+      double z = p[2] < -s[1] ? -s[1] : (p[2] > s[1] ? s[1] : p[2]);
+      n[0] = p[0]; n[1] = p[1]; n[2] = p[2] - z;
+      break;
+    }
+    case MRS_GEOM_ELLIPSOID: n[0] = p[0] / (s[0] * s[0]); n[1] = p[1] / (s[1] * s[1]); n[2] = p[2] / (s[2] * s[2]); break;
+    case MRS_GEOM_CYLINDER: {
+      double rr = sqrt(p[0] * p[0] + p[1] * p[1]);
+      if (fabs(p[2]) - s[1] > rr - s[0]) { n[0] = 0; n[1] = 0; n[2] = p[2] >= 0 ? 1 : -1; }
+      else { n[0] = p[0]; n[1] = p[1]; n[2] = 0; }
+      break;
+    }
+    case MRS_GEOM_BOX: {
+      int k = 0;
+      double best = fabs(p[0]) / s[0];
+      for (int i = 1; i < 3; ++i)
+        if (fabs(p[i]) / s[i] > best) { best = fabs(p[i]) / s[i]; k = i; }
+      n[0] = n[1] = n[2] = 0;
+      n[k] = p[k] >= 0 ? 1 : -1;
+      break;
+    }
+    default: break;
+  }
+}
+
+void orc_render_rgbd(const mrs_model_view* m, orc_data* d, int cam, float* depth, unsigned char* rgb) {
   orc_ws* w = (orc_ws*)d->ws;
   kinematics(m, d);
   int W = m->cam_resolution[2 * cam], H = m->cam_resolution[2 * cam + 1];
@@ -1889,9 +1922,32 @@ void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out)
     for (int col = 0; col < W; ++col) {
       double dc[3] = {(col + 0.5 - 0.5 * W) / f, (0.5 * H - row - 0.5) / f, -1}, vec[3];
       mat_vec(vec, cmat, dc);
-      double t = ray_scene(m, w, cpos, vec, -1, 0x7, znear, NULL);
-      out[(size_t)row * W + col] = (float)((t < 0 || t > zfar) ? zfar : t);
+      int g = -1;
+      double t = ray_scene(m, w, cpos, vec, -1, 0x7, znear, &g);
+      int hit = !(t < 0 || t > zfar);
+      if (depth) depth[(size_t)row * W + col] = (float)(hit ? t : zfar);
+      if (!rgb) continue;
+      unsigned char* px = rgb + ((size_t)row * W + col) * 3;
+      if (!hit) { px[0] = px[1] = px[2] = 0; continue; }
+      const double* gm = w->geom_xmat + 9 * g;
+      double dv[3], q[3], lv[3], nl[3], nw[3];
+      for (int i = 0; i < 3; ++i) dv[i] = cpos[i] + t * vec[i] - w->geom_xpos[3 * g + i];
+      matT_vec(q, gm, dv);
+      (void)lv;
+      local_normal(m->geom_type[g], m->geom_size + 3 * g, q, nl);
+      mat_vec(nw, gm, nl);
+      double c = -dot3(nw, vec) / sqrt(fmax(dot3(nw, nw) * dot3(vec, vec), 1e-300));
+      double k = 0.3 + 0.7 * (c > 0 ? c : 0);
+      for (int ch = 0; ch < 3; ++ch) {
+        double v = m->geom_rgba[4 * g + ch] * k;
+        v = v < 0 ? 0 : (v > 1 ? 1 : v);
+        px[ch] = (unsigned char)(v * 255.0 + 0.5);
+      }
     }
+}
+
+void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out) {
+  orc_render_rgbd(m, d, cam, out, NULL);
 }
 
 /* ------------------------------------------------------------------------ CPU baseline */

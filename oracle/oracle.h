@@ -50,6 +50,9 @@ double orc_ray(const mrs_model_view* m, orc_data* d, const double pnt[3], const 
                int bodyexclude, int* geomid);
 /* depth image (H*W floats, ROS row order, eye-space z, `far` on miss) of camera `cam` */
 void orc_render_depth(const mrs_model_view* m, orc_data* d, int cam, float* out);
+/* depth (may be NULL) and RGB8 [H][W][3] of camera `cam`: flat headlight shading of each pixel's
+ * nearest geom, black on a miss (the device's mrs_batch_render_rgbd) */
+void orc_render_rgbd(const mrs_model_view* m, orc_data* d, int cam, float* depth, unsigned char* rgb);
 /* contacts of the last forward: up to `max` records of {geom1, geom2, dist, pos[3], frame[9]} */
 int orc_efc(orc_data* d, int nv, int max, int* type, double* force, double* aref, double* R, double* pos,
             double* J);

@@ -97,6 +97,39 @@ def test_depth_plane_constant():
     np.testing.assert_allclose(img, z0, rtol=1e-6)  # eye-space z, not Euclidean range
 
 
+def test_rgb_plane_headlight_shading():
+    """colour KAT: a plane (rgba 0.8 0.5 0.2) seen straight down; pixel (x, y) in camera-frame slopes
+    gets rgba * (0.3 + 0.7 / sqrt(1 + x^2 + y^2)) (normal (0, 0, 1), ray (x, y, -1)); the depth is
+    unchanged by the colour pass"""
+    z0 = 1.7
+    m = sim.Model.from_string(PLANE_CAM.format(z0=z0, tilt='rgba="0.8 0.5 0.2 1"'))
+    d = binding.OracleData(m)
+    d.forward()
+    depth, rgb = d.render_rgbd(0)
+    np.testing.assert_array_equal(depth, d.render_depth(0))
+    H, W = depth.shape
+    f = 0.5 * H / np.tan(np.radians(30))
+    x = (np.arange(W) + 0.5 - 0.5 * W) / f
+    y = (0.5 * H - np.arange(H) - 0.5) / f
+    cos = 1 / np.sqrt(1 + x[None, :] ** 2 + y[:, None] ** 2)
+    want = np.clip(np.array([0.8, 0.5, 0.2])[None, None, :] * (0.3 + 0.7 * cos)[..., None], 0, 1) * 255 + 0.5
+    np.testing.assert_array_equal(rgb, np.floor(want).astype(np.uint8))
+
+
+def test_rgb_sphere_centre_and_background():
+    """a sphere in front of the camera: the centre pixel faces the ray (full rgba), rays that miss are
+    black"""
+    m = sim.Model.from_string("""<mujoco><worldbody>
+      <geom type="sphere" size="0.2" pos="0 0 -1" rgba="0.2 0.4 1 1"/>
+      <camera name="c" pos="0 0 0" fovy="60" resolution="65 49"/></worldbody></mujoco>""")
+    d = binding.OracleData(m)
+    d.forward()
+    depth, rgb = d.render_rgbd(0)
+    np.testing.assert_array_equal(rgb[24, 32], [51, 102, 255])
+    assert depth[24, 32] == pytest.approx(0.8, rel=1e-6)
+    np.testing.assert_array_equal(rgb[0, 0], [0, 0, 0])
+
+
 def test_depth_tilted_plane_rows():
     z0, alpha = 2.0, 0.2
     m = sim.Model.from_string(PLANE_CAM.format(z0=z0, tilt=f'euler="{alpha} 0 0"'))

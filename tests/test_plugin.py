@@ -365,6 +365,11 @@ def test_camera_topics(pkg_dir):
     assert np.all(np.isfinite(depth)) and np.all(depth > 0)
     img = s.last_image("/camera/color/image_raw")
     assert img["encoding"] == "rgb8" and img["step"] == 1280 * 3 and img["bytes"] == 1280 * 720 * 3
+    # colour from the same ray pass: lit where the depth hits a geom, black where it reads zfar
+    rgb = s.last_image_data("/camera/color/image_raw")
+    assert rgb.shape == (720, 1280, 3) and rgb.max() > 0
+    zfar = depth.max()
+    assert np.all(rgb[depth < zfar].max(axis=-1) > 0) and np.all(rgb[depth >= zfar] == 0)
 
 
 @pytest.mark.gpu
