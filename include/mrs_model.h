@@ -36,7 +36,7 @@ enum { MRS_DYN_NONE = 0 };
 enum { MRS_GAIN_FIXED = 0, MRS_GAIN_AFFINE = 1 };
 enum { MRS_BIAS_NONE = 0, MRS_BIAS_AFFINE = 1 };
 enum { MRS_OBJ_UNKNOWN = 0, MRS_OBJ_BODY = 1, MRS_OBJ_JOINT = 3, MRS_OBJ_GEOM = 5, MRS_OBJ_SITE = 6,
-       MRS_OBJ_CAMERA = 7, MRS_OBJ_ACTUATOR = 19, MRS_OBJ_SENSOR = 20 };
+       MRS_OBJ_CAMERA = 7, MRS_OBJ_MESH = 10, MRS_OBJ_ACTUATOR = 19, MRS_OBJ_SENSOR = 20 };
 enum { MRS_SENS_ACCELEROMETER = 1, MRS_SENS_GYRO = 3, MRS_SENS_FORCE = 4, MRS_SENS_TORQUE = 5,
        MRS_SENS_RANGEFINDER = 7, MRS_SENS_JOINTPOS = 9, MRS_SENS_JOINTVEL = 10,
        MRS_SENS_ACTUATORFRC = 15, MRS_SENS_FRAMEPOS = 25, MRS_SENS_FRAMEQUAT = 26 };
@@ -116,6 +116,15 @@ typedef struct mrs_model_view {
   /* candidate collision pairs [npair]: geoms of different weld groups, not parent-child welds,
    * contype/conaffinity compatible; the lower geom type first */
   const int *pair_geom1, *pair_geom2;
+
+  /* meshes (mjModel mesh_*): vertices [nmeshvert][3] in the mesh's inertial frame (MuJoCo recentres
+   * a mesh at its centre of mass and aligns it with its principal axes; geom_pos/geom_quat carry
+   * the offset), triangles [nmeshface][3] (vertex ids relative to mesh_vertadr), convex-hull vertex
+   * ids [nmeshhull] (relative to mesh_vertadr) used by collision; geom_dataid = mesh id or -1 */
+  int nmesh, nmeshvert, nmeshface, nmeshhull;
+  const int *geom_dataid, *mesh_vertadr, *mesh_vertnum, *mesh_faceadr, *mesh_facenum, *mesh_hulladr,
+      *mesh_hullnum, *mesh_face, *mesh_hull;
+  const double *mesh_vert;
 } mrs_model_view;
 
 #ifdef __cplusplus

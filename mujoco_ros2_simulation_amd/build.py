@@ -21,8 +21,8 @@ HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
 # fp32 division/sqrt via v_rcp/v_sqrt (<= 2.5 ulp) instead of the correctly-rounded sequences:
 # the parity tolerance is 1e-5 relative, and the ray/contact math is division-heavy
 HIP_FLAGS = ["-fno-hip-fp32-correctly-rounded-divide-sqrt"]
-CXX_SOURCES = ["capi.cc", "mjcf/compiler.cc", "mjcf/xml.cc"]
-HEADERS = ["hip/devmodel.h", "hip/batch.h", "mjcf/model.h", "mjcf/xml.h"]
+CXX_SOURCES = ["capi.cc", "mjcf/compiler.cc", "mjcf/mesh.cc", "mjcf/xml.cc"]
+HEADERS = ["hip/devmodel.h", "hip/batch.h", "mjcf/model.h", "mjcf/mesh.h", "mjcf/xml.h"]
 
 
 def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:

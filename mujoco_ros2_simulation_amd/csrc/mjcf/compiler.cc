@@ -5,9 +5,10 @@
 // classes with childclass/class inheritance, bodies (pos, quat/axisangle/euler/xyaxes/zaxis,
 // gravcomp), <inertial> (diaginertia/fullinertia), joints (hinge/slide/ball/free, range+autolimits,
 // damping, stiffness, armature, frictionloss, actuatorfrcrange, springref, ref, margin, solref/solimp
-// for limit and friction), <freejoint>, geoms (plane/sphere/capsule/ellipsoid/cylinder/box, fromto,
-// contype/conaffinity/condim/group/priority, friction, margin, gap, solmix, solref, solimp, rgba,
-// mass/density), sites, cameras (fixed), <frame>, <replicate count sep offset euler> with sensor
+// for limit and friction), <freejoint>, geoms (plane/sphere/capsule/ellipsoid/cylinder/box/mesh,
+// fromto, contype/conaffinity/condim/group/priority, friction, margin, gap, solmix, solref, solimp,
+// rgba, material, mass/density), <asset> meshes (OBJ/STL files or inline vertex/face, scale; meshdir)
+// and materials (rgba), sites, cameras (fixed), <frame>, <replicate count sep offset euler> with sensor
 // replication and zero-padded suffixes, actuators (motor/position/velocity/general with
 // dampratio->kv), sensors (rangefinder, jointpos, jointvel, actuatorfrc, framepos, framequat, gyro,
 // accelerometer, force, torque), <statistic>, <visual><map znear zfar>, <keyframe><key>.
@@ -27,6 +28,7 @@
 #include <sstream>
 #include <stdexcept>
 
+#include "mesh.h"
 #include "model.h"
 #include "xml.h"
 
@@ -185,6 +187,7 @@ struct Options {
   std::string eulerseq = "xyz";
   bool autolimits = true;
   int inertiafromgeom = 2;  // 0 false, 1 true, 2 auto
+  std::string meshdir;      // <compiler meshdir / assetdir>
 };
 
 // a rigid frame: child = frame ∘ local
@@ -212,6 +215,16 @@ struct GeomRec {
   double solref[2] = {0.02, 1}, solimp[5] = {0.9, 0.95, 0.001, 0.5, 2};
   double rgba[4] = {0.5, 0.5, 0.5, 1};
   double mass = -1, density = 1000;
+  int mesh = -1;  // mesh id (type mesh)
+};
+// a processed mesh asset: vertices in its inertial frame; pos/quat place that frame in the mesh file's
+// frame; volume and unit-density principal moments for the geom's mass
+struct MeshRec {
+  std::string name;
+  std::vector<double> vert;
+  std::vector<int> face, hull;
+  double pos[3] = {0, 0, 0}, quat[4] = {1, 0, 0, 0};
+  double volume = 0, inertia[3] = {0, 0, 0}, half[3] = {0, 0, 0}, rbound = 0;
 };
 struct SiteRec { std::string name; double pos[3] = {0, 0, 0}, quat[4] = {1, 0, 0, 0}; };
 struct CamRec {
@@ -255,6 +268,10 @@ struct Compiler {
   std::map<std::string, std::vector<std::string>> replica_suffixes;
   Model m;
   bool extent_given = false;
+  std::string basedir = ".";
+  std::vector<MeshRec> meshes;
+  std::map<std::string, int> mesh_ids;
+  std::map<std::string, std::vector<double>> materials;  // name -> rgba
 
   Compiler() {
     auto main = std::make_unique<DefaultClass>();
@@ -397,6 +414,106 @@ struct Compiler {
     if (auto* a = e->attr("autolimits")) opt.autolimits = (*a == "true");
     if (auto* a = e->attr("inertiafromgeom"))
       opt.inertiafromgeom = (*a == "true") ? 1 : (*a == "false") ? 0 : 2;
+    if (auto* a = e->attr("assetdir")) opt.meshdir = *a;
+    if (auto* a = e->attr("meshdir")) opt.meshdir = *a;
+  }
+
+  // ---- <asset>: meshes and materials.  A mesh is processed as MuJoCo's compiler does: faces from the
+  // file or the face attribute (else the convex hull's), volume / centre of mass / inertia from the
+  // triangles (the hull's if the surface encloses no volume), then the vertices are re-expressed in
+  // the inertial frame (centre of mass, principal axes, right-handed) and the geoms using the mesh
+  // are offset by that frame.
+  void parse_asset(const XmlElement* sec) {
+    for (auto& c : sec->children) {
+      const XmlElement* e = c.get();
+      if (e->tag == "material") {
+        double rgba[4] = {1, 1, 1, 1};
+        get_reals(e, nullptr, "material", "rgba", rgba, 4, true);
+        if (auto* n = e->attr("name")) materials[*n] = std::vector<double>(rgba, rgba + 4);
+        continue;
+      }
+      if (e->tag == "texture" || e->tag == "hfield" || e->tag == "skin" || e->tag == "model") {
+        if (e->tag == "hfield") fail(e, "height fields are not supported");
+        continue;
+      }
+      if (e->tag != "mesh") fail(e, "unsupported asset element");
+      MeshRec r;
+      MeshAsset a;
+      std::string file;
+      const bool has_file = get_str(e, nullptr, "mesh", "file", file);
+      if (has_file) {
+        std::string path = file;
+        if (!path.empty() && path[0] != '/') {
+          std::string dir = opt.meshdir;
+          if (dir.empty() || dir[0] != '/') dir = basedir + (dir.empty() ? "" : "/" + dir);
+          path = dir + "/" + file;
+        }
+        try {
+          a = load_mesh_file(path);
+        } catch (const std::exception& ex) {
+          fail(e, ex.what());
+        }
+      }
+      if (auto* v = e->attr("vertex")) {
+        if (has_file) fail(e, "mesh has both file and vertex");
+        a.vert = parse_reals(*v, e, "vertex");
+        if (a.vert.size() % 3 || a.vert.size() < 12) fail(e, "vertex needs at least 4 points (3 numbers each)");
+      }
+      if (auto* f = e->attr("face")) {
+        auto fv = parse_reals(*f, e, "face");
+        if (fv.size() % 3) fail(e, "face needs 3 vertex ids per triangle");
+        a.face.clear();
+        for (double x : fv) {
+          if (x < 0 || x >= static_cast<double>(a.vert.size() / 3)) fail(e, "face vertex id out of range");
+          a.face.push_back(static_cast<int>(x));
+        }
+      }
+      if (a.vert.empty()) fail(e, "mesh needs a file or a vertex attribute");
+      double scale[3] = {1, 1, 1};
+      get_reals(e, nullptr, "mesh", "scale", scale, 3, true);
+      for (size_t i = 0; i < a.vert.size(); ++i) a.vert[i] *= scale[i % 3];
+      if (scale[0] * scale[1] * scale[2] < 0)  // a mirroring scale flips the winding
+        for (size_t t = 0; t + 2 < a.face.size(); t += 3) std::swap(a.face[t + 1], a.face[t + 2]);
+      std::vector<int> hull_face;
+      try {
+        convex_hull(a.vert, hull_face, r.hull);
+      } catch (const std::exception& ex) {
+        fail(e, ex.what());
+      }
+      if (a.face.empty()) a.face = hull_face;
+      double vol, com[3], I[9];
+      mesh_mass_properties(a.vert, a.face, vol, com, I);
+      if (!(vol > 1e-12)) mesh_mass_properties(a.vert, hull_face, vol, com, I);
+      if (!(vol > 1e-12)) fail(e, "mesh volume is too small");
+      double ev[3], R[9];
+      eig3(ev, R, I);
+      mat2quat(r.quat, R);
+      quat2mat(R, r.quat);  // the frame the quaternion stores exactly
+      std::memcpy(r.pos, com, sizeof com);
+      r.volume = vol;
+      for (int k = 0; k < 3; ++k) r.inertia[k] = ev[k];
+      r.vert.resize(a.vert.size());
+      for (size_t i = 0; i < a.vert.size() / 3; ++i) {
+        const double d[3] = {a.vert[3 * i] - com[0], a.vert[3 * i + 1] - com[1], a.vert[3 * i + 2] - com[2]};
+        for (int k = 0; k < 3; ++k) {
+          const double x = R[k] * d[0] + R[3 + k] * d[1] + R[6 + k] * d[2];
+          r.vert[3 * i + k] = x;
+          r.half[k] = std::max(r.half[k], std::fabs(x));
+        }
+        r.rbound = std::max(r.rbound, norm3(&r.vert[3 * i]));
+      }
+      r.face = a.face;
+      std::string name;
+      if (!get_str(e, nullptr, "mesh", "name", name)) {
+        if (!has_file) fail(e, "a mesh without a file needs a name");
+        name = file.substr(file.find_last_of('/') + 1);
+        name = name.substr(0, name.find_last_of('.'));
+      }
+      r.name = name;
+      if (mesh_ids.count(name)) fail(e, "repeated mesh name '" + name + "'");
+      mesh_ids[name] = static_cast<int>(meshes.size());
+      meshes.push_back(std::move(r));
+    }
   }
   void parse_option(const XmlElement* e) {
     double v[3];
@@ -660,7 +777,8 @@ struct Compiler {
     else if (type == "ellipsoid") g.type = MRS_GEOM_ELLIPSOID;
     else if (type == "cylinder") g.type = MRS_GEOM_CYLINDER;
     else if (type == "box") g.type = MRS_GEOM_BOX;
-    else fail(e, "unsupported geom type '" + type + "' (mesh/hfield geoms are a later row, SURVEY.md §8f f3)");
+    else if (type == "mesh") g.type = MRS_GEOM_MESH;
+    else fail(e, "unsupported geom type '" + type + "'");
     get_reals(e, cls, tag, "size", g.size, 3);
     get_int(e, cls, tag, "contype", g.contype);
     get_int(e, cls, tag, "conaffinity", g.conaffinity);
@@ -673,7 +791,10 @@ struct Compiler {
     get_real(e, cls, tag, "solmix", g.solmix);
     get_reals(e, cls, tag, "solref", g.solref, 2, true);
     get_reals(e, cls, tag, "solimp", g.solimp, 5);
-    get_reals(e, cls, tag, "rgba", g.rgba, 4, true);
+    const bool rgba_given = get_reals(e, cls, tag, "rgba", g.rgba, 4, true);
+    std::string material;
+    if (!rgba_given && get_str(e, cls, tag, "material", material) && materials.count(material))
+      for (int k = 0; k < 4; ++k) g.rgba[k] = materials[material][k];
     get_real(e, cls, tag, "mass", g.mass);
     get_real(e, cls, tag, "density", g.density);
     if (g.condim != 1 && g.condim != 3) fail(e, "only condim 1 and 3 are supported");
@@ -696,6 +817,20 @@ struct Compiler {
     } else {
       get_reals(e, cls, tag, "pos", g.pos, 3, true);
       get_orientation(e, cls, tag, g.quat);
+    }
+    if (g.type == MRS_GEOM_MESH) {
+      std::string mesh;
+      if (!get_str(e, cls, tag, "mesh", mesh)) fail(e, "mesh geom needs a mesh attribute");
+      auto it = mesh_ids.find(mesh);
+      if (it == mesh_ids.end()) fail(e, "unknown mesh '" + mesh + "'");
+      g.mesh = it->second;
+      const MeshRec& r = meshes[g.mesh];
+      // geom frame = declared frame o the mesh's inertial frame
+      double off[3];
+      rot_vec_quat(off, r.pos, g.quat);
+      for (int k = 0; k < 3; ++k) g.pos[k] += off[k];
+      quat_mul(g.quat, g.quat, r.quat);
+      for (int k = 0; k < 3; ++k) g.size[k] = r.half[k];
     }
     frame.apply(g.pos, g.quat);
     return g;
@@ -1030,9 +1165,11 @@ struct Compiler {
           case MRS_GEOM_CYLINDER: rb = std::sqrt(G.size[0] * G.size[0] + G.size[1] * G.size[1]); break;
           case MRS_GEOM_ELLIPSOID: rb = std::max(G.size[0], std::max(G.size[1], G.size[2])); break;
           case MRS_GEOM_BOX: rb = norm3(G.size); break;
+          case MRS_GEOM_MESH: rb = meshes[G.mesh].rbound; break;
           default: rb = 0;
         }
         m.geom_rbound.push_back(rb);
+        m.geom_dataid.push_back(G.mesh);
         m.geom_friction.insert(m.geom_friction.end(), G.friction, G.friction + 3);
         m.geom_margin.push_back(G.margin);
         m.geom_gap.push_back(G.gap);
@@ -1112,7 +1249,7 @@ struct Compiler {
     for (int b = m.nbody - 1; b > 0; --b) m.body_subtreemass[m.body_parentid[b]] += m.body_subtreemass[b];
   }
 
-  static void geom_mass_inertia(const GeomRec& g, double& mass, double I[3]) {
+  void geom_mass_inertia(const GeomRec& g, double& mass, double I[3]) const {
     const double* s = g.size;
     double vol = 0;
     I[0] = I[1] = I[2] = 0;
@@ -1122,6 +1259,7 @@ struct Compiler {
       case MRS_GEOM_CYLINDER: vol = kPi * s[0] * s[0] * 2 * s[1]; break;
       case MRS_GEOM_ELLIPSOID: vol = 4.0 / 3 * kPi * s[0] * s[1] * s[2]; break;
       case MRS_GEOM_BOX: vol = 8 * s[0] * s[1] * s[2]; break;
+      case MRS_GEOM_MESH: vol = meshes[g.mesh].volume; break;
       default: vol = 0;
     }
     mass = g.mass >= 0 ? g.mass : g.density * vol;
@@ -1152,8 +1290,29 @@ struct Compiler {
         I[1] = mass * (s[0] * s[0] + s[2] * s[2]) / 3;
         I[2] = mass * (s[0] * s[0] + s[1] * s[1]) / 3;
         break;
+      case MRS_GEOM_MESH:  // unit-density principal moments scaled by the density
+        for (int k = 0; k < 3; ++k) I[k] = rho * meshes[g.mesh].inertia[k];
+        break;
       default: break;
     }
+  }
+  // mesh arrays of the model (after flatten: geoms reference meshes by id)
+  void flatten_meshes() {
+    m.nmesh = static_cast<int>(meshes.size());
+    std::vector<std::string> names;
+    for (const MeshRec& r : meshes) {
+      names.push_back(r.name);
+      m.mesh_vertadr.push_back(static_cast<int>(m.mesh_vert.size() / 3));
+      m.mesh_vertnum.push_back(static_cast<int>(r.vert.size() / 3));
+      m.mesh_faceadr.push_back(static_cast<int>(m.mesh_face.size() / 3));
+      m.mesh_facenum.push_back(static_cast<int>(r.face.size() / 3));
+      m.mesh_hulladr.push_back(static_cast<int>(m.mesh_hull.size()));
+      m.mesh_hullnum.push_back(static_cast<int>(r.hull.size()));
+      m.mesh_vert.insert(m.mesh_vert.end(), r.vert.begin(), r.vert.end());
+      m.mesh_face.insert(m.mesh_face.end(), r.face.begin(), r.face.end());
+      m.mesh_hull.insert(m.mesh_hull.end(), r.hull.begin(), r.hull.end());
+    }
+    m.names[MRS_OBJ_MESH] = names;
   }
   void geom_inertia(const BodyRec& B, double& mass, double ipos[3], double iquat[4], double inertia[3]) {
     mass = 0;
@@ -1428,7 +1587,8 @@ struct Compiler {
   }
 
   // ---- driver
-  Model compile(std::unique_ptr<XmlElement> root, const std::string& basedir) {
+  Model compile(std::unique_ptr<XmlElement> root, const std::string& base) {
+    basedir = base;
     if (root->tag != "mujoco") fail(root.get(), "root element must be <mujoco>");
     if (auto* n = root->attr("model")) m.model_name = *n;
     expand_includes(root.get(), basedir, 0);
@@ -1450,6 +1610,8 @@ struct Compiler {
           }
       }
     }
+    for (auto& c : root->children)
+      if (c->tag == "asset") parse_asset(c.get());
     // pass 2: world body tree
     BodyRec world;
     world.name = "world";
@@ -1457,6 +1619,7 @@ struct Compiler {
     for (auto& c : root->children)
       if (c->tag == "worldbody") parse_body_children(c.get(), 0, "", Frame(), "");
     flatten();
+    flatten_meshes();
     set0();
     // pass 3: elements that reference the tree
     for (auto& c : root->children) {
@@ -1579,6 +1742,12 @@ mrs_model_view Model::view() const {
   MRS_V(sensor_adr); MRS_V(sensor_cutoff);
   MRS_V(qpos0); MRS_V(qpos_spring); MRS_V(key_time); MRS_V(key_qpos); MRS_V(key_qvel); MRS_V(key_ctrl);
   MRS_V(pair_geom1); MRS_V(pair_geom2);
+  v.nmesh = nmesh;
+  v.nmeshvert = static_cast<int>(mesh_vert.size() / 3);
+  v.nmeshface = static_cast<int>(mesh_face.size() / 3);
+  v.nmeshhull = static_cast<int>(mesh_hull.size());
+  MRS_V(geom_dataid); MRS_V(mesh_vertadr); MRS_V(mesh_vertnum); MRS_V(mesh_faceadr); MRS_V(mesh_facenum);
+  MRS_V(mesh_hulladr); MRS_V(mesh_hullnum); MRS_V(mesh_face); MRS_V(mesh_hull); MRS_V(mesh_vert);
 #undef MRS_V
   return v;
 }

@@ -56,6 +56,12 @@ struct Model {
 
   std::vector<double> qpos0, qpos_spring;
   std::vector<double> key_time, key_qpos, key_qvel, key_ctrl;
+  // meshes: vertices in the mesh's inertial frame (centre of mass, principal axes), triangles, and the
+  // convex hull's vertex ids (relative to the mesh's first vertex); geom_dataid = mesh id or -1
+  int nmesh = 0;
+  std::vector<int> geom_dataid, mesh_vertadr, mesh_vertnum, mesh_faceadr, mesh_facenum, mesh_hulladr,
+      mesh_hullnum, mesh_face, mesh_hull;
+  std::vector<double> mesh_vert;
   // statically admissible collision pairs (mj_collision's broad-phase filters), lower geom type first
   std::vector<int> pair_geom1, pair_geom2;
 

@@ -86,6 +86,14 @@ _ARRAYS = [
     ("key_ctrl", "d", "nkey", "nu"),
     ("pair_geom1", "i", "npair", 1), ("pair_geom2", "i", "npair", 1),
 ]
+# mesh block (after the arrays above in struct mrs_model_view)
+_MESH_SIZES = ["nmesh", "nmeshvert", "nmeshface", "nmeshhull"]
+_MESH_ARRAYS = [
+    ("geom_dataid", "i", "ngeom", 1), ("mesh_vertadr", "i", "nmesh", 1), ("mesh_vertnum", "i", "nmesh", 1),
+    ("mesh_faceadr", "i", "nmesh", 1), ("mesh_facenum", "i", "nmesh", 1), ("mesh_hulladr", "i", "nmesh", 1),
+    ("mesh_hullnum", "i", "nmesh", 1), ("mesh_face", "i", "nmeshface", 3), ("mesh_hull", "i", "nmeshhull", 1),
+    ("mesh_vert", "d", "nmeshvert", 3),
+]
 
 
 class ModelView(C.Structure):
@@ -96,7 +104,9 @@ class ModelView(C.Structure):
                  ("cone", C.c_int), ("ls_iterations", C.c_int),
                  ("stat_extent", C.c_double), ("stat_center", C.c_double * 3), ("stat_meaninertia", C.c_double),
                  ("vis_znear", C.c_double), ("vis_zfar", C.c_double)] +
-                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _ARRAYS])
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _ARRAYS] +
+                [(n, C.c_int) for n in _MESH_SIZES] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _MESH_ARRAYS])
 
 
 _lib = None
@@ -179,14 +189,14 @@ class Model:
         self.view = ModelView()
         _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
         v = self.view
-        for n in _SIZES:
+        for n in _SIZES + _MESH_SIZES:
             setattr(self, n, getattr(v, n))
         for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "integrator", "solver",
                   "iterations", "disableflags",
                   "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
             setattr(self, n, getattr(v, n))
         self.gravity = np.array(v.gravity[:])
-        for name, kind, count, width in _ARRAYS:
+        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS:
             n = getattr(v, count)
             w = getattr(v, width) if isinstance(width, str) else width
             ptr = getattr(v, name)

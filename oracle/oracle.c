@@ -860,6 +860,313 @@ static int col_box_box(const double* p1, const double* R1, const double* h1, con
   return n;
 }
 
+/* ---- general convex pairs: ellipsoid, cylinder and mesh geoms (MuJoCo mjc_Convex, which runs
+ * libccd's Minkowski Portal Refinement, ccdMPRPenetration, on the two shapes' support functions with
+ * each shape inflated by margin/2).  Restated from the published MPR algorithm (Snethen, "XenoCollide",
+ * Game Programming Gems 7; libccd mpr.c): portal discovery, portal refinement, then penetration by
+ * expanding the portal until the support gain drops under mpr_tolerance (1e-6, mjOption default),
+ * at most mpr_iterations (50) expansions.  One contact: dist = margin - depth, normal from geom1 to
+ * geom2 (the Minkowski difference is geom1 - geom2), position midway between the two shapes'
+ * portal-interpolated surface points.  The device runs the same steps in fp32 (csrc/hip/step.hip
+ * mpr_penetration). */
+#define MPR_TOL 1e-6
+#define MPR_ITER 50
+#define MPR_EPS 1e-14
+typedef struct {
+  int type, nhull;
+  const double *pos, *mat, *size, *vert;
+  const int* hull;
+  double inflate;
+} orc_shape;
+typedef struct { double v[3], a[3], b[3]; } mpr_point; /* v = a - b: support of geom1 minus geom2 */
+
+static void shape_of(const mrs_model_view* m, orc_ws* w, int g, double margin, orc_shape* s) {
+  s->type = m->geom_type[g];
+  s->pos = w->geom_xpos + 3 * g;
+  s->mat = w->geom_xmat + 9 * g;
+  s->size = m->geom_size + 3 * g;
+  s->inflate = 0.5 * margin;
+  s->vert = NULL; s->hull = NULL; s->nhull = 0;
+  if (s->type == MRS_GEOM_MESH) {
+    int id = m->geom_dataid[g];
+    s->vert = m->mesh_vert + 3 * m->mesh_vertadr[id];
+    s->hull = m->mesh_hull + m->mesh_hulladr[id];
+    s->nhull = m->mesh_hullnum[id];
+  }
+}
+
+/* farthest point of the (inflated) shape along dir, world frame */
+static void shape_support(const orc_shape* s, const double dir[3], double out[3]) {
+  double l[3], p[3] = {0, 0, 0};
+  const double* z = s->size;
+  matT_vec(l, s->mat, dir);
+  switch (s->type) {
+    case MRS_GEOM_SPHERE:
+    case MRS_GEOM_CAPSULE: {
+      double n = norm3(l);
+      if (n > MINVAL) for (int i = 0; i < 3; ++i) p[i] = z[0] * l[i] / n;
+      if (s->type == MRS_GEOM_CAPSULE) p[2] += l[2] >= 0 ? z[1] : -z[1];
+      break;
+    }
+    case MRS_GEOM_ELLIPSOID: {
+      double t[3] = {z[0] * z[0] * l[0], z[1] * z[1] * l[1], z[2] * z[2] * l[2]};
+      double den = sqrt(t[0] * l[0] + t[1] * l[1] + t[2] * l[2]);
+      if (den > MINVAL) for (int i = 0; i < 3; ++i) p[i] = t[i] / den;
+      break;
+    }
+    case MRS_GEOM_CYLINDER: {
+      double rr = sqrt(l[0] * l[0] + l[1] * l[1]);
+      if (rr > MINVAL) { p[0] = z[0] * l[0] / rr; p[1] = z[0] * l[1] / rr; }
+      p[2] = l[2] >= 0 ? z[1] : -z[1];
+      break;
+    }
+    case MRS_GEOM_BOX:
+      for (int i = 0; i < 3; ++i) p[i] = l[i] >= 0 ? z[i] : -z[i];
+      break;
+    case MRS_GEOM_MESH: {
+      double best = -1e300;
+      for (int k = 0; k < s->nhull; ++k) {
+        const double* v = s->vert + 3 * s->hull[k];
+        double d = dot3(v, l);
+        if (d > best) { best = d; p[0] = v[0]; p[1] = v[1]; p[2] = v[2]; }
+      }
+      break;
+    }
+  }
+  mat_vec(out, s->mat, p);
+  double dn = norm3(dir);
+  for (int i = 0; i < 3; ++i) out[i] += s->pos[i] + (dn > MINVAL ? s->inflate * dir[i] / dn : 0);
+}
+
+static void mpr_support(const orc_shape* A, const orc_shape* B, const double dir[3], mpr_point* p) {
+  double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  shape_support(A, dir, p->a);
+  shape_support(B, nd, p->b);
+  for (int i = 0; i < 3; ++i) p->v[i] = p->a[i] - p->b[i];
+}
+static void tri_normal(double n[3], const double a[3], const double b[3], const double c[3]) {
+  double u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, v[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  cross3(n, u, v);
+  normalize3(n);
+}
+/* closest point to the origin on triangle abc (Ericson, Real-Time Collision Detection 5.1.5) */
+static void closest_on_triangle(const double a[3], const double b[3], const double c[3], double out[3]) {
+  double ab[3], ac[3], ap[3], bp[3], cp[3];
+  for (int i = 0; i < 3; ++i) {
+    ab[i] = b[i] - a[i]; ac[i] = c[i] - a[i];
+    ap[i] = -a[i]; bp[i] = -b[i]; cp[i] = -c[i];
+  }
+  double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { memcpy(out, a, 3 * sizeof(double)); return; }
+  double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { memcpy(out, b, 3 * sizeof(double)); return; }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    double t = d1 / (d1 - d3);
+    for (int i = 0; i < 3; ++i) out[i] = a[i] + t * ab[i];
+    return;
+  }
+  double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { memcpy(out, c, 3 * sizeof(double)); return; }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    double t = d2 / (d2 - d6);
+    for (int i = 0; i < 3; ++i) out[i] = a[i] + t * ac[i];
+    return;
+  }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int i = 0; i < 3; ++i) out[i] = b[i] + t * (c[i] - b[i]);
+    return;
+  }
+  double den = 1 / (va + vb + vc), v = vb * den, ww = vc * den;
+  for (int i = 0; i < 3; ++i) out[i] = a[i] + ab[i] * v + ac[i] * ww;
+}
+static void mpr_expand(mpr_point p[4], const mpr_point* v4) {
+  double x[3];
+  cross3(x, v4->v, p[0].v);
+  if (dot3(p[1].v, x) > 0) {
+    if (dot3(p[2].v, x) > 0) p[1] = *v4;
+    else p[3] = *v4;
+  } else {
+    if (dot3(p[3].v, x) > 0) p[2] = *v4;
+    else p[1] = *v4;
+  }
+}
+static int mpr_reach_tolerance(const mpr_point p[4], const mpr_point* v4, const double n[3]) {
+  double d4 = dot3(v4->v, n);
+  double g = fmin(d4 - dot3(p[1].v, n), fmin(d4 - dot3(p[2].v, n), d4 - dot3(p[3].v, n)));
+  return g <= MPR_TOL;
+}
+/* 0: origin inside (portal p[0..3] found), 1: touching at p[1], 2: origin on segment p[0]-p[1],
+ * -1: separated */
+static int mpr_discover(const orc_shape* A, const orc_shape* B, mpr_point p[4]) {
+  for (int i = 0; i < 3; ++i) { p[0].a[i] = A->pos[i]; p[0].b[i] = B->pos[i]; p[0].v[i] = A->pos[i] - B->pos[i]; }
+  if (dot3(p[0].v, p[0].v) < 1e-20) p[0].v[0] += 1e-5;
+  double dir[3] = {-p[0].v[0], -p[0].v[1], -p[0].v[2]};
+  normalize3(dir);
+  mpr_support(A, B, dir, &p[1]);
+  if (dot3(p[1].v, dir) <= 0) return -1;
+  cross3(dir, p[0].v, p[1].v);
+  if (dot3(dir, dir) < MPR_EPS) return dot3(p[1].v, p[1].v) < MPR_EPS ? 1 : 2;
+  normalize3(dir);
+  mpr_support(A, B, dir, &p[2]);
+  if (dot3(p[2].v, dir) <= 0) return -1;
+  double va[3], vb[3];
+  for (int i = 0; i < 3; ++i) { va[i] = p[1].v[i] - p[0].v[i]; vb[i] = p[2].v[i] - p[0].v[i]; }
+  cross3(dir, va, vb);
+  normalize3(dir);
+  if (dot3(dir, p[0].v) > 0) {
+    mpr_point t = p[1]; p[1] = p[2]; p[2] = t;
+    for (int i = 0; i < 3; ++i) dir[i] = -dir[i];
+  }
+  for (int it = 0; it < MPR_ITER; ++it) {
+    mpr_support(A, B, dir, &p[3]);
+    if (dot3(p[3].v, dir) <= 0) return -1;
+    double x[3];
+    int replaced = 0;
+    cross3(x, p[1].v, p[3].v);
+    if (dot3(x, p[0].v) < -MPR_EPS) { p[2] = p[3]; replaced = 1; }
+    else {
+      cross3(x, p[3].v, p[2].v);
+      if (dot3(x, p[0].v) < -MPR_EPS) { p[1] = p[3]; replaced = 1; }
+    }
+    if (!replaced) return 0;
+    for (int i = 0; i < 3; ++i) { va[i] = p[1].v[i] - p[0].v[i]; vb[i] = p[2].v[i] - p[0].v[i]; }
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  return 0;
+}
+static void mpr_position(const mpr_point p[4], double pos[3]) {
+  double n[3], x[3], b[4];
+  tri_normal(n, p[1].v, p[2].v, p[3].v);
+  cross3(x, p[1].v, p[2].v); b[0] = dot3(x, p[3].v);
+  cross3(x, p[3].v, p[2].v); b[1] = dot3(x, p[0].v);
+  cross3(x, p[0].v, p[1].v); b[2] = dot3(x, p[3].v);
+  cross3(x, p[2].v, p[1].v); b[3] = dot3(x, p[0].v);
+  double sum = b[0] + b[1] + b[2] + b[3];
+  if (sum <= MPR_EPS) {
+    b[0] = 0;
+    cross3(x, p[2].v, p[3].v); b[1] = dot3(x, n);
+    cross3(x, p[3].v, p[1].v); b[2] = dot3(x, n);
+    cross3(x, p[1].v, p[2].v); b[3] = dot3(x, n);
+    sum = b[1] + b[2] + b[3];
+  }
+  for (int i = 0; i < 3; ++i) {
+    double pa = 0, pb = 0;
+    for (int k = 0; k < 4; ++k) { pa += b[k] * p[k].a[i]; pb += b[k] * p[k].b[i]; }
+    pos[i] = 0.5 * (pa + pb) / sum;
+  }
+}
+/* returns 1 with depth (of the inflated shapes), unit normal (geom1 -> geom2) and position */
+static int mpr_penetration(const orc_shape* A, const orc_shape* B, double* depth, double nrm[3], double pos[3]) {
+  mpr_point p[4], v4;
+  int r = mpr_discover(A, B, p);
+  if (r < 0 || r == 1) return 0;
+  if (r == 2) {
+    for (int i = 0; i < 3; ++i) { nrm[i] = p[1].v[i]; pos[i] = 0.5 * (p[1].a[i] + p[1].b[i]); }
+    *depth = normalize3(nrm);
+    return 1;
+  }
+  /* refinement: expand until the portal holds the origin */
+  for (int it = 0;; ++it) {
+    double n[3];
+    tri_normal(n, p[1].v, p[2].v, p[3].v);
+    if (dot3(n, p[1].v) >= 0) break;
+    mpr_support(A, B, n, &v4);
+    if (dot3(v4.v, n) < 0 || mpr_reach_tolerance(p, &v4, n) || it >= MPR_ITER) return 0;
+    mpr_expand(p, &v4);
+  }
+  /* penetration: expand towards the surface of the Minkowski difference nearest the portal */
+  for (int it = 0;; ++it) {
+    double n[3];
+    tri_normal(n, p[1].v, p[2].v, p[3].v);
+    mpr_support(A, B, n, &v4);
+    if (mpr_reach_tolerance(p, &v4, n) || it > MPR_ITER) {
+      closest_on_triangle(p[1].v, p[2].v, p[3].v, nrm);
+      *depth = normalize3(nrm);
+      if (*depth < MINVAL) return 0;
+      mpr_position(p, pos);
+      return 1;
+    }
+    mpr_expand(p, &v4);
+  }
+}
+static int col_convex(const mrs_model_view* m, orc_ws* w, int g1, int g2, double margin, orc_contact* out, int n) {
+  orc_shape A, B;
+  shape_of(m, w, g1, margin, &A);
+  shape_of(m, w, g2, margin, &B);
+  double depth, nrm[3], pos[3];
+  if (!mpr_penetration(&A, &B, &depth, nrm, pos)) return n;
+  return add_contact(out, n, margin - depth, pos, nrm);
+}
+/* plane (geom1) vs ellipsoid: the support point along -normal (mjc_PlaneEllipsoid) */
+static int col_plane_convex_support(const mrs_model_view* m, orc_ws* w, const double* ppos, const double* pmat,
+                                    int g2, double margin, orc_contact* out, int n) {
+  orc_shape B;
+  shape_of(m, w, g2, 0, &B);
+  double nrm[3] = {pmat[2], pmat[5], pmat[8]}, nd[3] = {-nrm[0], -nrm[1], -nrm[2]}, s[3];
+  shape_support(&B, nd, s);
+  double dv[3] = {s[0] - ppos[0], s[1] - ppos[1], s[2] - ppos[2]};
+  double dist = dot3(dv, nrm);
+  if (dist > margin) return n;
+  double pos[3];
+  for (int i = 0; i < 3; ++i) pos[i] = s[i] - nrm[i] * dist / 2;
+  return add_contact(out, n, dist, pos, nrm);
+}
+/* plane vs cylinder (after mjc_PlaneCylinder): on each cap the rim point deepest along -normal, and
+ * on the deeper cap the two rim points at +-120 degrees from it (a resting cylinder stands on a
+ * triangle); the rim direction falls back to the cylinder's x axis when the axis is parallel to the
+ * normal */
+static int col_plane_cylinder(const double* ppos, const double* pmat, const double* cpos, const double* cmat,
+                              const double* size, double margin, orc_contact* out, int n) {
+  double nrm[3] = {pmat[2], pmat[5], pmat[8]}, ax[3] = {cmat[2], cmat[5], cmat[8]};
+  double an = dot3(ax, nrm), d[3];
+  for (int i = 0; i < 3; ++i) d[i] = -nrm[i] + an * ax[i];
+  if (dot3(d, d) < 1e-12) { d[0] = cmat[0]; d[1] = cmat[3]; d[2] = cmat[6]; }
+  normalize3(d);
+  double e[3];
+  cross3(e, ax, d);
+  /* the deeper cap: the one whose centre is lower along the normal */
+  double sdeep = an > 0 ? -1.0 : 1.0;
+  for (int cap = 0; cap < 2; ++cap) {
+    double sc = cap == 0 ? sdeep : -sdeep;
+    int npts = cap == 0 ? 3 : 1;
+    for (int k = 0; k < npts; ++k) {
+      double cu = k == 0 ? 1.0 : -0.5, cv = k == 0 ? 0.0 : (k == 1 ? 0.8660254037844386 : -0.8660254037844386);
+      double p[3], dv[3];
+      for (int i = 0; i < 3; ++i) p[i] = cpos[i] + sc * size[1] * ax[i] + size[0] * (cu * d[i] + cv * e[i]);
+      for (int i = 0; i < 3; ++i) dv[i] = p[i] - ppos[i];
+      double dist = dot3(dv, nrm);
+      if (dist > margin) continue;
+      double pos[3];
+      for (int i = 0; i < 3; ++i) pos[i] = p[i] - nrm[i] * dist / 2;
+      n = add_contact(out, n, dist, pos, nrm);
+    }
+  }
+  return n;
+}
+/* plane vs mesh: every convex-hull vertex within margin, in hull order (at most 8) */
+static int col_plane_mesh(const mrs_model_view* m, orc_ws* w, const double* ppos, const double* pmat, int g2,
+                          double margin, orc_contact* out, int n) {
+  orc_shape B;
+  shape_of(m, w, g2, 0, &B);
+  double nrm[3] = {pmat[2], pmat[5], pmat[8]};
+  for (int k = 0; k < B.nhull; ++k) {
+    double p[3], dv[3];
+    mat_vec(p, B.mat, B.vert + 3 * B.hull[k]);
+    for (int i = 0; i < 3; ++i) { p[i] += B.pos[i]; dv[i] = p[i] - ppos[i]; }
+    double dist = dot3(dv, nrm);
+    if (dist > margin) continue;
+    double pos[3];
+    for (int i = 0; i < 3; ++i) pos[i] = p[i] - nrm[i] * dist / 2;
+    n = add_contact(out, n, dist, pos, nrm);
+  }
+  return n;
+}
+
 static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, double margin, orc_contact* out) {
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const double *p1 = w->geom_xpos + 3 * g1, *p2 = w->geom_xpos + 3 * g2;
@@ -875,7 +1182,11 @@ static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, doubl
         n = col_plane_sphere(p1, m1, a2, s2[0], margin, out, 0);
         return col_plane_sphere(p1, m1, b2, s2[0], margin, out, n);
       case MRS_GEOM_BOX: return col_plane_box(p1, m1, p2, m2, s2, margin, out, 0);
+      case MRS_GEOM_ELLIPSOID: return col_plane_convex_support(m, w, p1, m1, g2, margin, out, 0);
+      case MRS_GEOM_CYLINDER: return col_plane_cylinder(p1, m1, p2, m2, s2, margin, out, 0);
+      case MRS_GEOM_MESH: return col_plane_mesh(m, w, p1, m1, g2, margin, out, 0);
     }
+    return -1;
   } else if (t1 == MRS_GEOM_SPHERE) {
     switch (t2) {
       case MRS_GEOM_SPHERE: return col_sphere_sphere(p1, s1[0], p2, s2[0], margin, out, 0);
@@ -899,6 +1210,8 @@ static int narrowphase(const mrs_model_view* m, orc_ws* w, int g1, int g2, doubl
   } else if (t1 == MRS_GEOM_BOX && t2 == MRS_GEOM_BOX) {
     return col_box_box(p1, m1, s1, p2, m2, s2, margin, out, 0);
   }
+  /* every other pair has an ellipsoid, cylinder or mesh: general convex (MPR) */
+  if (t1 != MRS_GEOM_HFIELD && t2 != MRS_GEOM_HFIELD) return col_convex(m, w, g1, g2, margin, out, 0);
   return -1; /* unsupported pair */
 }
 
@@ -1499,12 +1812,52 @@ static double ray_geom_local(int type, const double* s, const double lp[3], cons
   }
   return -1;
 }
+/* ray vs a mesh's triangles, both faces (mj_rayMesh): the geom's bounding box first (slab test on the
+ * half extents geom_size), then every triangle (Moller-Trumbore); *tri = the nearest triangle */
+static double ray_mesh(const mrs_model_view* m, int g, const double lp[3], const double lv[3], int* tri) {
+  const double* s = m->geom_size + 3 * g;
+  double tmin = -1e300, tmax = 1e300;
+  for (int i = 0; i < 3; ++i) {
+    if (fabs(lv[i]) < MINVAL) {
+      if (fabs(lp[i]) > s[i]) return -1;
+      continue;
+    }
+    double t1 = (-s[i] - lp[i]) / lv[i], t2 = (s[i] - lp[i]) / lv[i];
+    if (t1 > t2) { double t = t1; t1 = t2; t2 = t; }
+    tmin = fmax(tmin, t1);
+    tmax = fmin(tmax, t2);
+  }
+  if (tmax < tmin || tmax < 0) return -1;
+  int id = m->geom_dataid[g];
+  const double* V = m->mesh_vert + 3 * m->mesh_vertadr[id];
+  const int* F = m->mesh_face + 3 * m->mesh_faceadr[id];
+  double best = -1;
+  for (int f = 0; f < m->mesh_facenum[id]; ++f) {
+    const double *a = V + 3 * F[3 * f], *b = V + 3 * F[3 * f + 1], *c = V + 3 * F[3 * f + 2];
+    double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+    double pv[3], tv[3], qv[3];
+    cross3(pv, lv, e2);
+    double det = dot3(e1, pv);
+    if (fabs(det) < MINVAL) continue;
+    double inv = 1 / det;
+    for (int i = 0; i < 3; ++i) tv[i] = lp[i] - a[i];
+    double u = dot3(tv, pv) * inv;
+    if (u < 0 || u > 1) continue;
+    cross3(qv, tv, e1);
+    double v = dot3(lv, qv) * inv;
+    if (v < 0 || u + v > 1) continue;
+    double t = dot3(e2, qv) * inv;
+    if (t >= 0 && (best < 0 || t < best)) { best = t; if (tri) *tri = f; }
+  }
+  return best;
+}
 static double ray_geom(const mrs_model_view* m, orc_ws* w, int g, const double pnt[3], const double vec[3]) {
   const double* gp = w->geom_xpos + 3 * g;
   const double* gm = w->geom_xmat + 9 * g;
   double dv[3] = {pnt[0] - gp[0], pnt[1] - gp[1], pnt[2] - gp[2]}, lp[3], lv[3];
   matT_vec(lp, gm, dv);
   matT_vec(lv, gm, vec);
+  if (m->geom_type[g] == MRS_GEOM_MESH) return ray_mesh(m, g, lp, lv, NULL);
   return ray_geom_local(m->geom_type[g], m->geom_size + 3 * g, lp, lv);
 }
 /* geoms a ray may hit: not on the excluded body, not fully transparent (ray_eliminate) */
@@ -1933,8 +2286,23 @@ void orc_render_rgbd(const mrs_model_view* m, orc_data* d, int cam, float* depth
       double dv[3], q[3], lv[3], nl[3], nw[3];
       for (int i = 0; i < 3; ++i) dv[i] = cpos[i] + t * vec[i] - w->geom_xpos[3 * g + i];
       matT_vec(q, gm, dv);
-      (void)lv;
-      local_normal(m->geom_type[g], m->geom_size + 3 * g, q, nl);
+      if (m->geom_type[g] == MRS_GEOM_MESH) {  /* the hit triangle's normal */
+        double lpc[3], dc2[3];
+        int tri = 0;
+        for (int i = 0; i < 3; ++i) dc2[i] = cpos[i] - w->geom_xpos[3 * g + i];
+        matT_vec(lpc, gm, dc2);
+        matT_vec(lv, gm, vec);
+        ray_mesh(m, g, lpc, lv, &tri);
+        int id = m->geom_dataid[g];
+        const double* V = m->mesh_vert + 3 * m->mesh_vertadr[id];
+        const int* F = m->mesh_face + 3 * (m->mesh_faceadr[id] + tri);
+        double e1[3], e2[3];
+        for (int i = 0; i < 3; ++i) { e1[i] = V[3 * F[1] + i] - V[3 * F[0] + i]; e2[i] = V[3 * F[2] + i] - V[3 * F[0] + i]; }
+        cross3(nl, e1, e2);
+        if (dot3(nl, lv) > 0) for (int i = 0; i < 3; ++i) nl[i] = -nl[i];  /* two-sided */
+      } else {
+        local_normal(m->geom_type[g], m->geom_size + 3 * g, q, nl);
+      }
       mat_vec(nw, gm, nl);
       double c = -dot3(nw, vec) / sqrt(fmax(dot3(nw, nw) * dot3(vec, vec), 1e-300));
       double k = 0.3 + 0.7 * (c > 0 ? c : 0);
