@@ -120,7 +120,8 @@ def test_keyframe(tmp_path):
 
 
 @pytest.mark.parametrize("xml, msg", [
-    ("<mujoco><worldbody><body><geom type='mesh'/></body></worldbody></mujoco>", "unsupported geom type"),
+    ("<mujoco><worldbody><body><geom type='mesh'/></body></worldbody></mujoco>", "needs a mesh attribute"),
+    ("<mujoco><worldbody><body><geom type='hfield'/></body></worldbody></mujoco>", "unsupported geom type"),
     ("<mujoco><worldbody><body><joint/><geom size='1'/></body></worldbody>", "XML error"),
     ("<mujoco><actuator><motor joint='nope'/></actuator></mujoco>", "unknown joint"),
     ("<mujoco><worldbody><geom class='zz'/></worldbody></mujoco>", "unknown default class"),
