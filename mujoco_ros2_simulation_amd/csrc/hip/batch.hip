@@ -16,6 +16,7 @@
 #include "../mjcf/model.h"
 #include "batch.h"
 #include "devmodel.h"
+#include "raymesh.h"
 
 namespace mrs {
 
@@ -37,6 +38,11 @@ namespace {
 // parameter of the nearest hit is the eye-space z that OpenGL + the plugin's linearisation
 // (src/mujoco_cameras.cpp:222-235) produce; rows in ROS order (flip of :229-240 applied).
 constexpr int kMaxRenderGeoms = 256;
+// the model's meshes for the render kernels (mrs_model.h mesh arrays, device copies)
+struct MeshRef {
+  const float* vert;
+  const int *face, *dataid, *vertadr, *faceadr, *facenum;
+};
 
 // analytic ray primitive (same restatement of engine_ray as the step kernel's rangefinder)
 __device__ float ray_prim(int type, const float* s, const float lp[3], const float lv[3]) {
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
                                                     const float* geom_xmat, const float* cam_xpos,
                                                     const float* cam_xmat, int ncam, int cam, int env0, int W,
                                                     int H, float f, float znear, float zfar, float* out,
-                                                    unsigned char* rgb) {
+                                                    unsigned char* rgb, MeshRef mesh) {
   __shared__ float gp[kMaxRenderGeoms * 3];
   __shared__ float gm[kMaxRenderGeoms * 9];
   __shared__ float cpos[3], cmat[9];
@@ -261,7 +267,14 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
     const float lv[3] = {mm[0] * vec[0] + mm[3] * vec[1] + mm[6] * vec[2],
                          mm[1] * vec[0] + mm[4] * vec[1] + mm[7] * vec[2],
                          mm[2] * vec[0] + mm[5] * vec[1] + mm[8] * vec[2]};
-    const float tt = ray_prim(t, geom_size + 3 * g, lp, lv);
+    float tt;
+    if (t == MRS_GEOM_MESH) {
+      const int id = mesh.dataid[g];
+      tt = ray_mesh(mesh.vert + 3 * mesh.vertadr[id], mesh.face + 3 * mesh.faceadr[id], mesh.facenum[id],
+                    geom_size + 3 * g, lp, lv);
+    } else {
+      tt = ray_prim(t, geom_size + 3 * g, lp, lv);
+    }
     if (tt >= znear && (best < 0 || tt < best)) { best = tt; bestg = g; }
   }
   const bool hit = !(best < 0 || best > zfar);
@@ -276,7 +289,21 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
     for (int i = 0; i < 3; ++i)
       q[i] = mm[i] * dv[0] + mm[3 + i] * dv[1] + mm[6 + i] * dv[2] +
              best * (mm[i] * vec[0] + mm[3 + i] * vec[1] + mm[6 + i] * vec[2]);
-    local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
+    if (geom_type[bestg] == MRS_GEOM_MESH) {  // the hit triangle's normal, facing the ray
+      const int id = mesh.dataid[bestg];
+      const float* mv = mesh.vert + 3 * mesh.vertadr[id];
+      const int* mf = mesh.face + 3 * mesh.faceadr[id];
+      float lp[3], lv[3];
+      for (int i = 0; i < 3; ++i) {
+        lp[i] = mm[i] * dv[0] + mm[3 + i] * dv[1] + mm[6 + i] * dv[2];
+        lv[i] = mm[i] * vec[0] + mm[3 + i] * vec[1] + mm[6 + i] * vec[2];
+      }
+      int tri = 0;
+      ray_mesh(mv, mf, mesh.facenum[id], geom_size + 3 * bestg, lp, lv, &tri);
+      mesh_tri_normal(mv, mf, tri, lv, nl);
+    } else {
+      local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
+    }
     for (int i = 0; i < 3; ++i) nw[i] = mm[3 * i] * nl[0] + mm[3 * i + 1] * nl[1] + mm[3 * i + 2] * nl[2];
     shade(geom_rgba + 4 * bestg, lambert(nw, vec), px);
   }
@@ -301,7 +328,7 @@ struct DepthGeom {  // 28 floats in LDS
   float lp[3], A[9], size[3];  // row i of A = R'C is also the geom's axis i in the camera frame
   float cc[3], ext[3];         // cull: centre in the camera frame, oriented-box half extents
   float rgba[3];               // colour (RGB output)
-  int type, vis;
+  int type, vis, dataid;
 };
 __device__ __forceinline__ float ray_box_slab(const float* s, const float lp[3], const float lv[3]) {
   float tmin = -3.0e38f, tmax = 3.0e38f;
@@ -325,7 +352,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                                                        const float* geom_xpos, const float* geom_xmat,
                                                        const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
                                                        int env0, int W, int H, float f, float znear, float zfar,
-                                                       float* out, unsigned char* rgb) {
+                                                       float* out, unsigned char* rgb, MeshRef mesh) {
   __shared__ DepthGeom G[kDepthGeoms];
   const int env = env0 + blockIdx.x;
   const size_t eo = static_cast<size_t>(env);
@@ -351,11 +378,12 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       o.cc[i] = -(C[i] * d[0] + C[3 + i] * d[1] + C[6 + i] * d[2]);
     }
     o.type = geom_type[g];
+    o.dataid = o.type == MRS_GEOM_MESH ? mesh.dataid[g] : -1;
     for (int c = 0; c < 3; ++c) o.rgba[c] = geom_rgba[4 * g + c];
     const float s0 = o.size[0], s1 = o.size[1], s2 = o.size[2];
     float e[3] = {s0, s0, s0};
     switch (o.type) {
-      case MRS_GEOM_BOX: case MRS_GEOM_ELLIPSOID: e[0] = s0; e[1] = s1; e[2] = s2; break;
+      case MRS_GEOM_BOX: case MRS_GEOM_ELLIPSOID: case MRS_GEOM_MESH: e[0] = s0; e[1] = s1; e[2] = s2; break;
       case MRS_GEOM_CAPSULE: e[2] = s1 + s0; break;
       case MRS_GEOM_CYLINDER: e[2] = s1; break;
       default: break;
@@ -428,6 +456,9 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                              A[6] * dx + A[7] * dy[k] - A[8]};
         float t;
         if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
+        else if (type == MRS_GEOM_MESH)
+          t = ray_mesh(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid],
+                       mesh.facenum[o.dataid], sz, lp, lv);
         else t = ray_prim(type, sz, lp, lv);
         if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
@@ -450,7 +481,17 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
           const float v[3] = {dx, dy[k], -1.0f};
           float q[3], nl[3], nc[3];
           for (int i = 0; i < 3; ++i) q[i] = o.lp[i] + best[k] * (o.A[3 * i] * dx + o.A[3 * i + 1] * dy[k] - o.A[3 * i + 2]);
-          local_normal(o.type, o.size, q, nl);
+          if (o.type == MRS_GEOM_MESH) {  // the hit triangle's normal, facing the ray
+            const float* mv = mesh.vert + 3 * mesh.vertadr[o.dataid];
+            const int* mf = mesh.face + 3 * mesh.faceadr[o.dataid];
+            const float lv[3] = {o.A[0] * dx + o.A[1] * dy[k] - o.A[2], o.A[3] * dx + o.A[4] * dy[k] - o.A[5],
+                                 o.A[6] * dx + o.A[7] * dy[k] - o.A[8]};
+            int tri = 0;
+            ray_mesh(mv, mf, mesh.facenum[o.dataid], o.size, o.lp, lv, &tri);
+            mesh_tri_normal(mv, mf, tri, lv, nl);
+          } else {
+            local_normal(o.type, o.size, q, nl);
+          }
           for (int j = 0; j < 3; ++j) nc[j] = nl[0] * o.A[j] + nl[1] * o.A[3 + j] + nl[2] * o.A[6 + j];
           shade(o.rgba, lambert(nc, v), px);
         }
@@ -583,10 +624,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
         const int ga = m.pair_geom1[q], gb = m.pair_geom2[q];
         const int g1 = std::min(ga, gb), g2 = std::max(ga, gb);
         int ta = m.geom_type[ga], tb = m.geom_type[gb];
-        bool ok = (ta == MRS_GEOM_PLANE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
-                  (ta == MRS_GEOM_SPHERE && (tb == MRS_GEOM_SPHERE || tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
-                  (ta == MRS_GEOM_CAPSULE && (tb == MRS_GEOM_CAPSULE || tb == MRS_GEOM_BOX)) ||
-                  (ta == MRS_GEOM_BOX && tb == MRS_GEOM_BOX);
+        // every pair of the implemented types: dedicated primitives, plane-ellipsoid/cylinder/mesh,
+        // and MPR for the rest (step.hip narrowphase); plane-plane never collides, hfields are absent
+        bool ok = ta != MRS_GEOM_HFIELD && tb != MRS_GEOM_HFIELD && tb != MRS_GEOM_PLANE;
         if (!ok)
           throw UnsupportedError("collision pair of geom types " + std::to_string(ta) + "/" + std::to_string(tb) +
                                  " is not implemented (geoms " + std::to_string(g1) + "," + std::to_string(g2) + ")");
@@ -666,11 +706,13 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nfric = static_cast<int>(fric.size());
   d.nlim = static_cast<int>(lim.size());
   d.nrf = static_cast<int>(rf.size());
-  // contact capacity per env: requested, or (<= 0) the pairs' own maxima (8 for box-box, 4 for the
-  // other primitive pairs) clamped to [32, 128]
+  // contact capacity per env: requested, or (<= 0) the pairs' own maxima (8 for box-box and
+  // plane-mesh, 4 for the other pairs) clamped to [32, 128]
   int pair_max = 0;
-  for (size_t p = 0; p < pg1.size(); ++p)
-    pair_max += m.geom_type[pg1[p]] == MRS_GEOM_BOX && m.geom_type[pg2[p]] == MRS_GEOM_BOX ? kMaxPairCon : 4;
+  for (size_t p = 0; p < pg1.size(); ++p) {
+    const int ta = m.geom_type[pg1[p]], tb = m.geom_type[pg2[p]];
+    pair_max += (ta == MRS_GEOM_BOX && tb == MRS_GEOM_BOX) || (ta == MRS_GEOM_PLANE && tb == MRS_GEOM_MESH) ? kMaxPairCon : 4;
+  }
   const int cap = max_con_req > 0 ? max_con_req : std::min(128, std::max(32, pair_max));
   d.max_con = d.npair == 0 ? 0 : std::min(pair_max, cap);
   d.max_efc = d.nfric + 2 * d.nlim + 4 * d.max_con;
@@ -714,6 +756,10 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.body_tree, body_tree); P.addi(&d.dof_tree, dof_tree); P.addi(&d.tree_dofadr, tree_dofadr);
   P.addi(&d.tree_dofnum, tree_dofnum); P.addi(&d.tree_Moff, tree_Moff);
   P.addi(&d.geom_type, m.geom_type); P.addi(&d.geom_bodyid, m.geom_bodyid); P.addi(&d.geom_group, m.geom_group);
+  P.addi(&d.geom_dataid, m.geom_dataid);
+  P.addi(&d.mesh_vertadr, m.mesh_vertadr); P.addi(&d.mesh_faceadr, m.mesh_faceadr); P.addi(&d.mesh_facenum, m.mesh_facenum);
+  P.addi(&d.mesh_hulladr, m.mesh_hulladr); P.addi(&d.mesh_hullnum, m.mesh_hullnum); P.addi(&d.mesh_face, m.mesh_face);
+  P.addi(&d.mesh_hull, m.mesh_hull); P.addf(&d.mesh_vert, m.mesh_vert);
   P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
   P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
   P.addi(&d.pair_g1, pg1); P.addi(&d.pair_g2, pg2); P.addi(&d.pair_dim, pdim);
@@ -737,7 +783,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     if (m.geom_rgba[4 * g + 3] == 0) continue;
     rgeom.insert(rgeom.end(), {bits(g), bits(m.geom_type[g]), bits(m.geom_bodyid[g]),
                                static_cast<float>(m.geom_rbound[g]), static_cast<float>(m.geom_size[3 * g]),
-                               static_cast<float>(m.geom_size[3 * g + 1]), static_cast<float>(m.geom_size[3 * g + 2]), 0.0f});
+                               static_cast<float>(m.geom_size[3 * g + 1]), static_cast<float>(m.geom_size[3 * g + 2]),
+                               bits(m.geom_dataid[g])});
   }
   d.nrgeom = static_cast<int>(rgeom.size() / 8);
   P.addf(&d.rgeom, rgeom);
@@ -1197,16 +1244,17 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
   const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
   const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
   const DevModel& d = b->dm;
+  const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p, d.mesh_facenum.p};
   HIP_CHECK(hipEventRecord(b->ev0[1], b->stream));
   if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
     hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
   } else {
     dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
     hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
                        d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
   }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(b->ev1[1], b->stream));

@@ -105,8 +105,12 @@ struct DevModel {
   CPtr<int> Mpair;  // [nMpair][2] (i, j) with j = i or an ancestor dof of i
   CPtr<int> body_tree, dof_tree, tree_dofadr, tree_dofnum, tree_Moff;  // tree -1: world / no dofs
   // geoms
-  CPtr<int> geom_type, geom_bodyid, geom_group;
+  CPtr<int> geom_type, geom_bodyid, geom_group, geom_dataid;
   CPtr<float> geom_size, geom_pos, geom_quat, geom_rbound, geom_rgba;
+  // meshes (mrs_model.h): vertices in the mesh frame, triangles and convex-hull vertex ids (both
+  // relative to the mesh's first vertex)
+  CPtr<int> mesh_vertadr, mesh_faceadr, mesh_facenum, mesh_hulladr, mesh_hullnum, mesh_face, mesh_hull;
+  CPtr<float> mesh_vert;
   // candidate collision pairs (static filters applied; g1 has the smaller geom type)
   CPtr<int> pair_g1, pair_g2, pair_dim;
   CPtr<float> pair_margin, pair_gap, pair_friction /*3*/, pair_solref /*2*/, pair_solimp /*5*/;

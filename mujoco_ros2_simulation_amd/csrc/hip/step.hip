@@ -14,6 +14,7 @@
 #include <utility>
 
 #include "devmodel.h"
+#include "raymesh.h"
 
 namespace mrs {
 
@@ -632,10 +633,325 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
   return n;
 }
 
+// ---- general convex pairs (ellipsoid, cylinder, mesh): Minkowski Portal Refinement in fp32, the
+// same steps as the oracle's mpr_penetration (oracle.c; MuJoCo mjc_Convex via libccd's
+// ccdMPRPenetration with each shape inflated by margin/2, mpr_tolerance 1e-6, 50 iterations).  One
+// contact: dist = margin - depth, normal geom1 -> geom2, position midway between the shapes'
+// portal-interpolated surface points.  Lane-parallel like every narrow-phase routine (one pair per
+// lane); mesh hull vertices are read from the model block (per-lane global loads).
+constexpr float kMprTol = 1e-6f, kMprEps = 1e-10f;
+constexpr int kMprIter = 50;
+struct Shape {
+  int type, vadr, hadr, nhull;
+  float pos[3], mat[9], size[3], inflate;
+};
+struct MprPoint { float v[3], a[3], b[3]; };
+struct MeshTab { CPtr<float> vert; CPtr<int> hull; };  // the model's mesh vertices and hull ids
+
+__device__ __forceinline__ void shape_support(const MeshTab m, const Shape& s, const float dir[3], float out[3]) {
+  float l[3], p[3] = {0, 0, 0};
+  matT_vec(l, s.mat, dir);
+  const float* z = s.size;
+  switch (s.type) {
+    case MRS_GEOM_SPHERE:
+    case MRS_GEOM_CAPSULE: {
+      const float n = sqrtf(dot3(l, l));
+      if (n > kMinVal) for (int i = 0; i < 3; ++i) p[i] = z[0] * l[i] / n;
+      if (s.type == MRS_GEOM_CAPSULE) p[2] += l[2] >= 0 ? z[1] : -z[1];
+      break;
+    }
+    case MRS_GEOM_ELLIPSOID: {
+      const float t[3] = {z[0] * z[0] * l[0], z[1] * z[1] * l[1], z[2] * z[2] * l[2]};
+      const float den = sqrtf(t[0] * l[0] + t[1] * l[1] + t[2] * l[2]);
+      if (den > kMinVal) for (int i = 0; i < 3; ++i) p[i] = t[i] / den;
+      break;
+    }
+    case MRS_GEOM_CYLINDER: {
+      const float rr = sqrtf(l[0] * l[0] + l[1] * l[1]);
+      if (rr > kMinVal) { p[0] = z[0] * l[0] / rr; p[1] = z[0] * l[1] / rr; }
+      p[2] = l[2] >= 0 ? z[1] : -z[1];
+      break;
+    }
+    case MRS_GEOM_BOX:
+      for (int i = 0; i < 3; ++i) p[i] = l[i] >= 0 ? z[i] : -z[i];
+      break;
+    case MRS_GEOM_MESH: {
+      float best = -3.0e38f;
+      for (int k = 0; k < s.nhull; ++k) {
+        const int v = 3 * (s.vadr + m.hull[s.hadr + k]);
+        const float x = m.vert[v], y = m.vert[v + 1], w = m.vert[v + 2];
+        const float d = x * l[0] + y * l[1] + w * l[2];
+        if (d > best) { best = d; p[0] = x; p[1] = y; p[2] = w; }
+      }
+      break;
+    }
+    default: break;
+  }
+  mat_vec(out, s.mat, p);
+  const float dn = sqrtf(dot3(dir, dir));
+  const float k = dn > kMinVal ? s.inflate / dn : 0.0f;
+  for (int i = 0; i < 3; ++i) out[i] += s.pos[i] + k * dir[i];
+}
+__device__ __forceinline__ void mpr_support(const MeshTab m, const Shape& A, const Shape& B, const float dir[3],
+                                            MprPoint& p) {
+  const float nd[3] = {-dir[0], -dir[1], -dir[2]};
+  shape_support(m, A, dir, p.a);
+  shape_support(m, B, nd, p.b);
+  for (int i = 0; i < 3; ++i) p.v[i] = p.a[i] - p.b[i];
+}
+__device__ __forceinline__ void tri_normal(float n[3], const float a[3], const float b[3], const float c[3]) {
+  const float u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, v[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  cross3(n, u, v);
+  normalize3(n);
+}
+// closest point to the origin on triangle abc (Ericson 5.1.5)
+__device__ __forceinline__ void closest_on_triangle(const float a[3], const float b[3], const float c[3], float out[3]) {
+  float ab[3], ac[3], ap[3], bp[3], cp[3];
+  for (int i = 0; i < 3; ++i) {
+    ab[i] = b[i] - a[i]; ac[i] = c[i] - a[i];
+    ap[i] = -a[i]; bp[i] = -b[i]; cp[i] = -c[i];
+  }
+  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { for (int i = 0; i < 3; ++i) out[i] = a[i]; return; }
+  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { for (int i = 0; i < 3; ++i) out[i] = b[i]; return; }
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    const float t = d1 / (d1 - d3);
+    for (int i = 0; i < 3; ++i) out[i] = a[i] + t * ab[i];
+    return;
+  }
+  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { for (int i = 0; i < 3; ++i) out[i] = c[i]; return; }
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    const float t = d2 / (d2 - d6);
+    for (int i = 0; i < 3; ++i) out[i] = a[i] + t * ac[i];
+    return;
+  }
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int i = 0; i < 3; ++i) out[i] = b[i] + t * (c[i] - b[i]);
+    return;
+  }
+  const float den = 1.0f / (va + vb + vc), v = vb * den, w = vc * den;
+  for (int i = 0; i < 3; ++i) out[i] = a[i] + ab[i] * v + ac[i] * w;
+}
+__device__ __forceinline__ void mpr_expand(MprPoint p[4], const MprPoint& v4) {
+  float x[3];
+  cross3(x, v4.v, p[0].v);
+  if (dot3(p[1].v, x) > 0) {
+    if (dot3(p[2].v, x) > 0) p[1] = v4;
+    else p[3] = v4;
+  } else {
+    if (dot3(p[3].v, x) > 0) p[2] = v4;
+    else p[1] = v4;
+  }
+}
+__device__ __forceinline__ bool mpr_reach_tolerance(const MprPoint p[4], const MprPoint& v4, const float n[3]) {
+  const float d4 = dot3(v4.v, n);
+  const float g = fminf(d4 - dot3(p[1].v, n), fminf(d4 - dot3(p[2].v, n), d4 - dot3(p[3].v, n)));
+  return g <= kMprTol;
+}
+// 0: origin inside the portal cone, 1: touching, 2: origin on segment p0-p1, -1: separated
+__device__ __forceinline__ int mpr_discover(const MeshTab m, const Shape& A, const Shape& B, MprPoint p[4]) {
+  for (int i = 0; i < 3; ++i) { p[0].a[i] = A.pos[i]; p[0].b[i] = B.pos[i]; p[0].v[i] = A.pos[i] - B.pos[i]; }
+  if (dot3(p[0].v, p[0].v) < 1e-20f) p[0].v[0] += 1e-5f;
+  float dir[3] = {-p[0].v[0], -p[0].v[1], -p[0].v[2]};
+  normalize3(dir);
+  mpr_support(m, A, B, dir, p[1]);
+  if (dot3(p[1].v, dir) <= 0) return -1;
+  cross3(dir, p[0].v, p[1].v);
+  if (dot3(dir, dir) < kMprEps) return dot3(p[1].v, p[1].v) < kMprEps ? 1 : 2;
+  normalize3(dir);
+  mpr_support(m, A, B, dir, p[2]);
+  if (dot3(p[2].v, dir) <= 0) return -1;
+  float va[3], vb[3];
+  for (int i = 0; i < 3; ++i) { va[i] = p[1].v[i] - p[0].v[i]; vb[i] = p[2].v[i] - p[0].v[i]; }
+  cross3(dir, va, vb);
+  normalize3(dir);
+  if (dot3(dir, p[0].v) > 0) {
+    const MprPoint t = p[1];
+    p[1] = p[2];
+    p[2] = t;
+    for (int i = 0; i < 3; ++i) dir[i] = -dir[i];
+  }
+  for (int it = 0; it < kMprIter; ++it) {
+    mpr_support(m, A, B, dir, p[3]);
+    if (dot3(p[3].v, dir) <= 0) return -1;
+    float x[3];
+    bool replaced = false;
+    cross3(x, p[1].v, p[3].v);
+    if (dot3(x, p[0].v) < -kMprEps) { p[2] = p[3]; replaced = true; }
+    else {
+      cross3(x, p[3].v, p[2].v);
+      if (dot3(x, p[0].v) < -kMprEps) { p[1] = p[3]; replaced = true; }
+    }
+    if (!replaced) return 0;
+    for (int i = 0; i < 3; ++i) { va[i] = p[1].v[i] - p[0].v[i]; vb[i] = p[2].v[i] - p[0].v[i]; }
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  return 0;
+}
+__device__ __forceinline__ void mpr_position(const MprPoint p[4], float pos[3]) {
+  float n[3], x[3], b[4];
+  tri_normal(n, p[1].v, p[2].v, p[3].v);
+  cross3(x, p[1].v, p[2].v); b[0] = dot3(x, p[3].v);
+  cross3(x, p[3].v, p[2].v); b[1] = dot3(x, p[0].v);
+  cross3(x, p[0].v, p[1].v); b[2] = dot3(x, p[3].v);
+  cross3(x, p[2].v, p[1].v); b[3] = dot3(x, p[0].v);
+  float sum = b[0] + b[1] + b[2] + b[3];
+  if (sum <= kMprEps) {
+    b[0] = 0;
+    cross3(x, p[2].v, p[3].v); b[1] = dot3(x, n);
+    cross3(x, p[3].v, p[1].v); b[2] = dot3(x, n);
+    cross3(x, p[1].v, p[2].v); b[3] = dot3(x, n);
+    sum = b[1] + b[2] + b[3];
+  }
+  for (int i = 0; i < 3; ++i) {
+    float pa = 0, pb = 0;
+    for (int k = 0; k < 4; ++k) { pa += b[k] * p[k].a[i]; pb += b[k] * p[k].b[i]; }
+    pos[i] = 0.5f * (pa + pb) / sum;
+  }
+}
+// inlined: as an out-of-line call its ABI raised the G = 32 / 64 kernels from 128 / 168 VGPRs to
+// 246 (half the occupancy) for every model; inlined it only adds scratch to the convex path
+__device__ __forceinline__ bool mpr_penetration(const MeshTab m, const Shape A, const Shape B,
+                                                          float& depth, float nrm[3], float pos[3]) {
+  MprPoint p[4], v4;
+  const int r = mpr_discover(m, A, B, p);
+  if (r < 0 || r == 1) return false;
+  if (r == 2) {
+    for (int i = 0; i < 3; ++i) { nrm[i] = p[1].v[i]; pos[i] = 0.5f * (p[1].a[i] + p[1].b[i]); }
+    depth = normalize3(nrm);
+    return true;
+  }
+  for (int it = 0;; ++it) {
+    float n[3];
+    tri_normal(n, p[1].v, p[2].v, p[3].v);
+    if (dot3(n, p[1].v) >= 0) break;
+    mpr_support(m, A, B, n, v4);
+    if (dot3(v4.v, n) < 0 || mpr_reach_tolerance(p, v4, n) || it >= kMprIter) return false;
+    mpr_expand(p, v4);
+  }
+  for (int it = 0;; ++it) {
+    float n[3];
+    tri_normal(n, p[1].v, p[2].v, p[3].v);
+    mpr_support(m, A, B, n, v4);
+    if (mpr_reach_tolerance(p, v4, n) || it > kMprIter) {
+      closest_on_triangle(p[1].v, p[2].v, p[3].v, nrm);
+      depth = sqrtf(dot3(nrm, nrm));
+      if (depth < kMinVal) return false;
+      for (int i = 0; i < 3; ++i) nrm[i] /= depth;
+      mpr_position(p, pos);
+      return true;
+    }
+    mpr_expand(p, v4);
+  }
+}
+__device__ __forceinline__ void shape_of(const DevModel& m, int g, const float* p, const float* mat, const float* size,
+                                         float inflate, Shape& s) {
+  s.type = m.geom_type[g];
+  for (int i = 0; i < 3; ++i) { s.pos[i] = p[i]; s.size[i] = size[i]; }
+  for (int i = 0; i < 9; ++i) s.mat[i] = mat[i];
+  s.inflate = inflate;
+  s.vadr = s.hadr = s.nhull = 0;
+  if (s.type == MRS_GEOM_MESH) {
+    const int id = m.geom_dataid[g];
+    s.vadr = m.mesh_vertadr[id];
+    s.hadr = m.mesh_hulladr[id];
+    s.nhull = m.mesh_hullnum[id];
+  }
+}
+__device__ __forceinline__ int convex_convex(const DevModel& m, int g1, int g2, const float* p1, const float* m1, const float* s1,
+                             const float* p2, const float* m2, const float* s2, float margin, gCon* out) {
+  Shape A, B;
+  shape_of(m, g1, p1, m1, s1, 0.5f * margin, A);
+  shape_of(m, g2, p2, m2, s2, 0.5f * margin, B);
+  float depth, nrm[3], pos[3];
+  if (!mpr_penetration(MeshTab{m.mesh_vert, m.mesh_hull}, A, B, depth, nrm, pos)) return 0;
+  gCon& o = out[0];
+  for (int i = 0; i < 3; ++i) { o.pos[i] = pos[i]; o.nrm[i] = nrm[i]; }
+  o.dist = margin - depth;
+  return 1;
+}
+// plane (geom1) vs ellipsoid: the support point along -normal
+__device__ __forceinline__ int plane_support(const DevModel& m, int g2, const float* pp, const float* pm, const float* p2,
+                             const float* m2, const float* s2, float margin, gCon* out) {
+  Shape B;
+  shape_of(m, g2, p2, m2, s2, 0.0f, B);
+  const float nrm[3] = {pm[2], pm[5], pm[8]}, nd[3] = {-nrm[0], -nrm[1], -nrm[2]};
+  float s[3];
+  shape_support(MeshTab{m.mesh_vert, m.mesh_hull}, B, nd, s);
+  const float dv[3] = {s[0] - pp[0], s[1] - pp[1], s[2] - pp[2]};
+  const float dist = dot3(dv, nrm);
+  if (dist > margin) return 0;
+  gCon& o = out[0];
+  for (int i = 0; i < 3; ++i) { o.pos[i] = s[i] - nrm[i] * dist / 2; o.nrm[i] = nrm[i]; }
+  o.dist = dist;
+  return 1;
+}
+// plane vs cylinder (oracle.c col_plane_cylinder): deepest rim point of each cap, plus the rim points
+// at +-120 degrees on the deeper cap; the rim direction falls back to the cylinder's x axis when the
+// axis is parallel to the normal
+__device__ int plane_cylinder(const float* pp, const float* pm, const float* cp, const float* cm, const float* size,
+                              float margin, gCon* out) {
+  const float nrm[3] = {pm[2], pm[5], pm[8]}, ax[3] = {cm[2], cm[5], cm[8]};
+  const float an = dot3(ax, nrm);
+  float d[3];
+  for (int i = 0; i < 3; ++i) d[i] = -nrm[i] + an * ax[i];
+  if (dot3(d, d) < 1e-12f) { d[0] = cm[0]; d[1] = cm[3]; d[2] = cm[6]; }
+  normalize3(d);
+  float e[3];
+  cross3(e, ax, d);
+  const float sdeep = an > 0 ? -1.0f : 1.0f;
+  int n = 0;
+  for (int cap = 0; cap < 2; ++cap) {
+    const float sc = cap == 0 ? sdeep : -sdeep;
+    const int npts = cap == 0 ? 3 : 1;
+    for (int k = 0; k < npts; ++k) {
+      const float cu = k == 0 ? 1.0f : -0.5f, cv = k == 0 ? 0.0f : (k == 1 ? 0.8660254037844386f : -0.8660254037844386f);
+      float p[3], dv[3];
+      for (int i = 0; i < 3; ++i) p[i] = cp[i] + sc * size[1] * ax[i] + size[0] * (cu * d[i] + cv * e[i]);
+      for (int i = 0; i < 3; ++i) dv[i] = p[i] - pp[i];
+      const float dist = dot3(dv, nrm);
+      if (dist > margin) continue;
+      gCon& o = out[n++];
+      for (int i = 0; i < 3; ++i) { o.pos[i] = p[i] - nrm[i] * dist / 2; o.nrm[i] = nrm[i]; }
+      o.dist = dist;
+    }
+  }
+  return n;
+}
+// plane vs mesh: every convex-hull vertex within margin, in hull order (at most kMaxPairCon)
+__device__ __forceinline__ int plane_mesh(const DevModel& m, int g2, const float* pp, const float* pm, const float* bp,
+                          const float* bm, float margin, gCon* out) {
+  const float nrm[3] = {pm[2], pm[5], pm[8]};
+  const int id = m.geom_dataid[g2];
+  const int vadr = m.mesh_vertadr[id], hadr = m.mesh_hulladr[id], nh = m.mesh_hullnum[id];
+  int n = 0;
+  for (int k = 0; k < nh && n < kMaxPairCon; ++k) {
+    const int v = 3 * (vadr + m.mesh_hull[hadr + k]);
+    const float lv[3] = {m.mesh_vert[v], m.mesh_vert[v + 1], m.mesh_vert[v + 2]};
+    float p[3];
+    mat_vec(p, bm, lv);
+    for (int i = 0; i < 3; ++i) p[i] += bp[i];
+    const float dv[3] = {p[0] - pp[0], p[1] - pp[1], p[2] - pp[2]};
+    const float dist = dot3(dv, nrm);
+    if (dist > margin) continue;
+    gCon& o = out[n++];
+    for (int i = 0; i < 3; ++i) { o.pos[i] = p[i] - nrm[i] * dist / 2; o.nrm[i] = nrm[i]; }
+    o.dist = dist;
+  }
+  return n;
+}
+
 template <int G>
-__device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, const float* s1, const float* p2,
-                           const float* m2, const float* s2, float margin, gCon* out, const lfloat* gxpos,
-                           const lfloat* gxmat, CPtr<float> gsize, int g1, int g2) {
+__device__ int narrowphase(const DevModel& m, int t1, int t2, const float* p1, const float* m1, const float* s1,
+                           const float* p2, const float* m2, const float* s2, float margin, gCon* out,
+                           const lfloat* gxpos, const lfloat* gxmat, CPtr<float> gsize, int g1, int g2) {
   float a1[3], b1[3], a2[3], b2[3], c1[3], c2[3];
   int n = 0;
   if (t1 == MRS_GEOM_PLANE) {
@@ -646,6 +962,10 @@ __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, con
       return plane_sphere(p1, m1, b2, s2[0], margin, out, n);
     }
     if (t2 == MRS_GEOM_BOX) return plane_box(p1, m1, p2, m2, s2, margin, out, 0);
+    if (t2 == MRS_GEOM_ELLIPSOID) return plane_support(m, g2, p1, m1, p2, m2, s2, margin, out);
+    if (t2 == MRS_GEOM_CYLINDER) return plane_cylinder(p1, m1, p2, m2, s2, margin, out);
+    if (t2 == MRS_GEOM_MESH) return plane_mesh(m, g2, p1, m1, p2, m2, margin, out);
+    return 0;
   } else if (t1 == MRS_GEOM_SPHERE) {
     if (t2 == MRS_GEOM_SPHERE) return sphere_sphere(p1, s1[0], p2, s2[0], margin, out, 0);
     if (t2 == MRS_GEOM_CAPSULE) {
@@ -671,7 +991,8 @@ __device__ int narrowphase(int t1, int t2, const float* p1, const float* m1, con
 #endif
     return box_box<G>(gxpos, gxmat, gsize, g1, g2, margin, out);
   }
-  return 0;
+  // every other pair has an ellipsoid, cylinder or mesh: general convex (MPR)
+  return convex_convex(m, g1, g2, p1, m1, s1, p2, m2, s2, margin, out);
 }
 // mju_makeFrame: tangent basis from the contact normal
 __device__ __forceinline__ void make_frame(float f[9]) {
@@ -1565,7 +1886,7 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
         for (int i = 0; i < 9; ++i) { m1[i] = s[L.gxmat + 9 * g1 + i]; m2[i] = s[L.gxmat + 9 * g2 + i]; }
         float s1[3] = {m.geom_size[3 * g1], m.geom_size[3 * g1 + 1], m.geom_size[3 * g1 + 2]};
         float s2[3] = {m.geom_size[3 * g2], m.geom_size[3 * g2 + 1], m.geom_size[3 * g2 + 2]};
-        n = narrowphase<G>(t1, t2, p1, m1, s1, p2, m2, s2, margin, c, s + L.gxpos, s + L.gxmat, m.geom_size, g1, g2);
+        n = narrowphase<G>(m, t1, t2, p1, m1, s1, p2, m2, s2, margin, c, s + L.gxpos, s + L.gxmat, m.geom_size, g1, g2);
       }
       SUB_ADD(PH_COLL_NARROW, t_np);
     }
@@ -3317,7 +3638,14 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
         matT_vec(lp, gm, dv);
       }
       matT_vec(lv, gm, vec[j]);
-      const float t = ray_geom_local(type, gs, lp, lv);
+      float t;
+      if (type == MRS_GEOM_MESH) {  // wave-uniform mesh: its triangles arrive by scalar loads
+        const int id = __float_as_int(rec[7]);
+        t = ray_mesh(m.mesh_vert + 3 * m.mesh_vertadr[id], m.mesh_face + 3 * m.mesh_faceadr[id], m.mesh_facenum[id],
+                     gs, lp, lv);
+      } else {
+        t = ray_geom_local(type, gs, lp, lv);
+      }
       if (t >= 0 && (dist[j] < 0 || t < dist[j])) dist[j] = t;
     }
   }
