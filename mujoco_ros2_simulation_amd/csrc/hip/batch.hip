@@ -995,6 +995,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_item = take(d.blocked ? ne : 0);
   S.efc_fq = take(d.blocked ? ne : 0);
   S.efc_hdr = take(d.blocked ? 8 * ne : 0);
+  S.efc_quad = take(d.blocked ? 64 : 0);
   S.stage = take(d.npair > 0 ? 64 * kMaxPairCon * 7 : 0);  // <= 64 lanes x 8 contacts x 7 floats
   S.efc_n = take(1);
   S.sens = take(std::max(1, m.nsensordata));

@@ -56,6 +56,7 @@ struct ScratchLayout {
       efc_item,              // blocked mode: first row of the item starting at a record (int bits)
       efc_fq,                // blocked mode: row forces by record (global-record fallback path)
       efc_hdr,               // blocked mode: 8-float header of the item starting at a record
+      efc_quad,              // blocked mode: per pipe, its first 16 items (record | rows << 16)
       sens,                  // sensordata sink of idle lane groups (envs past n_envs)
       efc_n;                 // rows of the dense layout of the last forward (int bits; -1: none stored)
   int total;

@@ -2068,7 +2068,12 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
 // env's scratch in solver order, pipe p's rows at [start_p, start_p + n_p); each level k of a sweep
 // is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
 typedef float v4f __attribute__((ext_vector_type(4)));
-constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, pad x3
+constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, then the coupling
+                             // J_r M^-1 J_s' of row r to the earlier rows s < r of its item (3 floats)
+#ifndef MRS_REG_QUADS
+#define MRS_REG_QUADS 12
+#endif
+constexpr int kRegQuads = MRS_REG_QUADS;  // items per pipe of the item-blocked register solve
 #ifndef MRS_REG_LEVELS
 #define MRS_REG_LEVELS 48
 #endif
@@ -2462,6 +2467,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   // --- 3. records, one item per pipe per level: J of the item's rows from the contact Jacobian
   // (jc: normal and two tangent rows, pyramid edges jc0 +- mu jck), M^-1 of the three jc vectors in
   // one interleaved block solve, impedance once per item
+  gfloat* quadtab = scr + S.efc_quad;  // per pipe, its first 16 items in order: record | rows << 16
+  int my_nq = 0;                        // items of this lane's pipe
   {
     const int my_end = my_start + my_n;
     int qc = my_start;
@@ -2500,6 +2507,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       float mjc[3];
       pipe_msolve3(m, s + L.L, sm, pbase, jc, mjc);
       const float qv = d >= 0 ? s[L.qvel + d] : 0.0f, qs = d >= 0 ? s[L.qacc_smooth + d] : 0.0f;
+      if (act && slot == 0 && my_nq < 16) quadtab[pipe * 16 + my_nq] = __int_as_float(q0 | (nr << 16));
+      float MJk[3] = {0, 0, 0};  // M^-1 J' of the item's earlier rows (for the couplings)
       unroll<4>([&](auto jcst) {
         constexpr int j = decltype(jcst)::value;
         constexpr int k = 1 + (j >> 1);
@@ -2509,6 +2518,12 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         if (j == 0 || __any(act && j < nr)) {
           const float vel = gsum<P>(J * qv), jqs = gsum<P>(J * qs), jmj = gsum<P>(J * MJ);
           const float aref = -B * vel - pterm;
+          float cpl[3] = {0, 0, 0};
+          unroll<3>([&](auto sc) {
+            constexpr int s_ = decltype(sc)::value;
+            if constexpr (s_ < j) cpl[s_] = gsum<P>(J * MJk[s_]);
+          });
+          if constexpr (j < 3) MJk[j] = MJ;
           if (act && j < nr) {
             gfloat* o = rec + (q0 + j) * RF;
             o[slot] = J;
@@ -2520,19 +2535,215 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
               o[3 * P + 2] = jmj + R;
               o[3 * P + 3] = bound;
               o[3 * P + 4] = jqs - aref;
+              o[3 * P + 5] = cpl[0];
+              o[3 * P + 6] = cpl[1];
+              o[3 * P + 7] = cpl[2];
               rowof[q0 + j] = __int_as_float(r0 + j);
             }
           }
         }
       });
       qc += act ? nr : 0;
+      my_nq += act ? 1 : 0;
     }
   }
+  const int nq_max = uniform_int(wave_max(my_nq));
   wsync();
   SUB_ADD(PH_CON_REC, t_sub);
   t_sub = SUB_T();
   if (lane < nv) qa[lane] = qacc_s;
   const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+
+  // --- item-blocked register solve: P = 16 and at most kRegQuads items per pipe.  Item i of a pipe
+  // takes levels 4i..4i+3 (its 1 or 4 rows, the rest neutral: J = 0, R = a = 1, bounds [0, inf)), and
+  // all of an item's rows share one dof per slot (a contact's rows span the same two trees).  A sweep
+  // visits an item with one LDS read of qacc, the four J qacc sums as independent DPP reductions, the
+  // rows' Gauss-Seidel updates as a scalar chain through the couplings c_rs = J_r M^-1 J_s' (row r
+  // sees qacc + sum_{s<r} M^-1 J_s' df_s, so J_r qacc moves by sum c_rs df_s: the same iterates as
+  // the row-serial sweep), and one LDS write of qacc + sum_r M^-1 J_r' df_r.  Lane (pipe, slot) keeps
+  // J and M^-1 J' of its slot for every level; the scalars of level k live in slot k % 16.
+  if constexpr (P == 16) {
+    if (nq_max <= kRegQuads) {
+      constexpr int NQ = kRegQuads, NL = 4 * NQ, NB = NL / 16;
+      float Jr[NL], MJr[NL], sa[NB], sR[NB], sA[NB], sLo[NB], sHi[NB], sB[NB], fr[NB];
+      float sC0[NB], sC1[NB], sC2[NB];
+      unsigned dpk[(NQ + 3) / 4];
+      const unsigned dummy = static_cast<unsigned>(nv);
+      if (lane == 0) { qa[nv] = 0; tmp[nv] = 0; }
+      unroll<(NQ + 3) / 4>([&](auto ic) { dpk[decltype(ic)::value] = dummy * 0x01010101u; });
+      unroll<NB>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sa[i] = 0; sR[i] = 1; sA[i] = 1; sLo[i] = 0; sHi[i] = 3.0e38f; sB[i] = 0; fr[i] = 0;
+        sC0[i] = 0; sC1[i] = 0; sC2[i] = 0;
+      });
+      unroll<NQ>([&](auto qc) {
+        constexpr int i = decltype(qc)::value;
+        unroll<4>([&](auto rc) { Jr[4 * i + decltype(rc)::value] = 0; MJr[4 * i + decltype(rc)::value] = 0; });
+        if (i < nq_max) {
+          const bool act = i < my_nq;
+          const int qt = act ? __float_as_int(quadtab[pipe * 16 + i]) : 0;
+          const int q = qt & 0xffff, nr = qt >> 16;
+          const int d = __float_as_int(rec[q * RF + 2 * P + slot]);
+          if (act) {
+            const unsigned di = d >= 0 ? static_cast<unsigned>(d) : dummy;
+            dpk[i / 4] = (dpk[i / 4] & ~(0xffu << (8 * (i % 4)))) | (di << (8 * (i % 4)));
+          }
+          unroll<4>([&](auto rc) {
+            constexpr int r = decltype(rc)::value, k = 4 * i + r;
+            if (act && r < nr) {
+              const gfloat* o = rec + (q + r) * RF;
+              Jr[k] = o[slot];
+              MJr[k] = o[P + slot];
+              if (slot == k % 16) {
+                const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
+                const v4f sd = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P + 4);
+                sa[k / 16] = sc.x; sR[k / 16] = sc.y; sA[k / 16] = sc.z;
+                sLo[k / 16] = sc.w >= 0 ? -sc.w : 0.0f;     // friction: [-frictionloss, frictionloss]
+                sHi[k / 16] = sc.w >= 0 ? sc.w : 3.0e38f;   // others: [0, inf)
+                sB[k / 16] = sd.x;
+                sC0[k / 16] = sd.y; sC1[k / 16] = sd.z; sC2[k / 16] = sd.w;
+              }
+            }
+          });
+        }
+      });
+      wsync();
+      auto dof_of = [&](auto qc) {
+        constexpr int i = decltype(qc)::value;
+        return static_cast<int>(__builtin_amdgcn_ubfe(dpk[i / 4], 8 * (i % 4), 8));
+      };
+      // warm start
+      unroll<NQ>([&](auto qc) {
+        constexpr int i = decltype(qc)::value;
+        if (i < nq_max) {
+          const float w = warm ? s[L.qacc_ws + dof_of(qc)] : 0.0f;
+          unroll<4>([&](auto rc) {
+            constexpr int k = 4 * i + decltype(rc)::value;
+            float f = 0;
+            if (warm) {
+              const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+              const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
+              const float jar = gsum<16>(Jr[k] * w) - aref;
+              const float D = 1.0f / R;
+              if (lo < 0) f = jar <= -R * hi ? hi : (jar >= R * hi ? -hi : -D * jar);
+              else f = jar < 0 ? -D * jar : 0.0f;
+            }
+            if (slot == k % 16) fr[k / 16] = f;  // neutral rows: J = 0, aref = 0 -> f = 0
+          });
+        }
+      });
+      if (warm) {
+        if (lane < nv) tmp[lane] = 0;
+        wsync();
+        unroll<NQ>([&](auto qc) {
+          constexpr int i = decltype(qc)::value;
+          if (i < nq_max) {
+            const int d = dof_of(qc);
+            float acc = 0;
+            unroll<4>([&](auto rc) {
+              constexpr int k = 4 * i + decltype(rc)::value;
+              acc += MJr[k] * rowb<k % 16>(fr[k / 16]);
+            });
+            tmp[d] += acc;
+          }
+        });
+        wsync();
+        float cost = 0;
+        unroll<NQ>([&](auto qc) {
+          constexpr int i = decltype(qc)::value;
+          if (i < nq_max) {
+            const float t = tmp[dof_of(qc)];
+            unroll<4>([&](auto rc) {
+              constexpr int k = 4 * i + decltype(rc)::value;
+              const float jv = gsum<16>(Jr[k] * t);
+              const float f = rowb<k % 16>(fr[k / 16]), R = rowb<k % 16>(sR[k / 16]), b = rowb<k % 16>(sB[k / 16]);
+              cost += f * (0.5f * (jv + R * f) + b);
+            });
+          }
+        });
+        cost = gsum<64>(slot == 0 ? cost : 0.0f);
+        if (cost > 0) {
+          unroll<NB>([&](auto ic) { fr[decltype(ic)::value] = 0; });
+        } else if (lane < nv) {
+          qa[lane] += tmp[lane];
+        }
+        wsync();
+      }
+      SUB_ADD(PH_CON_WARM, t_sub);
+      t_sub = SUB_T();
+      // PGS sweeps, one item at a time
+      int slot_v = slot;
+      int nit = 0;
+      #pragma unroll 1
+      for (int it = 0; it < m.iterations; ++it) {
+#pragma unroll
+        for (int i = 0; i < (NQ + 3) / 4; ++i) asm volatile("" : "+v"(dpk[i]));
+        asm volatile("" : "+v"(slot_v));
+        float improvement = 0;
+        unroll<NQ>([&](auto qc) {
+          constexpr int i = decltype(qc)::value;
+          if (i < nq_max) {
+            const int d = dof_of(qc);
+            const float qd = qa[d];
+            float jq[4], df[4] = {0, 0, 0, 0};
+            unroll<4>([&](auto rc) {
+              constexpr int r = decltype(rc)::value;
+              jq[r] = gsum<16>(Jr[4 * i + r] * qd);
+            });
+            float upd = 0;
+            unroll<4>([&](auto rc) {
+              constexpr int r = decltype(rc)::value, k = 4 * i + r;
+              float c = jq[r];
+              if constexpr (r > 0) c += rowb<k % 16>(sC0[k / 16]) * df[0];
+              if constexpr (r > 1) c += rowb<k % 16>(sC1[k / 16]) * df[1];
+              if constexpr (r > 2) c += rowb<k % 16>(sC2[k / 16]) * df[2];
+              const float f0 = rowb<k % 16>(fr[k / 16]);
+              const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+              const float a = rowb<k % 16>(sA[k / 16]);
+              const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
+              const float res = c - aref + R * f0;
+              const float nf = __builtin_amdgcn_fmed3f(f0 - res * __builtin_amdgcn_rcpf(a), lo, hi);
+              df[r] = nf - f0;
+              upd += MJr[k] * df[r];
+              fr[k / 16] = slot_v == k % 16 ? nf : fr[k / 16];
+              improvement -= df[r] * res + 0.5f * df[r] * df[r] * a;
+            });
+            qa[d] = qd + upd;
+          }
+        });
+        improvement = gsum<64>(slot_v == 0 ? improvement : 0.0f);
+        nit = it + 1;
+        if (improvement * m.pgs_scale < m.tolerance) break;
+      }
+      if (lane == 0) s[L.niter] = __int_as_float(nit);
+      wsync();
+      SUB_ADD(PH_CON_PGS, t_sub);
+      // qfrc_constraint = J' f and the forces out (by row index, for mj_rnePostConstraint)
+      if (lane < nv) tmp[lane] = 0;
+      wsync();
+      unroll<NQ>([&](auto qc) {
+        constexpr int i = decltype(qc)::value;
+        if (i < nq_max) {
+          float acc = 0;
+          unroll<4>([&](auto rc) {
+            constexpr int k = 4 * i + decltype(rc)::value;
+            acc += Jr[k] * rowb<k % 16>(fr[k / 16]);
+          });
+          tmp[dof_of(qc)] += acc;
+        }
+      });
+      unroll<NB>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        const int i = 4 * b + slot / 4, r = slot % 4;  // level 16 b + slot = item i, row r
+        if (i < my_nq && i < NQ) {
+          const int qt = __float_as_int(quadtab[pipe * 16 + i]);
+          if (r < (qt >> 16)) ffg[__float_as_int(rowof[(qt & 0xffff) + r])] = fr[b];
+        }
+      });
+      wsync();
+      return lane < nv ? qa[lane] : 0.0f;
+    }
+  }
 
   // --- register-resident solve: P = 16 and at most kRegLevels rows per pipe.  Lane (pipe, slot)
   // keeps J, M^-1 J' and the dof of its slot for every level (slots outside the row's trees point at

@@ -534,6 +534,33 @@ def test_tall_stack_fallback_solver(monkeypatch):
     np.testing.assert_allclose(q[0, 2::7], [0.1 + 0.2 * k for k in range(5)], atol=6e-3)
 
 
+@pytest.mark.parametrize("condim, levels", [(1, "rows"), (3, "items")])
+def test_blocked_register_paths(condim, levels, monkeypatch):
+    """the two register-resident blocked solves on one-island towers of aligned boxes (4 contacts per
+    face): three boxes with condim 3 give 12 four-row contact items (the item-blocked solve's limit);
+    four boxes with condim 1 give 16 one-row items, more than 12 but within the row-level solve's 48
+    rows.  50 steps against the oracle"""
+    monkeypatch.setenv("MRS_GROUP", "64")
+    bodies = "".join(
+        f'<body pos="0 0 {0.1 + 0.2 * k + 0.001 * k:.4f}"><freejoint/>'
+        f'<geom type="box" size="0.1 0.1 0.1" mass="1" condim="{condim}"/></body>' for k in range(3 if condim == 3 else 4))
+    xml = f"""<mujoco><option timestep="0.002" solver="PGS" iterations="50"/><worldbody>
+    <geom type="plane" size="0 0 1" condim="{condim}"/>{bodies}</worldbody></mujoco>"""
+    model = sim.Model.from_string(xml)
+    b = sim.Batch(model, 2)
+    assert b.layout()["blocked"] == 1
+    d = binding.OracleData(model)
+    b.step(50)
+    d.step(50)
+    q = b.get(sim.FIELD_QPOS)
+    ncon = b.get(sim.FIELD_NCON)[:, 0]
+    b.close()
+    assert int(ncon[0]) == d.ncon
+    assert d.ncon == (12 if condim == 3 else 16)
+    np.testing.assert_allclose(q[0], d.qpos, atol=5e-5)
+    np.testing.assert_allclose(q[1], d.qpos, atol=5e-5)
+
+
 @pytest.mark.parametrize("v1", [False, True])
 def test_depth_all_primitives(v1, monkeypatch):
     """depth render of every primitive type (plane, sphere, capsule, cylinder, ellipsoid, rotated box,
