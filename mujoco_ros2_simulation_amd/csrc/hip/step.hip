@@ -32,10 +32,11 @@ typedef __attribute__((address_space(1))) float gfloat;
 
 // Phase inlining follows the register budget of the group width: with G <= 16 (2 waves/SIMD, 256
 // VGPRs) every phase is inlined into the kernel (measured C3: 0.829 ms per launch vs 0.889 out of
-// line, and 157 vs 384 MB of writes per launch without the callee-saved spills); with G >= 32 (4-8
-// waves/SIMD, 64-128 VGPRs) phases stay out of line so each gets its own register allocation.
-// Call sites use clang's statement attributes; -DMRS_PHASE_INLINE / -DMRS_PHASE_OUTLINE force one
-// policy for A/B builds.
+// line, and 157 vs 384 MB of writes per launch without the callee-saved spills); at G = 64 (blocked
+// mode, 3 waves/SIMD) too (C5: same speed, 4.3 GB per launch less traffic: the out-of-line phases'
+// callee-saved VGPR spills, ~26 KB each way per env-step); at G = 32 phases stay out of line so each
+// gets its own register allocation.  Call sites use clang's statement attributes;
+// -DMRS_PHASE_INLINE / -DMRS_PHASE_OUTLINE force one policy for A/B builds.
 #define MRS_PHASE
 #if defined(MRS_PHASE_INLINE)
 #define MRS_CALL(G, stmt) do { [[clang::always_inline]] stmt; } while (0)
@@ -44,7 +45,7 @@ typedef __attribute__((address_space(1))) float gfloat;
 #else
 #define MRS_CALL(G, stmt)                          \
   do {                                             \
-    if constexpr ((G) <= 16) {                     \
+    if constexpr ((G) != 32) {                     \
       [[clang::always_inline]] stmt;               \
     } else {                                       \
       [[clang::noinline]] stmt;                    \
