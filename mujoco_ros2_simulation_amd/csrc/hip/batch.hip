@@ -885,10 +885,60 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     int f; std::memcpy(&f, &ri[1], 4);
     if (!f || std::memcmp(&ri[0], &r0[0], 4) != 0 || ri[2] != r0[2] || ri[3] != r0[3] || ri[4] != r0[4]) d.rf_common = 0;
   }
+  // static lidars: when every rangefinder sits on a world-welded body, that body's world pose never
+  // changes, so the ray blocks' fan frames and the rays' origins / directions go to the world frame
+  // here (fp64) and the step kernel skips the per-step body rotation (rf_static_frame)
+  d.rf_static_frame = 0;
+  if (d.nrf > 0) {
+    bool all_static = true;
+    for (int k = 0; k < d.nrf; ++k) all_static = all_static && m.body_weldid[m.site_bodyid[m.sensor_objid[rf[k]]]] == 0;
+    d.rf_static_frame = all_static && !std::getenv("MRS_NO_STATIC_FRAME") ? 1 : 0;
+  }
+  auto body_world = [&](int b, double R[9], double p[3]) {  // world pose of a body without joints above it
+    double q[4] = {1, 0, 0, 0};
+    p[0] = p[1] = p[2] = 0;
+    std::vector<int> chain;
+    for (int x = b; x != 0; x = m.body_parentid[x]) chain.push_back(x);
+    for (auto it = chain.rbegin(); it != chain.rend(); ++it) {
+      const double* bp = &m.body_pos[3 * *it];
+      const double* bq = &m.body_quat[4 * *it];
+      const double Rq[9] = {q[0] * q[0] + q[1] * q[1] - q[2] * q[2] - q[3] * q[3], 2 * (q[1] * q[2] - q[0] * q[3]),
+                            2 * (q[1] * q[3] + q[0] * q[2]), 2 * (q[1] * q[2] + q[0] * q[3]),
+                            q[0] * q[0] - q[1] * q[1] + q[2] * q[2] - q[3] * q[3], 2 * (q[2] * q[3] - q[0] * q[1]),
+                            2 * (q[1] * q[3] - q[0] * q[2]), 2 * (q[2] * q[3] + q[0] * q[1]),
+                            q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3]};
+      for (int i = 0; i < 3; ++i) p[i] += Rq[3 * i] * bp[0] + Rq[3 * i + 1] * bp[1] + Rq[3 * i + 2] * bp[2];
+      const double t[4] = {q[0] * bq[0] - q[1] * bq[1] - q[2] * bq[2] - q[3] * bq[3],
+                           q[0] * bq[1] + q[1] * bq[0] + q[2] * bq[3] - q[3] * bq[2],
+                           q[0] * bq[2] - q[1] * bq[3] + q[2] * bq[0] + q[3] * bq[1],
+                           q[0] * bq[3] + q[1] * bq[2] - q[2] * bq[1] + q[3] * bq[0]};
+      const double tn = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3]);
+      for (int i = 0; i < 4; ++i) q[i] = t[i] / tn;
+    }
+    R[0] = q[0] * q[0] + q[1] * q[1] - q[2] * q[2] - q[3] * q[3]; R[1] = 2 * (q[1] * q[2] - q[0] * q[3]);
+    R[2] = 2 * (q[1] * q[3] + q[0] * q[2]); R[3] = 2 * (q[1] * q[2] + q[0] * q[3]);
+    R[4] = q[0] * q[0] - q[1] * q[1] + q[2] * q[2] - q[3] * q[3]; R[5] = 2 * (q[2] * q[3] - q[0] * q[1]);
+    R[6] = 2 * (q[1] * q[3] - q[0] * q[2]); R[7] = 2 * (q[2] * q[3] + q[0] * q[1]);
+    R[8] = q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3];
+  };
+  if (d.rf_static_frame) {
+    for (int blk = 0; blk < d.nrfblk; ++blk) {
+      float* r = &rfblk[16 * blk];
+      int body;
+      std::memcpy(&body, &r[0], 4);
+      double R[9], p[3];
+      body_world(body, R, p);
+      for (int v = 0; v < 4; ++v) {  // origin (a point), then a, b, c (directions)
+        const double x[3] = {r[2 + 3 * v], r[3 + 3 * v], r[4 + 3 * v]};
+        for (int i = 0; i < 3; ++i)
+          r[2 + 3 * v + i] = static_cast<float>(R[3 * i] * x[0] + R[3 * i + 1] * x[1] + R[3 * i + 2] * x[2] + (v == 0 ? p[i] : 0.0));
+      }
+    }
+  }
   P.addf(&d.rfblk, rfblk);
   // per-ray records: unit direction (z column of the site rotation) and sensordata address first
   // (one 16-byte load when the ray's pass shares body and origin), then body and origin in the body
-  // frame
+  // frame (the world frame for static lidars)
   std::vector<float> rfray;
   for (int k = 0; k < d.nrf; ++k) {
     const int site = m.sensor_objid[rf[k]];
@@ -896,10 +946,19 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     double dz[3] = {2 * (q[1] * q[3] + q[0] * q[2]), 2 * (q[2] * q[3] - q[0] * q[1]),
                     q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3]};
     const double n = std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]);
-    rfray.insert(rfray.end(), {static_cast<float>(dz[0] / n), static_cast<float>(dz[1] / n), static_cast<float>(dz[2] / n),
+    double dir[3] = {dz[0] / n, dz[1] / n, dz[2] / n}, org[3] = {m.site_pos[3 * site], m.site_pos[3 * site + 1], m.site_pos[3 * site + 2]};
+    if (d.rf_static_frame) {
+      double R[9], p[3];
+      body_world(m.site_bodyid[site], R, p);
+      const double d0[3] = {dir[0], dir[1], dir[2]}, o0[3] = {org[0], org[1], org[2]};
+      for (int i = 0; i < 3; ++i) {
+        dir[i] = R[3 * i] * d0[0] + R[3 * i + 1] * d0[1] + R[3 * i + 2] * d0[2];
+        org[i] = p[i] + R[3 * i] * o0[0] + R[3 * i + 1] * o0[1] + R[3 * i + 2] * o0[2];
+      }
+    }
+    rfray.insert(rfray.end(), {static_cast<float>(dir[0]), static_cast<float>(dir[1]), static_cast<float>(dir[2]),
                                bits(m.sensor_adr[rf[k]]), bits(m.site_bodyid[site]),
-                               static_cast<float>(m.site_pos[3 * site]), static_cast<float>(m.site_pos[3 * site + 1]),
-                               static_cast<float>(m.site_pos[3 * site + 2])});
+                               static_cast<float>(org[0]), static_cast<float>(org[1]), static_cast<float>(org[2])});
   }
   P.addf(&d.rfray, rfray);
 
@@ -958,7 +1017,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // starts at one point of one body, and the rays' static hits (DevModel::shr_*)
   d.shr_rf = d.nrgeom * 8;
   d.shr_rfst = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
-  d.shr_total = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
+  d.shr_blk = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
+  d.shr_total = d.shr_blk + 17 * d.nrfblk;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)

@@ -86,6 +86,11 @@ struct DevModel {
   // rf_static; rf_mode 2: the step kernel starts every ray from rf_static (staged in workgroup LDS
   // at shr_rfst) and tests only the moving geoms; 0: no split.  rf_static_mask: static ray-geom bits.
   int rf_mode, shr_rfst;
+  // every rangefinder body is world-welded: rfblk frames and rfray origins / directions are stored
+  // in the world frame (batch.hip), and the kernel uses them without the per-step body rotation
+  int rf_static_frame;
+  // the ray blocks' level-1 records (rfblk, 16 floats each, then the nrfblk slopes) at shr_blk
+  int shr_blk;
   unsigned rf_static_mask;
   float* rf_static;
   // options

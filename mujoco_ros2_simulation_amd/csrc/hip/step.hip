@@ -3758,13 +3758,16 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
   bool act[R];
   unsigned long long t_setup = SUB_T();
   if (common_body >= 0) {
-    // every ray of the pass starts at the same point of the same body: one rotation for all
+    // every ray of the pass starts at the same point of the same body: one rotation for all (none
+    // for a static lidar, whose rays are stored in the world frame)
     const int b = common_body;
-    float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
-    float bm[9], o[3];
-    quat2mat(bm, bq);
-    mat_vec(o, bm, common_o);
-    for (int i = 0; i < 3; ++i) o[i] += se[L.xpos + 3 * b + i];
+    float bm[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, o[3] = {common_o[0], common_o[1], common_o[2]};
+    if (!m.rf_static_frame) {
+      float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
+      quat2mat(bm, bq);
+      mat_vec(o, bm, common_o);
+      for (int i = 0; i < 3; ++i) o[i] += se[L.xpos + 3 * b + i];
+    }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int k = k0 + j * stride;
@@ -3773,7 +3776,8 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       const float dl[3] = {rr[0], rr[1], rr[2]};
       adr[j] = __float_as_int(rr[3]);
       bod[j] = b;
-      mat_vec(vec[j], bm, dl);
+      if (m.rf_static_frame) { vec[j][0] = dl[0]; vec[j][1] = dl[1]; vec[j][2] = dl[2]; }
+      else mat_vec(vec[j], bm, dl);
       for (int i = 0; i < 3; ++i) pnt[j][i] = o[i];
       // static split: start from the ray's hit on the world-welded geoms (never beaten: -1)
       dist[j] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + (act[j] ? k : 0)] : -1.0f;
@@ -3788,12 +3792,16 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       adr[j] = __float_as_int(rr[3]);
       const int b = __float_as_int(rr[4]);
       bod[j] = b;
-      float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
-      float bm[9];
-      quat2mat(bm, bq);
-      mat_vec(pnt[j], bm, ol);
-      for (int i = 0; i < 3; ++i) pnt[j][i] += se[L.xpos + 3 * b + i];
-      mat_vec(vec[j], bm, dl);
+      if (m.rf_static_frame) {
+        for (int i = 0; i < 3; ++i) { pnt[j][i] = ol[i]; vec[j][i] = dl[i]; }
+      } else {
+        float bq[4] = {se[L.xquat + 4 * b], se[L.xquat + 4 * b + 1], se[L.xquat + 4 * b + 2], se[L.xquat + 4 * b + 3]};
+        float bm[9];
+        quat2mat(bm, bq);
+        mat_vec(pnt[j], bm, ol);
+        for (int i = 0; i < 3; ++i) pnt[j][i] += se[L.xpos + 3 * b + i];
+        mat_vec(vec[j], bm, dl);
+      }
       dist[j] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + (act[j] ? k : 0)] : -1.0f;
     }
   }
@@ -3888,27 +3896,31 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
   // of the geom; planes by the direction range of the fan), one bitmask per block; lanes over geoms
   const unsigned all = m.nrgeom >= 32 ? 0xffffffffu : ((1u << m.nrgeom) - 1u);
   unsigned long long t_l1 = SUB_T();
-#if defined(MRS_DIAG_RAYS) && MRS_DIAG_RAYS == 2
+#if (defined(MRS_DIAG_RAYS) && MRS_DIAG_RAYS == 2) || defined(MRS_DIAG_NO_L1)
   if (false)  // diagnostic build: no level-1 test (all geoms)
 #endif
   #pragma unroll 1
   for (int blk = 0; blk < m.nrfblk; ++blk) {
-    const CPtr<float> br = m.rfblk + 16 * blk;
+    const lfloat* br = shared_lds(m) + m.shr_blk + 16 * blk;  // staged from rfblk at launch
     unsigned mask = all;
     if (__float_as_int(br[1])) {
       const int b = __float_as_int(br[0]);
-      const float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
-      float bmat[9];
-      quat2mat(bmat, bq);
       const float ol[3] = {br[2], br[3], br[4]}, al[3] = {br[5], br[6], br[7]};
       const float bl[3] = {br[8], br[9], br[10]}, cl[3] = {br[11], br[12], br[13]};
-      const float cth = br[14], sth = br[15], eps = m.rfblk[16 * m.nrfblk + blk];
+      const float cth = br[14], sth = br[15], eps = shared_lds(m)[m.shr_blk + 16 * m.nrfblk + blk];
       float o[3], a[3], bb[3], c[3];
-      mat_vec(o, bmat, ol);
-      for (int i = 0; i < 3; ++i) o[i] += s[L.xpos + 3 * b + i];
-      mat_vec(a, bmat, al);
-      mat_vec(bb, bmat, bl);
-      mat_vec(c, bmat, cl);
+      if (m.rf_static_frame) {  // frame already in the world (static lidar)
+        for (int i = 0; i < 3; ++i) { o[i] = ol[i]; a[i] = al[i]; bb[i] = bl[i]; c[i] = cl[i]; }
+      } else {
+        const float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
+        float bmat[9];
+        quat2mat(bmat, bq);
+        mat_vec(o, bmat, ol);
+        for (int i = 0; i < 3; ++i) o[i] += s[L.xpos + 3 * b + i];
+        mat_vec(a, bmat, al);
+        mat_vec(bb, bmat, bl);
+        mat_vec(c, bmat, cl);
+      }
       mask = 0;
       #pragma unroll 1
       for (int c0 = 0; c0 < m.nrgeom; c0 += G) {
@@ -3980,23 +3992,26 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
         const int k = base + lane + j * G;
         if (k >= m.nrf) continue;
         if (m.rf_mode == 1) m.rf_static[k] = -1.0f;
-        else if (MRS_SD_OK(sensordata))
-          sensordata[__float_as_int(m.rfray[8 * k + 3])] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + k] : -1.0f;
+        else if (MRS_SD_OK(sensordata)) {
+          const int adr = m.rf_common ? __float_as_int(shared_lds(m)[m.shr_rf + 4 * k + 3]) : __float_as_int(m.rfray[8 * k + 3]);
+          sensordata[adr] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + k] : -1.0f;
+        }
       }
       continue;
     }
     // shared body and origin for the whole pass when all its blocks are fans from one point
     int common_body = -1;
     float common_o[3] = {0, 0, 0};
+    const lfloat* blks = shared_lds(m) + m.shr_blk;
     if (m.rf_common) {
-      common_body = __float_as_int(m.rfblk[0]);
-      common_o[0] = m.rfblk[2]; common_o[1] = m.rfblk[3]; common_o[2] = m.rfblk[4];
+      common_body = __float_as_int(blks[0]);
+      common_o[0] = blks[2]; common_o[1] = blks[3]; common_o[2] = blks[4];
     } else if (m.nrfblk > 0) {
       const int b0 = base / kRayBlock, b1 = min(m.nrfblk, (base + G * R + kRayBlock - 1) / kRayBlock);
-      const CPtr<float> r0 = m.rfblk + 16 * b0;
+      const lfloat* r0 = blks + 16 * b0;
       bool same = __float_as_int(r0[1]) != 0;
       for (int blk = b0 + 1; blk < b1 && same; ++blk) {
-        const CPtr<float> ri = m.rfblk + 16 * blk;
+        const lfloat* ri = blks + 16 * blk;
         same = __float_as_int(ri[1]) != 0 && __float_as_int(ri[0]) == __float_as_int(r0[0]) && ri[2] == r0[2] &&
                ri[3] == r0[3] && ri[4] == r0[4];
       }
@@ -4008,6 +4023,9 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
     rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask, common_body, common_o);
   }
   if (!MRS_SD_OK(sensordata)) return;
+#ifdef MRS_DIAG_NO_OTHER
+  return;  // diagnostic build: rangefinders only
+#endif
   #pragma unroll 1
   for (int ks = lane; ks < m.nsens_other; ks += G) {
     const int sid = m.sens_other[ks];
@@ -4292,6 +4310,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     if (m.rf_mode == 2)
       #pragma unroll 1
       for (int i = threadIdx.x; i < m.nrf; i += blockDim.x) shr[m.shr_rfst + i] = m.rf_static[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < 17 * m.nrfblk; i += blockDim.x) shr[m.shr_blk + i] = m.rfblk[i];
   }
   __syncthreads();
   wsync();
