@@ -145,7 +145,7 @@ struct DevModel {
   // origin[3], in the body frame
   CPtr<float> rfray;
 };
-constexpr int kRayBlock = 64;
+constexpr int kRayBlock = 128;
 
 // waves per workgroup: 256-thread workgroups with lane groups (G < 64); one wave (one env) per
 // workgroup at G = 64, so LDS is granted per env (the C5 working set of ~13.5 KB fits 11 envs per
