@@ -777,6 +777,36 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addf(&d.sensor_cutoff, m.sensor_cutoff);
   P.addi(&d.fric_dof, fric); P.addi(&d.lim_jnt, lim); P.addi(&d.rf_sensor, rf);
   P.addi(&d.sens_other, other_sens);
+  // the non-ray sensors' descriptors, 16 floats each (staged in workgroup LDS at shr_sens): type,
+  // objtype, sensordata address, dim (int bits), cutoff, the object's qpos / dof / actuator / body
+  // index (int bits), the root body (int bits), then the site's or geom's local pos[3] and quat[4]
+  std::vector<float> sensrec;
+  {
+    auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+    for (int sid : other_sens) {
+      const int t = m.sensor_type[sid], ot = m.sensor_objtype[sid], id = m.sensor_objid[sid];
+      int a = id, root = 0;
+      double lp[3] = {0, 0, 0}, lq[4] = {1, 0, 0, 0};
+      if (t == MRS_SENS_JOINTPOS) a = m.jnt_qposadr[id];
+      else if (t == MRS_SENS_JOINTVEL) a = m.jnt_dofadr[id];
+      else if (t == MRS_SENS_ACCELEROMETER || t == MRS_SENS_FORCE || t == MRS_SENS_TORQUE || t == MRS_SENS_GYRO ||
+               ((t == MRS_SENS_FRAMEPOS || t == MRS_SENS_FRAMEQUAT) && ot == MRS_OBJ_SITE)) {
+        a = m.site_bodyid[id];
+        for (int i = 0; i < 3; ++i) lp[i] = m.site_pos[3 * id + i];
+        for (int i = 0; i < 4; ++i) lq[i] = m.site_quat[4 * id + i];
+      } else if ((t == MRS_SENS_FRAMEPOS || t == MRS_SENS_FRAMEQUAT) && ot != MRS_OBJ_BODY) {  // geom
+        a = m.geom_bodyid[id];
+        for (int i = 0; i < 4; ++i) lq[i] = m.geom_quat[4 * id + i];
+      }
+      if (a >= 0 && (t == MRS_SENS_ACCELEROMETER || t == MRS_SENS_FORCE || t == MRS_SENS_TORQUE)) root = m.body_rootid[a];
+      sensrec.insert(sensrec.end(), {fbits(t), fbits(ot), fbits(m.sensor_adr[sid]), fbits(m.sensor_dim[sid]),
+                                     static_cast<float>(m.sensor_cutoff[sid]), fbits(a), fbits(root),
+                                     static_cast<float>(lp[0]), static_cast<float>(lp[1]), static_cast<float>(lp[2]),
+                                     static_cast<float>(lq[0]), static_cast<float>(lq[1]), static_cast<float>(lq[2]),
+                                     static_cast<float>(lq[3]), fbits(id), 0.0f});
+    }
+  }
+  P.addf(&d.sensrec, sensrec);
   std::vector<float> rgeom;
   auto bits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
   for (int g = 0; g < m.ngeom; ++g) {
@@ -1018,7 +1048,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.shr_rf = d.nrgeom * 8;
   d.shr_rfst = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
   d.shr_blk = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
-  d.shr_total = d.shr_blk + 17 * d.nrfblk;
+  d.shr_sens = d.shr_blk + 17 * d.nrfblk;
+  d.shr_total = d.shr_sens + 16 * d.nsens_other;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)

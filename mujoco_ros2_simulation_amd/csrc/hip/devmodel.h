@@ -89,8 +89,9 @@ struct DevModel {
   // every rangefinder body is world-welded: rfblk frames and rfray origins / directions are stored
   // in the world frame (batch.hip), and the kernel uses them without the per-step body rotation
   int rf_static_frame;
-  // the ray blocks' level-1 records (rfblk, 16 floats each, then the nrfblk slopes) at shr_blk
-  int shr_blk;
+  // the ray blocks' level-1 records (rfblk, 16 floats each, then the nrfblk slopes) at shr_blk, the
+  // non-ray sensors' descriptors (sensrec, 16 floats each) at shr_sens
+  int shr_blk, shr_sens;
   unsigned rf_static_mask;
   float* rf_static;
   // options
@@ -133,6 +134,7 @@ struct DevModel {
   CPtr<int> sensor_type, sensor_objtype, sensor_objid, sensor_adr, sensor_dim;
   CPtr<float> sensor_cutoff;
   CPtr<int> fric_dof, lim_jnt, rf_sensor, sens_other;  // sens_other: non-rangefinder sensor ids
+  CPtr<float> sensrec;  // their descriptors (batch.hip), 16 floats each
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;

@@ -4034,24 +4034,25 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
 #endif
   #pragma unroll 1
   for (int ks = lane; ks < m.nsens_other; ks += G) {
-    const int sid = m.sens_other[ks];
-    const int t = m.sensor_type[sid], id = m.sensor_objid[sid];
-    gfloat* out = sensordata + m.sensor_adr[sid];
-    float cutoff = m.sensor_cutoff[sid];
-    int dim = m.sensor_dim[sid];
+    // the sensor's descriptor from workgroup LDS (batch.hip sensrec): no chain of dependent model loads
+    const lfloat* sr = shared_lds(m) + m.shr_sens + 16 * ks;
+    const int t = __float_as_int(sr[0]), id = __float_as_int(sr[14]), a = __float_as_int(sr[5]);
+    gfloat* out = sensordata + __float_as_int(sr[2]);
+    float cutoff = sr[4];
+    int dim = __float_as_int(sr[3]);
     switch (t) {
       case MRS_SENS_RANGEFINDER: continue;
-      case MRS_SENS_JOINTPOS: out[0] = s[L.qpos + m.jnt_qposadr[id]]; break;
-      case MRS_SENS_JOINTVEL: out[0] = s[L.qvel + m.jnt_dofadr[id]]; break;
+      case MRS_SENS_JOINTPOS: out[0] = s[L.qpos + a]; break;
+      case MRS_SENS_JOINTVEL: out[0] = s[L.qvel + a]; break;
       case MRS_SENS_ACTUATORFRC: out[0] = s[L.act_force + id]; break;
       case MRS_SENS_ACCELEROMETER:
       case MRS_SENS_FORCE:
       case MRS_SENS_TORQUE: {
         // mj_sensorAcc: com-based quantities moved to the site (mju_transformSpatial), site frame
-        const int b = m.site_bodyid[id], rt = m.body_rootid[b];
+        const int b = a, rt = __float_as_int(sr[6]);
         float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
-        float sp[3] = {m.site_pos[3 * id], m.site_pos[3 * id + 1], m.site_pos[3 * id + 2]};
-        float sq[4] = {m.site_quat[4 * id], m.site_quat[4 * id + 1], m.site_quat[4 * id + 2], m.site_quat[4 * id + 3]};
+        float sp[3] = {sr[7], sr[8], sr[9]};
+        float sq[4] = {sr[10], sr[11], sr[12], sr[13]};
         float r[3], q[4], sm[9], d[3], o3[3];
         rot_quat(r, sp, bq);
         for (int i = 0; i < 3; ++i) d[i] = s[L.xpos + 3 * b + i] + r[i] - s[L.scom + 3 * rt + i];
@@ -4088,14 +4089,14 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       case MRS_SENS_FRAMEPOS:
       case MRS_SENS_FRAMEQUAT:
       case MRS_SENS_GYRO: {
-        const int ot = m.sensor_objtype[sid];
+        const int ot = __float_as_int(sr[1]);
         float p[3], q[4];
         int b;
         if (ot == MRS_OBJ_SITE || t == MRS_SENS_GYRO) {
-          b = m.site_bodyid[id];
+          b = a;
           float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
-          float sp[3] = {m.site_pos[3 * id], m.site_pos[3 * id + 1], m.site_pos[3 * id + 2]};
-          float sq[4] = {m.site_quat[4 * id], m.site_quat[4 * id + 1], m.site_quat[4 * id + 2], m.site_quat[4 * id + 3]};
+          float sp[3] = {sr[7], sr[8], sr[9]};
+          float sq[4] = {sr[10], sr[11], sr[12], sr[13]};
           float r[3];
           rot_quat(r, sp, bq);
           for (int i = 0; i < 3; ++i) p[i] = s[L.xpos + 3 * b + i] + r[i];
@@ -4105,9 +4106,9 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
           for (int i = 0; i < 3; ++i) p[i] = s[L.xpos + 3 * b + i];
           for (int i = 0; i < 4; ++i) q[i] = s[L.xquat + 4 * b + i];
         } else {
-          b = m.geom_bodyid[id];
+          b = a;
           float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
-          float gq[4] = {m.geom_quat[4 * id], m.geom_quat[4 * id + 1], m.geom_quat[4 * id + 2], m.geom_quat[4 * id + 3]};
+          float gq[4] = {sr[10], sr[11], sr[12], sr[13]};
           for (int i = 0; i < 3; ++i) p[i] = s[L.gxpos + 3 * id + i];
           quat_mul(q, bq, gq);
         }
@@ -4318,6 +4319,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       for (int i = threadIdx.x; i < m.nrf; i += blockDim.x) shr[m.shr_rfst + i] = m.rf_static[i];
     #pragma unroll 1
     for (int i = threadIdx.x; i < 17 * m.nrfblk; i += blockDim.x) shr[m.shr_blk + i] = m.rfblk[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < 16 * m.nsens_other; i += blockDim.x) shr[m.shr_sens + i] = m.sensrec[i];
   }
   __syncthreads();
   wsync();
