@@ -777,6 +777,38 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addf(&d.sensor_cutoff, m.sensor_cutoff);
   P.addi(&d.fric_dof, fric); P.addi(&d.lim_jnt, lim); P.addi(&d.rf_sensor, rf);
   P.addi(&d.sens_other, other_sens);
+  // friction-loss rows and limited joints, 4 floats each, staged in workgroup LDS (shr_fric, shr_lim):
+  // a friction row's impedance is that of distance 0 at margin 0, so its R and reference stiffness
+  // B are model constants (computed here in fp32, the order the kernel used); limits: qpos address,
+  // margin, range
+  std::vector<float> fricrec, limrec;
+  {
+    auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+    auto clampf = [](float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); };
+    for (int j : fric) {
+      const float si0 = static_cast<float>(m.dof_solimp[5 * j]), si1 = static_cast<float>(m.dof_solimp[5 * j + 1]);
+      const float width = static_cast<float>(m.dof_solimp[5 * j + 2]);
+      const float dmin = clampf(si0, 0.0001f, 0.9999f), dmax = clampf(si1, 0.0001f, 0.9999f);
+      const float imp = (dmin == dmax || width <= 1e-15f) ? 0.5f * (dmin + dmax) : dmin;
+      float R = (1 - imp) * static_cast<float>(m.dof_invweight0[j]) / imp;
+      R = R > 1e-15f ? R : 1e-15f;
+      const float sr0 = static_cast<float>(m.dof_solref[2 * j]), sr1 = static_cast<float>(m.dof_solref[2 * j + 1]);
+      float B;
+      if (sr0 > 0) {
+        float tc = sr0;
+        if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * d.timestep) tc = 2 * d.timestep;
+        B = 2 / (dmax * tc);
+      } else {
+        B = -sr1 / dmax;
+      }
+      fricrec.insert(fricrec.end(), {fbits(j), R, B, static_cast<float>(m.dof_frictionloss[j])});
+    }
+    for (int j : lim)
+      limrec.insert(limrec.end(), {fbits(m.jnt_qposadr[j]), static_cast<float>(m.jnt_margin[j]),
+                                   static_cast<float>(m.jnt_range[2 * j]), static_cast<float>(m.jnt_range[2 * j + 1])});
+  }
+  P.addf(&d.fricrec, fricrec);
+  P.addf(&d.limrec, limrec);
   // the non-ray sensors' descriptors, 16 floats each (staged in workgroup LDS at shr_sens): type,
   // objtype, sensordata address, dim (int bits), cutoff, the object's qpos / dof / actuator / body
   // index (int bits), the root body (int bits), then the site's or geom's local pos[3] and quat[4]
@@ -1049,7 +1081,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.shr_rfst = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
   d.shr_blk = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
   d.shr_sens = d.shr_blk + 17 * d.nrfblk;
-  d.shr_total = d.shr_sens + 16 * d.nsens_other;
+  d.shr_fric = d.shr_sens + 16 * d.nsens_other;
+  d.shr_lim = d.shr_fric + 4 * d.nfric;
+  d.shr_total = d.shr_lim + 4 * d.nlim;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)

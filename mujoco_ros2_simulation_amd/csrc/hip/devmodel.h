@@ -92,6 +92,9 @@ struct DevModel {
   // the ray blocks' level-1 records (rfblk, 16 floats each, then the nrfblk slopes) at shr_blk, the
   // non-ray sensors' descriptors (sensrec, 16 floats each) at shr_sens
   int shr_blk, shr_sens;
+  // friction-loss rows (fricrec: dof, R, B, frictionloss) at shr_fric, limited joints (limrec: qpos
+  // address, margin, range) at shr_lim
+  int shr_fric, shr_lim;
   unsigned rf_static_mask;
   float* rf_static;
   // options
@@ -135,6 +138,7 @@ struct DevModel {
   CPtr<float> sensor_cutoff;
   CPtr<int> fric_dof, lim_jnt, rf_sensor, sens_other;  // sens_other: non-rangefinder sensor ids
   CPtr<float> sensrec;  // their descriptors (batch.hip), 16 floats each
+  CPtr<float> fricrec, limrec;  // 4 floats per friction-loss dof / limited joint (batch.hip)
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;

@@ -3296,33 +3296,23 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     if (!(m.disableflags & MRS_DSBL_LIMIT))
       #pragma unroll 1
       for (int k = lane; k < m.nlim; k += G) {
-        const int jid = m.lim_jnt[k];
-        const float q = s[L.qpos + m.jnt_qposadr[jid]], mg = m.jnt_margin[jid];
-        lim |= (q - m.jnt_range[2 * jid] < mg) | (m.jnt_range[2 * jid + 1] - q < mg);
+        const lfloat* lr = shared_lds(m) + m.shr_lim + 4 * k;  // qpos address, margin, range
+        const float q = s[L.qpos + __float_as_int(lr[0])], mg = lr[1];
+        lim |= (q - lr[2] < mg) | (lr[3] - q < mg);
       }
     if (m.solver == MRS_SOL_PGS && ncon == 0 && nf > 0 && nf <= 16 && !gany<G>(lim)) {
       if (lane == 0) scr[S.efc_n] = __int_as_float(-1);  // rows stay in registers
       int mydof = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
       if (lane < nf) {
-        const int j = m.fric_dof[lane];
+        // the row's model constants from workgroup LDS (batch.hip fricrec: dof, R, B, frictionloss)
+        const lfloat* fr = shared_lds(m) + m.shr_fric + 4 * lane;
+        const int j = __float_as_int(fr[0]);
         mydof = j;
-        const CPtr<float> sr = m.dof_solref + 2 * j, si = m.dof_solimp + 5 * j;
-        const float imp = impedance(si, 0.0f, 0.0f);
-        const float R = (1 - imp) * m.dof_invweight0[j] / imp;
-        myR = R > kMinVal ? R : kMinVal;
-        const float dmax = clampf(si[1], 0.0001f, 0.9999f);
-        float B;
-        if (sr[0] > 0) {
-          float tc = sr[0];
-          if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
-          B = 2 / (dmax * tc);
-        } else {
-          B = -sr[1] / dmax;
-        }
-        myaref = -B * s[L.qvel + j];  // friction rows have no position term
+        myR = fr[1];
+        myaref = -fr[2] * s[L.qvel + j];  // friction rows have no position term
         myb = s[L.qacc_smooth + j] - myaref;
-        myfl = m.dof_frictionloss[j];
+        myfl = fr[3];
       }
       // rows (and the dofs they touch) unrolled to 8 when the model has at most 8 friction dofs:
       // a quarter of the substitution code
@@ -4321,6 +4311,10 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     for (int i = threadIdx.x; i < 17 * m.nrfblk; i += blockDim.x) shr[m.shr_blk + i] = m.rfblk[i];
     #pragma unroll 1
     for (int i = threadIdx.x; i < 16 * m.nsens_other; i += blockDim.x) shr[m.shr_sens + i] = m.sensrec[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < 4 * m.nfric; i += blockDim.x) shr[m.shr_fric + i] = m.fricrec[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < 4 * m.nlim; i += blockDim.x) shr[m.shr_lim + i] = m.limrec[i];
   }
   __syncthreads();
   wsync();
