@@ -3351,6 +3351,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   gfloat* ff = scr + S.efc_f;
   gfloat* ARii = scr + S.efc_ARii;
   int nefc = 0;
+  unsigned long long t_sub = SUB_T();
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
   // keep ids in a small per-row int array inside the type slot (type*65536 + id)
   // --- friction loss rows
@@ -3457,6 +3458,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   }
   if (lane == 0) scr[S.efc_n] = __int_as_float(nefc);
   wsync();
+  SUB_ADD(PH_CON_ROWS, t_sub);
+  t_sub = SUB_T();
   if (nefc == 0) {
     if (lane < nv) s[L.qfrc_con + lane] = 0;
     wsync();
@@ -3528,6 +3531,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     ARii[r] = d + R;
   }
   wsync();
+  SUB_ADD(PH_CON_REC, t_sub);
+  t_sub = SUB_T();
   if (primal) {
     float qa;
     [[clang::noinline]] qa = solve_primal<G>(ENV_ARGS, nefc, m.solver == MRS_SOL_NEWTON);
@@ -3544,6 +3549,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     if (small) {
       const float qa = pgs_small16(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
       wsync();
+      SUB_ADD(PH_CON_PGS, t_sub);
       return qa;
     }
   }
