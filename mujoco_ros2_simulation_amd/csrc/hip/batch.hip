@@ -809,6 +809,42 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   P.addf(&d.fricrec, fricrec);
   P.addf(&d.limrec, limrec);
+  // smooth-force tables (step.hip smooth_forces), staged in workgroup LDS: per actuator (20 floats)
+  // qpos / dof address, gear, ctrl limit flag and range, gain type and prm[3], bias type and prm[3],
+  // force limit flag and range; per dof (16 floats) its single actuator (-1 none, -2 several: the
+  // actuator loop runs), that actuator's gear, the joint's actuator-force limit flag and range,
+  // joint type, stiffness, qpos address, qpos_spring, the dof's damping, body, subtree end and
+  // whether any body of the subtree has gravcomp
+  std::vector<float> actrec, dofrec;
+  {
+    auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+    for (int a = 0; a < m.nu; ++a) {
+      std::vector<float> r = {fbits(act_qadr[a]), fbits(act_dof[a]), act_gear[a], fbits(m.actuator_ctrllimited[a]),
+                              static_cast<float>(m.actuator_ctrlrange[2 * a]), static_cast<float>(m.actuator_ctrlrange[2 * a + 1]),
+                              fbits(m.actuator_gaintype[a]), act_gain[3 * a], act_gain[3 * a + 1], act_gain[3 * a + 2],
+                              fbits(m.actuator_biastype[a]), act_bias[3 * a], act_bias[3 * a + 1], act_bias[3 * a + 2],
+                              fbits(m.actuator_forcelimited[a]), static_cast<float>(m.actuator_forcerange[2 * a]),
+                              static_cast<float>(m.actuator_forcerange[2 * a + 1]), 0.0f, 0.0f, 0.0f};
+      actrec.insert(actrec.end(), r.begin(), r.end());
+    }
+    for (int j = 0; j < m.nv; ++j) {
+      int act = -1;
+      float gear = 0;
+      for (int a = 0; a < m.nu; ++a)
+        if (act_dof[a] == j) { act = act == -1 ? a : -2; gear = act_gear[a]; }
+      const int jid = m.dof_jntid[j], b = m.dof_bodyid[j];
+      int gc = 0;
+      for (int x = b; x < subtree_end[b]; ++x) gc |= m.body_gravcomp[x] != 0;
+      std::vector<float> r = {fbits(act), gear, fbits(m.jnt_actfrclimited[jid]), static_cast<float>(m.jnt_actfrcrange[2 * jid]),
+                              static_cast<float>(m.jnt_actfrcrange[2 * jid + 1]), fbits(m.jnt_type[jid]),
+                              static_cast<float>(m.jnt_stiffness[jid]), fbits(m.jnt_qposadr[jid]),
+                              static_cast<float>(m.qpos_spring[m.jnt_qposadr[jid]]), static_cast<float>(m.dof_damping[j]),
+                              fbits(b), fbits(subtree_end[b]), fbits(gc), 0.0f, 0.0f, 0.0f};
+      dofrec.insert(dofrec.end(), r.begin(), r.end());
+    }
+  }
+  P.addf(&d.actrec, actrec);
+  P.addf(&d.dofrec, dofrec);
   // the non-ray sensors' descriptors, 16 floats each (staged in workgroup LDS at shr_sens): type,
   // objtype, sensordata address, dim (int bits), cutoff, the object's qpos / dof / actuator / body
   // index (int bits), the root body (int bits), then the site's or geom's local pos[3] and quat[4]
@@ -1083,7 +1119,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.shr_sens = d.shr_blk + 17 * d.nrfblk;
   d.shr_fric = d.shr_sens + 16 * d.nsens_other;
   d.shr_lim = d.shr_fric + 4 * d.nfric;
-  d.shr_total = d.shr_lim + 4 * d.nlim;
+  d.shr_act = d.shr_lim + 4 * d.nlim;
+  d.shr_dof = d.shr_act + 20 * m.nu;
+  d.shr_total = d.shr_dof + 16 * m.nv;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)

@@ -95,6 +95,8 @@ struct DevModel {
   // friction-loss rows (fricrec: dof, R, B, frictionloss) at shr_fric, limited joints (limrec: qpos
   // address, margin, range) at shr_lim
   int shr_fric, shr_lim;
+  // smooth-force tables (actrec, 20 floats per actuator; dofrec, 16 floats per dof) at shr_act, shr_dof
+  int shr_act, shr_dof;
   unsigned rf_static_mask;
   float* rf_static;
   // options
@@ -139,6 +141,7 @@ struct DevModel {
   CPtr<int> fric_dof, lim_jnt, rf_sensor, sens_other;  // sens_other: non-rangefinder sensor ids
   CPtr<float> sensrec;  // their descriptors (batch.hip), 16 floats each
   CPtr<float> fricrec, limrec;  // 4 floats per friction-loss dof / limited joint (batch.hip)
+  CPtr<float> actrec, dofrec;   // smooth-force tables (batch.hip)
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;

@@ -1802,17 +1802,15 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   for (int a = lane; a < m.nu; a += G) {
     float force = 0;
     if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
-      const float gear = m.act_gear[a];
-      const float len = gear * s[L.qpos + m.act_qadr[a]], vel = gear * s[L.qvel + m.act_dof[a]];
+      const lfloat* ar = shared_lds(m) + m.shr_act + 20 * a;  // batch.hip actrec
+      const float gear = ar[2];
+      const float len = gear * s[L.qpos + __float_as_int(ar[0])], vel = gear * s[L.qvel + __float_as_int(ar[1])];
       float ctrl = s[L.ctrl + a];
-      if (m.act_ctrllimited[a] && !(m.disableflags & MRS_DSBL_CLAMPCTRL))
-        ctrl = clampf(ctrl, m.act_ctrlrange[2 * a], m.act_ctrlrange[2 * a + 1]);
-      const CPtr<float> g = m.act_gainprm + 3 * a;
-      const CPtr<float> bp = m.act_biasprm + 3 * a;
-      float gain = m.act_gaintype[a] == MRS_GAIN_AFFINE ? g[0] + g[1] * len + g[2] * vel : g[0];
-      float bias = m.act_biastype[a] == MRS_BIAS_AFFINE ? bp[0] + bp[1] * len + bp[2] * vel : 0.0f;
+      if (__float_as_int(ar[3]) && !(m.disableflags & MRS_DSBL_CLAMPCTRL)) ctrl = clampf(ctrl, ar[4], ar[5]);
+      float gain = __float_as_int(ar[6]) == MRS_GAIN_AFFINE ? ar[7] + ar[8] * len + ar[9] * vel : ar[7];
+      float bias = __float_as_int(ar[10]) == MRS_BIAS_AFFINE ? ar[11] + ar[12] * len + ar[13] * vel : 0.0f;
       force = gain * ctrl + bias;
-      if (m.act_forcelimited[a]) force = clampf(force, m.act_forcerange[2 * a], m.act_forcerange[2 * a + 1]);
+      if (__float_as_int(ar[14])) force = clampf(force, ar[15], ar[16]);
     }
     s[L.act_force + a] = force;
   }
@@ -1820,23 +1818,28 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   float qfs = 0;
   if (lane < nv) {
     const int j = lane;
+    const lfloat* dr = shared_lds(m) + m.shr_dof + 16 * j;  // batch.hip dofrec
     float qa = 0;
-    #pragma unroll 1
-    for (int a = 0; a < m.nu; ++a)
-      if (m.act_dof[a] == j) qa += m.act_gear[a] * s[L.act_force + a];
-    const int jid = m.dof_jntid[j];
-    if (m.jnt_actfrclimited[jid]) qa = clampf(qa, m.jnt_actfrcrange[2 * jid], m.jnt_actfrcrange[2 * jid + 1]);
+    const int da = __float_as_int(dr[0]);
+    if (da >= 0) {
+      qa = dr[1] * s[L.act_force + da];
+    } else if (da == -2) {
+      #pragma unroll 1
+      for (int a = 0; a < m.nu; ++a)
+        if (m.act_dof[a] == j) qa += m.act_gear[a] * s[L.act_force + a];
+    }
+    if (__float_as_int(dr[2])) qa = clampf(qa, dr[3], dr[4]);
     s[L.qfrc_act + j] = qa;
     float pas = 0;
     if (!(m.disableflags & MRS_DSBL_PASSIVE)) {
-      const int jt = m.jnt_type[jid];
-      if ((jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) && m.jnt_stiffness[jid] != 0) {
-        const int qadr = m.jnt_qposadr[jid];
-        pas -= m.jnt_stiffness[jid] * (s[L.qpos + qadr] - m.qpos_spring[qadr]);
+      const int jt = __float_as_int(dr[5]);
+      if ((jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) && dr[6] != 0) {
+        const int qadr = __float_as_int(dr[7]);
+        pas -= dr[6] * (s[L.qpos + qadr] - dr[8]);
       }
-      pas -= m.dof_damping[j] * s[L.qvel + j];
-      if (!(m.disableflags & MRS_DSBL_GRAVITY)) {
-        const int bj = m.dof_bodyid[j], e = m.body_subtree_end[bj];
+      pas -= dr[9] * s[L.qvel + j];
+      if (!(m.disableflags & MRS_DSBL_GRAVITY) && __float_as_int(dr[12])) {
+        const int bj = __float_as_int(dr[10]), e = __float_as_int(dr[11]);
         #pragma unroll 1
         for (int b = bj; b < e; ++b) {
           const float gc = m.body_gravcomp[b];
@@ -4321,6 +4324,10 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     for (int i = threadIdx.x; i < 4 * m.nfric; i += blockDim.x) shr[m.shr_fric + i] = m.fricrec[i];
     #pragma unroll 1
     for (int i = threadIdx.x; i < 4 * m.nlim; i += blockDim.x) shr[m.shr_lim + i] = m.limrec[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < 20 * m.nu; i += blockDim.x) shr[m.shr_act + i] = m.actrec[i];
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < 16 * m.nv; i += blockDim.x) shr[m.shr_dof + i] = m.dofrec[i];
   }
   __syncthreads();
   wsync();
