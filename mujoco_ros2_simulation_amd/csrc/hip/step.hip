@@ -4198,26 +4198,37 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   bool need_solve = false;
   float dg = 0;
   if (lane < nv) {
+    const lfloat* dr = shared_lds(m) + m.shr_dof + 16 * lane;  // batch.hip dofrec
+    const float damping = dr[9];
     if (m.integrator == MRS_INT_EULER) {
-      if (!(m.disableflags & MRS_DSBL_EULERDAMP) && m.dof_damping[lane] > 0) dg = m.dof_damping[lane];
+      if (!(m.disableflags & MRS_DSBL_EULERDAMP) && damping > 0) dg = damping;
     } else {
-      if (!(m.disableflags & MRS_DSBL_PASSIVE)) dg = m.dof_damping[lane];
-      if (!(m.disableflags & MRS_DSBL_ACTUATION))
-        #pragma unroll 1
-        for (int a = 0; a < m.nu; ++a) {
-          if (m.act_dof[a] != lane) continue;
-          if (m.act_forcelimited[a]) {
+      if (!(m.disableflags & MRS_DSBL_PASSIVE)) dg = damping;
+      if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
+        // velocity derivative of the actuators on this dof (the dof's single actuator from its
+        // table row; several: every actuator is checked)
+        auto act_dv = [&](int a) {
+          const lfloat* ar = shared_lds(m) + m.shr_act + 20 * a;  // batch.hip actrec
+          if (__float_as_int(ar[14])) {
             const float f = s[L.act_force + a];
-            if (f <= m.act_forcerange[2 * a] || f >= m.act_forcerange[2 * a + 1]) continue;
+            if (f <= ar[15] || f >= ar[16]) return;
           }
-          const float bv = m.act_biastype[a] == MRS_BIAS_AFFINE ? m.act_biasprm[3 * a + 2] : 0.0f;
-          const float gv = m.act_gaintype[a] == MRS_GAIN_AFFINE ? m.act_gainprm[3 * a + 2] : 0.0f;
+          const float bv = __float_as_int(ar[10]) == MRS_BIAS_AFFINE ? ar[13] : 0.0f;
+          const float gv = __float_as_int(ar[6]) == MRS_GAIN_AFFINE ? ar[9] : 0.0f;
           float ctrl = s[L.ctrl + a];
-          if (m.act_ctrllimited[a] && !(m.disableflags & MRS_DSBL_CLAMPCTRL))
-            ctrl = clampf(ctrl, m.act_ctrlrange[2 * a], m.act_ctrlrange[2 * a + 1]);
-          const float g = m.act_gear[a];
+          if (__float_as_int(ar[3]) && !(m.disableflags & MRS_DSBL_CLAMPCTRL)) ctrl = clampf(ctrl, ar[4], ar[5]);
+          const float g = ar[2];
           dg -= g * g * (bv + gv * ctrl);
+        };
+        const int da = __float_as_int(dr[0]);
+        if (da >= 0) {
+          act_dv(da);
+        } else if (da == -2) {
+          #pragma unroll 1
+          for (int a = 0; a < m.nu; ++a)
+            if (__float_as_int(shared_lds(m)[m.shr_act + 20 * a + 1]) == lane) act_dv(a);
         }
+      }
     }
   }
   need_solve = m.integrator != MRS_INT_EULER || gany<G>(dg != 0);
