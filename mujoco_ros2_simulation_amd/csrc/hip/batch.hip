@@ -845,6 +845,24 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   P.addf(&d.actrec, actrec);
   P.addf(&d.dofrec, dofrec);
+  // tree tables for the smooth dynamics (step.hip com_pos, make_M, com_vel, rne), staged in workgroup
+  // LDS: per body (8 floats) mass, subtree mass, root, parent, subtree end, dof address, dof count,
+  // pad; per (dof, ancestor-dof) pair of M (4 floats) i, j, body of i, armature when i == j
+  std::vector<float> bodytab, mpairtab;
+  {
+    auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+    for (int b = 0; b < m.nbody; ++b)
+      bodytab.insert(bodytab.end(), {static_cast<float>(m.body_mass[b]), static_cast<float>(m.body_subtreemass[b]),
+                                     fbits(m.body_rootid[b]), fbits(m.body_parentid[b]), fbits(subtree_end[b]),
+                                     fbits(m.body_dofadr[b]), fbits(m.body_dofnum[b]), 0.0f});
+    for (size_t q = 0; q + 1 < Mpair.size(); q += 2) {
+      const int i = Mpair[q], j = Mpair[q + 1];
+      mpairtab.insert(mpairtab.end(), {fbits(i), fbits(j), fbits(m.dof_bodyid[i]),
+                                       i == j ? static_cast<float>(m.dof_armature[i]) : 0.0f});
+    }
+  }
+  P.addf(&d.bodytab, bodytab);
+  P.addf(&d.mpairtab, mpairtab);
   // the non-ray sensors' descriptors, 16 floats each (staged in workgroup LDS at shr_sens): type,
   // objtype, sensordata address, dim (int bits), cutoff, the object's qpos / dof / actuator / body
   // index (int bits), the root body (int bits), then the site's or geom's local pos[3] and quat[4]
@@ -1121,12 +1139,18 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.shr_lim = d.shr_fric + 4 * d.nfric;
   d.shr_act = d.shr_lim + 4 * d.nlim;
   d.shr_dof = d.shr_act + 20 * m.nu;
-  d.shr_total = d.shr_dof + 16 * m.nv;
+  d.shr_body = d.shr_dof + 16 * m.nv;
+  d.shr_mpair = d.shr_body + 8 * m.nbody;
+  // the smooth-dynamics tables (from shr_act on) are staged only by lane-group kernels (G < 64);
+  // blocked mode (one env per workgroup) reads them from the model block instead of paying their LDS
+  // per env
+  const int shr_small = d.shr_act;
+  d.shr_total = d.shr_mpair + 4 * d.nMpair;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
   auto lds_bytes = [&](int g) {
-    return (static_cast<size_t>(L.total) * envs_per_block(g) + d.shr_total) * sizeof(float);
+    return (static_cast<size_t>(L.total) * envs_per_block(g) + (g == 64 ? shr_small : d.shr_total)) * sizeof(float);
   };
   // (narrow groups win even when they leave CUs idle: C4's 2048 envs run a 10-step launch in
   // 1.33 ms at G = 16 on 128 workgroups vs 4.0 ms at G = 64 on 512)
@@ -1138,6 +1162,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
   }
   d.blocked = b.group == 64 ? 1 : 0;
+  if (b.group == 64) d.shr_total = shr_small;
 
   if (d.blocked) lds_layout(true);
   d.shr_off = L.total * envs_per_block(b.group);

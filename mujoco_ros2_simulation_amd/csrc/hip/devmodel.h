@@ -97,6 +97,8 @@ struct DevModel {
   int shr_fric, shr_lim;
   // smooth-force tables (actrec, 20 floats per actuator; dofrec, 16 floats per dof) at shr_act, shr_dof
   int shr_act, shr_dof;
+  // tree tables (bodytab, 8 floats per body; mpairtab, 4 floats per pair of M) at shr_body, shr_mpair
+  int shr_body, shr_mpair;
   unsigned rf_static_mask;
   float* rf_static;
   // options
@@ -142,6 +144,7 @@ struct DevModel {
   CPtr<float> sensrec;  // their descriptors (batch.hip), 16 floats each
   CPtr<float> fricrec, limrec;  // 4 floats per friction-loss dof / limited joint (batch.hip)
   CPtr<float> actrec, dofrec;   // smooth-force tables (batch.hip)
+  CPtr<float> bodytab, mpairtab;  // tree tables of the smooth dynamics (batch.hip)
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;

@@ -1477,21 +1477,42 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   wsync();
 }
 
+// Smooth-dynamics tables (batch.hip actrec, dofrec, bodytab, mpairtab): from workgroup LDS with lane
+// groups, from the model block in blocked mode (G = 64, where LDS is per env)
+template <int G>
+__device__ __forceinline__ auto act_tab(const DevModel& m, int a) {
+  if constexpr (G == 64) return m.actrec + 20 * a; else return shared_lds(m) + m.shr_act + 20 * a;
+}
+template <int G>
+__device__ __forceinline__ auto dof_tab(const DevModel& m, int j) {
+  if constexpr (G == 64) return m.dofrec + 16 * j; else return shared_lds(m) + m.shr_dof + 16 * j;
+}
+// per body: mass, subtree mass, root, parent, subtree end, dof address, dof count
+template <int G>
+__device__ __forceinline__ auto body_tab(const DevModel& m, int b) {
+  if constexpr (G == 64) return m.bodytab + 8 * b; else return shared_lds(m) + m.shr_body + 8 * b;
+}
+template <int G>
+__device__ __forceinline__ auto mpair_tab(const DevModel& m, int p) {
+  if constexpr (G == 64) return m.mpairtab + 4 * p; else return shared_lds(m) + m.shr_mpair + 4 * p;
+}
+
 // mj_comPos: subtree coms of tree roots, cinert (parallel-axis part), cdof
 template <int G>
 __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
   ENV_UNPACK;
   #pragma unroll 1
   for (int b = lane; b < m.nbody; b += G) {
-    if (b != 0 && m.body_parentid[b] != 0) continue;
+    const auto bt = body_tab<G>(m, b);
+    if (b != 0 && __float_as_int(bt[3]) != 0) continue;
     float c[3] = {0, 0, 0};
-    const int e = m.body_subtree_end[b];
+    const int e = __float_as_int(bt[4]);
     #pragma unroll 4
     for (int k = b; k < e; ++k) {
-      const float mk = m.body_mass[k];
+      const float mk = body_tab<G>(m, k)[0];
       for (int i = 0; i < 3; ++i) c[i] += mk * s[L.xipos + 3 * k + i];
     }
-    const float sm = m.body_subtreemass[b];
+    const float sm = bt[1];
     for (int i = 0; i < 3; ++i) s[L.scom + 3 * b + i] = sm > kMinVal ? c[i] / sm : s[L.xipos + 3 * b + i];
   }
   wsync();
@@ -1499,8 +1520,9 @@ __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
   for (int b = lane; b < m.nbody; b += G) {
     lfloat* ci = s + L.cinert + 10 * b;
     if (b == 0) { for (int i = 0; i < 10; ++i) ci[i] = 0; continue; }
-    const int rt = m.body_rootid[b];
-    const float mass = m.body_mass[b];
+    const auto bt = body_tab<G>(m, b);
+    const int rt = __float_as_int(bt[2]);
+    const float mass = bt[0];
     float d[3];
     for (int i = 0; i < 3; ++i) d[i] = s[L.xipos + 3 * b + i] - s[L.scom + 3 * rt + i];
     ci[0] += mass * (d[1] * d[1] + d[2] * d[2]);
@@ -1552,7 +1574,7 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
   for (int b = lane; b < m.nbody; b += G) {
     float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (b != 0) {
-      const int e = m.body_subtree_end[b];
+      const int e = __float_as_int(body_tab<G>(m, b)[4]);
       #pragma unroll 4
       for (int k = b; k < e; ++k)
         for (int i = 0; i < 10; ++i) acc[i] += s[L.cinert + 10 * k + i];
@@ -1565,13 +1587,13 @@ __device__ MRS_PHASE void make_M(ENV_PARAMS) {
   wsync();
   #pragma unroll 1
   for (int p = lane; p < m.nMpair; p += G) {
-    const int i = m.Mpair[2 * p], j = m.Mpair[2 * p + 1];
+    const auto mp4 = mpair_tab<G>(m, p);  // i, j, body of i, armature
+    const int i = __float_as_int(mp4[0]), j = __float_as_int(mp4[1]);
     float buf[6], cd[6];
     for (int k = 0; k < 6; ++k) cd[k] = s[L.cdof + 6 * i + k];
-    mul_inert_vec(buf, s + L.crb + 10 * m.dof_bodyid[i], cd);
-    float v = 0;
+    mul_inert_vec(buf, s + L.crb + 10 * __float_as_int(mp4[2]), cd);
+    float v = mp4[3];
     for (int k = 0; k < 6; ++k) v += s[L.cdof + 6 * j + k] * buf[k];
-    if (i == j) v += m.dof_armature[i];
     s[L.M + midx<G>(m, i, j)] = v;
     s[L.M + midx<G>(m, j, i)] = v;
   }
@@ -1647,7 +1669,7 @@ __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
     const int b = lane;
     float v[6] = {0, 0, 0, 0, 0, 0};
     if (b >= 1 && b < m.nbody) {
-      const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      const int da = __float_as_int(body_tab<G>(m, b)[5]), nd = __float_as_int(body_tab<G>(m, b)[6]);
       #pragma unroll 1
       for (int j = da; j < da + nd; ++j) {
         const float qv = s[L.qvel + j];
@@ -1656,7 +1678,7 @@ __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
     }
     tree_prefix6<G>(m, s + L.cvel, b, v);
     if (b >= 1 && b < m.nbody) {
-      const int p = m.body_parentid[b];
+      const int p = __float_as_int(body_tab<G>(m, b)[3]);
       float cv[6];
       for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
       body_comvel(m, s, b, cv);
@@ -1733,7 +1755,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
     const int b = lane;
     float v[6] = {0, 0, 0, 0, 0, 0};
     if (b >= 1 && b < m.nbody) {
-      const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+      const int da = __float_as_int(body_tab<G>(m, b)[5]), nd = __float_as_int(body_tab<G>(m, b)[6]);
       #pragma unroll 1
       for (int j = da; j < da + nd; ++j) {
         const float qv = s[L.qvel + j];
@@ -1763,7 +1785,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
   for (int b = lane; b < m.nbody; b += G) {
     float acc[6] = {0, 0, 0, 0, 0, 0};
     if (b != 0) {
-      const int e = m.body_subtree_end[b];
+      const int e = __float_as_int(body_tab<G>(m, b)[4]);
       #pragma unroll 4
       for (int k = b; k < e; ++k)
         for (int i = 0; i < 6; ++i) acc[i] += s[L.cfrc + 6 * k + i];
@@ -1773,7 +1795,7 @@ __device__ MRS_PHASE void rne(ENV_PARAMS) {
   wsync();
   #pragma unroll 1
   for (int j = lane; j < m.nv; j += G) {
-    const int b = m.dof_bodyid[j];
+    const int b = __float_as_int(dof_tab<G>(m, j)[10]);  // body
     float v = 0;
     for (int i = 0; i < 6; ++i) v += s[L.cdof + 6 * j + i] * s[L.crb + 6 * b + i];
     s[L.qfrc_bias + j] = v;
@@ -1802,7 +1824,7 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   for (int a = lane; a < m.nu; a += G) {
     float force = 0;
     if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
-      const lfloat* ar = shared_lds(m) + m.shr_act + 20 * a;  // batch.hip actrec
+      const auto ar = act_tab<G>(m, a);
       const float gear = ar[2];
       const float len = gear * s[L.qpos + __float_as_int(ar[0])], vel = gear * s[L.qvel + __float_as_int(ar[1])];
       float ctrl = s[L.ctrl + a];
@@ -1818,7 +1840,7 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   float qfs = 0;
   if (lane < nv) {
     const int j = lane;
-    const lfloat* dr = shared_lds(m) + m.shr_dof + 16 * j;  // batch.hip dofrec
+    const auto dr = dof_tab<G>(m, j);
     float qa = 0;
     const int da = __float_as_int(dr[0]);
     if (da >= 0) {
@@ -4198,7 +4220,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   bool need_solve = false;
   float dg = 0;
   if (lane < nv) {
-    const lfloat* dr = shared_lds(m) + m.shr_dof + 16 * lane;  // batch.hip dofrec
+    const auto dr = dof_tab<G>(m, lane);
     const float damping = dr[9];
     if (m.integrator == MRS_INT_EULER) {
       if (!(m.disableflags & MRS_DSBL_EULERDAMP) && damping > 0) dg = damping;
@@ -4208,7 +4230,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
         // velocity derivative of the actuators on this dof (the dof's single actuator from its
         // table row; several: every actuator is checked)
         auto act_dv = [&](int a) {
-          const lfloat* ar = shared_lds(m) + m.shr_act + 20 * a;  // batch.hip actrec
+          const auto ar = act_tab<G>(m, a);
           if (__float_as_int(ar[14])) {
             const float f = s[L.act_force + a];
             if (f <= ar[15] || f >= ar[16]) return;
@@ -4226,7 +4248,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
         } else if (da == -2) {
           #pragma unroll 1
           for (int a = 0; a < m.nu; ++a)
-            if (__float_as_int(shared_lds(m)[m.shr_act + 20 * a + 1]) == lane) act_dv(a);
+            if (__float_as_int(act_tab<G>(m, a)[1]) == lane) act_dv(a);
         }
       }
     }
@@ -4335,10 +4357,16 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     for (int i = threadIdx.x; i < 4 * m.nfric; i += blockDim.x) shr[m.shr_fric + i] = m.fricrec[i];
     #pragma unroll 1
     for (int i = threadIdx.x; i < 4 * m.nlim; i += blockDim.x) shr[m.shr_lim + i] = m.limrec[i];
-    #pragma unroll 1
-    for (int i = threadIdx.x; i < 20 * m.nu; i += blockDim.x) shr[m.shr_act + i] = m.actrec[i];
-    #pragma unroll 1
-    for (int i = threadIdx.x; i < 16 * m.nv; i += blockDim.x) shr[m.shr_dof + i] = m.dofrec[i];
+    if constexpr (G < 64) {  // smooth-dynamics tables (blocked mode reads the model block)
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 20 * m.nu; i += blockDim.x) shr[m.shr_act + i] = m.actrec[i];
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 16 * m.nv; i += blockDim.x) shr[m.shr_dof + i] = m.dofrec[i];
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 8 * m.nbody; i += blockDim.x) shr[m.shr_body + i] = m.bodytab[i];
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 4 * m.nMpair; i += blockDim.x) shr[m.shr_mpair + i] = m.mpairtab[i];
+    }
   }
   __syncthreads();
   wsync();
