@@ -1141,11 +1141,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.shr_dof = d.shr_act + 20 * m.nu;
   d.shr_body = d.shr_dof + 16 * m.nv;
   d.shr_mpair = d.shr_body + 8 * m.nbody;
+  d.shr_jump = d.shr_mpair + 4 * d.nMpair;
   // the smooth-dynamics tables (from shr_act on) are staged only by lane-group kernels (G < 64);
   // blocked mode (one env per workgroup) reads them from the model block instead of paying their LDS
   // per env
   const int shr_small = d.shr_act;
-  d.shr_total = d.shr_mpair + 4 * d.nMpair;
+  d.shr_total = d.shr_jump + d.njump * m.nbody;
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)

@@ -99,6 +99,7 @@ struct DevModel {
   int shr_act, shr_dof;
   // tree tables (bodytab, 8 floats per body; mpairtab, 4 floats per pair of M) at shr_body, shr_mpair
   int shr_body, shr_mpair;
+  int shr_jump;  // the kinematics' pointer-jumping table (jump, int bits) with lane groups
   unsigned rf_static_mask;
   float* rf_static;
   // options

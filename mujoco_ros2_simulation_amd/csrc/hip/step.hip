@@ -1294,6 +1294,26 @@ __device__ __forceinline__ void chol_solve_serial(const lfloat* Lf, int nv, cons
   }
 }
 
+// Smooth-dynamics tables (batch.hip actrec, dofrec, bodytab, mpairtab): from workgroup LDS with lane
+// groups, from the model block in blocked mode (G = 64, where LDS is per env)
+template <int G>
+__device__ __forceinline__ auto act_tab(const DevModel& m, int a) {
+  if constexpr (G == 64) return m.actrec + 20 * a; else return shared_lds(m) + m.shr_act + 20 * a;
+}
+template <int G>
+__device__ __forceinline__ auto dof_tab(const DevModel& m, int j) {
+  if constexpr (G == 64) return m.dofrec + 16 * j; else return shared_lds(m) + m.shr_dof + 16 * j;
+}
+// per body: mass, subtree mass, root, parent, subtree end, dof address, dof count
+template <int G>
+__device__ __forceinline__ auto body_tab(const DevModel& m, int b) {
+  if constexpr (G == 64) return m.bodytab + 8 * b; else return shared_lds(m) + m.shr_body + 8 * b;
+}
+template <int G>
+__device__ __forceinline__ auto mpair_tab(const DevModel& m, int p) {
+  if constexpr (G == 64) return m.mpairtab + 4 * p; else return shared_lds(m) + m.shr_mpair + 4 * p;
+}
+
 // pose of body b from its parent's frame (P, Q): body offset, then its joints in order (mj_kinematics
 // per body).  With kJoints the world anchors/axes of the joints are written (P, Q must be the
 // parent's world frame then).  A free joint gives the world pose directly (its parent is the world).
@@ -1424,7 +1444,11 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
     wsync();
     #pragma unroll 1
     for (int r = 0; r < m.njump; ++r) {
-      const int a = (b >= 1 && b < m.nbody) ? m.jump[r * m.nbody + b] : -1;
+      int a = -1;
+      if (b >= 1 && b < m.nbody) {
+        if constexpr (G == 64) a = m.jump[r * m.nbody + b];
+        else a = __float_as_int(shared_lds(m)[m.shr_jump + r * m.nbody + b]);
+      }
       float ap[3], aq[4];
       if (a >= 0) {
         for (int i = 0; i < 3; ++i) ap[i] = s[L.xpos + 3 * a + i];
@@ -1444,7 +1468,7 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
     // every body from its parent's world pose (same values up to rounding, plus joint frames)
     float P[3] = {0, 0, 0}, Q[4] = {1, 0, 0, 0};
     if (b >= 1 && b < m.nbody) {
-      const int p = m.body_parentid[b];
+      const int p = __float_as_int(body_tab<G>(m, b)[3]);
       for (int i = 0; i < 3; ++i) P[i] = s[L.xpos + 3 * p + i];
       for (int i = 0; i < 4; ++i) Q[i] = s[L.xquat + 4 * p + i];
     }
@@ -1475,26 +1499,6 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
     for (int i = 0; i < 9; ++i) s[L.gxmat + 9 * g + i] = gm[i];
   }
   wsync();
-}
-
-// Smooth-dynamics tables (batch.hip actrec, dofrec, bodytab, mpairtab): from workgroup LDS with lane
-// groups, from the model block in blocked mode (G = 64, where LDS is per env)
-template <int G>
-__device__ __forceinline__ auto act_tab(const DevModel& m, int a) {
-  if constexpr (G == 64) return m.actrec + 20 * a; else return shared_lds(m) + m.shr_act + 20 * a;
-}
-template <int G>
-__device__ __forceinline__ auto dof_tab(const DevModel& m, int j) {
-  if constexpr (G == 64) return m.dofrec + 16 * j; else return shared_lds(m) + m.shr_dof + 16 * j;
-}
-// per body: mass, subtree mass, root, parent, subtree end, dof address, dof count
-template <int G>
-__device__ __forceinline__ auto body_tab(const DevModel& m, int b) {
-  if constexpr (G == 64) return m.bodytab + 8 * b; else return shared_lds(m) + m.shr_body + 8 * b;
-}
-template <int G>
-__device__ __forceinline__ auto mpair_tab(const DevModel& m, int p) {
-  if constexpr (G == 64) return m.mpairtab + 4 * p; else return shared_lds(m) + m.shr_mpair + 4 * p;
 }
 
 // mj_comPos: subtree coms of tree roots, cinert (parallel-axis part), cdof
@@ -4366,6 +4370,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       for (int i = threadIdx.x; i < 8 * m.nbody; i += blockDim.x) shr[m.shr_body + i] = m.bodytab[i];
       #pragma unroll 1
       for (int i = threadIdx.x; i < 4 * m.nMpair; i += blockDim.x) shr[m.shr_mpair + i] = m.mpairtab[i];
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < m.njump * m.nbody; i += blockDim.x) shr[m.shr_jump + i] = __int_as_float(m.jump[i]);
     }
   }
   __syncthreads();
