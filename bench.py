@@ -52,6 +52,9 @@ def parse():
                    help="c3: the BASELINE metric (default); c2: reference 2-DoF scene, 4096 envs, sensors off; "
                         "c4: mobile base + lidar + 640x480 depth camera; c5: contact-rich arm + 8 free boxes")
     p.add_argument("--render-every", type=int, default=100, help="C4: physics steps between depth frames")
+    p.add_argument("--render-sync", action="store_true",
+                   help="C4: render each frame on the batch stream between steps instead of the camera "
+                        "pipeline (pose snapshot, render concurrently with the following steps)")
     p.add_argument("--no-gather", action="store_true",
                    help="N>1: skip the end-of-period observation gather (on by default when N > 1)")
     return p.parse_args()
@@ -179,6 +182,7 @@ def main():
         every = max(1, args.render_every // args.period)
     torch.cuda.synchronize()
     step_ev, rend_ev = [], []
+    rend_async, rend_async_ms = [False], []
 
     def period(p: int, timed: bool):
         batch.set_ctrl_device(d_table[p].data_ptr())
@@ -190,13 +194,21 @@ def main():
             e[1].record(stream)
             step_ev.append(e)
         if render and (p + 1) % every == 0:
-            r = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
-            if r:
-                r[0].record(stream)
-            batch.render_depth_device(0, 0, n, frames.data_ptr())
-            if r:
-                r[1].record(stream)
-                rend_ev.append(r)
+            if args.render_sync:
+                r = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+                if r:
+                    r[0].record(stream)
+                batch.render_depth_device(0, 0, n, frames.data_ptr())
+                if r:
+                    r[1].record(stream)
+                    rend_ev.append(r)
+            else:
+                # the reference's camera thread: snapshot now, render while the next periods step.
+                # The previous frame's kernel time (HIP events on the render stream) is read first.
+                if rend_async[0]:
+                    rend_async_ms.append(batch.last_kernel_ms(1))
+                batch.render_async(0, 0, n, frames.data_ptr())
+                rend_async[0] = timed
         if gather is not None:
             # this period's observations into HBM buffers, then grouped sends to rank 0
             q, v = gather.start(p)
@@ -215,12 +227,18 @@ def main():
             period(args.warmup + k, True)
         if gather is not None:
             gather.gathered(args.warmup + args.steps - 1)
+        if render and not args.render_sync:
+            batch.render_wait()   # the last frame is part of the timed work
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
+    batch.sync()
     step_ms = float(np.mean([a.elapsed_time(b) for a, b in step_ev]))
-    rend_ms = float(np.mean([a.elapsed_time(b) for a, b in rend_ev])) if rend_ev else float("nan")
+    if rend_async[0]:
+        rend_async_ms.append(batch.last_kernel_ms(1))
+    rend_list = rend_async_ms if not args.render_sync else [a.elapsed_time(b) for a, b in rend_ev]
+    rend_ms = float(np.mean(rend_list)) if rend_list else float("nan")
     elapsed, step_ms, rend_ms = shard.max_over_ranks([t1 - t0, step_ms, rend_ms], device=dev)
 
     # sanity: states finite after the run (a diverged run would be invalid)
@@ -253,6 +271,9 @@ def main():
     sq_rec, sq_src = committed("sq", cfg, n, args.period)
     if render:
         config["depth_every_physics_steps"] = every * args.period
+        config["camera_pipeline"] = ("frames rendered on the batch stream between steps" if args.render_sync else
+                                     "pose snapshot on the batch stream, frame rendered on a second HIP stream "
+                                     "concurrently with the following steps (the reference's rendering thread)")
         bytes_frame = n * W * H * 4
         achieved = bytes_frame / (rend_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": roofline.PEAK_HBM_GBS, "unit": "GB/s",
@@ -289,7 +310,7 @@ def main():
         "config": config, "roofline": roof,
     }
     if render:
-        result["depth_frames_per_s"] = world * n * len(rend_ev) / elapsed
+        result["depth_frames_per_s"] = world * n * len(rend_list) / elapsed
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.period, args.cpu_seconds)
     if rank == 0:

@@ -118,6 +118,16 @@ int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float*
 int mrs_batch_render_rgbd(mrs_batch* b, int cam, int env0, int n, float* host_depth, unsigned char* host_rgb);
 /* same, into device buffers */
 int mrs_batch_render_rgbd_device(mrs_batch* b, int cam, int env0, int n, float* d_depth, unsigned char* d_rgb);
+/* camera pipeline (the reference's rendering thread: mjv_copyData of the live data under the sim
+ * mutex, then mjv_updateScene + mjr_render of the copy while PhysicsLoop steps on,
+ * src/mujoco_cameras.cpp:204-215): snapshot the poses of the last step on the batch stream, then
+ * render depth (and colour when d_rgb is not NULL) from the snapshot on the batch's own render stream,
+ * concurrently with the steps queued after this call.  Device buffers as mrs_batch_render_rgbd_device.
+ * A later snapshot waits until the previous asynchronous render has read the old one. */
+int mrs_batch_render_async(mrs_batch* b, int cam, int env0, int n, float* d_depth, unsigned char* d_rgb);
+/* order the batch stream after the last asynchronous render (its frames are complete for any work
+ * queued on the batch stream afterwards; mrs_batch_sync also waits for it) */
+int mrs_batch_render_wait(mrs_batch* b);
 /* mjData.contact of env `env` after its last step / forward (the output of mj_collision, SURVEY.md
  * §8a row a2.3): up to `max` contacts in mj_collision's order -- geom [max][2] int32 (geom1, geom2,
  * the lower geom type first), dist [max], pos [max][3], frame [max][9] fp64 (normal = frame[0:3]);

@@ -224,6 +224,20 @@ int mrs_batch_render_rgbd_device(mrs_batch* b, int cam, int env0, int n, float* 
   });
 }
 
+int mrs_batch_render_async(mrs_batch* b, int cam, int env0, int n, float* d_depth, unsigned char* d_rgb) {
+  return guarded([&] {
+    if (!b || !d_depth) throw std::invalid_argument("null argument");
+    mrs::batch_render_async(b->impl, cam, env0, n, d_depth, d_rgb);
+  });
+}
+
+int mrs_batch_render_wait(mrs_batch* b) {
+  return guarded([&] {
+    if (!b) throw std::invalid_argument("null batch");
+    mrs::batch_render_wait(b->impl);
+  });
+}
+
 int mrs_batch_get_contacts(mrs_batch* b, int env, int max, int* geom, double* dist, double* pos, double* frame) {
   int ncon = 0;
   const int rc = guarded([&] {

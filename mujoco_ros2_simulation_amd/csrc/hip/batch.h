@@ -25,6 +25,8 @@ void batch_set_ctrl_device(BatchImpl* b, const float* d_ctrl);
 void batch_launch(BatchImpl* b, int n_steps, bool forward_only);
 // rgb (may be null): n * H * W * 3 bytes, same host/device side as out
 void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out, unsigned char* rgb = nullptr);
+void batch_render_async(BatchImpl* b, int cam, int env0, int n, float* d_out, unsigned char* d_rgb);
+void batch_render_wait(BatchImpl* b);
 int batch_get_contacts(BatchImpl* b, int env, int max, int* geom, double* dist, double* pos, double* frame);
 int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force);
 void batch_get_field_device(BatchImpl* b, int field, float* d_out, int env0, int n);

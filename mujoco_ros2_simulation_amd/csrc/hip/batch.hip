@@ -543,6 +543,12 @@ struct BatchImpl {
   bool ev_valid[2] = {false, false};
   std::vector<float> staging;
   std::vector<int> pair_g1, pair_g2;  // host copy of the static collision pairs (contact export)
+  // camera pipeline (batch_render_async): pose snapshot + side stream, as the reference's rendering
+  // thread renders its mjv_copyData snapshot while PhysicsLoop steps on (src/mujoco_cameras.cpp:204-215)
+  hipStream_t rstream = nullptr;
+  hipEvent_t snap_ev = nullptr, rend_ev = nullptr;
+  bool rend_pending = false;
+  float *snap_gpos = nullptr, *snap_gmat = nullptr, *snap_cpos = nullptr, *snap_cmat = nullptr;
 };
 
 namespace {
@@ -1288,7 +1294,11 @@ void batch_free(BatchImpl* b) {
   if (!b) return;
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
+  if (b->rstream) (void)hipStreamSynchronize(b->rstream);
   for (void* p : b->allocs) (void)hipFree(p);
+  if (b->snap_ev) (void)hipEventDestroy(b->snap_ev);
+  if (b->rend_ev) (void)hipEventDestroy(b->rend_ev);
+  if (b->rstream) (void)hipStreamDestroy(b->rstream);
   for (int k = 0; k < 2; ++k) {
     if (b->ev0[k]) (void)hipEventDestroy(b->ev0[k]);
     if (b->ev1[k]) (void)hipEventDestroy(b->ev1[k]);
@@ -1414,11 +1424,46 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   b->ev_valid[0] = true;
 }
 
-void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out, unsigned char* rgb_out) {
+namespace {
+struct Poses { const float *gpos, *gmat, *cpos, *cmat; };
+
+void check_render_args(const BatchImpl* b, int cam, int env0, int n) {
   const Model& m = *b->model;
   if (cam < 0 || cam >= m.ncam) throw std::invalid_argument("camera index out of range");
   if (env0 < 0 || n < 1 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
   if (m.ngeom > kMaxRenderGeoms) throw UnsupportedError("too many geoms for the depth kernel");
+}
+
+// depth (+ colour) kernel launch on `stream` from the given geom / camera poses, bracketed by the
+// batch's render timing events
+void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned char* drgb, const Poses& ps,
+                   hipStream_t stream) {
+  const Model& m = *b->model;
+  const int W = m.cam_resolution[2 * cam], H = m.cam_resolution[2 * cam + 1];
+  const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
+  const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
+  const DevModel& d = b->dm;
+  const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p, d.mesh_facenum.p};
+  HIP_CHECK(hipEventRecord(b->ev0[1], stream));
+  if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
+    hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
+                       d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
+  } else {
+    dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
+    hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
+                       d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
+  }
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(b->ev1[1], stream));
+  b->ev_valid[1] = true;
+}
+}  // namespace
+
+void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out, unsigned char* rgb_out) {
+  check_render_args(b, cam, env0, n);
+  const Model& m = *b->model;
   HIP_CHECK(hipSetDevice(b->device));
   const int W = m.cam_resolution[2 * cam], H = m.cam_resolution[2 * cam + 1];
   const size_t bytes = static_cast<size_t>(n) * W * H * sizeof(float);
@@ -1431,30 +1476,51 @@ void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool
     dout = static_cast<float*>(tmp);
     if (rgb_out) drgb = static_cast<unsigned char*>(tmp) + bytes;
   }
-  const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
-  const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
-  const DevModel& d = b->dm;
-  const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p, d.mesh_facenum.p};
-  HIP_CHECK(hipEventRecord(b->ev0[1], b->stream));
-  if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
-    hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
-                       d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
-  } else {
-    dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
-    hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, b->stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
-                       d.geom_rgba.p, m.ngeom, b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
-  }
-  HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(b->ev1[1], b->stream));
-  b->ev_valid[1] = true;
+  if (b->rend_pending) HIP_CHECK(hipStreamWaitEvent(b->stream, b->rend_ev, 0));  // one render at a time
+  render_launch(b, cam, env0, n, dout, drgb, Poses{b->st.geom_xpos, b->st.geom_xmat, b->st.cam_xpos, b->st.cam_xmat},
+                b->stream);
   if (!device_out) {
     HIP_CHECK(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, b->stream));
     if (rgb_out) HIP_CHECK(hipMemcpyAsync(rgb_out, drgb, rgb_bytes, hipMemcpyDeviceToHost, b->stream));
     HIP_CHECK(hipFreeAsync(tmp, b->stream));
     HIP_CHECK(hipStreamSynchronize(b->stream));
   }
+}
+
+// Camera pipeline: the poses of the last step are copied into a snapshot on the batch stream (so the
+// copy is ordered after that step and before the next), then the frame is rendered from the snapshot
+// on the batch's render stream while later steps run on the batch stream.  A new snapshot waits for
+// the previous asynchronous render to finish reading the old one.  batch_render_wait orders the
+// batch stream after the last render (frames complete for anything queued later).
+void batch_render_async(BatchImpl* b, int cam, int env0, int n, float* d_out, unsigned char* d_rgb) {
+  check_render_args(b, cam, env0, n);
+  const Model& m = *b->model;
+  HIP_CHECK(hipSetDevice(b->device));
+  const size_t ng = static_cast<size_t>(b->n) * std::max(1, m.ngeom), nc = static_cast<size_t>(b->n) * std::max(1, m.ncam);
+  if (!b->rstream) {
+    HIP_CHECK(hipStreamCreateWithFlags(&b->rstream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&b->snap_ev, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&b->rend_ev, hipEventDisableTiming));
+    b->snap_gpos = static_cast<float*>(dalloc(*b, ng * 3 * sizeof(float)));
+    b->snap_gmat = static_cast<float*>(dalloc(*b, ng * 9 * sizeof(float)));
+    b->snap_cpos = static_cast<float*>(dalloc(*b, nc * 3 * sizeof(float)));
+    b->snap_cmat = static_cast<float*>(dalloc(*b, nc * 9 * sizeof(float)));
+  }
+  if (b->rend_pending) HIP_CHECK(hipStreamWaitEvent(b->stream, b->rend_ev, 0));
+  HIP_CHECK(hipMemcpyAsync(b->snap_gpos, b->st.geom_xpos, ng * 3 * sizeof(float), hipMemcpyDeviceToDevice, b->stream));
+  HIP_CHECK(hipMemcpyAsync(b->snap_gmat, b->st.geom_xmat, ng * 9 * sizeof(float), hipMemcpyDeviceToDevice, b->stream));
+  HIP_CHECK(hipMemcpyAsync(b->snap_cpos, b->st.cam_xpos, nc * 3 * sizeof(float), hipMemcpyDeviceToDevice, b->stream));
+  HIP_CHECK(hipMemcpyAsync(b->snap_cmat, b->st.cam_xmat, nc * 9 * sizeof(float), hipMemcpyDeviceToDevice, b->stream));
+  HIP_CHECK(hipEventRecord(b->snap_ev, b->stream));
+  HIP_CHECK(hipStreamWaitEvent(b->rstream, b->snap_ev, 0));
+  render_launch(b, cam, env0, n, d_out, d_rgb, Poses{b->snap_gpos, b->snap_gmat, b->snap_cpos, b->snap_cmat}, b->rstream);
+  HIP_CHECK(hipEventRecord(b->rend_ev, b->rstream));
+  b->rend_pending = true;
+}
+
+void batch_render_wait(BatchImpl* b) {
+  HIP_CHECK(hipSetDevice(b->device));
+  if (b->rend_pending) HIP_CHECK(hipStreamWaitEvent(b->stream, b->rend_ev, 0));
 }
 
 // mjData.contact of the last forward pass of one env (geom1/geom2 as mj_collision orders them: pair
@@ -1537,6 +1603,7 @@ void batch_get_field_device(BatchImpl* b, int field, float* d_out, int env0, int
 void batch_sync(BatchImpl* b) {
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipStreamSynchronize(b->stream));
+  if (b->rstream) HIP_CHECK(hipStreamSynchronize(b->rstream));
 }
 
 double batch_last_kernel_ms(BatchImpl* b, int kind) {

@@ -2000,6 +2000,162 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       });
     }
   });
+  // Delassus rows (mj_solPGS's efc_AR): lane r holds AR_rs = J_r M^-1 J_s' (+ R_r on the diagonal)
+  // for every s; each (r, s <= r) product is one group sum, mirrored into lane s
+  float AR[KR];
+  float myA = 1, myf = 0;  // lane r: A_rr and the force of row r
+  unroll<KR>([&](auto rc) { AR[decltype(rc)::value] = 0.0f; });
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    unroll<r + 1>([&](auto sc) {
+      constexpr int c = decltype(sc)::value;
+      if (r < rmax) {
+        const float a = gsum<16>(Jt[r] * MJt[c]);
+        if constexpr (c == r) {
+          if (lane == r) { AR[r] = a + myR; myA = AR[r]; }
+        } else {
+          if (lane == r) AR[c] = a;
+          if (lane == c) AR[r] = a;
+        }
+      }
+    });
+  });
+  // warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost
+  // f' (0.5 AR f + b) is negative.  Lane r owns row r: it alone computes the row's force, which every
+  // lane then takes from it by broadcast
+  if (!(m.disableflags & MRS_DSBL_WARMSTART)) {
+    const float qw = lane < nv ? s[L.qacc_ws + lane] : 0.0f;
+    float myjar = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) {
+        const float jr = gsum<16>(Jt[r] * qw);
+        if (lane == r) myjar = jr - myaref;
+      }
+    });
+    {
+      const float D = 1.0f / myR;
+      myf = lane >= nefc ? 0.0f
+                         : (myfl > 0 ? (myjar <= -myR * myfl ? myfl : (myjar >= myR * myfl ? -myfl : -D * myjar))
+                                     : (myjar < 0 ? -D * myjar : 0.0f));
+    }
+    float arf = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) arf += AR[r] * rowb<r>(myf);
+    });
+    const float cost = gsum<16>(lane < rmax ? myf * (0.5f * arf + myb) : 0.0f);
+    if (cost > 0) myf = 0;
+  }
+  // PGS sweeps on the dual (mj_solPGS): forces replicated in every lane; lane t keeps the residual
+  // g_t = b_t + sum_s AR_ts f_s, recomputed at the start of each sweep and moved by AR_tr delta_r after
+  // row r's update, so a row costs one broadcast of its residual and one FMA per lane instead of a
+  // group reduction of J_r qacc
+  float f[KR], bA[KR], iA[KR], flo[KR], fhi[KR];
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    f[r] = rowb<r>(myf); bA[r] = rowb<r>(myA); iA[r] = 1.0f / bA[r];
+    const float fl = rowb<r>(myfl);
+    flo[r] = fl > 0 ? -fl : 0.0f;
+    fhi[r] = fl > 0 ? fl : __builtin_inff();
+  });
+  const float myb0 = lane < rmax ? myb : 0.0f;
+  int nit = 0;  // sweeps done (mjData.solver_niter)
+  #pragma unroll 1
+  for (int it = 0; it < m.iterations; ++it) {
+    float ga = myb0, gb = 0, gc = 0, gd = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) {
+        float& acc = (r & 3) == 0 ? ga : (r & 3) == 1 ? gb : (r & 3) == 2 ? gc : gd;
+        acc += AR[r] * f[r];
+      }
+    });
+    float g = (ga + gb) + (gc + gd);
+    float improvement = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (r < rmax) {
+        const float res = rowb<r>(g);
+        const float nf = __builtin_amdgcn_fmed3f(f[r] - res * iA[r], flo[r], fhi[r]);
+        const float delta = nf - f[r];
+        g += AR[r] * delta;
+        f[r] = nf;
+        improvement -= delta * res + 0.5f * delta * delta * bA[r];
+      }
+    });
+    nit = it + 1;
+    if (improvement * m.pgs_scale < m.tolerance) break;
+  }
+  float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if (r < rmax) qa += MJt[r] * f[r];
+  });
+  if (lane == 0) s[L.niter] = __int_as_float(nit);
+  float qc = 0;
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if (r < rmax) qc += Jt[r] * f[r];
+    if (lane == r) myf = f[r];
+  });
+  if (lane < nv) s[L.qfrc_con + lane] = qc;
+  // row forces (mj_rnePostConstraint's contact forces, mrs_batch_get_efc)
+  // (the friction-loss fast path stores them only when force/torque sensors read them)
+  if (ff && (!kUnit || (m.acc_sens & 2)) && lane < nefc) ff[lane] = myf;
+  return qa;
+}
+
+// The same PGS in qacc form (each row's residual is a group sum of J_r qacc): used for the
+// friction-loss unit rows, whose systems converge in a few sweeps, where the dual form's O(rows^2)
+// Delassus set-up costs more than its shorter sweep chain saves (C3: 179 vs 171 M env-steps/s)
+template <bool kUnit = false, int KR = 16>
+__device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
+                                             float myR, float myaref, float myb, float myfl, float qacc_s,
+                                             int lane, int mydof = -1) {
+  const LdsLayout& L = m.L;
+  const int nv = m.nv;
+  // J and M^-1 J' columns per row in registers; row scalars (R, aref, b, bound, diagonal of A, force)
+  // stay in the row's own lane and reach the other lanes by DPP row broadcasts when used
+  float Jt[KR], MJt[KR];
+  if (lane >= nefc) { myR = 1; myaref = 0; myb = 0; myfl = 0; }
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if constexpr (kUnit)
+      Jt[r] = (r < nefc && lane == __float_as_int(rowb<r>(__int_as_float(mydof)))) ? 1.0f : 0.0f;
+    else
+      Jt[r] = (r < nefc && lane < nv) ? J[r * nv + lane] : 0.0f;
+    MJt[r] = Jt[r];
+  });
+  // M^-1 J' for all rows at once: forward then backward substitution with L (Cholesky of M, LDS)
+  unroll<KR>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i < nv) {
+      const float inv = 1.0f / s[L.L + i * nv + i];
+      const float lji = (lane > i && lane < nv) ? s[L.L + lane * nv + i] : 0.0f;
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (r < rmax) {
+          const float xi = rowb<i>(MJt[r]) * inv;
+          MJt[r] = lane == i ? xi : MJt[r] - lji * xi;
+        }
+      });
+    }
+  });
+  unroll<KR>([&](auto ic) {
+    constexpr int i = KR - 1 - decltype(ic)::value;
+    if (i < nv) {
+      const float inv = 1.0f / s[L.L + i * nv + i];
+      const float lij = lane < i ? s[L.L + i * nv + lane] : 0.0f;
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (r < rmax) {
+          const float zi = rowb<i>(MJt[r]) * inv;
+          MJt[r] = lane == i ? zi : MJt[r] - lij * zi;
+        }
+      });
+    }
+  });
   float myA = 1, myf = 0;  // lane r: A_rr = J_r M^-1 J_r' + R_r and the force of row r
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
@@ -3347,9 +3503,9 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       // a quarter of the substitution code
       float qa;
       if (nf <= 8 && m.nv <= 8)
-        qa = pgs_small16<true, 8>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+        qa = pgs_small16_qacc<true, 8>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
       else
-        qa = pgs_small16<true, 16>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+        qa = pgs_small16_qacc<true, 16>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
       wsync();
       return qa;
     }

@@ -147,6 +147,8 @@ def lib() -> C.CDLL:
         L.mrs_batch_render_depth_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.mrs_batch_render_rgbd.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.mrs_batch_render_rgbd_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.mrs_batch_render_async.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.mrs_batch_render_wait.argtypes = [C.c_void_p]
         L.mrs_batch_sync.argtypes = [C.c_void_p]
         L.mrs_batch_get_contacts.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p]
@@ -326,6 +328,15 @@ class Batch:
 
     def render_depth_device(self, cam: int, env0: int, n: int, dptr: int) -> None:
         _check(lib().mrs_batch_render_depth_device(self._h, cam, env0, n, C.c_void_p(dptr)))
+
+    def render_async(self, cam: int, env0: int, n: int, depth_ptr: int, rgb_ptr: int = 0) -> None:
+        """snapshot the last step's poses, render from the snapshot concurrently with later steps"""
+        _check(lib().mrs_batch_render_async(self._h, cam, env0, n, C.c_void_p(depth_ptr),
+                                             C.c_void_p(rgb_ptr) if rgb_ptr else None))
+
+    def render_wait(self) -> None:
+        """order the batch stream after the last asynchronous render"""
+        _check(lib().mrs_batch_render_wait(self._h))
 
     def contacts(self, env: int = 0, max_n: int = 256):
         """mjData.contact of `env` after the last step/forward: (geom [n, 2] int32, dist [n],

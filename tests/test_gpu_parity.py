@@ -620,3 +620,38 @@ def test_rgbd_all_primitives():
         diff = np.abs(rgb[e].astype(int) - wrgb.astype(int)).max(axis=-1)
         assert (diff <= 1).mean() >= 0.99, (diff <= 1).mean()
     assert len({tuple(c) for c in wrgb.reshape(-1, 3)[::97]}) > 20  # shaded, not flat
+
+
+def test_camera_pipeline_snapshot():
+    """mrs_batch_render_async renders the poses of the step it was queued after (its snapshot), while
+    the following steps move the bodies: frames equal a synchronous render of that same state, and
+    colour equals the synchronous colour pass"""
+    import torch
+    from conftest import ROOT
+    model = sim.Model.load(ROOT / "scenes" / "mobile_base.xml")
+    n = 64
+    envs = np.arange(n)
+    W, H = (int(v) for v in model.cam_resolution[0])
+    b = sim.Batch(model, n)
+    b.set(sim.FIELD_QPOS, synth.initial_qpos(model, envs))
+    b.set(sim.FIELD_CTRL, synth.ctrl_table(model, envs, 1, 10)[0])
+    b.step(30)
+    want = torch.empty((n, H, W), dtype=torch.float32, device="cuda")
+    want_rgb = torch.empty((n, H, W, 3), dtype=torch.uint8, device="cuda")
+    b.render_rgbd_device(0, 0, n, want.data_ptr(), want_rgb.data_ptr())
+    b.sync()
+    got = torch.full((n, H, W), -7.0, dtype=torch.float32, device="cuda")
+    got_rgb = torch.zeros((n, H, W, 3), dtype=torch.uint8, device="cuda")
+    b.render_async(0, 0, n, got.data_ptr(), got_rgb.data_ptr())
+    b.step(50)                       # moves the base while the frame renders
+    b.render_wait()
+    b.sync()
+    assert torch.equal(got, want)
+    assert torch.equal(got_rgb, want_rgb)
+    # a second frame after more steps differs (the snapshot is refreshed), and again matches
+    b.render_async(0, 0, n, got.data_ptr(), 0)
+    b.sync()
+    b.render_depth_device(0, 0, n, want.data_ptr())
+    b.sync()
+    assert torch.equal(got, want)
+    b.close()
