@@ -2048,22 +2048,21 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     if (cost > 0) myf = 0;
   }
   // PGS sweeps on the dual (mj_solPGS): forces replicated in every lane; lane t keeps the residual
-  // g_t = b_t + sum_s AR_ts f_s, recomputed at the start of each sweep and moved by AR_tr delta_r after
-  // row r's update, so a row costs one broadcast of its residual and one FMA per lane instead of a
-  // group reduction of J_r qacc
-  float f[KR], bA[KR], iA[KR], flo[KR], fhi[KR];
+  // g_t = b_t + sum_s AR_ts f_s (computed once, then moved by AR_tr delta_r after row r's update), so
+  // a row costs one broadcast of its residual and one FMA per lane instead of a group reduction of
+  // J_r qacc.  Lane r also keeps row r's residual and step of the sweep; the sweep's cost improvement
+  // sum_r -(delta_r res_r + 0.5 A_rr delta_r^2) (every term >= 0) is one group sum at its end.
+  float f[KR], iA[KR], flo[KR], fhi[KR];
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    f[r] = rowb<r>(myf); bA[r] = rowb<r>(myA); iA[r] = 1.0f / bA[r];
+    f[r] = rowb<r>(myf); iA[r] = 1.0f / rowb<r>(myA);
     const float fl = rowb<r>(myfl);
     flo[r] = fl > 0 ? -fl : 0.0f;
     fhi[r] = fl > 0 ? fl : __builtin_inff();
   });
-  const float myb0 = lane < rmax ? myb : 0.0f;
-  int nit = 0;  // sweeps done (mjData.solver_niter)
-  #pragma unroll 1
-  for (int it = 0; it < m.iterations; ++it) {
-    float ga = myb0, gb = 0, gc = 0, gd = 0;
+  float g;
+  {
+    float ga = lane < rmax ? myb : 0.0f, gb = 0, gc = 0, gd = 0;
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
@@ -2071,19 +2070,25 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
         acc += AR[r] * f[r];
       }
     });
-    float g = (ga + gb) + (gc + gd);
-    float improvement = 0;
+    g = (ga + gb) + (gc + gd);
+  }
+  const float halfA = 0.5f * myA;
+  int nit = 0;  // sweeps done (mjData.solver_niter)
+  #pragma unroll 1
+  for (int it = 0; it < m.iterations; ++it) {
+    float myres = 0, mydelta = 0;
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
         const float res = rowb<r>(g);
         const float nf = __builtin_amdgcn_fmed3f(f[r] - res * iA[r], flo[r], fhi[r]);
         const float delta = nf - f[r];
+        if (lane == r) { myres = g; mydelta = delta; }
         g += AR[r] * delta;
         f[r] = nf;
-        improvement -= delta * res + 0.5f * delta * delta * bA[r];
       }
     });
+    const float improvement = gsum<16>(-mydelta * (myres + halfA * mydelta));
     nit = it + 1;
     if (improvement * m.pgs_scale < m.tolerance) break;
   }
