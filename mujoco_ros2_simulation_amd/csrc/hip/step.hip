@@ -2074,24 +2074,31 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   }
   const float halfA = 0.5f * myA;
   int nit = 0;  // sweeps done (mjData.solver_niter)
-  #pragma unroll 1
-  for (int it = 0; it < m.iterations; ++it) {
-    float myres = 0, mydelta = 0;
-    unroll<KR>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if (r < rmax) {
+  // the sweep is unrolled to the wave's row count rounded up to 4 (rows past rmax are the zero rows,
+  // which never move): no per-row bound tests inside the sweep
+  auto sweeps = [&](auto nc) {
+    constexpr int N = decltype(nc)::value;
+    #pragma unroll 1
+    for (int it = 0; it < m.iterations; ++it) {
+      float myres = 0, mydelta = 0;
+      unroll<N>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
         const float res = rowb<r>(g);
         const float nf = __builtin_amdgcn_fmed3f(f[r] - res * iA[r], flo[r], fhi[r]);
         const float delta = nf - f[r];
         if (lane == r) { myres = g; mydelta = delta; }
         g += AR[r] * delta;
         f[r] = nf;
-      }
-    });
-    const float improvement = gsum<16>(-mydelta * (myres + halfA * mydelta));
-    nit = it + 1;
-    if (improvement * m.pgs_scale < m.tolerance) break;
-  }
+      });
+      const float improvement = gsum<16>(-mydelta * (myres + halfA * mydelta));
+      nit = it + 1;
+      if (improvement * m.pgs_scale < m.tolerance) break;
+    }
+  };
+  if (KR <= 4 || rmax <= 4) sweeps(std::integral_constant<int, (KR < 4 ? KR : 4)>{});
+  else if (KR <= 8 || rmax <= 8) sweeps(std::integral_constant<int, (KR < 8 ? KR : 8)>{});
+  else if (KR <= 12 || rmax <= 12) sweeps(std::integral_constant<int, (KR < 12 ? KR : 12)>{});
+  else sweeps(std::integral_constant<int, KR>{});
   float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
