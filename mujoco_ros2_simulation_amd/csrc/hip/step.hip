@@ -2073,6 +2073,11 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     g = (ga + gb) + (gc + gd);
   }
   const float halfA = 0.5f * myA;
+  float niA[KR], lof[KR], hif[KR];
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    niA[r] = -iA[r]; lof[r] = flo[r] - f[r]; hif[r] = fhi[r] - f[r];
+  });
   int nit = 0;  // sweeps done (mjData.solver_niter)
   // the sweep is unrolled to the wave's row count rounded up to 4 (rows past rmax are the zero rows,
   // which never move): no per-row bound tests inside the sweep
@@ -2083,12 +2088,13 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       float myres = 0, mydelta = 0;
       unroll<N>([&](auto rc) {
         constexpr int r = decltype(rc)::value;
-        const float res = rowb<r>(g);
-        const float nf = __builtin_amdgcn_fmed3f(f[r] - res * iA[r], flo[r], fhi[r]);
-        const float delta = nf - f[r];
+        // the step itself is clamped: delta = med3(-res / A, lo - f, hi - f), with lo - f and hi - f
+        // carried instead of f (one op fewer per row than clamping f and differencing)
+        const float delta = __builtin_amdgcn_fmed3f(rowb<r>(g) * niA[r], lof[r], hif[r]);
         if (lane == r) { myres = g; mydelta = delta; }
         g += AR[r] * delta;
-        f[r] = nf;
+        lof[r] -= delta;
+        hif[r] -= delta;
       });
       const float improvement = gsum<16>(-mydelta * (myres + halfA * mydelta));
       nit = it + 1;
@@ -2099,6 +2105,10 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   else if (KR <= 8 || rmax <= 8) sweeps(std::integral_constant<int, (KR < 8 ? KR : 8)>{});
   else if (KR <= 12 || rmax <= 12) sweeps(std::integral_constant<int, (KR < 12 ? KR : 12)>{});
   else sweeps(std::integral_constant<int, KR>{});
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    f[r] = flo[r] - lof[r];
+  });
   float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
