@@ -4228,7 +4228,9 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
 #ifdef MRS_RAY_BATCH
   passes(std::integral_constant<int, MRS_RAY_BATCH>{});
 #else
+  // (a lidar of at most 2 G rays takes 2 per lane: one pass with no idle ray slots; C4's 32 beams)
   if (G < 64 && m.nrf > G * RayBatch<G>::value) passes(std::integral_constant<int, 2 * RayBatch<G>::value>{});
+  else if (G < 64 && RayBatch<G>::value > 2 && m.nrf <= 2 * G) passes(std::integral_constant<int, 2>{});
   else passes(std::integral_constant<int, RayBatch<G>::value>{});
 #endif
   if (!MRS_SD_OK(sensordata)) return;
