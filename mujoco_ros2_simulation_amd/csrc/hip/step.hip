@@ -1959,6 +1959,9 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
                                              int lane, int mydof = -1) {
   const LdsLayout& L = m.L;
   const int nv = m.nv;
+  // instantiated per row count KR (the wave's rmax rounded up to 4 at the call site): rows past the
+  // wave's own are zero rows, so every row loop runs to the compile-time KR without bound tests
+  rmax = KR;
   // J and M^-1 J' columns per row in registers; row scalars (R, aref, b, bound, diagonal of A, force)
   // stay in the row's own lane and reach the other lanes by DPP row broadcasts when used
   float Jt[KR], MJt[KR];
@@ -3754,7 +3757,11 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     for (int bit = 16; bit >= 1; bit >>= 1)
       if (__ballot(mine >= rmax + bit) != 0) rmax += bit;
     if (small) {
-      const float qa = pgs_small16(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      float qa;
+      if (rmax <= 4) qa = pgs_small16<false, 4>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      else if (rmax <= 8) qa = pgs_small16<false, 8>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      else if (rmax <= 12) qa = pgs_small16<false, 12>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      else qa = pgs_small16<false, 16>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
       wsync();
       SUB_ADD(PH_CON_PGS, t_sub);
       return qa;
