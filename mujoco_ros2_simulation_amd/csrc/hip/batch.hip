@@ -631,8 +631,11 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
         const int g1 = std::min(ga, gb), g2 = std::max(ga, gb);
         int ta = m.geom_type[ga], tb = m.geom_type[gb];
         // every pair of the implemented types: dedicated primitives, plane-ellipsoid/cylinder/mesh,
-        // and MPR for the rest (step.hip narrowphase); plane-plane never collides, hfields are absent
-        bool ok = ta != MRS_GEOM_HFIELD && tb != MRS_GEOM_HFIELD && tb != MRS_GEOM_PLANE;
+        // and MPR for the rest (step.hip narrowphase); plane-plane pairs (a plane on a moving body
+        // against another plane) are skipped, as mj_collision has no plane-plane collider; hfields
+        // are absent
+        if (ta == MRS_GEOM_PLANE && tb == MRS_GEOM_PLANE) continue;
+        bool ok = ta != MRS_GEOM_HFIELD && tb != MRS_GEOM_HFIELD;
         if (!ok)
           throw UnsupportedError("collision pair of geom types " + std::to_string(ta) + "/" + std::to_string(tb) +
                                  " is not implemented (geoms " + std::to_string(g1) + "," + std::to_string(g2) + ")");
@@ -1523,9 +1526,8 @@ void batch_render_wait(BatchImpl* b) {
   if (b->rend_pending) HIP_CHECK(hipStreamWaitEvent(b->stream, b->rend_ev, 0));
 }
 
-// mjData.contact of the last forward pass of one env (geom1/geom2 as mj_collision orders them: pair
-// order g1 < g2 with the lower geom type first, then the narrow phase's order).  Records are read from
-// the env's contact scratch (step.hip collision(): pair id, dist, pos, frame).  Returns ncon.
+// mjData.efc_* of the last forward pass of one env (type, dense J rows, R, aref, force).  Returns
+// nefc: 0 when no row was built (constraints disabled, or none active).
 int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force) {
   if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
   if (max < 0) throw std::invalid_argument("negative capacity");
@@ -1559,6 +1561,9 @@ int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* 
   return nefc;
 }
 
+// mjData.contact of the last forward pass of one env (geom1/geom2 as mj_collision orders them: pair
+// order g1 < g2 with the lower geom type first, then the narrow phase's order).  Records are read from
+// the env's contact scratch (step.hip collision(): pair id, dist, pos, frame).  Returns ncon.
 int batch_get_contacts(BatchImpl* b, int env, int max, int* geom, double* dist, double* pos, double* frame) {
   if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
   if (max < 0) throw std::invalid_argument("negative capacity");

@@ -1953,7 +1953,8 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
 // are zero rows with R = 1, which never move.
 // kUnit: every row's Jacobian is the unit vector of the dof held in lane r's `mydof` (dof friction
 // loss rows), built in registers instead of read from the global rows J
-template <bool kUnit = false, int KR = 16>
+// KV: the dof loops' unroll bound (>= nv; the call site picks 8 or 16), separate from the row count
+template <bool kUnit = false, int KR = 16, int KV = 16>
 __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
                                              float myR, float myaref, float myb, float myfl, float qacc_s,
                                              int lane, int mydof = -1) {
@@ -1975,7 +1976,7 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     MJt[r] = Jt[r];
   });
   // M^-1 J' for all rows at once: forward then backward substitution with L (Cholesky of M, LDS)
-  unroll<KR>([&](auto ic) {
+  unroll<KV>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     if (i < nv) {
       const float inv = 1.0f / s[L.L + i * nv + i];
@@ -1989,8 +1990,8 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       });
     }
   });
-  unroll<KR>([&](auto ic) {
-    constexpr int i = KR - 1 - decltype(ic)::value;
+  unroll<KV>([&](auto ic) {
+    constexpr int i = KV - 1 - decltype(ic)::value;
     if (i < nv) {
       const float inv = 1.0f / s[L.L + i * nv + i];
       const float lij = lane < i ? s[L.L + i * nv + lane] : 0.0f;
@@ -3757,11 +3758,16 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     for (int bit = 16; bit >= 1; bit >>= 1)
       if (__ballot(mine >= rmax + bit) != 0) rmax += bit;
     if (small) {
-      float qa;
-      if (rmax <= 4) qa = pgs_small16<false, 4>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
-      else if (rmax <= 8) qa = pgs_small16<false, 8>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
-      else if (rmax <= 12) qa = pgs_small16<false, 12>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
-      else qa = pgs_small16<false, 16>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      // rows unrolled to the wave's row count, the substitutions to the model's dof count (nv can
+      // exceed the row count: a free body with one contact, an arm with one active limit)
+      auto solve = [&](auto kv) {
+        constexpr int KV = decltype(kv)::value;
+        if (rmax <= 4) return pgs_small16<false, 4, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        if (rmax <= 8) return pgs_small16<false, 8, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        if (rmax <= 12) return pgs_small16<false, 12, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        return pgs_small16<false, 16, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+      };
+      float qa = nv <= 8 ? solve(std::integral_constant<int, 8>{}) : solve(std::integral_constant<int, 16>{});
       wsync();
       SUB_ADD(PH_CON_PGS, t_sub);
       return qa;
@@ -4390,7 +4396,10 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   if (!(m.diag_skip & 2)) MRS_CALL(G, ncon = collision<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COLL);
   float qacc = qacc_s;
-  if (lane == 0) s[L.niter] = __int_as_float(0);
+  if (lane == 0) {
+    s[L.niter] = __int_as_float(0);
+    scr[S.efc_n] = __int_as_float(0);  // no rows unless constraints() builds some (mrs_batch_get_efc)
+  }
   if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = constraints<G>(ENV_ARGS, ncon, qacc_s));
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;

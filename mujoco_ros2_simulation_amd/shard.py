@@ -15,11 +15,13 @@ def env_ids(rank: int, envs_per_rank: int) -> np.ndarray:
     return rank * envs_per_rank + np.arange(envs_per_rank)
 
 
-def spawn(nprocs: int, argv: list[str]) -> int:
+def spawn(nprocs: int, argv: list[str], grace: float = 10.0, poll: float = 0.1) -> int:
     """Start `nprocs` ranks of `argv` (a Python command line) as child processes with the torchrun
     environment (RANK, LOCAL_RANK = GPU index, WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free port) and
-    wait for them; returns the first non-zero exit code (0 if all succeed).  The caller must not have
-    touched the GPU: each child owns one device."""
+    wait for them; returns the first non-zero exit code (0 if all succeed).  A rank that fails ends the
+    job: its siblings (blocked in the rendezvous or a collective until the backend's timeout otherwise)
+    are terminated, then killed after `grace` seconds.  The caller must not have touched the GPU: each
+    child owns one device."""
     import socket
     import subprocess
     import sys
@@ -31,9 +33,28 @@ def spawn(nprocs: int, argv: list[str]) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
                    LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    import time
+    first_bad = 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            first_bad = bad[0]
+            break
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(poll)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.monotonic() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.0, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return first_bad
 
 
 def init(backend: str | None = None):

@@ -277,6 +277,8 @@ class Batch:
         return out
 
     def set(self, field: int, values, env0: int = 0) -> None:
+        if self._dim(field) == 0:  # e.g. ctrl of a model without actuators
+            return
         a = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self._dim(field))
         _check(lib().mrs_batch_set_field(self._h, field, a.ctypes.data, env0, a.shape[0]))
 

@@ -198,3 +198,55 @@ def test_reseeded_step_parity(scene, solver, n, steps, vtol):
     assert ncon.max() > 0
     assert flips <= 0.01 * n * steps
     assert wq <= RTOL and wv <= vtol
+
+
+FREE_SPHERE = """<mujoco>
+  <option solver="PGS" iterations="50"/>
+  <worldbody>
+    <geom type="plane" size="5 5 0.1"/>
+    <body pos="0 0 0.1">
+      <freejoint/>
+      <geom type="sphere" size="0.1" condim="{condim}"/>
+    </body>
+  </worldbody>
+</mujoco>"""
+
+ARM_LIMIT = """<mujoco>
+  <option solver="PGS" iterations="50"/>
+  <worldbody>
+    <body>
+      <joint type="hinge" axis="0 1 0" range="-0.05 0.05" limited="true"/>
+      <geom type="capsule" fromto="0 0 0 0.5 0 0" size="0.04"/>
+      <body pos="0.5 0 0">
+        <joint type="hinge" axis="0 1 0"/>
+        <geom type="capsule" fromto="0 0 0 0.5 0 0" size="0.04"/>
+        <body pos="0.5 0 0">
+          <joint type="hinge" axis="0 0 1"/>
+          <geom type="capsule" fromto="0 0 0 0.3 0 0" size="0.03"/>
+          <body pos="0.3 0 0">
+            <joint type="hinge" axis="0 1 0"/>
+            <geom type="sphere" size="0.05"/>
+          </body>
+        </body>
+      </body>
+    </body>
+  </worldbody>
+</mujoco>"""
+
+
+@pytest.mark.parametrize("xml, min_rows", [(FREE_SPHERE.format(condim=3), 4), (FREE_SPHERE.format(condim=1), 1),
+                                           (ARM_LIMIT, 1)], ids=["free-sphere-pyramid", "free-sphere-frictionless",
+                                                                 "arm-one-limit"])
+def test_g16_dense_pgs_more_dofs_than_rows(xml, min_rows, monkeypatch):
+    """G = 16 register PGS (step.hip pgs_small16) when nv exceeds the row count: a free sphere on a
+    plane (nv = 6, one contact: 4 pyramid rows or 1 frictionless row) and a 4-dof arm hanging against
+    one joint limit (1 row).  The substitutions forming M^-1 J' must run over every dof, not only the
+    first `rows` of them.  100 steps, qpos/qvel within 1e-5 of scale of the oracle"""
+    monkeypatch.setenv("MRS_GROUP", "16")
+    model = sim.Model.from_string(xml, str(SCENES))
+    assert model.nv > min_rows
+    q, v, qr, vr, layout, iters = _rollout_both(model, 8, 100)
+    assert layout["group"] == 16
+    eq, ev = _rel(q, qr), _rel(v, vr)
+    print(f"nv={model.nv}: qpos {eq:.2e} qvel {ev:.2e}")
+    assert eq <= RTOL and ev <= RTOL

@@ -140,3 +140,17 @@ def test_bench_rejects_mismatched_world():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode != 0 and "does not match WORLD_SIZE=3" in r.stderr
+
+
+def test_spawn_fails_fast():
+    """a rank that dies ends the job: shard.spawn returns its exit code and terminates the siblings
+    instead of waiting for them (they would sit in the rendezvous until the backend timeout)"""
+    import time
+    from mujoco_ros2_simulation_amd import shard
+    code = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(3)\n"
+            "time.sleep(300)\n")
+    t0 = time.monotonic()
+    rc = shard.spawn(3, ["-c", code], grace=5.0)
+    assert rc == 3
+    assert time.monotonic() - t0 < 60
