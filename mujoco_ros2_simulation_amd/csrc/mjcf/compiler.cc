@@ -43,6 +43,8 @@ constexpr double kMinVal = 1e-15;
   std::string where = e ? (" (line " + std::to_string(e->line) + ", <" + e->tag + ">)") : "";
   throw std::runtime_error("MJCF error: " + msg + where);
 }
+// a valid MJCF construct this compiler does not restate: rejected at load instead of ignored
+[[noreturn]] void unsupported(const XmlElement* e, const std::string& msg) { fail(e, "not supported: " + msg); }
 
 // ---------------------------------------------------------------- fp64 3D math
 struct V3 { double v[3]; };
@@ -188,6 +190,9 @@ struct Options {
   bool autolimits = true;
   int inertiafromgeom = 2;  // 0 false, 1 true, 2 auto
   std::string meshdir;      // <compiler meshdir / assetdir>
+  int inertiagroup[2] = {0, 5};  // inertiagrouprange: geom groups that contribute to inertia
+  double boundmass = 0, boundinertia = 0, settotalmass = -1;
+  bool balanceinertia = false, strippath = false;
 };
 
 // a rigid frame: child = frame ∘ local
@@ -416,6 +421,48 @@ struct Compiler {
       opt.inertiafromgeom = (*a == "true") ? 1 : (*a == "false") ? 0 : 2;
     if (auto* a = e->attr("assetdir")) opt.meshdir = *a;
     if (auto* a = e->attr("meshdir")) opt.meshdir = *a;
+    auto boolean = [&](const char* name, bool& out) {
+      if (auto* a = e->attr(name)) {
+        if (*a == "true") out = true;
+        else if (*a == "false") out = false;
+        else fail(e, std::string(name) + " must be true or false");
+      }
+    };
+    auto real = [&](const char* name, double& out) {
+      if (auto* a = e->attr(name)) out = parse_reals(*a, e, name).at(0);
+    };
+    // mass / inertia post-processing of mjCBody::Compile and mjCModel (settotalmass)
+    real("boundmass", opt.boundmass);
+    real("boundinertia", opt.boundinertia);
+    real("settotalmass", opt.settotalmass);
+    boolean("balanceinertia", opt.balanceinertia);
+    boolean("strippath", opt.strippath);
+    if (auto* a = e->attr("inertiagrouprange")) {
+      auto v = parse_reals(*a, e, "inertiagrouprange");
+      if (v.size() != 2) fail(e, "inertiagrouprange needs 2 values");
+      opt.inertiagroup[0] = static_cast<int>(v[0]);
+      opt.inertiagroup[1] = static_cast<int>(v[1]);
+    }
+    // accepted with no effect here: options of the viewer, the asset loader and the compiler's
+    // threading / saving, which do not change the compiled dynamics, rays or depth
+    bool unused = false;
+    boolean("usethread", unused);
+    boolean("saveinertial", unused);
+    if (e->attr("texturedir")) {}
+    // options that would change the model and are not restated: rejected rather than ignored
+    for (const char* name : {"discardvisual", "fusestatic", "fitaabb", "alignfree"}) {
+      bool on = false;
+      boolean(name, on);
+      if (on) unsupported(e, std::string("<compiler ") + name + "=\"true\"> is not supported");
+    }
+    if (auto* a = e->attr("coordinate"))
+      if (*a != "local") unsupported(e, "<compiler coordinate=\"" + *a + "\"> is not supported");
+    static const std::set<std::string> known = {
+        "angle", "eulerseq", "autolimits", "inertiafromgeom", "assetdir", "meshdir", "texturedir", "boundmass",
+        "boundinertia", "settotalmass", "balanceinertia", "strippath", "inertiagrouprange", "usethread",
+        "saveinertial", "discardvisual", "fusestatic", "fitaabb", "alignfree", "coordinate"};
+    for (auto& kv : e->attrs)
+      if (!known.count(kv.first)) unsupported(e, "unknown <compiler> attribute '" + kv.first + "'");
   }
 
   // ---- <asset>: meshes and materials.  A mesh is processed as MuJoCo's compiler does: faces from the
@@ -442,6 +489,10 @@ struct Compiler {
       std::string file;
       const bool has_file = get_str(e, nullptr, "mesh", "file", file);
       if (has_file) {
+        if (opt.strippath) {  // <compiler strippath>: keep the file name only
+          const size_t k = file.find_last_of("/\\");
+          if (k != std::string::npos) file = file.substr(k + 1);
+        }
         std::string path = file;
         if (!path.empty() && path[0] != '/') {
           std::string dir = opt.meshdir;
@@ -1238,12 +1289,38 @@ struct Compiler {
       } else if (from_geom) {
         geom_inertia(B, mass, ipos, iquat, inertia);
       }
+      if (b != 0) {
+        // mjCBody::Compile: lower bounds, then the triangle inequality of the principal inertia
+        // (balanceinertia replaces a violating triple by its mean, otherwise the model is rejected)
+        mass = std::max(mass, opt.boundmass);
+        for (double& v : inertia) v = std::max(v, opt.boundinertia);
+        const double tol = 1e-12 * (inertia[0] + inertia[1] + inertia[2]);
+        if (inertia[0] + inertia[1] < inertia[2] - tol || inertia[0] + inertia[2] < inertia[1] - tol ||
+            inertia[1] + inertia[2] < inertia[0] - tol) {
+          if (!opt.balanceinertia)
+            fail(nullptr, "inertia of body '" + B.name + "' must satisfy A + B >= C; use 'balanceinertia' to fix");
+          const double mean = (inertia[0] + inertia[1] + inertia[2]) / 3;
+          inertia[0] = inertia[1] = inertia[2] = mean;
+        }
+      }
       m.body_mass.push_back(mass);
       m.body_ipos.insert(m.body_ipos.end(), ipos, ipos + 3);
       m.body_iquat.insert(m.body_iquat.end(), iquat, iquat + 4);
       m.body_inertia.insert(m.body_inertia.end(), inertia, inertia + 3);
       if (b != 0 && m.body_weldid[b] == b && mass < 1e-10)
         fail(nullptr, "moving body '" + B.name + "' has zero mass");
+    }
+    if (opt.settotalmass > 0) {
+      // scale every body's mass and inertia so that the model's total mass is settotalmass
+      double total = 0;
+      for (int b = 1; b < m.nbody; ++b) total += m.body_mass[b];
+      if (total > kMinVal) {
+        const double sc = opt.settotalmass / total;
+        for (int b = 1; b < m.nbody; ++b) {
+          m.body_mass[b] *= sc;
+          for (int i = 0; i < 3; ++i) m.body_inertia[3 * b + i] *= sc;
+        }
+      }
     }
     m.body_subtreemass = m.body_mass;
     for (int b = m.nbody - 1; b > 0; --b) m.body_subtreemass[m.body_parentid[b]] += m.body_subtreemass[b];
@@ -1318,9 +1395,11 @@ struct Compiler {
     mass = 0;
     double com[3] = {0, 0, 0};
     std::vector<double> gm;
+    auto counts = [&](const GeomRec& g) { return g.group >= opt.inertiagroup[0] && g.group <= opt.inertiagroup[1]; };
     for (auto& g : B.geoms) {
       double I[3], mg;
       geom_mass_inertia(g, mg, I);
+      if (!counts(g)) mg = 0;  // inertiagrouprange: geoms of other groups carry no mass
       gm.push_back(mg);
       mass += mg;
       for (int i = 0; i < 3; ++i) com[i] += mg * g.pos[i];
@@ -1330,6 +1409,7 @@ struct Compiler {
     double T[9] = {0};
     for (size_t k = 0; k < B.geoms.size(); ++k) {
       const GeomRec& g = B.geoms[k];
+      if (!counts(g)) continue;
       double I[3], mg, R[9];
       geom_mass_inertia(g, mg, I);
       quat2mat(R, g.quat);

@@ -42,7 +42,9 @@ std::optional<LidarData> get_lidar_data(const hardware_interface::HardwareInfo& 
   d.laserscan_topic = p("laserscan_topic").value_or("/scan");
   d.range_min = p("range_min") ? std::stod(*p("range_min")) : 0.0;
   d.range_max = p("range_max") ? std::stod(*p("range_max")) : 1000.0;
-  d.sensor_indexes.assign(std::max(0, d.num_rangefinders), -1);
+  // scan indices no rangefinder maps to keep address 0 and so publish sensordata[0], as the
+  // reference's value-initialised resize does (reference :98, read at :261-263)
+  d.sensor_indexes.assign(std::max(0, d.num_rangefinders), 0);
 
   auto& msg = d.laser_scan_msg;
   msg.header.frame_id = d.frame_name;
@@ -130,7 +132,7 @@ void MujocoLidar::update() {
     auto& ranges = lidar.laser_scan_msg.ranges;
     for (size_t k = 0; k < lidar.sensor_indexes.size(); ++k) {
       const int adr = lidar.sensor_indexes[k];
-      const double r = adr >= 0 ? snapshot_[adr] : -1.0;
+      const double r = adr >= 0 && adr < static_cast<int>(snapshot_.size()) ? snapshot_[adr] : -1.0;
       // out-of-range readings (including MuJoCo's -1 "no hit") become -1 (reference :265-269)
       ranges[k] = static_cast<float>((r < lidar.range_min || r > lidar.range_max) ? -1.0 : r);
     }

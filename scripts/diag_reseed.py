@@ -14,8 +14,9 @@ from mujoco_ros2_simulation_amd import sim, synth  # noqa: E402
 scene, solver, n, steps = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 path = ROOT / "scenes" / f"{scene}.xml"
 it = 50 if solver == "PGS" else 100
-m = sim.Model.from_string(path.read_text().replace('solver="PGS" iterations="50"', f'solver="{solver}" iterations="{it}"'),
-                          str(path.parent))
+tol = sys.argv[5] if len(sys.argv) > 5 else None  # optional <option tolerance> override
+opt = f'solver="{solver}" iterations="{it}"' + (f' tolerance="{tol}"' if tol is not None else "")
+m = sim.Model.from_string(path.read_text().replace('solver="PGS" iterations="50"', opt), str(path.parent))
 envs = np.arange(n)
 q0 = synth.initial_qpos(m, envs)
 tab = synth.ctrl_table(m, envs, steps // 10 + 1, 10)

@@ -135,3 +135,63 @@ def test_errors(xml, msg):
 def test_missing_file():
     with pytest.raises(sim.MrsError):
         sim.Model.load("/nonexistent/model.xml")
+
+
+def _body_model(compiler: str, inertial: str = '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.1 0.5"/>',
+                extra: str = ""):
+    xml = f"""<mujoco><compiler {compiler}/>
+      <worldbody><body name="b"><freejoint/>{inertial}</body>{extra}</worldbody></mujoco>"""
+    return sim.Model.from_string(xml, ".")
+
+
+def test_compiler_balanceinertia():
+    """the converter's intermediate URDF sets <compiler balanceinertia="true">
+    (scripts/make_mjcf_from_robot_description.py:60): a principal inertia violating A + B >= C is
+    replaced by its mean; without the flag the model is rejected (mjCBody::Compile)"""
+    m = _body_model('balanceinertia="true"')
+    np.testing.assert_allclose(m.body_inertia[1], [0.7 / 3] * 3, rtol=1e-12)
+    with pytest.raises(sim.MrsError, match="A \\+ B >= C"):
+        _body_model("")
+    ok = _body_model('balanceinertia="true"', '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.2 0.25"/>')
+    np.testing.assert_allclose(ok.body_inertia[1], [0.1, 0.2, 0.25])
+
+
+def test_compiler_mass_bounds_and_total():
+    """boundmass / boundinertia are lower bounds per body; settotalmass scales every body's mass and
+    inertia so the total is the given value"""
+    m = _body_model('boundmass="3" boundinertia="0.3"', '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.2 0.25"/>')
+    assert m.body_mass[1] == 3
+    np.testing.assert_allclose(m.body_inertia[1], [0.3, 0.3, 0.3])
+    extra = '<body name="c" pos="1 0 0"><freejoint/><inertial pos="0 0 0" mass="6" diaginertia="1 1 1"/></body>'
+    m = _body_model('settotalmass="4"', '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.2 0.25"/>', extra)
+    np.testing.assert_allclose(m.body_mass[1:], [1.0, 3.0], rtol=1e-12)
+    np.testing.assert_allclose(m.body_inertia[1], [0.05, 0.1, 0.125], rtol=1e-12)
+    np.testing.assert_allclose(m.body_inertia[2], [0.5, 0.5, 0.5], rtol=1e-12)
+
+
+def test_compiler_inertiagrouprange():
+    """geoms outside inertiagrouprange carry no mass when inertia comes from geoms"""
+    geoms = ('<geom type="sphere" size="0.1" mass="1"/>'
+             '<geom type="sphere" size="0.1" pos="1 0 0" mass="3" group="4"/>')
+    m = _body_model("", geoms)
+    assert m.body_mass[1] == pytest.approx(4)
+    m = _body_model('inertiagrouprange="0 3"', geoms)
+    assert m.body_mass[1] == pytest.approx(1)
+    np.testing.assert_allclose(m.body_ipos[1], [0, 0, 0], atol=1e-12)
+
+
+@pytest.mark.parametrize("attr", ['discardvisual="true"', 'fusestatic="true"', 'fitaabb="true"',
+                                  'alignfree="true"', 'coordinate="global"', 'bogus="1"'])
+def test_compiler_rejects_unrestated_options(attr):
+    """<compiler> options that would change the compiled model and are not restated are rejected at
+    load instead of silently ignored"""
+    with pytest.raises(sim.MrsError, match="not supported"):
+        _body_model(attr, '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.2 0.25"/>')
+
+
+def test_compiler_accepts_converter_options():
+    """the converter's <compiler> line (assetdir, balanceinertia, discardvisual="false",
+    strippath="false") loads"""
+    m = _body_model('assetdir="assets" balanceinertia="true" discardvisual="false" strippath="false" angle="radian"',
+                    '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.2 0.25"/>')
+    assert m.nbody == 2
