@@ -48,9 +48,12 @@ def parse():
     p.add_argument("--scene", default=None, help="override the config's scene")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
-    p.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c3",
-                   help="c3: the BASELINE metric (default); c2: reference 2-DoF scene, 4096 envs, sensors off; "
+    p.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c3",
+                   help="c3: the BASELINE metric (default); c1: the reference scene, 1 env, through the plugin host "
+                        "(MujocoSystemInterface, headless), paced and unpaced; "
+                        "c2: reference 2-DoF scene, 4096 envs, sensors off; "
                         "c4: mobile base + lidar + 640x480 depth camera; c5: contact-rich arm + 8 free boxes")
+    p.add_argument("--c1-seconds", type=float, default=3.0, help="C1: wall seconds of the paced measurement")
     p.add_argument("--render-every", type=int, default=100, help="C4: physics steps between depth frames")
     p.add_argument("--render-sync", action="store_true",
                    help="C4: render each frame on the batch stream between steps instead of the camera "
@@ -134,6 +137,110 @@ def ref_scene_xml(sensors: bool) -> tuple[str, str]:
     return xml, str(REF_SCENE.parent)
 
 
+# ------------------------------------------------------------------------------------------------ C1
+def run_c1(args):
+    """BASELINE.json configs[0]: the reference's own scene, 1 env, driven through
+    the plugin host exactly as the controller manager drives MujocoSystemInterface (headless=true,
+    test/test_resources/test_robot.urdf with its <ros2_control> block; libmrs_plugin.so over the GPU
+    batch, no CPU path).  Two rates:
+    * paced: the physics thread (PhysicsLoop, reference src/mujoco_system_interface.cpp:1629-1780)
+      with the URDF's sim_speed_factor 3.0 while a 50 Hz controller loop calls write()/read() -- sim
+      steps per wall second, 1500 by construction of the pacing;
+    * unpaced (the reported value): physics_thread=false, controller cycles back to back, each one
+      write() + 10 physics steps (one fused launch) + read() -- the plumbing ceiling of one env."""
+    import tempfile
+    from mujoco_ros2_simulation_amd import plugin, sim
+    gold = ROOT / "tests" / "golden"
+    share = Path(tempfile.mkdtemp(prefix="mrs_c1_")) / "mujoco_ros2_control"
+    share.mkdir()
+    os.symlink(gold / "ref_scenes", share / "test_resources")
+    os.symlink(gold / "ref_config", share / "config")
+    urdf = gold / "ref_config" / "test_robot.urdf"
+
+    def system(**params):
+        s = plugin.System(urdf, {"use_pid": "false", "headless": "true"}, {"mujoco_ros2_control": str(share)})
+        for k, v in params.items():
+            s.set_param(k, v)
+        if s.on_init() != plugin.SUCCESS:
+            raise RuntimeError("on_init failed")
+        s.on_activate()
+        s.set_command("joint1/position", 0.5)
+        s.set_command("joint2/position", -0.5)
+        return s
+
+    ctrl_period = 1.0 / 50  # test/config/controllers.yaml:3
+    # paced: the physics thread against the wall clock
+    s = system()
+    h = s.get_model()["timestep"]
+    speed = float(s.param("sim_speed_factor"))
+    end = time.monotonic() + 0.5
+    while time.monotonic() < end:
+        s.write(ctrl_period); time.sleep(ctrl_period); s.read()
+    t0w, t0s = time.monotonic(), s.sim_time
+    end = t0w + args.c1_seconds
+    while time.monotonic() < end:
+        s.write(ctrl_period); time.sleep(ctrl_period); s.read()
+    paced = (s.sim_time - t0s) / h / (time.monotonic() - t0w)
+    s.close()
+    # unpaced: synchronous controller cycles
+    s = system(physics_thread="false")
+    bh = s.batch_handle()
+    for _ in range(args.warmup):
+        s.cycle(ctrl_period, args.period)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s.cycle(ctrl_period, args.period)
+        kms.append(sim.lib().mrs_batch_last_kernel_ms(bh, 0))
+    elapsed = time.perf_counter() - t0
+    q = np.array([s.state("joint1/position"), s.state("joint2/position")])
+    assert np.all(np.isfinite(q))
+    # single physics steps, one per call (each a launch + synchronous state copy)
+    n1 = max(50, args.steps)
+    t1 = time.perf_counter()
+    for _ in range(n1):
+        s.step(1)
+    single = n1 / (time.perf_counter() - t1)
+    s.close()
+    value = args.steps * args.period / elapsed
+    kernel_ms = float(np.mean(kms))
+    result = {
+        "metric": "env-steps/sec, reference scene, 1 env through MujocoSystemInterface headless (C1)",
+        "value": value, "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "the reference's test robot (test/test_resources/test_robot.urdf + scene.xml), commands [0.5, -0.5]",
+        "config": {"workload": "C1: resources/scene.xml (2-DoF test robot), 1 env, plugin host, headless",
+                   "envs_per_gpu": 1, "physics_steps_per_bench_step": args.period, "timestep": h,
+                   "bench_step": "one controller cycle: write() + 10 physics steps (one launch) + read()",
+                   "parallelism": "none (1 env)"},
+        "paced_steps_per_s": paced, "paced_expected": speed / h, "sim_speed_factor": speed,
+        "unpaced_single_step_per_s": single,
+        "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None,
+                     "traffic": None, "kernel": "step_kernel<16, false> (10-step launch of 1 env)",
+                     "kernel_ms": kernel_ms,
+                     "note": "one env occupies one 16-lane group of one wave: a launch- and copy-latency "
+                             "measurement, not a roofline one; host overhead per cycle = ms_per_step - kernel_ms"},
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import binding
+        cores, visible, quota, cpu_model = host_cores()
+        m = sim.Model.load(gold / "ref_scenes" / "scene.xml")
+        d = binding.OracleData(m)
+        d.ctrl[:] = [0.5, -0.5]
+        steps, t2 = 0, time.perf_counter()
+        while time.perf_counter() - t2 < min(args.cpu_seconds, 5.0):
+            d.step(1000)
+            steps += 1000
+        secs = time.perf_counter() - t2
+        result["cpu_baseline"] = {"value": steps / secs, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                                  "cpu_model": cpu_model,
+                                  "sample": f"1 env x {steps} mj_step of the same scene, fp64 CPU restatement "
+                                            f"(oracle/oracle.c, not upstream MuJoCo), 1 thread, {secs:.1f} s"}
+    print(json.dumps(result), flush=True)
+
+
 # ------------------------------------------------------------------------------------------------ run
 def main():
     args = parse()
@@ -144,6 +251,10 @@ def main():
         sys.exit(shard.spawn(args.gpus, [str(Path(__file__).resolve())] + sys.argv[1:]))
     if world_env and world_env != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE={world_env}")
+    if args.config == "c1":
+        if args.gpus != 1:
+            sys.exit("bench.py: --config c1 is the single-env plumbing case (1 GPU)")
+        return run_c1(args)
 
     import torch
     import torch.distributed as dist
@@ -297,6 +408,16 @@ def main():
                 "flops_per_env_step_structural": detailed_flops,
                 "algorithmic_bytes_per_env_step": roofline.bytes_per_env_step(model, args.period),
                 "note": "fp32 vector-ALU bound path (no GEMM-shaped work at these sizes); peak = fp32 VALU rate"}
+    fl_rec, fl_src = committed("flops", cfg, n, args.period)
+    if not render:
+        roof["frac_model"] = roof["frac"]
+        if fl_rec:
+            # executed fp32 VALU work of the same kernel (rocprofv3 SQ_INSTS_VALU_*_F32 /
+            # SQ_INSTS_VALU_FLOPS_FP32 of this bench command, scripts/flops_summary.py), timed here
+            fe = fl_rec["flops_executed_per_env_step"]
+            roof["flops_executed_per_env_step"] = fe
+            roof["frac_executed"] = n * args.period * fe / (step_ms * 1e-3) / 1e12 / roofline.PEAK_FP32_TFLOPS
+            roof["flops_executed_source"] = fl_src
     if sq_rec:
         # measured from SQ counters of the same command (rocprofv3 --pmc, scripts/sq_summary.py)
         roof["valu_measured"] = {k: sq_rec[k] for k in ("valu_issue_frac", "valu_tflops_upper", "valu_frac_upper",

@@ -21,6 +21,7 @@ for c in $CFGS; do
   ps=5; [ $c = c4 ] && ps=200
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$c -o run -- python3 bench.py --config $c --steps $ps --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch_$c.log 2>&1 || exit $?
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$c -o run -- python3 bench.py --config $c --steps $ps --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write_$c.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_flops_$c -o run -- python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_flops_$c.log 2>&1 || exit $?
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq_$c -o run -- python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_sq_$c.log 2>&1 || exit $?
 done
 tail -3 gpurun_out/pytest_gpu.log

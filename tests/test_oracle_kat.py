@@ -35,7 +35,7 @@ def test_mass_matrix_closed_form(s2_model, q2):
 
 SERVO = """<mujoco><compiler angle="radian"/><option timestep="0.002" integrator="{integ}" gravity="0 0 -9.81"/>
 <worldbody><body><joint name="j" axis="0 0 1" damping="{b}"/>
-<inertial pos="0 0 0" mass="1" diaginertia="0.1 0.1 {I}"/></body></worldbody>
+<inertial pos="0 0 0" mass="1" diaginertia="{I} {I} {I}"/></body></worldbody>
 <actuator><position joint="j" kp="{kp}" kv="{kv}"/></actuator></mujoco>"""
 
 
