@@ -496,6 +496,9 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
   float d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   float best_face = -1e30f, best_edge = -1e30f, nf[3] = {0, 0, 0}, ne[3] = {0, 0, 0};
   int face_axis = -1, edge_i = -1, edge_j = -1;
+  // a later face axis must beat the best by more than `tie` (oracle.c col_box_box): resting faces have
+  // equal separations along both boxes' normals, and rounding must not pick the reference face
+  const float tie = 1e-5f * (h1[0] + h1[1] + h1[2] + h2[0] + h2[1] + h2[2]);
   #pragma unroll 1
   for (int k = 0; k < 15; ++k) {
     float L[3];
@@ -512,7 +515,7 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
     if (sep > margin) return 0;
     const float sg = sv >= 0 ? 1.0f : -1.0f;
     if (k < 6) {
-      if (sep > best_face) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
+      if (sep > best_face + tie) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
     } else if (sep > best_edge) {
       best_edge = sep; edge_i = (k - 6) / 3; edge_j = (k - 6) % 3;
       for (int c = 0; c < 3; ++c) ne[c] = sg * L[c];

@@ -796,6 +796,11 @@ static int col_box_box(const double* p1, const double* R1, const double* h1, con
   for (int i = 0; i < 3; ++i) { box_axis(R1, i, A[i]); box_axis(R2, i, B[i]); }
   double best_face = -1e30, best_edge = -1e30, nf[3] = {0, 0, 0}, ne[3] = {0, 0, 0};
   int face_axis = -1, edge_i = -1, edge_j = -1;
+  /* a later face axis must beat the best by more than `tie` (1e-5 of the summed half sizes): two boxes
+   * resting face on face have equal separations along both boxes' normals, and rounding alone must not
+   * decide which face is the reference (it decides the order of the clipped polygon, which is the
+   * Gauss-Seidel row order of the solver) */
+  const double tie = 1e-5 * (h1[0] + h1[1] + h1[2] + h2[0] + h2[1] + h2[2]);
   for (int k = 0; k < 15; ++k) {
     double L[3];
     if (k < 3) memcpy(L, A[k], sizeof L);
@@ -811,7 +816,7 @@ static int col_box_box(const double* p1, const double* R1, const double* h1, con
     if (sep > margin) return n;
     double sg = s >= 0 ? 1.0 : -1.0;
     if (k < 6) {
-      if (sep > best_face) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
+      if (sep > best_face + tie) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
     } else if (sep > best_edge) {
       best_edge = sep; edge_i = (k - 6) / 3; edge_j = (k - 6) % 3;
       for (int c = 0; c < 3; ++c) ne[c] = sg * L[c];

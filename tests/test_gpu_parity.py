@@ -655,3 +655,89 @@ def test_camera_pipeline_snapshot():
     b.sync()
     assert torch.equal(got, want)
     b.close()
+
+
+def _reseeded_sensors(model, n, steps, period=10, settle=0):
+    """every GPU step starts from the oracle's fp64 state rounded to fp32 (qpos, qvel,
+    qacc_warmstart, ctrl), given identically to a second oracle instance; returns per sensor the
+    worst |gpu - oracle| over all env-steps and the sensor's largest |oracle value|, plus the worst
+    relative qpos / qvel errors and the contact-count mismatches"""
+    envs = np.arange(n)
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, (steps + settle) // period + 1, period)
+    orc = [binding.OracleData(model) for _ in envs]
+    ref = [binding.OracleData(model) for _ in envs]
+    for e, d in enumerate(orc):
+        d.qpos[:] = qpos0[e]
+    for t in range(settle):
+        for e, d in enumerate(orc):
+            if t % period == 0 and model.nu:
+                d.ctrl[:] = table[t // period, e]
+            d.step()
+    b = sim.Batch(model, n)
+    err = np.zeros(model.nsensor)
+    mag = np.zeros(model.nsensor)
+    wq = wv = 0.0
+    flips = 0
+    for t in range(settle, settle + steps):
+        for e, (d, r) in enumerate(zip(orc, ref)):
+            if t % period == 0 and model.nu:
+                d.ctrl[:] = table[t // period, e]
+            for k in ("qpos", "qvel", "qacc_warmstart", "ctrl"):
+                getattr(r, k)[:] = getattr(d, k).astype(np.float32)
+        for f, k in ((sim.FIELD_QPOS, "qpos"), (sim.FIELD_QVEL, "qvel"), (sim.FIELD_QACC_WARMSTART, "qacc_warmstart"),
+                     (sim.FIELD_CTRL, "ctrl")):
+            b.set(f, np.array([getattr(r, k) for r in ref]))
+        b.step(1)
+        for d, r in zip(orc, ref):
+            r.step()
+            d.step()
+        nc, nr = b.get(sim.FIELD_NCON)[:, 0].astype(int), np.array([r.ncon for r in ref])
+        ok = nc == nr
+        flips += int(np.sum(~ok))
+        s, sr = b.get(sim.FIELD_SENSORDATA)[ok], np.array([r.sensordata for r in ref])[ok]
+        q, v = b.get(sim.FIELD_QPOS)[ok], b.get(sim.FIELD_QVEL)[ok]
+        qr, vr = np.array([r.qpos for r in ref])[ok], np.array([r.qvel for r in ref])[ok]
+        if ok.any():
+            wq = max(wq, float(np.max(np.abs(q - qr) / _scale(qr))))
+            wv = max(wv, float(np.max(np.abs(v - vr) / _scale(vr))))
+            for i in range(model.nsensor):
+                a, dim = model.sensor_adr[i], model.sensor_dim[i]
+                err[i] = max(err[i], float(np.max(np.abs(s[:, a:a + dim] - sr[:, a:a + dim]))))
+                mag[i] = max(mag[i], float(np.max(np.abs(sr[:, a:a + dim]))))
+    b.close()
+    return err, mag, wq, wv, flips
+
+
+@pytest.mark.parametrize("group", [16, 64])
+def test_imu_ft_reseeded_1e5(group, monkeypatch):
+    """row f2 at the north-star tolerance: framequat / gyro / accelerometer / force / torque (what
+    read() maps, reference src/mujoco_system_interface.cpp:1069-1095) after every one of 200
+    re-seeded steps (motor torques, a box landing on the floor) within 1e-5 of each sensor's scale
+    max(1, largest |value|) -- the same bound as qpos / qvel.  Re-seeding removes the trajectory
+    divergence that the 400-step rollout test (test_imu_ft_sensor_parity) has to tolerate."""
+    monkeypatch.setenv("MRS_GROUP", str(group))
+    model = sim.Model.load(IMU_FT)
+    err, mag, wq, wv, flips = _reseeded_sensors(model, 16, 200)
+    rel = err / np.maximum(mag, 1.0)
+    for i in range(model.nsensor):
+        print(f"{model.id2name(sim.OBJ_SENSOR, i):14s} max |err| {err[i]:.2e}  scale {mag[i]:.3g}  rel {rel[i]:.2e}")
+    print(f"qpos {wq:.2e} qvel {wv:.2e} flips {flips}")
+    assert flips <= 0.01 * 16 * 200
+    assert wq <= 1e-5 and wv <= 1e-5
+    worst = int(np.argmax(rel))
+    assert rel.max() <= 1e-5, (model.id2name(sim.OBJ_SENSOR, worst), rel.max())
+
+
+@pytest.mark.parametrize("group", [16, 64])
+def test_contact_parity_reseeded_1e5(group, monkeypatch):
+    """CONTACT_SCENE (sphere, capsule on a ledge, box; PGS 50) over 300 re-seeded steps: contact
+    counts equal (at most 1% of env-steps excepted, a contact at fp32 rounding distance of its
+    threshold) and qpos / qvel within 1e-5 of scale per step -- test_contact_parity_short_horizon's
+    2e-3 is the free-running divergence, not the per-step arithmetic"""
+    monkeypatch.setenv("MRS_GROUP", str(group))
+    model = sim.Model.from_string(CONTACT_SCENE)
+    err, mag, wq, wv, flips = _reseeded_sensors(model, 8, 300)
+    print(f"G={group}: qpos {wq:.2e} qvel {wv:.2e} flips {flips}")
+    assert flips <= 0.01 * 8 * 300
+    assert wq <= 1e-5 and wv <= 1e-5

@@ -180,24 +180,28 @@ def _reseeded(model, n, steps, period=10, settle=20):
     return worst_q, worst_v, np.array(ncon), flips
 
 
-@pytest.mark.parametrize("scene, solver, n, steps, vtol", [("arm_boxes", "PGS", 64, 200, 2e-3),
-                                                           ("mobile_base", "PGS", 64, 200, RTOL),
-                                                           ("arm_boxes", "Newton", 16, 200, RTOL),
-                                                           ("mobile_base", "Newton", 64, 200, RTOL)])
-def test_reseeded_step_parity(scene, solver, n, steps, vtol):
+@pytest.mark.parametrize("scene, solver, n, steps, tol", [("arm_boxes", "PGS", 64, 200, None),
+                                                          ("arm_boxes", "PGS", 64, 200, 0),
+                                                          ("mobile_base", "PGS", 64, 200, None),
+                                                          ("arm_boxes", "Newton", 16, 200, None),
+                                                          ("mobile_base", "Newton", 64, 200, None)])
+def test_reseeded_step_parity(scene, solver, n, steps, tol):
     """C5 (arm + 8 boxes, blocked mode) and C4 (mobile base) with their PGS 50 iterations and under
-    Newton: every one of 200 steps from the oracle's state, qpos within 1e-5 of scale, qvel within
-    1e-5 -- except C5 under its unconverged 50-sweep PGS: the sweep improvement of fp32 PGS reaches
-    the 1e-8 tolerance 15-30 sweeps before fp64's (tests/emulation: fp32 row-serial PGS on the same
-    rows stops at 20-37 sweeps where fp64 runs all 50), so qacc differs by ~1e-2 and qvel by up to
-    ~1e-3 per step; under Newton the same scene holds 1e-5"""
-    model = with_solver(SCENES / f"{scene}.xml", solver, 50 if solver == "PGS" else 100)
+    Newton: every one of 200 steps from the oracle's state, qpos and qvel within 1e-5 of scale.
+    C5 also runs with tolerance="0" (both sides do all 50 sweeps), which separates the arithmetic from
+    the stop rule.  (Round 2 held C5-PGS only to 2e-3: the cause was not fp32 PGS arithmetic nor the
+    stop rule -- both sides stop at the same sweep in >98% of env-steps -- but the box-box reference
+    face picked by rounding between two equal separations, which rotates the clipped polygon and so
+    the Gauss-Seidel row order of an unconverged solve; step.hip / oracle.c box_box now break that tie
+    deterministically.)"""
+    it = (50 if solver == "PGS" else 100) if tol is None else f'50" tolerance="{tol}'
+    model = with_solver(SCENES / f"{scene}.xml", solver, it)
     wq, wv, ncon, flips = _reseeded(model, n, steps)
     print(f"{scene} {solver}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts per env "
           f"{ncon.mean():.1f}; contact-count flips {flips} of {n * steps} env-steps")
     assert ncon.max() > 0
     assert flips <= 0.01 * n * steps
-    assert wq <= RTOL and wv <= vtol
+    assert wq <= RTOL and wv <= RTOL
 
 
 FREE_SPHERE = """<mujoco>
