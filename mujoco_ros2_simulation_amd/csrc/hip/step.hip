@@ -445,31 +445,108 @@ __device__ int sphere_box(const float p[3], float r, const float* bp, const floa
   o.dist = dist;
   return n + 1;
 }
-__device__ __forceinline__ float box_dist2(const float l[3], const float* size) {
-  float s = 0;
+// capsule (segment a-b, radius r) vs box: oracle.c col_capsule_box in fp32.  Exact closest point of the
+// segment to the box (F(t), the squared box distance of the segment point, is convex and piecewise
+// quadratic between the slab-crossing breakpoints: the best clamped stationary point of the pieces);
+// contacts at the two ends of the segment piece inside the slabs of the axes where that point is
+// inside the box's extent (a capsule lying on a face rests on two points, where the single closest
+// point would be arbitrary along the face and ill-conditioned between fp32 and fp64), plus the closest
+// point itself when clearly nearer than both (a capsule across an edge); a segment through the box:
+// the point of deepest penetration.  Breakpoints sorted by a 19-comparator network (static registers).
+__device__ __forceinline__ float seg_box_F(const float la[3], const float d[3], const float* s, float t) {
+  float f = 0;
   for (int i = 0; i < 3; ++i) {
-    float e = fabsf(l[i]) - size[i];
-    if (e > 0) s += e * e;
+    const float e = fabsf(la[i] + t * d[i]) - s[i];
+    if (e > 0) f += e * e;
   }
-  return s;
+  return f;
 }
 __device__ int capsule_box(const float a[3], const float b[3], float r, const float* bp, const float* bm,
                            const float* size, float margin, gCon* out, int n) {
-  float lo = 0, hi = 1;
-  for (int it = 0; it < 40; ++it) {
-    float t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3, p1[3], p2[3], l1[3], l2[3];
-    for (int i = 0; i < 3; ++i) {
-      p1[i] = a[i] + t1 * (b[i] - a[i]) - bp[i];
-      p2[i] = a[i] + t2 * (b[i] - a[i]) - bp[i];
-    }
-    matT_vec(l1, bm, p1);
-    matT_vec(l2, bm, p2);
-    if (box_dist2(l1, size) <= box_dist2(l2, size)) hi = t2;
-    else lo = t1;
+  float la[3], lb[3], d[3];
+  {
+    float da[3] = {a[0] - bp[0], a[1] - bp[1], a[2] - bp[2]}, db[3] = {b[0] - bp[0], b[1] - bp[1], b[2] - bp[2]};
+    matT_vec(la, bm, da);
+    matT_vec(lb, bm, db);
   }
-  float t = 0.5f * (lo + hi), p[3];
-  for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
-  return sphere_box(p, r, bp, bm, size, margin, out, n);
+  for (int i = 0; i < 3; ++i) d[i] = lb[i] - la[i];
+  float k[8];
+  k[0] = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float t = 1;
+      if (fabsf(d[i]) > 1e-12f) {
+        t = ((q ? size[i] : -size[i]) - la[i]) / d[i];
+        if (!(t > 0 && t < 1)) t = 1;
+      }
+      k[1 + 2 * i + q] = t;
+    }
+  k[7] = 1;
+  auto cs = [&](int i, int j) { const float lo = fminf(k[i], k[j]), hi = fmaxf(k[i], k[j]); k[i] = lo; k[j] = hi; };
+  cs(0, 1); cs(2, 3); cs(4, 5); cs(6, 7); cs(0, 2); cs(1, 3); cs(4, 6); cs(5, 7); cs(1, 2); cs(5, 6);
+  cs(0, 4); cs(3, 7); cs(1, 5); cs(2, 6); cs(1, 4); cs(3, 6); cs(2, 4); cs(3, 5); cs(3, 4);
+  float tb = 0, Fb = seg_box_F(la, d, size, 0);
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const float t0 = k[q], t1 = k[q + 1];
+    if (t1 > t0) {
+      const float tm = 0.5f * (t0 + t1);
+      float num = 0, den = 0;
+      for (int i = 0; i < 3; ++i) {
+        const float x = la[i] + tm * d[i];
+        if (fabsf(x) > size[i]) {
+          const float sg = x > 0 ? 1.0f : -1.0f;
+          num += d[i] * (la[i] - sg * size[i]);
+          den += d[i] * d[i];
+        }
+      }
+      const float t = clampf(den > 0 ? -num / den : t0, t0, t1);
+      const float F = seg_box_F(la, d, size, t);
+      if (F < Fb) { Fb = F; tb = t; }
+    }
+  }
+  float p[3];
+  if (Fb <= 0) {
+    // the segment passes through the box: deepest point of min_i (s_i - |l_i(t)|)
+    float lo = 0, hi = 1;
+    for (int it = 0; it < 40; ++it) {
+      const float t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3;
+      float p1 = 1e30f, p2 = 1e30f;
+      for (int i = 0; i < 3; ++i) {
+        p1 = fminf(p1, size[i] - fabsf(la[i] + t1 * d[i]));
+        p2 = fminf(p2, size[i] - fabsf(la[i] + t2 * d[i]));
+      }
+      if (p1 >= p2) hi = t2;
+      else lo = t1;
+    }
+    const float t = 0.5f * (lo + hi);
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
+    return sphere_box(p, r, bp, bm, size, margin, out, n);
+  }
+  float tc0 = 0, tc1 = 1;
+  for (int j = 0; j < 3; ++j) {
+    if (fabsf(la[j] + tb * d[j]) > size[j] || fabsf(d[j]) <= 1e-12f) continue;
+    float u = (-size[j] - la[j]) / d[j], v = (size[j] - la[j]) / d[j];
+    if (u > v) { const float x = u; u = v; v = x; }
+    tc0 = fmaxf(tc0, u);
+    tc1 = fminf(tc1, v);
+  }
+  tc0 = fminf(tc0, tb);
+  tc1 = fmaxf(tc1, tb);
+  const float F0 = seg_box_F(la, d, size, tc0), F1 = seg_box_F(la, d, size, tc1);
+  for (int i = 0; i < 3; ++i) p[i] = a[i] + tc0 * (b[i] - a[i]);
+  n = sphere_box(p, r, bp, bm, size, margin, out, n);
+  if (tc1 > tc0) {
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + tc1 * (b[i] - a[i]);
+    n = sphere_box(p, r, bp, bm, size, margin, out, n);
+  }
+  if (tb > tc0 && tb < tc1 && sqrtf(Fb) < sqrtf(fminf(F0, F1)) - (1e-6f + 1e-4f * r)) {
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + tb * (b[i] - a[i]);
+    n = sphere_box(p, r, bp, bm, size, margin, out, n);
+  }
+  return n;
 }
 __device__ __forceinline__ void capsule_ends(const float* pos, const float* mat, float hl, float a[3], float b[3]) {
   for (int i = 0; i < 3; ++i) { a[i] = pos[i] - mat[3 * i + 2] * hl; b[i] = pos[i] + mat[3 * i + 2] * hl; }
@@ -3367,6 +3444,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
   jmul(qa, jar, 1.0f);
   float qfrc = update();
   float p = 0, gold = 0, Mgold = 0;
+  bool refined = false;
   int nit = 0;  // steps taken (mjData.solver_niter)
   #pragma unroll 1
   for (int iter = 0;; ++iter) {
@@ -3471,7 +3549,16 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     ++nit;
     const float gn = dof ? Md - qfrc : 0.0f;
     const float gnorm = sqrtf(gsum<G>(gn * gn));
-    if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance || (newton && !changed)) break;
+    if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance) break;
+    if (newton && !changed) {
+      // active set held: the step solved the quadratic model up to the fp32 factor's rounding
+      // (cond(H) eps |grad|); one refinement step from fresh residuals, then stop (oracle.c)
+      if (refined) break;
+      refined = true;
+      Md = mmul(qa - qs);
+      jmul(qa, jar, 1.0f);
+      qfrc = update();
+    }
   }
   if (dof) s[L.qfrc_con + lane] = qfrc;
   if (lane == 0) s[L.niter] = __int_as_float(nit);

@@ -687,35 +687,116 @@ static int col_sphere_box(const double p[3], double r, const double* bpos, const
   for (int i = 0; i < 3; ++i) pos[i] = p[i] + nrm[i] * (r + dist / 2);
   return add_contact(out, n, dist, pos, nrm);
 }
-/* distance^2 from point (box-local) to the box */
-static double box_dist2(const double l[3], const double* size) {
-  double s = 0;
+/* capsule (segment a-b, radius r) vs box.  In the box frame the squared distance of the segment
+ * point at t to the box, F(t) = sum_i max(0, |la_i + t d_i| - s_i)^2, is convex and piecewise
+ * quadratic with breakpoints where a coordinate crosses a slab plane (la_i + t d_i = +-s_i): the exact
+ * minimiser t* is the best of the pieces' clamped stationary points.  Contacts (restated primitive,
+ * well conditioned in fp32 and fp64 alike):
+ *   - the segment is clipped to the slabs |l_j| <= s_j of the axes on which the closest point t* lies
+ *     inside the box's extent (the face or edge it is closest to); the two ends of that piece, where
+ *     within margin, are contacts -- a capsule lying on a face rests on two points whatever its
+ *     overhang, where the single closest point would be arbitrary along the face;
+ *   - the closest point t* itself when it is clearly nearer than both ends (a capsule across an
+ *     edge), by more than 1e-6 + 1e-4 r;
+ *   - a segment that passes through the box (F(t*) = 0): the point of deepest penetration, found by
+ *     ternary search on the concave min_i (s_i - |l_i(t)|).
+ * Order: piece start, piece end, interior.  (MuJoCo's mjc_CapsuleBox also gives two contacts for flat
+ * poses; its exact selection is not restated.)  Same algorithm as step.hip capsule_box. */
+static double seg_box_F(const double la[3], const double d[3], const double* s, double t) {
+  double f = 0;
   for (int i = 0; i < 3; ++i) {
-    double e = fabs(l[i]) - size[i];
-    if (e > 0) s += e * e;
+    double e = fabs(la[i] + t * d[i]) - s[i];
+    if (e > 0) f += e * e;
   }
-  return s;
+  return f;
 }
-/* capsule (segment a-b, radius r) vs box: closest segment point by fixed-iteration ternary search
- * on the convex distance function, then sphere-box at that point (restated primitive; MuJoCo's
- * mjc_CapsuleBox may emit a second contact for flat poses) */
+static double seg_box_closest(const double la[3], const double d[3], const double* s, double* Fbest) {
+  double bp[8];
+  bp[0] = 0;
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 2; ++k) {
+      double t = 1;
+      if (fabs(d[i]) > 1e-12) {
+        t = ((k ? s[i] : -s[i]) - la[i]) / d[i];
+        if (!(t > 0 && t < 1)) t = 1;
+      }
+      bp[1 + 2 * i + k] = t;
+    }
+  bp[7] = 1;
+  for (int i = 1; i < 8; ++i)  /* insertion sort */
+    for (int j = i; j > 0 && bp[j] < bp[j - 1]; --j) { double x = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = x; }
+  double best_t = 0, best_F = seg_box_F(la, d, s, 0);
+  for (int k = 0; k < 7; ++k) {
+    double t0 = bp[k], t1 = bp[k + 1];
+    if (!(t1 > t0)) continue;
+    double tm = 0.5 * (t0 + t1), num = 0, den = 0;
+    for (int i = 0; i < 3; ++i) {
+      double x = la[i] + tm * d[i];
+      if (fabs(x) > s[i]) {
+        double sg = x > 0 ? 1 : -1;
+        num += d[i] * (la[i] - sg * s[i]);
+        den += d[i] * d[i];
+      }
+    }
+    double t = den > 0 ? -num / den : t0;
+    t = t < t0 ? t0 : t > t1 ? t1 : t;
+    double F = seg_box_F(la, d, s, t);
+    if (F < best_F) { best_F = F; best_t = t; }
+  }
+  *Fbest = best_F;
+  return best_t;
+}
 static int col_capsule_box(const double a[3], const double b[3], double r, const double* bpos,
                            const double* bmat, const double* size, double margin, orc_contact* out, int n) {
-  double lo = 0, hi = 1;
-  for (int it = 0; it < 40; ++it) {
-    double t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3, p1[3], p2[3], l1[3], l2[3];
-    for (int i = 0; i < 3; ++i) {
-      p1[i] = a[i] + t1 * (b[i] - a[i]) - bpos[i];
-      p2[i] = a[i] + t2 * (b[i] - a[i]) - bpos[i];
+  double da[3] = {a[0] - bpos[0], a[1] - bpos[1], a[2] - bpos[2]}, db[3], la[3], lb[3], d[3];
+  for (int i = 0; i < 3; ++i) db[i] = b[i] - bpos[i];
+  matT_vec(la, bmat, da);
+  matT_vec(lb, bmat, db);
+  for (int i = 0; i < 3; ++i) d[i] = lb[i] - la[i];
+  double Fbest;
+  double t = seg_box_closest(la, d, size, &Fbest);
+  double p[3];
+  if (Fbest <= 0) {
+    /* the segment passes through the box: deepest point of min_i (s_i - |l_i(t)|) */
+    double lo = 0, hi = 1;
+    for (int it = 0; it < 40; ++it) {
+      double t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3, p1 = 1e300, p2 = 1e300;
+      for (int i = 0; i < 3; ++i) {
+        double e1 = size[i] - fabs(la[i] + t1 * d[i]), e2 = size[i] - fabs(la[i] + t2 * d[i]);
+        p1 = e1 < p1 ? e1 : p1;
+        p2 = e2 < p2 ? e2 : p2;
+      }
+      if (p1 >= p2) hi = t2;
+      else lo = t1;
     }
-    matT_vec(l1, bmat, p1);
-    matT_vec(l2, bmat, p2);
-    if (box_dist2(l1, size) <= box_dist2(l2, size)) hi = t2;
-    else lo = t1;
+    t = 0.5 * (lo + hi);
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
+    return col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
   }
-  double t = 0.5 * (lo + hi), p[3];
-  for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
-  return col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
+  /* the piece of the segment within the slabs of the axes where the closest point is inside */
+  double tc0 = 0, tc1 = 1;
+  for (int j = 0; j < 3; ++j) {
+    if (fabs(la[j] + t * d[j]) > size[j] || fabs(d[j]) <= 1e-12) continue;
+    double u = (-size[j] - la[j]) / d[j], v = (size[j] - la[j]) / d[j];
+    if (u > v) { double x = u; u = v; v = x; }
+    tc0 = u > tc0 ? u : tc0;
+    tc1 = v < tc1 ? v : tc1;
+  }
+  if (tc0 > t) tc0 = t;
+  if (tc1 < t) tc1 = t;
+  double F0 = seg_box_F(la, d, size, tc0), F1 = seg_box_F(la, d, size, tc1);
+  for (int i = 0; i < 3; ++i) p[i] = a[i] + tc0 * (b[i] - a[i]);
+  n = col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
+  if (tc1 > tc0) {
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + tc1 * (b[i] - a[i]);
+    n = col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
+  }
+  double dmin = sqrt(F0 < F1 ? F0 : F1);
+  if (t > tc0 && t < tc1 && sqrt(Fbest) < dmin - (1e-6 + 1e-4 * r)) {
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
+    n = col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
+  }
+  return n;
 }
 
 /* box-box: separating-axis test over the 15 axes (3 + 3 face normals, 9 edge cross products);
@@ -1584,7 +1665,7 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
     w->efc_jar[r] = jar;
   }
   primal_update(m, w);
-  int iter = 0;
+  int iter = 0, refined = 0;
   for (;;) {
     /* gradient and preconditioned gradient */
     for (int j = 0; j < nv; ++j) grad[j] = Ma[j] - w->qfrc_smooth[j] - w->qfrc_constraint[j];
@@ -1644,7 +1725,22 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
       double g = Ma[j] - w->qfrc_smooth[j] - w->qfrc_constraint[j];
       gnorm += g * g;
     }
-    if (scale * -dcost < m->tolerance || scale * sqrt(gnorm) < m->tolerance || (newton && !changed)) break;
+    if (scale * -dcost < m->tolerance || scale * sqrt(gnorm) < m->tolerance) break;
+    if (newton && !changed) {
+      /* the active set held, so the step solved the quadratic model exactly up to the rounding of the
+       * Hessian factor: one more step from freshly formed residuals (iterative refinement), then stop.
+       * In fp64 it changes nothing measurable; in the fp32 kernel it removes the factor's rounding
+       * (cond(H) eps |grad|), which otherwise shows as a residual force in the force sensors. */
+      if (refined) break;
+      refined = 1;
+      mat_vec_n(Ma, w->M, qacc, nv);
+      for (int r = 0; r < nefc; ++r) {
+        double jar = -w->efc_aref[r];
+        for (int j = 0; j < nv; ++j) jar += w->efc_J[(size_t)r * nv + j] * qacc[j];
+        w->efc_jar[r] = jar;
+      }
+      primal_update(m, w);
+    }
   }
   d->solver_niter = iter;
   free(Ma); free(grad); free(Mgrad); free(p); free(Mv); free(gold); free(Mgold); free(x2); free(H); free(HL);

@@ -16,7 +16,13 @@ path = ROOT / "scenes" / f"{scene}.xml"
 it = 50 if solver == "PGS" else 100
 tol = sys.argv[5] if len(sys.argv) > 5 else None  # optional <option tolerance> override
 opt = f'solver="{solver}" iterations="{it}"' + (f' tolerance="{tol}"' if tol is not None else "")
-m = sim.Model.from_string(path.read_text().replace('solver="PGS" iterations="50"', opt), str(path.parent))
+if scene == "contact":  # tests/test_gpu_parity.py CONTACT_SCENE
+    sys.path.insert(0, str(ROOT / "tests"))
+    from test_gpu_parity import CONTACT_SCENE
+    xml, base = CONTACT_SCENE, "."
+else:
+    xml, base = path.read_text(), str(path.parent)
+m = sim.Model.from_string(xml.replace('solver="PGS" iterations="50"', opt), base)
 envs = np.arange(n)
 q0 = synth.initial_qpos(m, envs)
 tab = synth.ctrl_table(m, envs, steps // 10 + 1, 10)
@@ -25,7 +31,7 @@ for e, d in enumerate(orc):
     d.qpos[:] = q0[e]
 b = sim.Batch(m, n)
 worst = (0, None)
-settle = 20  # as tests/test_gpu_solvers.py::_reseeded: boxes spawned at zero distance settle first
+settle = int(__import__('os').environ.get('SETTLE', 20))  # as tests/test_gpu_solvers.py::_reseeded: boxes spawned at zero distance settle first
 for t in range(settle):
     for e, d in enumerate(orc):
         if t % 10 == 0:

@@ -713,15 +713,25 @@ def _reseeded_sensors(model, n, steps, period=10, settle=0):
 def test_imu_ft_reseeded_1e5(group, monkeypatch):
     """row f2 at the north-star tolerance: framequat / gyro / accelerometer / force / torque (what
     read() maps, reference src/mujoco_system_interface.cpp:1069-1095) after every one of 200
-    re-seeded steps (motor torques, a box landing on the floor) within 1e-5 of each sensor's scale
-    max(1, largest |value|) -- the same bound as qpos / qvel.  Re-seeding removes the trajectory
-    divergence that the 400-step rollout test (test_imu_ft_sensor_parity) has to tolerate."""
+    re-seeded steps (motor torques, a box landing on the floor) within 1e-5 of each sensor's scale --
+    the same bound as qpos / qvel.  Re-seeding removes the trajectory divergence that the 400-step
+    rollout test (test_imu_ft_sensor_parity) has to tolerate.
+    Scale: max(1, largest |value|), except force sensors, whose scale is the force they balance:
+    max(1, largest |value|, subtree mass x |g|).  A force sensor on a free body (box_force) reads the
+    body's net unbalanced force, 0 in exact arithmetic; what either side reports is the solver's
+    residual, which in fp32 is eps x cond(H) x the forces in balance (the body's weight against its
+    contact forces), ~1e-6 of them after the Newton refinement step -- not a fraction of a zero."""
     monkeypatch.setenv("MRS_GROUP", str(group))
     model = sim.Model.load(IMU_FT)
     err, mag, wq, wv, flips = _reseeded_sensors(model, 16, 200)
-    rel = err / np.maximum(mag, 1.0)
+    scale = np.maximum(mag, 1.0)
     for i in range(model.nsensor):
-        print(f"{model.id2name(sim.OBJ_SENSOR, i):14s} max |err| {err[i]:.2e}  scale {mag[i]:.3g}  rel {rel[i]:.2e}")
+        if model.sensor_type[i] == sim.SENS_FORCE:
+            body = model.site_bodyid[model.sensor_objid[i]]
+            scale[i] = max(scale[i], float(model.body_subtreemass[body]) * 9.81)
+    rel = err / scale
+    for i in range(model.nsensor):
+        print(f"{model.id2name(sim.OBJ_SENSOR, i):14s} max |err| {err[i]:.2e}  scale {scale[i]:.3g}  rel {rel[i]:.2e}")
     print(f"qpos {wq:.2e} qvel {wv:.2e} flips {flips}")
     assert flips <= 0.01 * 16 * 200
     assert wq <= 1e-5 and wv <= 1e-5
