@@ -2370,6 +2370,10 @@ constexpr int kRegQuads = MRS_REG_QUADS;  // items per pipe of the item-blocked 
 #define MRS_REG_LEVELS 48
 #endif
 constexpr int kRegLevels = MRS_REG_LEVELS;  // rows per pipe of the register-resident solve
+#ifndef MRS_DUAL_LEVELS
+#define MRS_DUAL_LEVELS 48
+#endif
+constexpr int kDualLevels = MRS_DUAL_LEVELS;  // rows per pipe of the island-dual register solve (x16)
 
 __device__ __forceinline__ int slot_dof(const DevModel& m, int t1, int t2, int slot) {
   if (t1 < 0) return -1;
@@ -2392,6 +2396,22 @@ __device__ __forceinline__ SlotMap slot_map(const lfloat* s, const LdsLayout& L,
   SlotMap r{-1, 0, 0, 0, 0};
   if (t1 >= 0 && slot < a.num) { r.d = a.adr + slot; r.li = slot; r.n = a.num; r.off = a.off; }
   else if (t1 >= 0 && t2 >= 0 && slot - a.num < b.num) { r.d = b.adr + slot - a.num; r.li = slot - a.num; r.n = b.num; r.off = b.off; r.sb = a.num; }
+  return r;
+}
+// slot -> (dof, tree segment) in an island's frame: its trees (packed t + 1 per byte, tree order) laid
+// out one after the other
+__device__ __forceinline__ SlotMap island_slot_map(const lfloat* s, const LdsLayout& L, unsigned pack, int slot) {
+  SlotMap r{-1, 0, 0, 0, 0};
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = static_cast<int>((pack >> (8 * q)) & 0xffu) - 1;
+    if (t >= 0) {
+      const TreeInfo ti = tree_lds(s, L, t);
+      if (r.d < 0 && slot >= base && slot < base + ti.num) { r.d = ti.adr + slot - base; r.li = slot - base; r.n = ti.num; r.off = ti.off; r.sb = base; }
+      base += ti.num;
+    }
+  }
   return r;
 }
 // trees of a row from its descriptor: t1 >= 0 unless the row touches no dof; t2 = -1 for one tree
@@ -2651,6 +2671,23 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       if (lane == k) cnt += ck;
     }
   }
+  // island slot frames: an island's trees in tree order, each tree's dofs consecutive (lane t: its
+  // tree's slot offset `ioff` in its island; lane i: island i's dof count and up to 4 trees packed
+  // (t + 1) per byte).  When every island with rows fits the pipe (<= P dofs, <= 4 trees), every row
+  // of an island holds J and M^-1 J' over the same slots, so J_r M^-1 J_s' of any two rows of an
+  // island is a plain slot-wise dot product (the dual solver's Delassus rows).
+  int idof = 0, itr = 0;
+  unsigned ipack = 0;
+  #pragma unroll 1
+  for (int k = 0; k < m.ntree; ++k) {
+    const int lk = __builtin_amdgcn_readlane(lbl, k);
+    if (lk == lane) {
+      if (itr < 4) ipack |= static_cast<unsigned>(k + 1) << (8 * itr);
+      ++itr;
+      idof += m.tree_dofnum[k];
+    }
+  }
+  const bool isl_ok = !__any(cnt > 0 && (idof > P || itr > 4));
   // longest-processing-time: largest island first onto the least loaded pipe
   int load[NP];
   unroll<NP>([&](auto pc) { load[decltype(pc)::value] = 0; });
@@ -2746,7 +2783,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       gfloat* h = hdr + 8 * q0;
       h[0] = __int_as_float(r0);
       h[1] = __int_as_float(code);
-      h[2] = __int_as_float((t1 + 1) | ((t2 + 1) << 8) | (nr << 16) | (dim << 20));
+      h[2] = __int_as_float((t1 + 1) | ((t2 + 1) << 8) | (nr << 16) | (dim << 20) | ((t1 < 0 ? 0xff : il) << 24));
       h[3] = mu;
       h[4] = R; h[5] = B; h[6] = pterm; h[7] = bound;
       itemat[q0] = jval;  // J value of a friction / limit row at its dof
@@ -2775,8 +2812,11 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       const int r0 = __float_as_int(h0.x), code = __float_as_int(h0.y), pk = __float_as_int(h0.z);
       const float mu = h0.w, R = h1.x, B = h1.y, pterm = h1.z, bound = h1.w;
       const int t = code >> 16, id = code & 0xffff;
-      const int t1 = (pk & 0xff) - 1, t2 = ((pk >> 8) & 0xff) - 1, nr = (pk >> 16) & 0xf, dim = pk >> 20;
-      const SlotMap sm = slot_map(s, L, t1, t2, slot);
+      const int t1 = (pk & 0xff) - 1, t2 = ((pk >> 8) & 0xff) - 1, nr = (pk >> 16) & 0xf, dim = (pk >> 20) & 0xf;
+      const int isl = (pk >> 24) & 0xff;
+      const unsigned ip = static_cast<unsigned>(__shfl(static_cast<int>(ipack), isl == 0xff ? 0 : isl));
+      const SlotMap sm = isl_ok ? (isl == 0xff ? SlotMap{-1, 0, 0, 0, 0} : island_slot_map(s, L, ip, slot))
+                                : slot_map(s, L, t1, t2, slot);
       const int d = sm.d;
       float jc[3] = {0, 0, 0};
       if (t == EFC_CONTACT) {
@@ -2845,6 +2885,194 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   t_sub = SUB_T();
   if (lane < nv) qa[lane] = qacc_s;
   const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+
+  // --- island-dual register solve (P = 16, island slot frames, at most kDualLevels rows per pipe).
+  // mj_solPGS on the dual, as the oracle's fwd_constraint: row r's residual g_r = b_r + sum_s AR_rs f_s
+  // is kept, not recomputed from qacc.  Lane (pipe, slot) holds the rows at levels 16 j + slot of its
+  // pipe ("held rows") with their Delassus rows AR[j][l] = J_(16j+slot) M^-1 J_l' (+ R on the
+  // diagonal) for every level l of the pipe, zero across islands.  A level l is then branch-free and
+  // touches no memory: the owner lane's clamped step delta = med3(-g / A, lo - f, hi - f), one DPP row
+  // broadcast of it folded into the FMAs g_r += AR_rl delta of every held row (the same Gauss-Seidel
+  // iterates as the row-serial sweep), and the owner's share of the sweep improvement -delta (res +
+  // A delta / 2) -- no LDS round trip of qacc and no reduction on the chain.  AR is formed once per
+  // step from the records: lane slot's held row J (16 slots) times each level's M^-1 J' broadcast slot
+  // by slot (DPP row broadcast folded into the FMA).
+  if constexpr (P == 16) {
+    if (isl_ok && nlev <= kDualLevels) {
+      constexpr int NL = kDualLevels, NJ = NL / 16;
+      float AR[NJ][NL];
+      float g[NJ], lof[NJ], hif[NJ], nia[NJ], hA[NJ], bb[NJ], fr[NJ];
+      int hisl[NJ];  // island tag of each held row: the dof of its slot 0 (-1: none)
+      // held-row scalars from the records (neutral rows past the pipe's own: J = 0, bounds [0, inf))
+      unroll<NJ>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int k = 16 * j + slot;
+        const bool act = k < my_n;
+        const gfloat* o = rec + (act ? my_start + k : 0) * RF;
+        const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
+        const float bound = sc.w;
+        lof[j] = act && bound >= 0 ? -bound : 0.0f;       // friction loss: [-frictionloss, frictionloss]
+        hif[j] = act && bound >= 0 ? bound : 3.0e38f;     // others: [0, inf)
+        bb[j] = act ? o[3 * P + 4] : 0.0f;
+        fr[j] = act ? sc.y : 0.0f;                        // R, folded into the diagonal below
+        hisl[j] = act ? __float_as_int(o[2 * P]) : -1;
+      });
+      // AR[j][l] = J_(16j+slot) . M^-1 J_l': the held row's J over its 16 slots in registers, each
+      // level's M^-1 J' (lane = slot) broadcast slot by slot into the FMAs; one held row at a time
+      unroll<NJ>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int k = 16 * j + slot;
+        const bool act = k < my_n;
+        const gfloat* o = rec + (act ? my_start + k : 0) * RF;
+        float Jt[16];
+        unroll<4>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          const v4f v = *(const __attribute__((address_space(1))) v4f*)(o + 4 * q);
+          Jt[4 * q] = act ? v.x : 0.0f; Jt[4 * q + 1] = act ? v.y : 0.0f;
+          Jt[4 * q + 2] = act ? v.z : 0.0f; Jt[4 * q + 3] = act ? v.w : 0.0f;
+        });
+        unroll<NL>([&](auto lc) {
+          constexpr int l = decltype(lc)::value;
+          AR[j][l] = 0.0f;
+          if (l < nlev) {
+            const float mj = l < my_n ? rec[(my_start + l) * RF + P + slot] : 0.0f;
+            const int il = __float_as_int(rowb<l % 16>(__int_as_float(hisl[l / 16])));
+            float a0 = 0, a1 = 0;
+            unroll<16>([&](auto sc) {
+              constexpr int q = decltype(sc)::value;
+              if constexpr (q & 1) a1 += Jt[q] * rowb<q>(mj);
+              else a0 += Jt[q] * rowb<q>(mj);
+            });
+            float a = a0 + a1;
+            const bool diag = l / 16 == j && slot == l % 16;
+            if (diag) a += fr[j];  // + R_rr
+            AR[j][l] = (hisl[j] == il && hisl[j] >= 0) || diag ? a : 0.0f;
+          }
+        });
+      });
+      // the held rows' diagonal A_rr = J_r M^-1 J_r' + R from AR itself (the step and the residual
+      // update use the same value, as the oracle's AR)
+      unroll<NJ>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        float A = 0;
+        unroll<16>([&](auto oc) {
+          constexpr int o = decltype(oc)::value;
+          if (16 * j + o < NL) A = slot == o ? AR[j][16 * j + o] : A;
+        });
+        A = 16 * j + slot < my_n ? A : 1.0f;
+        nia[j] = -1.0f / A;
+        hA[j] = 0.5f * A;
+      });
+      SUB_ADD(PH_CON_REC, t_sub);
+      t_sub = SUB_T();
+      // warm start: forces of mj_constraintUpdate at qacc_warmstart (J of the held row over its
+      // island's slots, qacc_warmstart gathered at the slots' dofs), kept if the dual cost is negative
+      unroll<NJ>([&](auto jc) { fr[decltype(jc)::value] = 0.0f; });
+      if (warm) {
+        float jar[NJ];
+        unroll<NJ>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const int k = 16 * j + slot;
+          const bool act = k < my_n;
+          const gfloat* o = rec + (act ? my_start + k : 0) * RF;
+          float acc = act ? -o[3 * P] : 0.0f;  // -aref
+          #pragma unroll 4
+          for (int q = 0; q < 16; ++q) {
+            const int d = act ? __float_as_int(o[2 * P + q]) : -1;
+            const float J = act ? o[q] : 0.0f;
+            acc += d >= 0 ? J * s[L.qacc_ws + d] : 0.0f;
+          }
+          jar[j] = acc;
+        });
+        unroll<NJ>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const int k = 16 * j + slot;
+          if (k < my_n) {
+            const float R = rec[(my_start + k) * RF + 3 * P + 1];
+            const float D = 1.0f / R, hi = hif[j];
+            fr[j] = lof[j] < 0 ? (jar[j] <= -R * hi ? hi : (jar[j] >= R * hi ? -hi : -D * jar[j]))
+                               : (jar[j] < 0 ? -D * jar[j] : 0.0f);
+          }
+        });
+      }
+      // residuals g = b + AR f; warm start kept if the dual cost f' (AR f / 2 + b) = f' (g + b) / 2 < 0
+      unroll<NJ>([&](auto jc) { g[decltype(jc)::value] = bb[decltype(jc)::value]; });
+      if (warm) {
+        unroll<NL>([&](auto lc) {
+          constexpr int l = decltype(lc)::value;
+          if (l < nlev) {
+            const float fl = rowb<l % 16>(fr[l / 16]);
+            unroll<NJ>([&](auto jc) { g[decltype(jc)::value] += AR[decltype(jc)::value][l] * fl; });
+          }
+        });
+        float c = 0;
+        unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; c += fr[j] * (g[j] + bb[j]); });
+        if (gsum<64>(c) > 0) {
+          unroll<NJ>([&](auto jc) { fr[decltype(jc)::value] = 0.0f; g[decltype(jc)::value] = bb[decltype(jc)::value]; });
+        }
+      }
+      // lo - f and hi - f carried instead of f
+      unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; lof[j] -= fr[j]; hif[j] -= fr[j]; });
+      SUB_ADD(PH_CON_WARM, t_sub);
+      t_sub = SUB_T();
+      int slot_v = slot;
+      int nit = 0;
+      #pragma unroll 1
+      for (int it = 0; it < m.iterations; ++it) {
+        asm volatile("" : "+v"(slot_v));
+        float imp = 0;
+        unroll<NL>([&](auto kc) {
+          constexpr int k = decltype(kc)::value, j = k / 16, o = k % 16;
+          if (k < nlev) {
+            const float cand = __builtin_amdgcn_fmed3f(g[j] * nia[j], lof[j], hif[j]);
+            const float dm = slot_v == o ? cand : 0.0f;
+            imp = fmaf(dm, fmaf(hA[j], dm, g[j]), imp);
+            lof[j] -= dm;
+            hif[j] -= dm;
+            const float dl = rowb<o>(cand);
+            unroll<NJ>([&](auto jc) { g[decltype(jc)::value] += AR[decltype(jc)::value][k] * dl; });
+          }
+        });
+        const float improvement = -gsum<64>(imp);
+        nit = it + 1;
+        if (improvement * m.pgs_scale < m.tolerance) break;
+      }
+      if (lane == 0) s[L.niter] = __int_as_float(nit);
+      SUB_ADD(PH_CON_PGS, t_sub);
+      // forces f = lo - (lo - f); qfrc_constraint = J' f and qacc = qacc_smooth + M^-1 J' f per level
+      unroll<NJ>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int k = 16 * j + slot;
+        const float bound = k < my_n ? rec[(my_start + k) * RF + 3 * P + 3] : -1.0f;
+        fr[j] = (bound >= 0 ? -bound : 0.0f) - lof[j];
+      });
+      if (lane < nv) tmp[lane] = 0;
+      if (lane == 0) { qa[nv] = 0; tmp[nv] = 0; }
+      wsync();
+      #pragma unroll 1
+      for (int l = 0; l < nlev; ++l) {
+        const int q = l < my_n ? my_start + l : 0;
+        const gfloat* o = rec + q * RF;
+        const int d = l < my_n ? __float_as_int(o[2 * P + slot]) : -1;
+        const float J = o[slot], MJ = o[P + slot];
+        // the level's force from its owner lane l % 16 (runtime lane: one readlane per pipe via shfl)
+        float f = 0;
+        unroll<NJ>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const float fj = __shfl(fr[j], pbase + (l & 15));
+          if ((l >> 4) == j) f = fj;
+        });
+        if (d >= 0) { tmp[d] += J * f; qa[d] += MJ * f; }
+      }
+      unroll<NJ>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int k = 16 * j + slot;
+        if (k < my_n) ffg[__float_as_int(rowof[my_start + k])] = fr[j];
+      });
+      wsync();
+      return lane < nv ? qa[lane] : 0.0f;
+    }
+  }
 
   // --- item-blocked register solve: P = 16 and at most kRegQuads items per pipe.  Item i of a pipe
   // takes levels 4i..4i+3 (its 1 or 4 rows, the rest neutral: J = 0, R = a = 1, bounds [0, inf)), and
@@ -3552,8 +3780,10 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance) break;
     if (newton && !changed) {
       // active set held: the step solved the quadratic model up to the fp32 factor's rounding
-      // (cond(H) eps |grad|); one refinement step from fresh residuals, then stop (oracle.c)
-      if (refined) break;
+      // (cond(H) eps |grad|); one refinement step from fresh residuals, then stop (oracle.c) -- unless
+      // the residual is already at the rounding level of the gradient's own terms
+      const bool floor = fabsf(gn) <= 64.0f * __FLT_EPSILON__ * (fabsf(Md) + fabsf(qfrc));
+      if (refined || !gany<G>(!floor)) break;
       refined = true;
       Md = mmul(qa - qs);
       jmul(qa, jar, 1.0f);
@@ -4589,7 +4819,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
 // workgroup -> 2 workgroups per CU -> 2 waves per SIMD, 256 VGPRs)
 template <int G>
 #ifndef MRS_G64_WAVES
-#define MRS_G64_WAVES 3
+#define MRS_G64_WAVES 2
 #endif
 struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 

@@ -10,6 +10,7 @@
  */
 #include "oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <pthread.h>
 #include <sched.h>
@@ -1730,8 +1731,14 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
       /* the active set held, so the step solved the quadratic model exactly up to the rounding of the
        * Hessian factor: one more step from freshly formed residuals (iterative refinement), then stop.
        * In fp64 it changes nothing measurable; in the fp32 kernel it removes the factor's rounding
-       * (cond(H) eps |grad|), which otherwise shows as a residual force in the force sensors. */
-      if (refined) break;
+       * (cond(H) eps |grad|), which otherwise shows as a residual force in the force sensors.  Skipped
+       * when the residual is already within 64 eps of the gradient's own terms. */
+      int above = 0; /* residual above the rounding level of the gradient's terms (DBL_EPSILON here) */
+      for (int j = 0; j < nv; ++j) {
+        double g = Ma[j] - w->qfrc_smooth[j] - w->qfrc_constraint[j];
+        above |= fabs(g) > 64 * DBL_EPSILON * (fabs(Ma[j] - w->qfrc_smooth[j]) + fabs(w->qfrc_constraint[j]));
+      }
+      if (refined || !above) break;
       refined = 1;
       mat_vec_n(Ma, w->M, qacc, nv);
       for (int r = 0; r < nefc; ++r) {
