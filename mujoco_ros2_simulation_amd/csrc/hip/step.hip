@@ -2900,68 +2900,73 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   if constexpr (P == 16) {
     if (isl_ok && nlev <= kDualLevels) {
       constexpr int NL = kDualLevels, NJ = NL / 16;
-      float AR[NJ][NL];
-      float g[NJ], lof[NJ], hif[NJ], nia[NJ], hA[NJ], bb[NJ], fr[NJ];
+      typedef float v2f __attribute__((ext_vector_type(2)));
+      // ARn[j][l] = -AR_rl / A_rr of held row r = 16 j + slot: the sweeps carry the normalised
+      // residual gn_r = -g_r / A_rr (the unclamped step), so a level's step is one med3 of it
+      float ARn[NJ][NL];
+      float gn[NJ], nia[NJ], A[NJ], bb[NJ], fr[NJ];
+      v2f lh[NJ];    // (lo - f, hi - f) of each held row
       int hisl[NJ];  // island tag of each held row: the dof of its slot 0 (-1: none)
-      // held-row scalars from the records (neutral rows past the pipe's own: J = 0, bounds [0, inf))
-      unroll<NJ>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        const int k = 16 * j + slot;
-        const bool act = k < my_n;
-        const gfloat* o = rec + (act ? my_start + k : 0) * RF;
-        const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
-        const float bound = sc.w;
-        lof[j] = act && bound >= 0 ? -bound : 0.0f;       // friction loss: [-frictionloss, frictionloss]
-        hif[j] = act && bound >= 0 ? bound : 3.0e38f;     // others: [0, inf)
-        bb[j] = act ? o[3 * P + 4] : 0.0f;
-        fr[j] = act ? sc.y : 0.0f;                        // R, folded into the diagonal below
-        hisl[j] = act ? __float_as_int(o[2 * P]) : -1;
-      });
-      // AR[j][l] = J_(16j+slot) . M^-1 J_l': the held row's J over its 16 slots in registers, each
-      // level's M^-1 J' (lane = slot) broadcast slot by slot into the FMAs; one held row at a time
-      unroll<NJ>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        const int k = 16 * j + slot;
-        const bool act = k < my_n;
-        const gfloat* o = rec + (act ? my_start + k : 0) * RF;
-        float Jt[16];
-        unroll<4>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          const v4f v = *(const __attribute__((address_space(1))) v4f*)(o + 4 * q);
-          Jt[4 * q] = act ? v.x : 0.0f; Jt[4 * q + 1] = act ? v.y : 0.0f;
-          Jt[4 * q + 2] = act ? v.z : 0.0f; Jt[4 * q + 3] = act ? v.w : 0.0f;
+      {
+        float Jt[NJ][16];
+        // held-row scalars and J over its 16 slots from the records (neutral rows past the pipe's
+        // own: J = 0, bounds [0, inf))
+        unroll<NJ>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const int k = 16 * j + slot;
+          const bool act = k < my_n;
+          const gfloat* o = rec + (act ? my_start + k : 0) * RF;
+          unroll<4>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const v4f v = *(const __attribute__((address_space(1))) v4f*)(o + 4 * q);
+            Jt[j][4 * q] = act ? v.x : 0.0f; Jt[j][4 * q + 1] = act ? v.y : 0.0f;
+            Jt[j][4 * q + 2] = act ? v.z : 0.0f; Jt[j][4 * q + 3] = act ? v.w : 0.0f;
+          });
+          const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
+          const float bound = sc.w;
+          lh[j] = (v2f){act && bound >= 0 ? -bound : 0.0f,     // friction loss: [-frictionloss, frictionloss]
+                        act && bound >= 0 ? bound : 3.0e38f};  // others: [0, inf)
+          bb[j] = act ? o[3 * P + 4] : 0.0f;
+          fr[j] = act ? sc.y : 0.0f;                           // R, folded into the diagonal below
+          hisl[j] = act ? __float_as_int(o[2 * P]) : -1;
         });
+        // AR[j][l] = J_(16j+slot) . M^-1 J_l': each level's M^-1 J' (lane = slot) read once and
+        // broadcast slot by slot into the FMAs of the three held rows
         unroll<NL>([&](auto lc) {
           constexpr int l = decltype(lc)::value;
-          AR[j][l] = 0.0f;
+          unroll<NJ>([&](auto jc) { ARn[decltype(jc)::value][l] = 0.0f; });
           if (l < nlev) {
             const float mj = l < my_n ? rec[(my_start + l) * RF + P + slot] : 0.0f;
             const int il = __float_as_int(rowb<l % 16>(__int_as_float(hisl[l / 16])));
-            float a0 = 0, a1 = 0;
-            unroll<16>([&](auto sc) {
-              constexpr int q = decltype(sc)::value;
-              if constexpr (q & 1) a1 += Jt[q] * rowb<q>(mj);
-              else a0 += Jt[q] * rowb<q>(mj);
+            unroll<NJ>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              float a0 = 0, a1 = 0;
+              unroll<16>([&](auto sc) {
+                constexpr int q = decltype(sc)::value;
+                if constexpr (q & 1) a1 += Jt[j][q] * rowb<q>(mj);
+                else a0 += Jt[j][q] * rowb<q>(mj);
+              });
+              float a = a0 + a1;
+              const bool diag = l / 16 == j && slot == l % 16;
+              if (diag) a += fr[j];  // + R_rr
+              ARn[j][l] = (hisl[j] == il && hisl[j] >= 0) || diag ? a : 0.0f;
             });
-            float a = a0 + a1;
-            const bool diag = l / 16 == j && slot == l % 16;
-            if (diag) a += fr[j];  // + R_rr
-            AR[j][l] = (hisl[j] == il && hisl[j] >= 0) || diag ? a : 0.0f;
           }
         });
-      });
-      // the held rows' diagonal A_rr = J_r M^-1 J_r' + R from AR itself (the step and the residual
-      // update use the same value, as the oracle's AR)
+      }
+      // A_rr from AR itself (the step and the residual update use the same value, as the oracle's AR),
+      // then the rows normalised by -1 / A_rr
       unroll<NJ>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        float A = 0;
+        float a = 0;
         unroll<16>([&](auto oc) {
           constexpr int o = decltype(oc)::value;
-          if (16 * j + o < NL) A = slot == o ? AR[j][16 * j + o] : A;
+          if constexpr (16 * j + o < NL) a = slot == o ? ARn[j][16 * j + o] : a;
         });
-        A = 16 * j + slot < my_n ? A : 1.0f;
-        nia[j] = -1.0f / A;
-        hA[j] = 0.5f * A;
+        a = 16 * j + slot < my_n ? a : 1.0f;
+        A[j] = a;
+        nia[j] = -1.0f / a;
+        unroll<NL>([&](auto lc) { ARn[j][decltype(lc)::value] *= nia[j]; });
       });
       SUB_ADD(PH_CON_REC, t_sub);
       t_sub = SUB_T();
@@ -2969,71 +2974,71 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       // island's slots, qacc_warmstart gathered at the slots' dofs), kept if the dual cost is negative
       unroll<NJ>([&](auto jc) { fr[decltype(jc)::value] = 0.0f; });
       if (warm) {
-        float jar[NJ];
         unroll<NJ>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
           const int k = 16 * j + slot;
           const bool act = k < my_n;
           const gfloat* o = rec + (act ? my_start + k : 0) * RF;
-          float acc = act ? -o[3 * P] : 0.0f;  // -aref
+          float jar = act ? -o[3 * P] : 0.0f;  // -aref
           #pragma unroll 4
           for (int q = 0; q < 16; ++q) {
             const int d = act ? __float_as_int(o[2 * P + q]) : -1;
             const float J = act ? o[q] : 0.0f;
-            acc += d >= 0 ? J * s[L.qacc_ws + d] : 0.0f;
+            jar += d >= 0 ? J * s[L.qacc_ws + d] : 0.0f;
           }
-          jar[j] = acc;
-        });
-        unroll<NJ>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          const int k = 16 * j + slot;
-          if (k < my_n) {
-            const float R = rec[(my_start + k) * RF + 3 * P + 1];
-            const float D = 1.0f / R, hi = hif[j];
-            fr[j] = lof[j] < 0 ? (jar[j] <= -R * hi ? hi : (jar[j] >= R * hi ? -hi : -D * jar[j]))
-                               : (jar[j] < 0 ? -D * jar[j] : 0.0f);
+          if (act) {
+            const float R = o[3 * P + 1];
+            const float D = 1.0f / R, hi = lh[j].y;
+            fr[j] = lh[j].x < 0 ? (jar <= -R * hi ? hi : (jar >= R * hi ? -hi : -D * jar))
+                                : (jar < 0 ? -D * jar : 0.0f);
           }
         });
       }
-      // residuals g = b + AR f; warm start kept if the dual cost f' (AR f / 2 + b) = f' (g + b) / 2 < 0
-      unroll<NJ>([&](auto jc) { g[decltype(jc)::value] = bb[decltype(jc)::value]; });
+      // normalised residuals gn = -(b + AR f) / A; warm start kept if the dual cost
+      // f' (AR f / 2 + b) = f' (g + b) / 2 is negative
+      unroll<NJ>([&](auto jc) { gn[decltype(jc)::value] = nia[decltype(jc)::value] * bb[decltype(jc)::value]; });
       if (warm) {
         unroll<NL>([&](auto lc) {
           constexpr int l = decltype(lc)::value;
           if (l < nlev) {
             const float fl = rowb<l % 16>(fr[l / 16]);
-            unroll<NJ>([&](auto jc) { g[decltype(jc)::value] += AR[decltype(jc)::value][l] * fl; });
+            unroll<NJ>([&](auto jc) { gn[decltype(jc)::value] += ARn[decltype(jc)::value][l] * fl; });
           }
         });
         float c = 0;
-        unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; c += fr[j] * (g[j] + bb[j]); });
+        unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; c += fr[j] * (bb[j] - A[j] * gn[j]); });
         if (gsum<64>(c) > 0) {
-          unroll<NJ>([&](auto jc) { fr[decltype(jc)::value] = 0.0f; g[decltype(jc)::value] = bb[decltype(jc)::value]; });
+          unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; fr[j] = 0.0f; gn[j] = nia[j] * bb[j]; });
         }
       }
-      // lo - f and hi - f carried instead of f
-      unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; lof[j] -= fr[j]; hif[j] -= fr[j]; });
+      unroll<NJ>([&](auto jc) { constexpr int j = decltype(jc)::value; lh[j] -= (v2f){fr[j], fr[j]}; });
       SUB_ADD(PH_CON_WARM, t_sub);
       t_sub = SUB_T();
+      // sweeps: level k's owner (slot k % 16, held row k / 16) takes the clamped step, every held row
+      // of the pipe moves its normalised residual by ARn delta (DPP row broadcast of the step folded
+      // into the FMA); the owner's improvement term -delta (res + A delta / 2) = A delta (gn - delta/2)
+      // is accumulated per held row and scaled by A once per sweep
       int slot_v = slot;
       int nit = 0;
       #pragma unroll 1
       for (int it = 0; it < m.iterations; ++it) {
         asm volatile("" : "+v"(slot_v));
-        float imp = 0;
+        float impj[NJ];
+        unroll<NJ>([&](auto jc) { impj[decltype(jc)::value] = 0.0f; });
         unroll<NL>([&](auto kc) {
           constexpr int k = decltype(kc)::value, j = k / 16, o = k % 16;
           if (k < nlev) {
-            const float cand = __builtin_amdgcn_fmed3f(g[j] * nia[j], lof[j], hif[j]);
+            const float cand = __builtin_amdgcn_fmed3f(gn[j], lh[j].x, lh[j].y);
             const float dm = slot_v == o ? cand : 0.0f;
-            imp = fmaf(dm, fmaf(hA[j], dm, g[j]), imp);
-            lof[j] -= dm;
-            hif[j] -= dm;
+            impj[j] = fmaf(dm, fmaf(-0.5f, dm, gn[j]), impj[j]);
+            lh[j] -= (v2f){dm, dm};
             const float dl = rowb<o>(cand);
-            unroll<NJ>([&](auto jc) { g[decltype(jc)::value] += AR[decltype(jc)::value][k] * dl; });
+            unroll<NJ>([&](auto jc) { gn[decltype(jc)::value] += ARn[decltype(jc)::value][k] * dl; });
           }
         });
-        const float improvement = -gsum<64>(imp);
+        float imp = 0;
+        unroll<NJ>([&](auto jc) { imp += A[decltype(jc)::value] * impj[decltype(jc)::value]; });
+        const float improvement = gsum<64>(imp);
         nit = it + 1;
         if (improvement * m.pgs_scale < m.tolerance) break;
       }
@@ -3044,7 +3049,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         constexpr int j = decltype(jc)::value;
         const int k = 16 * j + slot;
         const float bound = k < my_n ? rec[(my_start + k) * RF + 3 * P + 3] : -1.0f;
-        fr[j] = (bound >= 0 ? -bound : 0.0f) - lof[j];
+        fr[j] = (bound >= 0 ? -bound : 0.0f) - lh[j].x;
       });
       if (lane < nv) tmp[lane] = 0;
       if (lane == 0) { qa[nv] = 0; tmp[nv] = 0; }
@@ -3055,8 +3060,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         const gfloat* o = rec + q * RF;
         const int d = l < my_n ? __float_as_int(o[2 * P + slot]) : -1;
         const float J = o[slot], MJ = o[P + slot];
-        // the level's force from its owner lane l % 16 (runtime lane: one readlane per pipe via shfl)
-        float f = 0;
+        float f = 0;  // the level's force, from its owner lane l % 16 of the pipe
         unroll<NJ>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
           const float fj = __shfl(fr[j], pbase + (l & 15));
