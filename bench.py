@@ -48,11 +48,12 @@ def parse():
     p.add_argument("--scene", default=None, help="override the config's scene")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
-    p.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c3",
+    p.add_argument("--config", choices=["c1", "c2", "c3", "c3m", "c4", "c5"], default="c3",
                    help="c3: the BASELINE metric (default); c1: the reference scene, 1 env, through the plugin host "
                         "(MujocoSystemInterface, headless), paced and unpaced; "
                         "c2: reference 2-DoF scene, 4096 envs, sensors off; "
-                        "c4: mobile base + lidar + 640x480 depth camera; c5: contact-rich arm + 8 free boxes")
+                        "c4: mobile base + lidar + 640x480 depth camera; c5: contact-rich arm + 8 free boxes; "
+                        "c3m: C3 with mesh link shells and a 6912-triangle statue + a 640x480 camera (ray hierarchy)")
     p.add_argument("--c1-seconds", type=float, default=3.0, help="C1: wall seconds of the paced measurement")
     p.add_argument("--render-every", type=int, default=100, help="C4: physics steps between depth frames")
     p.add_argument("--render-sync", action="store_true",
@@ -118,7 +119,7 @@ def cpu_baseline(model, period: int, target_s: float):
 def committed(kind: str, cfg: str, envs: int, period: int):
     """newest committed rocprofv3 PMC summary `profiles/r*/<kind>_<cfg>.json` of this same bench
     command (scripts/gpu_full.sh -> scripts/pmc_summary.py); None for other workload sizes"""
-    default_envs = {"c2": 4096, "c3": 8192, "c4": 2048, "c5": 8192}
+    default_envs = {"c2": 4096, "c3": 8192, "c3m": 8192, "c4": 2048, "c5": 8192}
     if cfg not in default_envs or envs != default_envs[cfg] or period != 10:
         return None, None
     found = sorted(ROOT.glob(f"profiles/r*/{kind}_{cfg}.json"))
@@ -272,9 +273,9 @@ def main():
         model = sim.Model.from_string(xml, base)
         scene_name = "scene"
     else:
-        scene_name = {"c3": "arm7_lidar", "c4": "mobile_base", "c5": "arm_boxes"}[cfg]
+        scene_name = {"c3": "arm7_lidar", "c3m": "arm7_mesh", "c4": "mobile_base", "c5": "arm_boxes"}[cfg]
         model = sim.Model.load(ROOT / "scenes" / f"{scene_name}.xml")
-    n = args.envs or {"c2": 4096, "c3": 8192, "c4": 2048, "c5": 8192}[cfg]
+    n = args.envs or {"c2": 4096, "c3": 8192, "c3m": 8192, "c4": 2048, "c5": 8192}[cfg]
     env_ids = shard.env_ids(rank, n)
     P = args.warmup + args.steps
     d_table = torch.from_numpy(synth.ctrl_table(model, env_ids, P, args.period).astype(np.float32)).to(dev)
@@ -286,7 +287,7 @@ def main():
     gather = None
     if world > 1 and not args.no_gather:
         gather = shard.ObsGather(n, [model.nq, model.nv], device=dev)
-    render = cfg == "c4"
+    render = cfg in ("c4", "c3m")
     if render:
         W, H = int(model.cam_resolution[0, 0]), int(model.cam_resolution[0, 1])
         frames = torch.empty((n, H, W), dtype=torch.float32, device=dev)
@@ -365,6 +366,8 @@ def main():
         "c2": f"reference 2-DoF scene (C2: resources/scene.xml, sensors disabled, {solver})",
         "c3": f"{scene_name} (C3: 7-DoF arm + {nrf}-ray lidar, {solver})",
         "c4": f"{scene_name} (C4: free base + 2 wheels, {nrf}-ray lidar, 640x480 depth, {solver})",
+        "c3m": f"{scene_name} (C3 with mesh link shells + a 6912-triangle statue, {nrf}-ray lidar, "
+               f"640x480 depth, {solver})",
         "c5": f"{scene_name} (C5: 7-DoF arm + 8 free boxes, {solver} {model.iterations} iterations)",
     }[cfg]
     metric = {
@@ -372,6 +375,7 @@ def main():
         "c3": METRIC,
         "c4": "env-steps/sec (whole node), mobile base + 32-beam lidar + 640x480 depth camera (C4)",
         "c5": "env-steps/sec (whole node), contact-rich arm + 8 free boxes (C5)",
+        "c3m": "env-steps/sec (whole node), mesh robot: C3 + mesh shells, statue, 640x480 depth (C3m)",
     }[cfg]
     config = {"workload": workload, "envs_per_gpu": n, "global_envs": world * n,
               "physics_steps_per_bench_step": args.period, "timestep": model.timestep,

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -42,6 +43,8 @@ constexpr int kMaxRenderGeoms = 256;
 struct MeshRef {
   const float* vert;
   const int *face, *dataid, *vertadr, *faceadr, *facenum;
+  const float* bvh;           // bounding volume hierarchies (8 floats per node, build_mesh_bvh)
+  const int *bvhadr, *bvhnum;  // per mesh: first node, node count (0: no hierarchy, every triangle)
 };
 
 // analytic ray primitive (same restatement of engine_ray as the step kernel's rangefinder)
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
     if (t == MRS_GEOM_MESH) {
       const int id = mesh.dataid[g];
       tt = ray_mesh(mesh.vert + 3 * mesh.vertadr[id], mesh.face + 3 * mesh.faceadr[id], mesh.facenum[id],
-                    geom_size + 3 * g, lp, lv);
+                    geom_size + 3 * g, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id]);
     } else {
       tt = ray_prim(t, geom_size + 3 * g, lp, lv);
     }
@@ -299,7 +302,8 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
         lv[i] = mm[i] * vec[0] + mm[3 + i] * vec[1] + mm[6 + i] * vec[2];
       }
       int tri = 0;
-      ray_mesh(mv, mf, mesh.facenum[id], geom_size + 3 * bestg, lp, lv, &tri);
+      ray_mesh(mv, mf, mesh.facenum[id], geom_size + 3 * bestg, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id],
+               mesh.bvhnum[id], &tri);
       mesh_tri_normal(mv, mf, tri, lv, nl);
     } else {
       local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
@@ -458,7 +462,8 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
         else if (type == MRS_GEOM_MESH)
           t = ray_mesh(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid],
-                       mesh.facenum[o.dataid], sz, lp, lv);
+                       mesh.facenum[o.dataid], sz, lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
+                       mesh.bvhnum[o.dataid]);
         else t = ray_prim(type, sz, lp, lv);
         if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
@@ -487,7 +492,8 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
             const float lv[3] = {o.A[0] * dx + o.A[1] * dy[k] - o.A[2], o.A[3] * dx + o.A[4] * dy[k] - o.A[5],
                                  o.A[6] * dx + o.A[7] * dy[k] - o.A[8]};
             int tri = 0;
-            ray_mesh(mv, mf, mesh.facenum[o.dataid], o.size, o.lp, lv, &tri);
+            ray_mesh(mv, mf, mesh.facenum[o.dataid], o.size, o.lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
+                     mesh.bvhnum[o.dataid], &tri);
             mesh_tri_normal(mv, mf, tri, lv, nl);
           } else {
             local_normal(o.type, o.size, q, nl);
@@ -559,6 +565,78 @@ void* dalloc(BatchImpl& b, size_t bytes) {
   HIP_CHECK(hipMemsetAsync(p, 0, bytes ? bytes : 16, b.stream));
   b.allocs.push_back(p);
   return p;
+}
+
+// Per-mesh bounding volume hierarchy for rays (rangefinders, depth and colour): a binary tree over a
+// mesh's triangles in depth-first order; each node stores its AABB, inflated by 1e-5 of the mesh's
+// extent so that the fp32 slab test never rejects a triangle that Moller-Trumbore hits, and the index
+// of the node after its subtree (stackless traversal, raymesh.h).  Leaves hold up to 4 consecutive
+// triangles of the mesh's device face list, which is reordered for it (face ids stay relative to the
+// mesh's vertices; only ties between triangles at equal ray parameter can pick a different triangle).
+// Meshes of at most 64 triangles keep no hierarchy: a wave tests their triangles with scalar loads.
+void build_mesh_bvh(const Model& m, std::vector<int>& face_out, std::vector<float>& node,
+                    std::vector<int>& adr, std::vector<int>& num) {
+  face_out = m.mesh_face;
+  const int nmesh = static_cast<int>(m.mesh_faceadr.size());
+  adr.assign(std::max(1, nmesh), 0);
+  num.assign(std::max(1, nmesh), 0);
+  auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+  for (int k = 0; k < nmesh; ++k) {
+    const int fa = m.mesh_faceadr[k], fn = m.mesh_facenum[k], va = m.mesh_vertadr[k];
+    adr[k] = static_cast<int>(node.size() / 8);
+    if (fn <= 64 || std::getenv("MRS_NO_BVH")) continue;  // MRS_NO_BVH: every triangle (tests' A/B)
+    struct Tri { double lo[3], hi[3], c[3]; int f[3]; };
+    std::vector<Tri> tris(fn);
+    double mlo[3] = {1e300, 1e300, 1e300}, mhi[3] = {-1e300, -1e300, -1e300};
+    for (int f = 0; f < fn; ++f) {
+      Tri& t = tris[f];
+      for (int c = 0; c < 3; ++c) { t.lo[c] = 1e300; t.hi[c] = -1e300; t.f[c] = m.mesh_face[3 * (fa + f) + c]; }
+      for (int v = 0; v < 3; ++v)
+        for (int c = 0; c < 3; ++c) {
+          const double x = m.mesh_vert[3 * (va + t.f[v]) + c];
+          t.lo[c] = std::min(t.lo[c], x); t.hi[c] = std::max(t.hi[c], x);
+        }
+      for (int c = 0; c < 3; ++c) {
+        t.c[c] = 0.5 * (t.lo[c] + t.hi[c]);
+        mlo[c] = std::min(mlo[c], t.lo[c]); mhi[c] = std::max(mhi[c], t.hi[c]);
+      }
+    }
+    const double pad = 1e-5 * std::max(1e-9, std::max(mhi[0] - mlo[0], std::max(mhi[1] - mlo[1], mhi[2] - mlo[2])));
+    std::vector<float> nodes;
+    std::function<void(int, int)> build = [&](int b, int e) {
+      const int me = static_cast<int>(nodes.size() / 8);
+      double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, clo[3] = {1e300, 1e300, 1e300},
+             chi[3] = {-1e300, -1e300, -1e300};
+      for (int i = b; i < e; ++i)
+        for (int c = 0; c < 3; ++c) {
+          lo[c] = std::min(lo[c], tris[i].lo[c]); hi[c] = std::max(hi[c], tris[i].hi[c]);
+          clo[c] = std::min(clo[c], tris[i].c[c]); chi[c] = std::max(chi[c], tris[i].c[c]);
+        }
+      for (int c = 0; c < 3; ++c) nodes.push_back(static_cast<float>(lo[c] - pad));
+      nodes.push_back(0);
+      for (int c = 0; c < 3; ++c) nodes.push_back(static_cast<float>(hi[c] + pad));
+      nodes.push_back(fbits(-1));
+      if (e - b <= 4) {
+        nodes[8 * me + 7] = fbits((b << 8) | (e - b));
+      } else {
+        int ax = 0;
+        for (int c = 1; c < 3; ++c)
+          if (chi[c] - clo[c] > chi[ax] - clo[ax]) ax = c;
+        const int mid = (b + e) / 2;
+        std::nth_element(tris.begin() + b, tris.begin() + mid, tris.begin() + e,
+                         [ax](const Tri& x, const Tri& y) { return x.c[ax] < y.c[ax]; });
+        build(b, mid);
+        build(mid, e);
+      }
+      nodes[8 * me + 3] = fbits(static_cast<int>(nodes.size() / 8));
+    };
+    build(0, fn);
+    for (int f = 0; f < fn; ++f)
+      for (int c = 0; c < 3; ++c) face_out[3 * (fa + f) + c] = tris[f].f[c];
+    num[k] = static_cast<int>(nodes.size() / 8);
+    node.insert(node.end(), nodes.begin(), nodes.end());
+  }
+  if (node.empty()) node.assign(8, 0.0f);
 }
 
 void build_devmodel(BatchImpl& b, int max_con_req) {
@@ -766,8 +844,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.tree_dofnum, tree_dofnum); P.addi(&d.tree_Moff, tree_Moff);
   P.addi(&d.geom_type, m.geom_type); P.addi(&d.geom_bodyid, m.geom_bodyid); P.addi(&d.geom_group, m.geom_group);
   P.addi(&d.geom_dataid, m.geom_dataid);
+  std::vector<int> bvh_face, bvh_adr, bvh_num;
+  std::vector<float> bvh_node;
+  build_mesh_bvh(m, bvh_face, bvh_node, bvh_adr, bvh_num);
   P.addi(&d.mesh_vertadr, m.mesh_vertadr); P.addi(&d.mesh_faceadr, m.mesh_faceadr); P.addi(&d.mesh_facenum, m.mesh_facenum);
-  P.addi(&d.mesh_hulladr, m.mesh_hulladr); P.addi(&d.mesh_hullnum, m.mesh_hullnum); P.addi(&d.mesh_face, m.mesh_face);
+  P.addi(&d.mesh_hulladr, m.mesh_hulladr); P.addi(&d.mesh_hullnum, m.mesh_hullnum); P.addi(&d.mesh_face, bvh_face);
+  P.addi(&d.mesh_bvhadr, bvh_adr); P.addi(&d.mesh_bvhnum, bvh_num); P.addf(&d.mesh_bvh, bvh_node);
   P.addi(&d.mesh_hull, m.mesh_hull); P.addf(&d.mesh_vert, m.mesh_vert);
   P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
   P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
@@ -1192,7 +1274,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_rowof = take(d.blocked ? ne : 0);
   S.efc_item = take(d.blocked ? ne : 0);
   S.efc_fq = take(d.blocked ? ne : 0);
-  S.efc_hdr = take(d.blocked ? 8 * ne : 0);
+  S.efc_hdr = take(d.blocked ? 24 * ne : 0);  // step.hip kHdr
   S.efc_quad = take(d.blocked ? 64 : 0);
   S.stage = take(d.npair > 0 ? 64 * kMaxPairCon * 7 : 0);  // <= 64 lanes x 8 contacts x 7 floats
   S.efc_n = take(1);
@@ -1446,7 +1528,8 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
   const float f = static_cast<float>(0.5 * H / std::tan(m.cam_fovy[cam] * M_PI / 360.0));
   const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
   const DevModel& d = b->dm;
-  const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p, d.mesh_facenum.p};
+  const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p,
+                     d.mesh_facenum.p, d.mesh_bvh.p, d.mesh_bvhadr.p, d.mesh_bvhnum.p};
   HIP_CHECK(hipEventRecord(b->ev0[1], stream));
   if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
     hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,

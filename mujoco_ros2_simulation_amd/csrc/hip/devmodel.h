@@ -126,6 +126,10 @@ struct DevModel {
   // relative to the mesh's first vertex)
   CPtr<int> mesh_vertadr, mesh_faceadr, mesh_facenum, mesh_hulladr, mesh_hullnum, mesh_face, mesh_hull;
   CPtr<float> mesh_vert;
+  // ray hierarchies (batch.hip build_mesh_bvh; mesh_face is reordered to their leaves): per mesh the
+  // first node and the node count (0: none), 8 floats per node
+  CPtr<int> mesh_bvhadr, mesh_bvhnum;
+  CPtr<float> mesh_bvh;
   // candidate collision pairs (static filters applied; g1 has the smaller geom type)
   CPtr<int> pair_g1, pair_g2, pair_dim;
   CPtr<float> pair_margin, pair_gap, pair_friction /*3*/, pair_solref /*2*/, pair_solimp /*5*/;

@@ -1,46 +1,95 @@
 // Ray vs mesh, shared by the step kernel's rangefinders (step.hip) and the depth / colour kernels
 // (batch.hip).  mj_rayMesh restated (oracle.c ray_mesh): the ray in the geom frame (origin lp,
 // direction lv) is first tested against the geom's bounding box (half extents s, slab test), then
-// against every triangle, both faces (Moller-Trumbore).  `vert` / `face` point at the mesh's own
-// vertices and triangles (face ids relative to vert).  Returns the nearest t >= 0, or -1; *tri gets
-// the nearest triangle when tri is not null.
+// against the triangles, both faces (Moller-Trumbore) -- the ones the mesh's bounding volume
+// hierarchy does not rule out.  `vert` / `face` point at the mesh's own vertices and triangles (face
+// ids relative to vert).  Returns the nearest t >= 0, or -1; *tri gets the nearest triangle when tri
+// is not null.
 #pragma once
 
-template <class PV, class PF, class PS>
-__device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS s, const float lp[3],
-                                          const float lv[3], int* tri = nullptr) {
+// one triangle, both faces (Moller-Trumbore); t >= 0 of the hit or -1
+template <class PV, class PF>
+__device__ __forceinline__ float ray_tri(PV vert, PF face, int f, const float lp[3], const float lv[3]) {
+  const int ia = 3 * face[3 * f], ib = 3 * face[3 * f + 1], ic = 3 * face[3 * f + 2];
+  const float a[3] = {vert[ia], vert[ia + 1], vert[ia + 2]};
+  const float e1[3] = {vert[ib] - a[0], vert[ib + 1] - a[1], vert[ib + 2] - a[2]};
+  const float e2[3] = {vert[ic] - a[0], vert[ic + 1] - a[1], vert[ic + 2] - a[2]};
+  const float pv[3] = {lv[1] * e2[2] - lv[2] * e2[1], lv[2] * e2[0] - lv[0] * e2[2], lv[0] * e2[1] - lv[1] * e2[0]};
+  const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+  if (fabsf(det) < 1e-15f) return -1;
+  const float inv = 1.0f / det;
+  const float tv[3] = {lp[0] - a[0], lp[1] - a[1], lp[2] - a[2]};
+  const float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
+  if (u < 0 || u > 1) return -1;
+  const float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
+  const float v = (lv[0] * qv[0] + lv[1] * qv[1] + lv[2] * qv[2]) * inv;
+  if (v < 0 || u + v > 1) return -1;
+  const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
+  return t >= 0 ? t : -1;
+}
+
+// slab test of the ray against an axis-aligned box [lo, hi]: the entry parameter, or 3e38 on a miss
+__device__ __forceinline__ float ray_aabb(const float lo[3], const float hi[3], const float lp[3], const float lv[3],
+                                          const float iv[3]) {
   float tmin = -3.0e38f, tmax = 3.0e38f;
   for (int i = 0; i < 3; ++i) {
     if (fabsf(lv[i]) < 1e-15f) {
-      if (fabsf(lp[i]) > s[i]) return -1;
+      if (lp[i] < lo[i] || lp[i] > hi[i]) return 3.0e38f;
       continue;
     }
-    const float t1 = (-s[i] - lp[i]) / lv[i], t2 = (s[i] - lp[i]) / lv[i];
+    const float t1 = (lo[i] - lp[i]) * iv[i], t2 = (hi[i] - lp[i]) * iv[i];
     tmin = fmaxf(tmin, fminf(t1, t2));
     tmax = fminf(tmax, fmaxf(t1, t2));
   }
-  if (tmax < tmin || tmax < 0) return -1;
+  return (tmax < tmin || tmax < 0) ? 3.0e38f : tmin;
+}
+
+// The nearest hit over the triangles is the same whichever triangles the bounding volumes let
+// through (each triangle's t is computed by ray_tri alike); only ties between triangles at equal t
+// may resolve to a different triangle (its normal shades the colour image).
+// bvh / nnode: the mesh's bounding volume hierarchy (batch.hip build_mesh_bvh): 8 floats per node in
+// depth-first order -- AABB lo, the index of the node after its subtree (int bits), AABB hi, and for a
+// leaf (first << 8 | count) of its triangles in `face` (int bits; -1 for an inner node).  Stackless
+// traversal: a missed box, a box entered past the nearest hit, or a leaf jumps to the skip index, an
+// inner node that is hit descends to its first child (the next node).  nnode = 0: every triangle.
+template <class PV, class PF, class PS, class PN>
+__device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS s, const float lp[3],
+                                          const float lv[3], PN bvh, int nnode, int* tri = nullptr) {
+  {
+    const float lo[3] = {-s[0], -s[1], -s[2]}, hi[3] = {s[0], s[1], s[2]};
+    const float iv[3] = {1.0f / lv[0], 1.0f / lv[1], 1.0f / lv[2]};
+    if (ray_aabb(lo, hi, lp, lv, iv) == 3.0e38f) return -1;
+  }
   float best = -1;
-  for (int f = 0; f < nface; ++f) {
-    const int ia = 3 * face[3 * f], ib = 3 * face[3 * f + 1], ic = 3 * face[3 * f + 2];
-    const float a[3] = {vert[ia], vert[ia + 1], vert[ia + 2]};
-    const float e1[3] = {vert[ib] - a[0], vert[ib + 1] - a[1], vert[ib + 2] - a[2]};
-    const float e2[3] = {vert[ic] - a[0], vert[ic + 1] - a[1], vert[ic + 2] - a[2]};
-    const float pv[3] = {lv[1] * e2[2] - lv[2] * e2[1], lv[2] * e2[0] - lv[0] * e2[2], lv[0] * e2[1] - lv[1] * e2[0]};
-    const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
-    if (fabsf(det) < 1e-15f) continue;
-    const float inv = 1.0f / det;
-    const float tv[3] = {lp[0] - a[0], lp[1] - a[1], lp[2] - a[2]};
-    const float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
-    if (u < 0 || u > 1) continue;
-    const float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
-    const float v = (lv[0] * qv[0] + lv[1] * qv[1] + lv[2] * qv[2]) * inv;
-    if (v < 0 || u + v > 1) continue;
-    const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
-    if (t >= 0 && (best < 0 || t < best)) {
-      best = t;
-      if (tri) *tri = f;
+  if (nnode <= 0) {
+    for (int f = 0; f < nface; ++f) {
+      const float t = ray_tri(vert, face, f, lp, lv);
+      if (t >= 0 && (best < 0 || t < best)) {
+        best = t;
+        if (tri) *tri = f;
+      }
     }
+    return best;
+  }
+  const float iv[3] = {1.0f / lv[0], 1.0f / lv[1], 1.0f / lv[2]};
+  int i = 0;
+  while (i < nnode) {
+    const int o = 8 * i;
+    const float lo[3] = {bvh[o], bvh[o + 1], bvh[o + 2]}, hi[3] = {bvh[o + 4], bvh[o + 5], bvh[o + 6]};
+    const int skip = __float_as_int(bvh[o + 3]), leaf = __float_as_int(bvh[o + 7]);
+    const float te = ray_aabb(lo, hi, lp, lv, iv);
+    const bool hit = te != 3.0e38f && (best < 0 || te <= best);
+    if (hit && leaf >= 0) {
+      const int f0 = leaf >> 8, nf = leaf & 0xff;
+      for (int f = f0; f < f0 + nf; ++f) {
+        const float t = ray_tri(vert, face, f, lp, lv);
+        if (t >= 0 && (best < 0 || t < best)) {
+          best = t;
+          if (tri) *tri = f;
+        }
+      }
+    }
+    i = hit && leaf < 0 ? i + 1 : skip;
   }
   return best;
 }

@@ -2360,6 +2360,7 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
 // env's scratch in solver order, pipe p's rows at [start_p, start_p + n_p); each level k of a sweep
 // is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
 typedef float v4f __attribute__((ext_vector_type(4)));
+constexpr int kHdr = 24;     // item header floats (blocked mode; batch.hip sizes efc_hdr to match)
 constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, then the coupling
                              // J_r M^-1 J_s' of row r to the earlier rows s < r of its item (3 floats)
 #ifndef MRS_REG_QUADS
@@ -2780,12 +2781,26 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       }
       const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (ps - mg);
       const float jval = t == EFC_FRICTION ? 1.0f : (t == EFC_LIMIT ? floss[r0] : 0.0f);
-      gfloat* h = hdr + 8 * q0;
+      gfloat* h = hdr + kHdr * q0;
       h[0] = __int_as_float(r0);
       h[1] = __int_as_float(code);
       h[2] = __int_as_float((t1 + 1) | ((t2 + 1) << 8) | (nr << 16) | (dim << 20) | ((t1 < 0 ? 0xff : il) << 24));
       h[3] = mu;
       h[4] = R; h[5] = B; h[6] = pterm; h[7] = bound;
+      // what the records phase reads per item, copied here where 64 items load at once: the contact's
+      // position, bodies and frame (no dependent chain contact -> pair -> geom -> body per item there),
+      // or the friction / limit row's dof and J value
+      if (t == EFC_CONTACT) {
+        const gfloat* crec = scr + S.con + kConRec * id;
+        const int p = __float_as_int(crec[0]);
+        const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+        for (int i = 0; i < 3; ++i) h[8 + i] = crec[2 + i];
+        h[11] = __int_as_float(b1 | (b2 << 16));
+        for (int i = 0; i < 9; ++i) h[12 + i] = crec[5 + i];
+      } else {
+        h[8] = jval;
+        h[11] = __int_as_float(t == EFC_FRICTION ? id : m.jnt_dofadr[id]);
+      }
       itemat[q0] = jval;  // J value of a friction / limit row at its dof
     }
   }
@@ -2801,14 +2816,33 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   {
     const int my_end = my_start + my_n;
     int qc = my_start;
+    // the item headers are read one item ahead (loads in flight while the current item is built)
+    struct Hdr { v4f a, b, c, d, e; float f; };
+    auto load_hdr = [&](int q) {
+      const gfloat* h = hdr + kHdr * q;
+      Hdr o;
+      o.a = *(const __attribute__((address_space(1))) v4f*)h;
+      o.b = *(const __attribute__((address_space(1))) v4f*)(h + 4);
+      o.c = *(const __attribute__((address_space(1))) v4f*)(h + 8);
+      o.d = *(const __attribute__((address_space(1))) v4f*)(h + 12);
+      o.e = *(const __attribute__((address_space(1))) v4f*)(h + 16);
+      o.f = h[20];
+      return o;
+    };
+    Hdr nxt = load_hdr(qc < my_end ? qc : 0);
     #pragma unroll 1
     for (;;) {
       const bool act = qc < my_end;
       if (!__any(act)) break;
       const int q0 = act ? qc : 0;  // record 0 always starts an item
-      const gfloat* h = hdr + 8 * q0;
-      const v4f h0 = *(const __attribute__((address_space(1))) v4f*)h;
-      const v4f h1 = *(const __attribute__((address_space(1))) v4f*)(h + 4);
+      const Hdr cur = nxt;
+      const v4f h0 = cur.a, h1 = cur.b, h2 = cur.c, h3 = cur.d, h4 = cur.e;
+      const float h20 = cur.f;
+      {
+        const int nr_ = (__float_as_int(h0.z) >> 16) & 0xf;
+        const int qn = qc + (act ? nr_ : 0);
+        nxt = load_hdr(qn < my_end ? qn : 0);
+      }
       const int r0 = __float_as_int(h0.x), code = __float_as_int(h0.y), pk = __float_as_int(h0.z);
       const float mu = h0.w, R = h1.x, B = h1.y, pterm = h1.z, bound = h1.w;
       const int t = code >> 16, id = code & 0xffff;
@@ -2821,20 +2855,19 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       float jc[3] = {0, 0, 0};
       if (t == EFC_CONTACT) {
         if (d >= 0) {
-          const gfloat* crec = scr + S.con + kConRec * id;
-          const int p = __float_as_int(crec[0]);
-          const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
-          const float cp[3] = {crec[2], crec[3], crec[4]};
+          const int bb = __float_as_int(h2.w);
+          const int b1 = bb & 0xffff, b2 = bb >> 16;
+          const float cp[3] = {h2.x, h2.y, h2.z};
+          const float fr[9] = {h3.x, h3.y, h3.z, h3.w, h4.x, h4.y, h4.z, h4.w, h20};
           float c1[3], c2[3];
           jac_col(m, s, b1, cp, d, c1);
           jac_col(m, s, b2, cp, d, c2);
           const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
-          for (int i = 0; i < 3; ++i) jc[i] = crec[5 + 3 * i] * dc[0] + crec[6 + 3 * i] * dc[1] + crec[7 + 3 * i] * dc[2];
+          for (int i = 0; i < 3; ++i) jc[i] = fr[3 * i] * dc[0] + fr[3 * i + 1] * dc[1] + fr[3 * i + 2] * dc[2];
         }
       } else {
-        // friction loss: e_dof; limit: +-e_dof (value kept in itemat)
-        const int dof = t == EFC_FRICTION ? id : m.jnt_dofadr[id];
-        jc[0] = d == dof ? itemat[q0] : 0.0f;
+        // friction loss: e_dof; limit: +-e_dof (dof and J value in the header)
+        jc[0] = d == __float_as_int(h2.w) ? h2.x : 0.0f;
       }
       float mjc[3];
       pipe_msolve3(m, s + L.L, sm, pbase, jc, mjc);
@@ -4402,7 +4435,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       if (type == MRS_GEOM_MESH) {  // wave-uniform mesh: its triangles arrive by scalar loads
         const int id = __float_as_int(rec[7]);
         t = ray_mesh(m.mesh_vert + 3 * m.mesh_vertadr[id], m.mesh_face + 3 * m.mesh_faceadr[id], m.mesh_facenum[id],
-                     gs, lp, lv);
+                     gs, lp, lv, m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id]);
       } else {
         t = ray_geom_local(type, gs, lp, lv);
       }
