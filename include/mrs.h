@@ -159,7 +159,9 @@ int mrs_debug_phase_cycles(double* out, int n, int reset);
 /* diagnostics: the batch's kernel configuration -- out[0] lanes per env (group width), [1] LDS floats
  * per env, [2] scratch floats per env, [3] blocked mode (tree-blocked M + sparse constraint rows),
  * [4] dof slots per constraint row (pipe width), [5] constraint-row capacity, [6] contact capacity,
- * [7] kinematic trees with dofs.  Returns the number of values written. */
+ * [7] kinematic trees with dofs, [8] workgroup-shared LDS floats, [9] lidar rays read from the
+ * workgroup's LDS table (1) or the model block (0), [10] one workgroup per CU (16-lane groups kept for
+ * tables past the two-per-CU budget).  Returns the number of values written. */
 int mrs_debug_batch_layout(const mrs_batch* b, int* out, int n);
 
 #ifdef __cplusplus

@@ -22,7 +22,7 @@ HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
 # the parity tolerance is 1e-5 relative, and the ray/contact math is division-heavy
 HIP_FLAGS = ["-fno-hip-fp32-correctly-rounded-divide-sqrt"]
 CXX_SOURCES = ["capi.cc", "mjcf/compiler.cc", "mjcf/mesh.cc", "mjcf/xml.cc"]
-HEADERS = ["hip/devmodel.h", "hip/batch.h", "mjcf/model.h", "mjcf/mesh.h", "mjcf/xml.h"]
+HEADERS = ["hip/devmodel.h", "hip/batch.h", "hip/raymesh.h", "mjcf/model.h", "mjcf/mesh.h", "mjcf/xml.h"]
 
 
 def _newer(src: Path, dst: Path, deps: list[Path]) -> bool:

@@ -273,8 +273,9 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
     float tt;
     if (t == MRS_GEOM_MESH) {
       const int id = mesh.dataid[g];
+      int tri;
       tt = ray_mesh(mesh.vert + 3 * mesh.vertadr[id], mesh.face + 3 * mesh.faceadr[id], mesh.facenum[id],
-                    geom_size + 3 * g, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id]);
+                         geom_size + 3 * g, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id], &tri);
     } else {
       tt = ray_prim(t, geom_size + 3 * g, lp, lv);
     }
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
       }
       int tri = 0;
       ray_mesh(mv, mf, mesh.facenum[id], geom_size + 3 * bestg, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id],
-               mesh.bvhnum[id], &tri);
+                    mesh.bvhnum[id], &tri);
       mesh_tri_normal(mv, mf, tri, lv, nl);
     } else {
       local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
@@ -461,9 +462,12 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         float t;
         if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
         else if (type == MRS_GEOM_MESH)
+        {
+          int tri;
           t = ray_mesh(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid],
                        mesh.facenum[o.dataid], sz, lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
-                       mesh.bvhnum[o.dataid]);
+                       mesh.bvhnum[o.dataid], &tri);
+        }
         else t = ray_prim(type, sz, lp, lv);
         if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                                  o.A[6] * dx + o.A[7] * dy[k] - o.A[8]};
             int tri = 0;
             ray_mesh(mv, mf, mesh.facenum[o.dataid], o.size, o.lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
-                     mesh.bvhnum[o.dataid], &tri);
+                          mesh.bvhnum[o.dataid], &tri);
             mesh_tri_normal(mv, mf, tri, lv, nl);
           } else {
             local_normal(o.type, o.size, q, nl);
@@ -536,6 +540,7 @@ struct BatchImpl {
   const Model* model = nullptr;
   int n = 0, device = 0;
   int group = 64;  // lanes per environment in the step kernel (64/group envs per wavefront)
+  int g16_one_wg = 0;  // G = 16 with one workgroup per CU (tables past the two-per-CU budget)
   DevModel dm{};
   DevModel* d_dm = nullptr;  // device copy of dm
   LdsLayout& L = dm.L;
@@ -1222,22 +1227,26 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.rf_static = d.rf_mode ? static_cast<float*>(dalloc(b, std::max(1, d.nrf) * sizeof(float))) : nullptr;
   // workgroup-shared tables: ray-geom records, the per-ray direction + address when every ray
   // starts at one point of one body, and the rays' static hits (DevModel::shr_*)
-  d.shr_rf = d.nrgeom * 8;
-  d.shr_rfst = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
-  d.shr_blk = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
-  d.shr_sens = d.shr_blk + 17 * d.nrfblk;
-  d.shr_fric = d.shr_sens + 16 * d.nsens_other;
-  d.shr_lim = d.shr_fric + 4 * d.nfric;
-  d.shr_act = d.shr_lim + 4 * d.nlim;
-  d.shr_dof = d.shr_act + 20 * m.nu;
-  d.shr_body = d.shr_dof + 16 * m.nv;
-  d.shr_mpair = d.shr_body + 8 * m.nbody;
-  d.shr_jump = d.shr_mpair + 4 * d.nMpair;
-  // the smooth-dynamics tables (from shr_act on) are staged only by lane-group kernels (G < 64);
-  // blocked mode (one env per workgroup) reads them from the model block instead of paying their LDS
-  // per env
-  const int shr_small = d.shr_act;
-  d.shr_total = d.shr_jump + d.njump * m.nbody;
+  int shr_small = 0;
+  auto layout_shared = [&]() {
+    d.shr_rf = d.nrgeom * 8;
+    d.shr_rfst = d.shr_rf + (d.rf_common ? 4 * d.nrf : 0);
+    d.shr_blk = d.shr_rfst + (d.rf_mode == 2 ? d.nrf : 0);
+    d.shr_sens = d.shr_blk + 17 * d.nrfblk;
+    d.shr_fric = d.shr_sens + 16 * d.nsens_other;
+    d.shr_lim = d.shr_fric + 4 * d.nfric;
+    d.shr_act = d.shr_lim + 4 * d.nlim;
+    d.shr_dof = d.shr_act + 20 * m.nu;
+    d.shr_body = d.shr_dof + 16 * m.nv;
+    d.shr_mpair = d.shr_body + 8 * m.nbody;
+    d.shr_jump = d.shr_mpair + 4 * d.nMpair;
+    // the smooth-dynamics tables (from shr_act on) are staged only by lane-group kernels (G < 64);
+    // blocked mode (one env per workgroup) reads them from the model block instead of paying their
+    // LDS per env
+    shr_small = d.shr_act;
+    d.shr_total = d.shr_jump + d.njump * m.nbody;
+  };
+  layout_shared();
   // lanes per environment: the narrowest group that still gives every dof its own lane (the
   // dense M / Cholesky / PGS phases are lane-per-dof) and keeps a workgroup's LDS within 80 KB
   // (two workgroups per CU); MRS_GROUP overrides (16, 32 or 64)
@@ -1249,6 +1258,21 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   b.group = 64;
   for (int g : {32, 16})
     if (m.nv <= g && lds_bytes(g) <= 80 * 1024) b.group = g;
+  // a 16-lane model whose workgroup tables outgrow the two-per-CU budget (a dense lidar: the per-ray
+  // direction table is 16 B per ray) keeps its 16-lane groups rather than dropping to 32 (~4x slower
+  // on C3): the per-ray table moves out of LDS (rays read from the model block, L1/L2-resident: the
+  // pass's non-common path).  MRS_G16_ONE_WG also allows one workgroup per CU (up to 160 KB)
+  b.g16_one_wg = 0;
+  if (b.group > 16 && m.nv <= 16) {
+    if (d.rf_common) {
+      d.rf_common = 0;
+      layout_shared();
+      if (lds_bytes(16) <= 80 * 1024) b.group = 16;
+    }
+    // (one 160 KB workgroup per CU was measured slower than 32-lane groups on the mesh robot: 27 vs
+    // 15 ms per 10-step launch -- a single wave per SIMD cannot hide its memory latency)
+    if (b.group > 16 && lds_bytes(16) <= 160 * 1024 && std::getenv("MRS_G16_ONE_WG")) { b.group = 16; b.g16_one_wg = 1; }
+  }
   if (const char* e = std::getenv("MRS_GROUP")) {
     const int g = std::atoi(e);
     if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
@@ -1395,10 +1419,10 @@ void batch_free(BatchImpl* b) {
 int batch_num_envs(const BatchImpl* b) { return b->n; }
 
 int batch_layout(const BatchImpl* b, int* out, int n) {
-  const int v[8] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
-                    b->dm.max_con, b->dm.ntree};
+  const int v[11] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
+                     b->dm.max_con, b->dm.ntree, b->dm.shr_total, b->dm.rf_common, b->g16_one_wg};
   int k = 0;
-  for (; k < n && k < 8; ++k) out[k] = v[k];
+  for (; k < n && k < 11; ++k) out[k] = v[k];
   return k;
 }
 

@@ -50,8 +50,12 @@ __device__ __forceinline__ float ray_aabb(const float lo[3], const float hi[3], 
 // bvh / nnode: the mesh's bounding volume hierarchy (batch.hip build_mesh_bvh): 8 floats per node in
 // depth-first order -- AABB lo, the index of the node after its subtree (int bits), AABB hi, and for a
 // leaf (first << 8 | count) of its triangles in `face` (int bits; -1 for an inner node).  Stackless
-// traversal: a missed box, a box entered past the nearest hit, or a leaf jumps to the skip index, an
-// inner node that is hit descends to its first child (the next node).  nnode = 0: every triangle.
+// traversal per lane: a missed box, a box entered past the nearest hit, or a leaf jumps to the skip
+// index, an inner node that is hit descends to its first child (the next node); both successors are
+// loaded while a node is tested, so a step costs one memory latency.  nnode = 0: every triangle.
+// (A wave-coherent packet walk -- node index by ballot, scalar loads -- measured slower at both call
+// sites on the mesh robot: step 26.7 vs 12.8 ms, depth 501 vs 442 ms: the union of 64 rays' paths
+// visits far more nodes than one ray's.)
 template <class PV, class PF, class PS, class PN>
 __device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS s, const float lp[3],
                                           const float lv[3], PN bvh, int nnode, int* tri = nullptr) {
@@ -64,32 +68,36 @@ __device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS 
   if (nnode <= 0) {
     for (int f = 0; f < nface; ++f) {
       const float t = ray_tri(vert, face, f, lp, lv);
-      if (t >= 0 && (best < 0 || t < best)) {
-        best = t;
-        if (tri) *tri = f;
-      }
+      if (t >= 0 && (best < 0 || t < best)) { best = t; if (tri) *tri = f; }
     }
     return best;
   }
   const float iv[3] = {1.0f / lv[0], 1.0f / lv[1], 1.0f / lv[2]};
+  struct Node { float lo[3], hi[3]; int skip, leaf; };
+  auto load = [&](int k) {
+    const int o = 8 * k;
+    Node n;
+    n.lo[0] = bvh[o]; n.lo[1] = bvh[o + 1]; n.lo[2] = bvh[o + 2]; n.skip = __float_as_int(bvh[o + 3]);
+    n.hi[0] = bvh[o + 4]; n.hi[1] = bvh[o + 5]; n.hi[2] = bvh[o + 6]; n.leaf = __float_as_int(bvh[o + 7]);
+    return n;
+  };
   int i = 0;
+  Node cur = load(0);
   while (i < nnode) {
-    const int o = 8 * i;
-    const float lo[3] = {bvh[o], bvh[o + 1], bvh[o + 2]}, hi[3] = {bvh[o + 4], bvh[o + 5], bvh[o + 6]};
-    const int skip = __float_as_int(bvh[o + 3]), leaf = __float_as_int(bvh[o + 7]);
-    const float te = ray_aabb(lo, hi, lp, lv, iv);
+    const Node down = load(i + 1 < nnode ? i + 1 : i);
+    const Node side = load(cur.skip < nnode ? cur.skip : i);
+    const float te = ray_aabb(cur.lo, cur.hi, lp, lv, iv);
     const bool hit = te != 3.0e38f && (best < 0 || te <= best);
-    if (hit && leaf >= 0) {
-      const int f0 = leaf >> 8, nf = leaf & 0xff;
+    if (hit && cur.leaf >= 0) {
+      const int f0 = cur.leaf >> 8, nf = cur.leaf & 0xff;
       for (int f = f0; f < f0 + nf; ++f) {
         const float t = ray_tri(vert, face, f, lp, lv);
-        if (t >= 0 && (best < 0 || t < best)) {
-          best = t;
-          if (tri) *tri = f;
-        }
+        if (t >= 0 && (best < 0 || t < best)) { best = t; if (tri) *tri = f; }
       }
     }
-    i = hit && leaf < 0 ? i + 1 : skip;
+    const bool descend = hit && cur.leaf < 0;
+    i = descend ? i + 1 : cur.skip;
+    cur = descend ? down : side;
   }
   return best;
 }

@@ -4345,9 +4345,18 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     for (int j = 0; j < R; ++j) {
       const int k = k0 + j * stride;
       act[j] = k < m.nrf;
-      const lfloat* rr = shared_lds(m) + m.shr_rf + 4 * (act[j] ? k : 0);
-      const float dl[3] = {rr[0], rr[1], rr[2]};
-      adr[j] = __float_as_int(rr[3]);
+      // the ray table is staged in workgroup LDS only when every ray shares body and origin
+      // (rf_common); a pass that shares them in a model that does not reads the model block
+      float dl[3];
+      if (m.rf_common) {
+        const lfloat* rr = shared_lds(m) + m.shr_rf + 4 * (act[j] ? k : 0);
+        dl[0] = rr[0]; dl[1] = rr[1]; dl[2] = rr[2];
+        adr[j] = __float_as_int(rr[3]);
+      } else {
+        const CPtr<float> rr = m.rfray + 8 * (act[j] ? k : 0);
+        dl[0] = rr[0]; dl[1] = rr[1]; dl[2] = rr[2];
+        adr[j] = __float_as_int(rr[3]);
+      }
       bod[j] = b;
       if (m.rf_static_frame) { vec[j][0] = dl[0]; vec[j][1] = dl[1]; vec[j][2] = dl[2]; }
       else mat_vec(vec[j], bm, dl);

@@ -167,6 +167,81 @@ def test_rollout_parity(scene, n_envs, steps, group, monkeypatch):
         print(f"  {len(bad)} rangefinder outliers / flips, all grazing a silhouette")
 
 
+ARM7_1080 = ARM7.parent / "arm7_lidar1080.xml"
+
+
+TWO_LIDARS = """<mujoco><compiler angle="radian"/><option timestep="0.002"/>
+  <worldbody><geom type="plane" size="0 0 1"/>
+    <geom type="box" pos="1.5 0 0.5" size="0.2 0.6 0.5"/>
+    <geom type="sphere" pos="-1.2 0.8 0.6" size="0.3"/>
+    <body name="lidar_a" pos="0 0 0.5" quat="0.5 0.5 0.5 0.5">
+      <replicate count="90" sep="-" euler="0 0.0698132 0"><site name="ra"/></replicate>
+    </body>
+    <body name="lidar_b" pos="0.3 -0.4 0.7" quat="0.5 0.5 0.5 0.5">
+      <replicate count="90" sep="-" euler="0 0.0698132 0"><site name="rb"/></replicate>
+    </body>
+    <body name="ball" pos="0.8 0.3 0.5"><freejoint/><geom type="sphere" size="0.15"/></body>
+  </worldbody>
+  <sensor><rangefinder name="la" site="ra"/><rangefinder name="lb" site="rb"/></sensor></mujoco>"""
+
+
+def test_two_lidars_on_two_bodies():
+    """two replicate-built lidars on different bodies: no single ray frame for the model (rays read
+    from the model block), each pass still shares one lidar's body and origin; ranges against the
+    oracle within 2e-5 on >= 99.5% of rays, hit / miss identical on >= 99.8%"""
+    model = sim.Model.from_string(TWO_LIDARS)
+    n = 8
+    b = sim.Batch(model, n)
+    assert b.layout()["rf_common"] == 0
+    q = np.tile(model.qpos0, (n, 1))
+    q[:, 0] += np.linspace(-0.3, 0.3, n)
+    b.set(sim.FIELD_QPOS, q)
+    b.forward()
+    sd = b.get(sim.FIELD_SENSORDATA)
+    b.close()
+    same = close = total = 0
+    for e in range(n):
+        d = binding.OracleData(model)
+        d.qpos[:] = q[e]
+        d.forward()
+        ref = d.sensordata
+        same += int(np.sum((sd[e] >= 0) == (ref >= 0)))
+        close += int(np.sum(np.abs(sd[e] - ref) <= 2e-5 * np.maximum(np.abs(ref), 1)))
+        total += len(ref)
+    assert same >= 0.998 * total and close >= 0.995 * total, (same, close, total)
+
+
+def test_lidar1080_stays_on_16_lane_groups():
+    """a 1080-beam lidar on C3's arm: the per-ray table no longer fits the two-workgroups-per-CU LDS
+    budget, and the batch keeps its 16-lane groups (rays read from the model block) instead of
+    falling to 32-lane groups; 300 steps within 1e-5 of the oracle, rangefinders as in
+    test_rollout_parity"""
+    model = sim.Model.load(ARM7_1080)
+    b = sim.Batch(model, 16)
+    lay = b.layout()
+    b.close()
+    print(lay)
+    assert lay["group"] == 16
+    n_envs, steps, period = 16, 300, 10
+    envs = np.arange(n_envs)
+    qpos0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    ref = _oracle_rollout(model, qpos0, table, period, [steps])
+    got = _gpu_rollout(model, qpos0, table, period, [steps])
+    q_ref, v_ref, s_ref = ref[steps]
+    q, v, s = got[steps]
+    assert np.max(np.abs(q - q_ref) / _scale(q_ref)) <= RTOL
+    assert np.max(np.abs(v - v_ref) / _scale(v_ref)) <= RTOL
+    rf = np.array([i for i in range(model.nsensor) if model.sensor_type[i] == sim.SENS_RANGEFINDER])
+    adr = model.sensor_adr[rf]
+    assert len(rf) == 1080
+    flip = (s[:, adr] < 0) != (s_ref[:, adr] < 0)
+    assert np.mean(flip) <= 0.002
+    hit = (s_ref[:, adr] >= 0) & (s[:, adr] >= 0)
+    err = np.abs(s[:, adr][hit] - s_ref[:, adr][hit]) / np.maximum(1.0, s_ref[:, adr][hit])
+    assert np.mean(err > 2e-5) <= 0.005 and np.median(err) < 1e-6
+
+
 @pytest.mark.parametrize("group", [16, 64])
 def test_forward_lidar_closed_form(group, monkeypatch):
     monkeypatch.setenv("MRS_GROUP", str(group))
