@@ -1107,7 +1107,7 @@ enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 // around each phase, summed per wave and added to a device table at the end of the kernel.
 enum { PH_KIN, PH_COMPOS, PH_MAKEM, PH_CHOL, PH_COMVEL, PH_RNE, PH_SMOOTH, PH_COLL, PH_CONSTR, PH_SENS,
        PH_INTEG, PH_CHECK, PH_SENS_L1, PH_SENS_SETUP, PH_SENS_GEOMS, PH_CON_ROWS, PH_CON_REC, PH_CON_WARM,
-       PH_CON_PGS, PH_COLL_NARROW, PH_COLL_OUT, PH_COUNT };
+       PH_CON_PGS, PH_COLL_NARROW, PH_COLL_OUT, PH_CON_DEL, PH_COUNT };
 #ifdef MRS_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[PH_COUNT];
 #define SUB_T() __builtin_amdgcn_s_memtime()
@@ -3001,7 +3001,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         nia[j] = -1.0f / a;
         unroll<NL>([&](auto lc) { ARn[j][decltype(lc)::value] *= nia[j]; });
       });
-      SUB_ADD(PH_CON_REC, t_sub);
+      SUB_ADD(PH_CON_DEL, t_sub);
       t_sub = SUB_T();
       // warm start: forces of mj_constraintUpdate at qacc_warmstart (J of the held row over its
       // island's slots, qacc_warmstart gathered at the slots' dofs), kept if the dual cost is negative

@@ -166,7 +166,7 @@ def lib() -> C.CDLL:
 PHASES = ["kinematics", "com_pos", "make_M", "cholesky", "com_vel", "rne", "smooth_forces", "collision",
           "constraints", "sensors", "integrate", "checks", "sensors.level1", "sensors.setup", "sensors.geoms",
           "constraints.rows", "constraints.records", "constraints.warmstart", "constraints.pgs",
-          "collision.narrow", "collision.out"]
+          "collision.narrow", "collision.out", "constraints.delassus"]
 
 
 def phase_cycles(reset: bool = False) -> dict | None:

@@ -5,7 +5,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM secti
 FETCH_SIZE reports half of the bytes of wide coalesced streaming reads, so it is doubled here;
 WRITE_SIZE is taken as is.
 Usage: python scripts/pmc_summary.py OUT.json [cfg]
-  cfg c3 / c5: the fused multi-step launches (step_kernel<G, false>); c4: the depth kernel.
+  cfg c2 / c3 / c5: the fused multi-step launches (step_kernel<G, false>); c4 / c3m: the depth kernel.
 """
 import csv
 import json
@@ -14,7 +14,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 CFG = sys.argv[2] if len(sys.argv) > 2 else "c3"
-KERNEL = "depth_kernel" if CFG == "c4" else "step_kernel"
+KERNEL = "depth_kernel" if CFG in ("c4", "c3m") else "step_kernel"
 
 
 def per_launch(name: str) -> tuple[float, str, int]:
@@ -30,7 +30,7 @@ def per_launch(name: str) -> tuple[float, str, int]:
 
 fetch_kib, kname, n1 = per_launch("fetch")
 write_kib, _, n2 = per_launch("write")
-steps = 200 if CFG == "c4" else 5  # C4: 20 depth frames
+steps = {"c4": 200, "c3m": 20}.get(CFG, 5)  # C4: 20 depth frames, C3m: 2
 rec = {
     "kernel": kname,
     "config": CFG,
