@@ -422,6 +422,9 @@ def main():
             roof["flops_executed_per_env_step"] = fe
             roof["frac_executed"] = n * args.period * fe / (step_ms * 1e-3) / 1e12 / roofline.PEAK_FP32_TFLOPS
             roof["flops_executed_source"] = fl_src
+            roof["flops_executed_note"] = ("fp32 VALU instructions x 64 lanes (2 per FMA) of this kernel, "
+                                           "rocprofv3 SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32: an upper bound "
+                                           "(idle lanes of a 16-lane group count)")
     if sq_rec:
         # measured from SQ counters of the same command (rocprofv3 --pmc, scripts/sq_summary.py)
         roof["valu_measured"] = {k: sq_rec[k] for k in ("valu_issue_frac", "valu_tflops_upper", "valu_frac_upper",

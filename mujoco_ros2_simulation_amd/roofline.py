@@ -77,6 +77,9 @@ def _ancestors(m, i):
 SURVEY_PER_ENV_STEP = {
     "scene": (2.0e3, 72.0),          # C2: reference 2-DoF scene, dynamics only
     "arm7_lidar": (1.9e5, 1692.0),   # C3: 7-DoF arm + 360-ray lidar
+    # C3 with a 1080-beam lidar: SURVEY's C3 formula (rays x 12 geoms x ~40 + ~15k dynamics) at 1080
+    # rays; bytes: state 7 x 9 floats + 1080 ranges
+    "arm7_lidar1080": (1080 * 12 * 40 + 1.5e4, 4.0 * (63 + 1080 + 3)),
     "arm_boxes": (3.3e6, 1852.0),    # C5: arm + 8 free boxes, PGS 50 iterations
 }
 

@@ -6,8 +6,10 @@ SQ_INSTS_VALU_TRANS_F32, SQ_INSTS_VALU_FLOPS_FP32, SQ_WAVES, GRBM_GUI_ACTIVE.
 Per launch of the dominant kernel (step_kernel<G, false> or depth_kernel_v2):
   flops_fullwave  = 64 x (2 FMA + ADD + MUL + TRANS) instructions: every fp32 VALU instruction counted
                     as 64 active lanes (an upper bound: idle lanes of a 16-lane group are counted)
-  flops_counter   = SQ_INSTS_VALU_FLOPS_FP32 (gfx950: the hardware's fp32 flop count, MFMA excluded)
-  flops_executed  = flops_counter when it does not exceed flops_fullwave, else flops_fullwave
+  flops_counter   = SQ_INSTS_VALU_FLOPS_FP32 (gfx950: "FLOPS per instruction on float 32"), reported raw:
+                    it reads ~2% of flops_fullwave on C3, so its unit (per-SE sampling, per-instruction
+                    rather than per-lane counting) is not the lane-flop count this needs, and it is not used
+  flops_executed  = flops_fullwave (an upper bound: lanes idle in a 16-lane group's dof phases count)
   flops_executed_per_env_step = flops_executed / (envs x physics steps per launch)
 Kernel time: the bench line of the same config (gpurun_out/bench_<cfg>.json, in-bench HIP events).
 Usage: python scripts/flops_summary.py OUT.json cfg [envs] [steps_per_launch]
@@ -37,7 +39,7 @@ kms = bench["roofline"].get("step_kernel_ms") or bench["roofline"]["kernel_ms"]
 full = 64 * (2 * avg["SQ_INSTS_VALU_FMA_F32"] + avg["SQ_INSTS_VALU_ADD_F32"] + avg["SQ_INSTS_VALU_MUL_F32"]
              + avg["SQ_INSTS_VALU_TRANS_F32"])
 cnt = avg.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0)
-executed = cnt if 0 < cnt <= full * 1.0001 else full
+executed = full
 units = ENVS * STEPS
 tf = executed / (kms * 1e-3) / 1e12
 rec = {
