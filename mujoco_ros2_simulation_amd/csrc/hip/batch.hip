@@ -785,6 +785,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     d.pipe_w = 8;
     while (d.pipe_w < widest) d.pipe_w *= 2;
   }
+  d.sparse_off = std::getenv("MRS_SPARSE_OFF") ? std::atoi(std::getenv("MRS_SPARSE_OFF")) & 7 : 0;
   std::vector<int> fric, lim, rf;
   for (int j = 0; j < m.nv; ++j) if (m.dof_frictionloss[j] > 0) fric.push_back(j);
   for (int j = 0; j < m.njnt; ++j)
@@ -1294,7 +1295,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_J = take(dn * nv); S.efc_MJ = take(dn * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(dn); S.efc_aref = take(dn);
   S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));
-  S.efc_rec = take(d.blocked ? ne * (3 * d.pipe_w + 8) : 0);
+  S.efc_rec = take(d.blocked ? ne * (2 * d.pipe_w + 12) : 0);  // step.hip RF
   S.efc_rowof = take(d.blocked ? ne : 0);
   S.efc_item = take(d.blocked ? ne : 0);
   S.efc_fq = take(d.blocked ? ne : 0);

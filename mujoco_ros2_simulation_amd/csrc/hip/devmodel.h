@@ -51,7 +51,7 @@ struct LdsLayout {
 struct ScratchLayout {
   int efc_J, efc_MJ, efc_type, efc_pos, efc_margin, efc_floss, efc_R, efc_aref, efc_b, efc_f,
       efc_ARii, con, stage,  // contact records (kConRec floats each); per-lane narrow-phase staging
-      efc_rec,               // blocked mode: row records in solver order (3 * pipe_w + 8 floats each)
+      efc_rec,               // blocked mode: row records in solver order (2 * pipe_w + 12 floats each)
       efc_rowof,             // blocked mode: row index of each record (int bits)
       efc_item,              // blocked mode: first row of the item starting at a record (int bits)
       efc_fq,                // blocked mode: row forces by record (global-record fallback path)
@@ -75,6 +75,9 @@ struct DevModel {
   // kinematic trees with dofs; blocked: M per tree + sparse constraint rows (set when G = 64);
   // pipe_w: dof slots per constraint row in the sparse solver (64 / pipe_w rows in flight per wave)
   int ntree, tree_nmax, nMblk, blocked, pipe_w;
+  // sparse solver paths switched off (tests, A/B): bit 0 island-dual, bit 1 item-blocked, bit 2
+  // register-resident (all off: the global-record solve); MRS_SPARSE_OFF
+  int sparse_off;
   // workgroup-shared LDS tables (one copy per workgroup, after its envs' working sets; offsets in
   // floats from the start of the dynamic LDS): the ray-geom records (8 floats each) at shr_off, and
   // when rf_common the per-ray direction + sensordata address (4 floats each) at shr_off + shr_rf.

@@ -2361,8 +2361,9 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
 // is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
 typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int kHdr = 24;     // item header floats (blocked mode; batch.hip sizes efc_hdr to match)
-constexpr int kRecScal = 8;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, then the coupling
-                             // J_r M^-1 J_s' of row r to the earlier rows s < r of its item (3 floats)
+constexpr int kRecScal = 12;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, then the coupling
+                              // J_r M^-1 J_s' of row r to the earlier rows s < r of its item (3 floats),
+                              // J qacc_warmstart - aref, 3 pad
 #ifndef MRS_REG_QUADS
 #define MRS_REG_QUADS 12
 #endif
@@ -2499,6 +2500,73 @@ __device__ __forceinline__ void pipe_msolve3(const DevModel& m, const lfloat* Lf
     }
   }
 }
+// y = L^-1 v, the forward half of pipe_msolve3.  With M = L L' per tree, a row's record holds
+// Y = L^-1 J' over its slots only: J_r M^-1 J_s' = Y_r . Y_s, and the solvers that track qacc work on
+// w = L' qacc instead (J qacc = Y . w, and a force step df moves w by Y df); tree_epilogue maps back.
+__device__ __forceinline__ void pipe_lsolve3(const DevModel& m, const lfloat* Lf, const SlotMap& sm, int pbase,
+                                             const float v[3], float x[3]) {
+  const int li = sm.li, n = sm.n;
+  const lfloat* Lb = Lf + sm.off;
+  for (int i = 0; i < 3; ++i) x[i] = sm.d >= 0 ? v[i] : 0.0f;
+  const int src = pbase + sm.sb;
+  #pragma unroll 1
+  for (int k = 0; k < m.tree_nmax; ++k) {
+    float xs[3];
+    for (int i = 0; i < 3; ++i) xs[i] = __shfl(x[i], src + k);
+    if (k < n) {
+      const float inv = 1.0f / Lb[k * n + k];
+      const float lik = li > k ? Lb[li * n + k] : 0.0f;
+      for (int i = 0; i < 3; ++i) {
+        const float xk = xs[i] * inv;
+        x[i] = li == k ? xk : (li > k ? x[i] - lik * xk : x[i]);
+      }
+    }
+  }
+}
+// lane per dof (blocked mode, nv <= 64): the dof's tree segment in the LDS factor
+struct DofTree { int adr, li, n; const lfloat* Lb; };
+__device__ __forceinline__ DofTree dof_tree_lds(const DevModel& m, const lfloat* s, const LdsLayout& L, int lane) {
+  DofTree r{0, 0, 0, s + L.L};
+  if (lane < m.nv) {
+    const TreeInfo ti = tree_lds(s, L, m.dof_tree[lane]);
+    r.adr = ti.adr; r.li = lane - ti.adr; r.n = ti.num; r.Lb += ti.off;
+  }
+  return r;
+}
+// w = L' q per tree (lane per dof)
+__device__ __forceinline__ float tree_lt_mul(const DevModel& m, const DofTree& t, float q) {
+  float w = 0;
+  #pragma unroll 1
+  for (int k = 0; k < m.tree_nmax; ++k) {
+    const float qk = __shfl(q, min(t.adr + k, 63));
+    if (k >= t.li && k < t.n) w += t.Lb[k * t.n + t.li] * qk;
+  }
+  return w;
+}
+// sparse solver epilogue: z = sum_r Y_r f_r per dof in tmp -> qfrc_constraint = J' f = L z (written
+// to tmp) and qacc = qacc_smooth + M^-1 J' f = qacc_smooth + L'^-1 z (written to qa and returned)
+__device__ __forceinline__ float tree_epilogue(const DevModel& m, const lfloat* s, const LdsLayout& L, lfloat* tmp,
+                                               lfloat* qa, float qacc_s, int lane) {
+  const DofTree t = dof_tree_lds(m, s, L, lane);
+  const float z = lane < m.nv ? tmp[lane] : 0.0f;
+  float y = 0, acc = z, x = 0;
+  #pragma unroll 1
+  for (int k = 0; k < m.tree_nmax; ++k) {
+    const float zk = __shfl(z, min(t.adr + k, 63));
+    if (k <= t.li && k < t.n) y += t.Lb[t.li * t.n + k] * zk;
+  }
+  #pragma unroll 1
+  for (int k = m.tree_nmax - 1; k >= 0; --k) {
+    if (t.li == k && k < t.n) x = acc / t.Lb[k * t.n + k];
+    const float xs = __shfl(x, min(t.adr + k, 63));
+    if (k < t.n && t.li < k) acc -= t.Lb[k * t.n + t.li] * xs;
+  }
+  const float qacc = qacc_s + x;
+  wsync();
+  if (lane < m.nv) { tmp[lane] = y; qa[lane] = qacc; }
+  wsync();
+  return lane < m.nv ? qacc : 0.0f;
+}
 __device__ __forceinline__ int wave_max(int v) {
   #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
@@ -2508,21 +2576,29 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mask), 0));
 }
+// v = own on lanes O, O + 16, O + 32, O + 48 (slot O of every 16-lane pipe), other elsewhere: one
+// v_cndmask with a constant lane mask (no per-use compare)
+template <int O>
+__device__ __forceinline__ float sel_slot16(float own, float other) {
+  constexpr unsigned long long mask = 0x0001000100010001ull << O;
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(own), "s"(mask));
+  return r;
+}
 // one record as the sweeps read it
 template <int P>
 struct RowRec {
-  float J, MJ, aref, R, a, bound;
+  float Y, aref, R, a, bound;
   int d;
 };
 template <int P>
 __device__ __forceinline__ RowRec<P> load_rec(const gfloat* rec, int q, int slot) {
-  constexpr int RF = 3 * P + kRecScal;
+  constexpr int RF = 2 * P + kRecScal;
   const gfloat* r = rec + q * RF;
   RowRec<P> o;
-  o.J = r[slot];
-  o.MJ = r[P + slot];
-  o.d = __float_as_int(r[2 * P + slot]);
-  const v4f sc = *(const __attribute__((address_space(1))) v4f*)(r + 3 * P);
+  o.Y = r[slot];
+  o.d = __float_as_int(r[P + slot]);
+  const v4f sc = *(const __attribute__((address_space(1))) v4f*)(r + 2 * P);
   o.aref = sc.x; o.R = sc.y; o.a = sc.z; o.bound = sc.w;
   return o;
 }
@@ -2533,7 +2609,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   ncon = uniform_int(ncon);
   constexpr int NP = 64 / P;
-  constexpr int RF = 3 * P + kRecScal;
+  constexpr int RF = 2 * P + kRecScal;
   const int pipe = lane / P, slot = lane % P, pbase = pipe * P;
   const int nv = m.nv, ME = m.max_efc;
   gfloat* type = scr + S.efc_type;
@@ -2809,10 +2885,12 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   t_sub = SUB_T();
 
   // --- 3. records, one item per pipe per level: J of the item's rows from the contact Jacobian
-  // (jc: normal and two tangent rows, pyramid edges jc0 +- mu jck), M^-1 of the three jc vectors in
-  // one interleaved block solve, impedance once per item
+  // (jc: normal and two tangent rows, pyramid edges jc0 +- mu jck), Y = L^-1 J' of the three jc
+  // vectors in one interleaved forward substitution, impedance once per item; the row scalars that
+  // need J itself (J qvel, J qacc_smooth, J qacc_warmstart) are taken here, so records hold Y only
   gfloat* quadtab = scr + S.efc_quad;  // per pipe, its first 16 items in order: record | rows << 16
   int my_nq = 0;                        // items of this lane's pipe
+  const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
   {
     const int my_end = my_start + my_n;
     int qc = my_start;
@@ -2869,40 +2947,36 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         // friction loss: e_dof; limit: +-e_dof (dof and J value in the header)
         jc[0] = d == __float_as_int(h2.w) ? h2.x : 0.0f;
       }
-      float mjc[3];
-      pipe_msolve3(m, s + L.L, sm, pbase, jc, mjc);
+      float yc[3];
+      pipe_lsolve3(m, s + L.L, sm, pbase, jc, yc);
       const float qv = d >= 0 ? s[L.qvel + d] : 0.0f, qs = d >= 0 ? s[L.qacc_smooth + d] : 0.0f;
+      const float qw = warm && d >= 0 ? s[L.qacc_ws + d] : 0.0f;
       if (act && slot == 0 && my_nq < 16) quadtab[pipe * 16 + my_nq] = __int_as_float(q0 | (nr << 16));
-      float MJk[3] = {0, 0, 0};  // M^-1 J' of the item's earlier rows (for the couplings)
+      float Yk[3] = {0, 0, 0};  // Y of the item's earlier rows (for the couplings)
       unroll<4>([&](auto jcst) {
         constexpr int j = decltype(jcst)::value;
         constexpr int k = 1 + (j >> 1);
         constexpr float sg = (j & 1) ? -1.0f : 1.0f;
         const float J = dim == 1 ? jc[0] : jc[0] + sg * mu * jc[k];
-        const float MJ = dim == 1 ? mjc[0] : mjc[0] + sg * mu * mjc[k];
+        const float Y = dim == 1 ? yc[0] : yc[0] + sg * mu * yc[k];
         if (j == 0 || __any(act && j < nr)) {
-          const float vel = gsum<P>(J * qv), jqs = gsum<P>(J * qs), jmj = gsum<P>(J * MJ);
+          const float vel = gsum<P>(J * qv), jqs = gsum<P>(J * qs), yy = gsum<P>(Y * Y);
+          const float jw = warm ? gsum<P>(J * qw) : 0.0f;
           const float aref = -B * vel - pterm;
           float cpl[3] = {0, 0, 0};
           unroll<3>([&](auto sc) {
             constexpr int s_ = decltype(sc)::value;
-            if constexpr (s_ < j) cpl[s_] = gsum<P>(J * MJk[s_]);
+            if constexpr (s_ < j) cpl[s_] = gsum<P>(Y * Yk[s_]);
           });
-          if constexpr (j < 3) MJk[j] = MJ;
+          if constexpr (j < 3) Yk[j] = Y;
           if (act && j < nr) {
             gfloat* o = rec + (q0 + j) * RF;
-            o[slot] = J;
-            o[P + slot] = MJ;
-            o[2 * P + slot] = __int_as_float(d);
+            o[slot] = Y;
+            o[P + slot] = __int_as_float(d);
             if (slot == 0) {
-              o[3 * P + 0] = aref;
-              o[3 * P + 1] = R;
-              o[3 * P + 2] = jmj + R;
-              o[3 * P + 3] = bound;
-              o[3 * P + 4] = jqs - aref;
-              o[3 * P + 5] = cpl[0];
-              o[3 * P + 6] = cpl[1];
-              o[3 * P + 7] = cpl[2];
+              *(__attribute__((address_space(1))) v4f*)(o + 2 * P) = (v4f){aref, R, yy + R, bound};
+              *(__attribute__((address_space(1))) v4f*)(o + 2 * P + 4) = (v4f){jqs - aref, cpl[0], cpl[1], cpl[2]};
+              o[2 * P + 8] = jw - aref;
               rowof[q0 + j] = __int_as_float(r0 + j);
             }
           }
@@ -2916,8 +2990,12 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   wsync();
   SUB_ADD(PH_CON_REC, t_sub);
   t_sub = SUB_T();
-  if (lane < nv) qa[lane] = qacc_s;
-  const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
+  // the qacc-tracking solvers below work on w = L' qacc (the dual solve does not read qa)
+  const DofTree dtree = dof_tree_lds(m, s, L, lane);
+  {
+    const float ws = tree_lt_mul(m, dtree, qacc_s);
+    if (lane < nv) qa[lane] = ws;
+  }
 
   // --- island-dual register solve (P = 16, island slot frames, at most kDualLevels rows per pipe).
   // mj_solPGS on the dual, as the oracle's fwd_constraint: row r's residual g_r = b_r + sum_s AR_rs f_s
@@ -2931,8 +3009,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   // step from the records: lane slot's held row J (16 slots) times each level's M^-1 J' broadcast slot
   // by slot (DPP row broadcast folded into the FMA).
   if constexpr (P == 16) {
-    if (isl_ok && nlev <= kDualLevels) {
+    if (isl_ok && nlev <= kDualLevels && !(m.sparse_off & 1)) {
       constexpr int NL = kDualLevels, NJ = NL / 16;
+      const int nch = (nlev + 15) >> 4;  // 16-level chunks of the sweeps (AR zero past nlev)
       typedef float v2f __attribute__((ext_vector_type(2)));
       // ARn[j][l] = -AR_rl / A_rr of held row r = 16 j + slot: the sweeps carry the normalised
       // residual gn_r = -g_r / A_rr (the unclamped step), so a level's step is one med3 of it
@@ -2955,21 +3034,21 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
             Jt[j][4 * q] = act ? v.x : 0.0f; Jt[j][4 * q + 1] = act ? v.y : 0.0f;
             Jt[j][4 * q + 2] = act ? v.z : 0.0f; Jt[j][4 * q + 3] = act ? v.w : 0.0f;
           });
-          const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
+          const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 2 * P);
           const float bound = sc.w;
           lh[j] = (v2f){act && bound >= 0 ? -bound : 0.0f,     // friction loss: [-frictionloss, frictionloss]
                         act && bound >= 0 ? bound : 3.0e38f};  // others: [0, inf)
-          bb[j] = act ? o[3 * P + 4] : 0.0f;
+          bb[j] = act ? o[2 * P + 4] : 0.0f;
           fr[j] = act ? sc.y : 0.0f;                           // R, folded into the diagonal below
-          hisl[j] = act ? __float_as_int(o[2 * P]) : -1;
+          hisl[j] = act ? __float_as_int(o[P]) : -1;
         });
-        // AR[j][l] = J_(16j+slot) . M^-1 J_l': each level's M^-1 J' (lane = slot) read once and
-        // broadcast slot by slot into the FMAs of the three held rows
+        // AR[j][l] = Y_(16j+slot) . Y_l: each level's Y (lane = slot) read once and broadcast slot
+        // by slot into the FMAs of the three held rows
         unroll<NL>([&](auto lc) {
           constexpr int l = decltype(lc)::value;
           unroll<NJ>([&](auto jc) { ARn[decltype(jc)::value][l] = 0.0f; });
           if (l < nlev) {
-            const float mj = l < my_n ? rec[(my_start + l) * RF + P + slot] : 0.0f;
+            const float mj = l < my_n ? rec[(my_start + l) * RF + slot] : 0.0f;
             const int il = __float_as_int(rowb<l % 16>(__int_as_float(hisl[l / 16])));
             unroll<NJ>([&](auto jc) {
               constexpr int j = decltype(jc)::value;
@@ -3003,8 +3082,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       });
       SUB_ADD(PH_CON_DEL, t_sub);
       t_sub = SUB_T();
-      // warm start: forces of mj_constraintUpdate at qacc_warmstart (J of the held row over its
-      // island's slots, qacc_warmstart gathered at the slots' dofs), kept if the dual cost is negative
+      // warm start: forces of mj_constraintUpdate at qacc_warmstart (J qacc_warmstart - aref from
+      // the record), kept if the dual cost is negative
       unroll<NJ>([&](auto jc) { fr[decltype(jc)::value] = 0.0f; });
       if (warm) {
         unroll<NJ>([&](auto jc) {
@@ -3012,15 +3091,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           const int k = 16 * j + slot;
           const bool act = k < my_n;
           const gfloat* o = rec + (act ? my_start + k : 0) * RF;
-          float jar = act ? -o[3 * P] : 0.0f;  // -aref
-          #pragma unroll 4
-          for (int q = 0; q < 16; ++q) {
-            const int d = act ? __float_as_int(o[2 * P + q]) : -1;
-            const float J = act ? o[q] : 0.0f;
-            jar += d >= 0 ? J * s[L.qacc_ws + d] : 0.0f;
-          }
+          const float jar = act ? o[2 * P + 8] : 0.0f;
           if (act) {
-            const float R = o[3 * P + 1];
+            const float R = o[2 * P + 1];
             const float D = 1.0f / R, hi = lh[j].y;
             fr[j] = lh[j].x < 0 ? (jar <= -R * hi ? hi : (jar >= R * hi ? -hi : -D * jar))
                                 : (jar < 0 ? -D * jar : 0.0f);
@@ -3051,55 +3124,63 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       // of the pipe moves its normalised residual by ARn delta (DPP row broadcast of the step folded
       // into the FMA); the owner's improvement term -delta (res + A delta / 2) = A delta (gn - delta/2)
       // is accumulated per held row and scaled by A once per sweep
-      int slot_v = slot;
+      // A held row moves its own bounds and improvement term only at its own level, and reads them
+      // nowhere else in the sweep, so the owner just keeps its residual at that level (gb, one lane
+      // select with a constant lane mask) and the bounds / improvement of all held rows are updated
+      // together after the sweep: a level is med3 + DPP broadcast + the FMAs + one select.  Levels run
+      // in chunks of 16 (levels past nlev hold neutral rows: zero AR rows, step 0).
       int nit = 0;
       #pragma unroll 1
       for (int it = 0; it < m.iterations; ++it) {
-        asm volatile("" : "+v"(slot_v));
-        float impj[NJ];
-        unroll<NJ>([&](auto jc) { impj[decltype(jc)::value] = 0.0f; });
-        unroll<NL>([&](auto kc) {
-          constexpr int k = decltype(kc)::value, j = k / 16, o = k % 16;
-          if (k < nlev) {
-            const float cand = __builtin_amdgcn_fmed3f(gn[j], lh[j].x, lh[j].y);
-            const float dm = slot_v == o ? cand : 0.0f;
-            impj[j] = fmaf(dm, fmaf(-0.5f, dm, gn[j]), impj[j]);
-            lh[j] -= (v2f){dm, dm};
-            const float dl = rowb<o>(cand);
-            unroll<NJ>([&](auto jc) { gn[decltype(jc)::value] += ARn[decltype(jc)::value][k] * dl; });
+        float gb[NJ];
+        unroll<NJ>([&](auto jc) { gb[decltype(jc)::value] = gn[decltype(jc)::value]; });
+        unroll<NJ>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if (j < nch) {
+            unroll<16>([&](auto oc) {
+              constexpr int o = decltype(oc)::value, k = 16 * j + o;
+              const float cand = __builtin_amdgcn_fmed3f(gn[j], lh[j].x, lh[j].y);
+              gb[j] = sel_slot16<o>(gn[j], gb[j]);
+              const float dl = rowb<o>(cand);
+              unroll<NJ>([&](auto jc2) { gn[decltype(jc2)::value] += ARn[decltype(jc2)::value][k] * dl; });
+            });
           }
         });
         float imp = 0;
-        unroll<NJ>([&](auto jc) { imp += A[decltype(jc)::value] * impj[decltype(jc)::value]; });
+        unroll<NJ>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const float dm = __builtin_amdgcn_fmed3f(gb[j], lh[j].x, lh[j].y);
+          imp += A[j] * fmaf(dm, fmaf(-0.5f, dm, gb[j]), 0.0f);
+          lh[j] -= (v2f){dm, dm};
+        });
         const float improvement = gsum<64>(imp);
         nit = it + 1;
         if (improvement * m.pgs_scale < m.tolerance) break;
       }
       if (lane == 0) s[L.niter] = __int_as_float(nit);
       SUB_ADD(PH_CON_PGS, t_sub);
-      // forces f = lo - (lo - f); qfrc_constraint = J' f and qacc = qacc_smooth + M^-1 J' f per level
+      // forces f = lo - (lo - f); z = sum Y' f per level, then qfrc_constraint and qacc from z
       unroll<NJ>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const int k = 16 * j + slot;
-        const float bound = k < my_n ? rec[(my_start + k) * RF + 3 * P + 3] : -1.0f;
+        const float bound = k < my_n ? rec[(my_start + k) * RF + 2 * P + 3] : -1.0f;
         fr[j] = (bound >= 0 ? -bound : 0.0f) - lh[j].x;
       });
       if (lane < nv) tmp[lane] = 0;
-      if (lane == 0) { qa[nv] = 0; tmp[nv] = 0; }
       wsync();
       #pragma unroll 1
       for (int l = 0; l < nlev; ++l) {
         const int q = l < my_n ? my_start + l : 0;
         const gfloat* o = rec + q * RF;
-        const int d = l < my_n ? __float_as_int(o[2 * P + slot]) : -1;
-        const float J = o[slot], MJ = o[P + slot];
+        const int d = l < my_n ? __float_as_int(o[P + slot]) : -1;
+        const float Y = o[slot];
         float f = 0;  // the level's force, from its owner lane l % 16 of the pipe
         unroll<NJ>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
           const float fj = __shfl(fr[j], pbase + (l & 15));
           if ((l >> 4) == j) f = fj;
         });
-        if (d >= 0) { tmp[d] += J * f; qa[d] += MJ * f; }
+        if (d >= 0) tmp[d] += Y * f;
       }
       unroll<NJ>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -3107,7 +3188,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         if (k < my_n) ffg[__float_as_int(rowof[my_start + k])] = fr[j];
       });
       wsync();
-      return lane < nv ? qa[lane] : 0.0f;
+      return tree_epilogue(m, s, L, tmp, qa, qacc_s, lane);
     }
   }
 
@@ -3117,12 +3198,13 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   // visits an item with one LDS read of qacc, the four J qacc sums as independent DPP reductions, the
   // rows' Gauss-Seidel updates as a scalar chain through the couplings c_rs = J_r M^-1 J_s' (row r
   // sees qacc + sum_{s<r} M^-1 J_s' df_s, so J_r qacc moves by sum c_rs df_s: the same iterates as
-  // the row-serial sweep), and one LDS write of qacc + sum_r M^-1 J_r' df_r.  Lane (pipe, slot) keeps
-  // J and M^-1 J' of its slot for every level; the scalars of level k live in slot k % 16.
+  // the row-serial sweep), and one LDS write of qacc + sum_r M^-1 J_r' df_r -- all in w = L' qacc,
+  // where J qacc = Y . w and a step moves w by Y df.  Lane (pipe, slot) keeps Y of its slot for every
+  // level; the scalars of level k live in slot k % 16.
   if constexpr (P == 16) {
-    if (nq_max <= kRegQuads) {
+    if (nq_max <= kRegQuads && !(m.sparse_off & 2)) {
       constexpr int NQ = kRegQuads, NL = 4 * NQ, NB = NL / 16;
-      float Jr[NL], MJr[NL], sa[NB], sR[NB], sA[NB], sLo[NB], sHi[NB], sB[NB], fr[NB];
+      float Yr[NL], sa[NB], sR[NB], sA[NB], sLo[NB], sHi[NB], sB[NB], sW[NB], fr[NB];
       float sC0[NB], sC1[NB], sC2[NB];
       unsigned dpk[(NQ + 3) / 4];
       const unsigned dummy = static_cast<unsigned>(nv);
@@ -3130,17 +3212,17 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       unroll<(NQ + 3) / 4>([&](auto ic) { dpk[decltype(ic)::value] = dummy * 0x01010101u; });
       unroll<NB>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        sa[i] = 0; sR[i] = 1; sA[i] = 1; sLo[i] = 0; sHi[i] = 3.0e38f; sB[i] = 0; fr[i] = 0;
+        sa[i] = 0; sR[i] = 1; sA[i] = 1; sLo[i] = 0; sHi[i] = 3.0e38f; sB[i] = 0; sW[i] = 0; fr[i] = 0;
         sC0[i] = 0; sC1[i] = 0; sC2[i] = 0;
       });
       unroll<NQ>([&](auto qc) {
         constexpr int i = decltype(qc)::value;
-        unroll<4>([&](auto rc) { Jr[4 * i + decltype(rc)::value] = 0; MJr[4 * i + decltype(rc)::value] = 0; });
+        unroll<4>([&](auto rc) { Yr[4 * i + decltype(rc)::value] = 0; });
         if (i < nq_max) {
           const bool act = i < my_nq;
           const int qt = act ? __float_as_int(quadtab[pipe * 16 + i]) : 0;
           const int q = qt & 0xffff, nr = qt >> 16;
-          const int d = __float_as_int(rec[q * RF + 2 * P + slot]);
+          const int d = __float_as_int(rec[q * RF + P + slot]);
           if (act) {
             const unsigned di = d >= 0 ? static_cast<unsigned>(d) : dummy;
             dpk[i / 4] = (dpk[i / 4] & ~(0xffu << (8 * (i % 4)))) | (di << (8 * (i % 4)));
@@ -3149,16 +3231,16 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
             constexpr int r = decltype(rc)::value, k = 4 * i + r;
             if (act && r < nr) {
               const gfloat* o = rec + (q + r) * RF;
-              Jr[k] = o[slot];
-              MJr[k] = o[P + slot];
+              Yr[k] = o[slot];
               if (slot == k % 16) {
-                const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
-                const v4f sd = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P + 4);
+                const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 2 * P);
+                const v4f sd = *(const __attribute__((address_space(1))) v4f*)(o + 2 * P + 4);
                 sa[k / 16] = sc.x; sR[k / 16] = sc.y; sA[k / 16] = sc.z;
                 sLo[k / 16] = sc.w >= 0 ? -sc.w : 0.0f;     // friction: [-frictionloss, frictionloss]
                 sHi[k / 16] = sc.w >= 0 ? sc.w : 3.0e38f;   // others: [0, inf)
                 sB[k / 16] = sd.x;
                 sC0[k / 16] = sd.y; sC1[k / 16] = sd.z; sC2[k / 16] = sd.w;
+                sW[k / 16] = o[2 * P + 8];
               }
             }
           });
@@ -3173,14 +3255,13 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       unroll<NQ>([&](auto qc) {
         constexpr int i = decltype(qc)::value;
         if (i < nq_max) {
-          const float w = warm ? s[L.qacc_ws + dof_of(qc)] : 0.0f;
           unroll<4>([&](auto rc) {
             constexpr int k = 4 * i + decltype(rc)::value;
             float f = 0;
             if (warm) {
-              const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+              const float R = rowb<k % 16>(sR[k / 16]);
               const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
-              const float jar = gsum<16>(Jr[k] * w) - aref;
+              const float jar = rowb<k % 16>(sW[k / 16]);
               const float D = 1.0f / R;
               if (lo < 0) f = jar <= -R * hi ? hi : (jar >= R * hi ? -hi : -D * jar);
               else f = jar < 0 ? -D * jar : 0.0f;
@@ -3199,7 +3280,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
             float acc = 0;
             unroll<4>([&](auto rc) {
               constexpr int k = 4 * i + decltype(rc)::value;
-              acc += MJr[k] * rowb<k % 16>(fr[k / 16]);
+              acc += Yr[k] * rowb<k % 16>(fr[k / 16]);
             });
             tmp[d] += acc;
           }
@@ -3212,7 +3293,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
             const float t = tmp[dof_of(qc)];
             unroll<4>([&](auto rc) {
               constexpr int k = 4 * i + decltype(rc)::value;
-              const float jv = gsum<16>(Jr[k] * t);
+              const float jv = gsum<16>(Yr[k] * t);
               const float f = rowb<k % 16>(fr[k / 16]), R = rowb<k % 16>(sR[k / 16]), b = rowb<k % 16>(sB[k / 16]);
               cost += f * (0.5f * (jv + R * f) + b);
             });
@@ -3245,7 +3326,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
             float jq[4], df[4] = {0, 0, 0, 0};
             unroll<4>([&](auto rc) {
               constexpr int r = decltype(rc)::value;
-              jq[r] = gsum<16>(Jr[4 * i + r] * qd);
+              jq[r] = gsum<16>(Yr[4 * i + r] * qd);
             });
             float upd = 0;
             unroll<4>([&](auto rc) {
@@ -3261,7 +3342,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
               const float res = c - aref + R * f0;
               const float nf = __builtin_amdgcn_fmed3f(f0 - res * __builtin_amdgcn_rcpf(a), lo, hi);
               df[r] = nf - f0;
-              upd += MJr[k] * df[r];
+              upd += Yr[k] * df[r];
               fr[k / 16] = slot_v == k % 16 ? nf : fr[k / 16];
               improvement -= df[r] * res + 0.5f * df[r] * df[r] * a;
             });
@@ -3284,7 +3365,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           float acc = 0;
           unroll<4>([&](auto rc) {
             constexpr int k = 4 * i + decltype(rc)::value;
-            acc += Jr[k] * rowb<k % 16>(fr[k / 16]);
+            acc += Yr[k] * rowb<k % 16>(fr[k / 16]);
           });
           tmp[dof_of(qc)] += acc;
         }
@@ -3298,46 +3379,46 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         }
       });
       wsync();
-      return lane < nv ? qa[lane] : 0.0f;
+      return tree_epilogue(m, s, L, tmp, qa, qacc_s, lane);
     }
   }
 
-  // --- register-resident solve: P = 16 and at most kRegLevels rows per pipe.  Lane (pipe, slot)
-  // keeps J, M^-1 J' and the dof of its slot for every level (slots outside the row's trees point at
-  // a dummy LDS word after qacc, with J = M^-1 J' = 0); the row scalars and the force of level k live
+  // --- register-resident solve: P = 16 and at most kRegLevels rows per pipe, on w = L' qacc.  Lane
+  // (pipe, slot) keeps Y and the dof of its slot for every level (slots outside the row's trees point
+  // at a dummy LDS word after qacc, with Y = 0); the row scalars and the force of level k live
   // in slot k % 16 and reach the pipe by one DPP row broadcast each.  A level is branch-free: pipes
   // with fewer rows run neutral rows (J = 0, R = a = 1, bounds [0, inf)), whose force stays 0.
   // Sweeps touch LDS only for qacc.
   if constexpr (P == 16) {
-    if (nlev <= kRegLevels) {
+    if (nlev <= kRegLevels && !(m.sparse_off & 4)) {
       constexpr int NL = kRegLevels, NB = NL / 16;
-      float Jr[NL], MJr[NL], sa[NB], sR[NB], sA[NB], sLo[NB], sHi[NB], fr[NB];
+      float Yr[NL], sa[NB], sR[NB], sA[NB], sLo[NB], sHi[NB], sW[NB], fr[NB];
       unsigned dpk[NL / 4];
       const unsigned dummy = static_cast<unsigned>(nv);
       if (lane == 0) { qa[nv] = 0; tmp[nv] = 0; }
       unroll<NL / 4>([&](auto ic) { dpk[decltype(ic)::value] = dummy * 0x01010101u; });
       unroll<NB>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        sa[i] = 0; sR[i] = 1; sA[i] = 1; sLo[i] = 0; sHi[i] = 3.0e38f; fr[i] = 0;
+        sa[i] = 0; sR[i] = 1; sA[i] = 1; sLo[i] = 0; sHi[i] = 3.0e38f; sW[i] = 0; fr[i] = 0;
       });
       unroll<NL>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        Jr[k] = 0; MJr[k] = 0;
+        Yr[k] = 0;
         if (k < nlev) {
           const bool act = k < my_n;
           const gfloat* o = rec + (act ? my_start + k : 0) * RF;
-          const int d = __float_as_int(o[2 * P + slot]);
+          const int d = __float_as_int(o[P + slot]);
           if (act) {
-            Jr[k] = o[slot];
-            MJr[k] = o[P + slot];
+            Yr[k] = o[slot];
             const unsigned di = d >= 0 ? static_cast<unsigned>(d) : dummy;
             dpk[k / 4] = (dpk[k / 4] & ~(0xffu << (8 * (k % 4)))) | (di << (8 * (k % 4)));
           }
           if (act && slot == k % 16) {
-            const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 3 * P);
+            const v4f sc = *(const __attribute__((address_space(1))) v4f*)(o + 2 * P);
             sa[k / 16] = sc.x; sR[k / 16] = sc.y; sA[k / 16] = sc.z;
             sLo[k / 16] = sc.w >= 0 ? -sc.w : 0.0f;     // friction: [-frictionloss, frictionloss]
             sHi[k / 16] = sc.w >= 0 ? sc.w : 3.0e38f;   // others: [0, inf)
+            sW[k / 16] = o[2 * P + 8];
           }
         }
       });
@@ -3350,12 +3431,11 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       unroll<NL>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         if (k < nlev) {
-          const int d = dof_of(kc);
           float f = 0;
           if (warm) {
-            const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
+            const float R = rowb<k % 16>(sR[k / 16]);
             const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
-            const float jar = gsum<16>(Jr[k] * s[L.qacc_ws + d]) - aref;
+            const float jar = rowb<k % 16>(sW[k / 16]);
             const float D = 1.0f / R;
             if (lo < 0) f = jar <= -R * hi ? hi : (jar >= R * hi ? -hi : -D * jar);
             else f = jar < 0 ? -D * jar : 0.0f;
@@ -3370,7 +3450,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           constexpr int k = decltype(kc)::value;
           if (k < nlev) {
             const int d = dof_of(kc);
-            tmp[d] += MJr[k] * rowb<k % 16>(fr[k / 16]);
+            tmp[d] += Yr[k] * rowb<k % 16>(fr[k / 16]);
           }
         });
         wsync();
@@ -3379,9 +3459,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           constexpr int k = decltype(kc)::value;
           if (k < nlev) {
             const int d = dof_of(kc);
-            const float jv = gsum<16>(Jr[k] * tmp[d]);
+            const float jv = gsum<16>(Yr[k] * tmp[d]);
             const float f = rowb<k % 16>(fr[k / 16]), R = rowb<k % 16>(sR[k / 16]);
-            const float b = rec[(k < my_n ? my_start + k : 0) * RF + 3 * P + 4];
+            const float b = rec[(k < my_n ? my_start + k : 0) * RF + 2 * P + 4];
             if (k < my_n) cost += f * (0.5f * (jv + R * f) + b);
           }
         });
@@ -3415,11 +3495,11 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
             const float aref = rowb<k % 16>(sa[k / 16]), R = rowb<k % 16>(sR[k / 16]);
             const float a = rowb<k % 16>(sA[k / 16]);
             const float lo = rowb<k % 16>(sLo[k / 16]), hi = rowb<k % 16>(sHi[k / 16]);
-            const float jq = gsum<16>(Jr[k] * qd);
+            const float jq = gsum<16>(Yr[k] * qd);
             const float res = jq - aref + R * f0;
             const float nf = __builtin_amdgcn_fmed3f(f0 - res * __builtin_amdgcn_rcpf(a), lo, hi);
             const float delta = nf - f0;
-            qa[d] = qd + MJr[k] * delta;
+            qa[d] = qd + Yr[k] * delta;
             fr[k / 16] = slot_v == k % 16 ? nf : fr[k / 16];
             improvement -= delta * res + 0.5f * delta * delta * a;
           }
@@ -3438,7 +3518,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         constexpr int k = decltype(kc)::value;
         if (k < nlev) {
           const int d = dof_of(kc);
-          tmp[d] += Jr[k] * rowb<k % 16>(fr[k / 16]);
+          tmp[d] += Yr[k] * rowb<k % 16>(fr[k / 16]);
         }
       });
       unroll<NB>([&](auto ic) {
@@ -3447,7 +3527,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         if (k < my_n) ffg[__float_as_int(rowof[my_start + k])] = fr[i];
       });
       wsync();
-      return lane < nv ? qa[lane] : 0.0f;
+      return tree_epilogue(m, s, L, tmp, qa, qacc_s, lane);
     }
   }
 
@@ -3459,7 +3539,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     const RowRec<P> w = load_rec<P>(rec, q, slot);
     float f = 0;
     if (warm) {
-      const float jar = gsum<P>(act && w.d >= 0 ? w.J * s[L.qacc_ws + w.d] : 0.0f) - w.aref;
+      const float jar = rec[q * RF + 2 * P + 8];
       const float D = 1.0f / w.R;
       if (w.bound >= 0) f = jar <= -w.R * w.bound ? w.bound : (jar >= w.R * w.bound ? -w.bound : -D * jar);
       else f = jar < 0 ? -D * jar : 0.0f;
@@ -3475,7 +3555,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       const bool act = k < my_n;
       const int q = act ? my_start + k : 0;
       const RowRec<P> w = load_rec<P>(rec, q, slot);
-      if (act && w.d >= 0) tmp[w.d] += w.MJ * fl[q];
+      if (act && w.d >= 0) tmp[w.d] += w.Y * fl[q];
     }
     wsync();
     float cost = 0;
@@ -3484,9 +3564,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       const bool act = k < my_n;
       const int q = act ? my_start + k : 0;
       const RowRec<P> w = load_rec<P>(rec, q, slot);
-      const float jv = gsum<P>(act && w.d >= 0 ? w.J * tmp[w.d] : 0.0f);
+      const float jv = gsum<P>(act && w.d >= 0 ? w.Y * tmp[w.d] : 0.0f);
       const float f = fl[q];
-      const float b = rec[q * RF + 3 * P + 4];
+      const float b = rec[q * RF + 2 * P + 4];
       if (act && slot == 0) cost += f * (0.5f * (jv + w.R * f) + b);
     }
     cost = gsum<64>(cost);
@@ -3514,13 +3594,13 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       const bool mine = act && w.d >= 0;
       const float qd = mine ? qa[w.d] : 0.0f;
       const float f0 = fl[q];
-      const float jq = gsum<P>(mine ? w.J * qd : 0.0f);
+      const float jq = gsum<P>(mine ? w.Y * qd : 0.0f);
       const float res = jq - w.aref + w.R * f0;
       float nf = f0 - res / w.a;
       if (w.bound >= 0) nf = clampf(nf, -w.bound, w.bound);
       else if (nf < 0) nf = 0;
       const float delta = nf - f0;
-      if (mine && delta != 0) qa[w.d] = qd + w.MJ * delta;
+      if (mine && delta != 0) qa[w.d] = qd + w.Y * delta;
       if (act && slot == 0) fl[q] = nf;
       if (act) improvement -= delta * res + 0.5f * delta * delta * w.a;
     }
@@ -3532,7 +3612,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   if (lane == 0) s[L.niter] = __int_as_float(nit);
   wsync();
 
-  // --- 6. qfrc_constraint = J' f (per dof in row order: a dof's rows are in one pipe); forces out
+  // --- 6. z = sum Y' f (per dof in row order: a dof's rows are in one pipe), then qfrc_constraint
+  // and qacc from it; forces out
   if (lane < nv) tmp[lane] = 0;
   wsync();
   #pragma unroll 1
@@ -3540,12 +3621,12 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     const bool act = k < my_n;
     const int q = act ? my_start + k : 0;
     const RowRec<P> w = load_rec<P>(rec, q, slot);
-    if (act && w.d >= 0) tmp[w.d] += w.J * fl[q];
+    if (act && w.d >= 0) tmp[w.d] += w.Y * fl[q];
   }
   #pragma unroll 1
   for (int q = lane; q < nefc; q += 64) ffg[__float_as_int(rowof[q])] = fl[q];
   wsync();
-  return lane < nv ? qa[lane] : 0.0f;
+  return tree_epilogue(m, s, L, tmp, qa, qacc_s, lane);
 }
 
 // ---------------------------------------------------------------- primal solvers (Newton, CG)
