@@ -1205,6 +1205,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.niter = take(1);
     L.rfmask = take(std::max(1, d.nrfblk));
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
+    L.dofb = blocked ? take(2 * nv) : 0;
     // primal solvers in blocked mode: H = M + J'DJ couples the trees a contact joins, so it is
     // stored dense (dense mode builds H in the factor slot L.L instead)
     L.H = blocked && m.solver != MRS_SOL_PGS ? take(nv * nv) : 0;

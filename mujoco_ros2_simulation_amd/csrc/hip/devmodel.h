@@ -41,6 +41,7 @@ struct LdsLayout {
       qfrc_act, qfrc_smooth, qacc_smooth, qacc, qfrc_con, act_force,
       rfmask,  // per ray block: bitmask of candidate ray geoms (int bits)
       trees,   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
+      dofb,    // blocked mode: per dof its body and that body's subtree end (int bits; jac_col)
       H,       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
       niter;   // constraint solver iterations of the last forward (int bits)
   int total;  // floats per env (multiple of 4)

@@ -1898,6 +1898,19 @@ __device__ __forceinline__ void jac_col(const DevModel& m, const lfloat* s, int 
   for (int i = 0; i < 3; ++i) col[i] = cd[3 + i] + cr[i];
 }
 
+// blocked mode: jac_col with the dof's body and subtree end from the env's LDS table and the body's
+// root given (no dependent chain of model-table loads per contact row)
+__device__ __forceinline__ void jac_col_blk(const lfloat* s, const LdsLayout& L, int b, int root, const float pnt[3],
+                                            int j, float col[3]) {
+  const int bj = __float_as_int(s[L.dofb + 2 * j]), be = __float_as_int(s[L.dofb + 2 * j + 1]);
+  if (!(b >= bj && b < be)) { col[0] = col[1] = col[2] = 0; return; }
+  const lfloat* c = s + L.scom + 3 * root;
+  const lfloat* cd = s + L.cdof + 6 * j;
+  float off[3] = {pnt[0] - c[0], pnt[1] - c[1], pnt[2] - c[2]}, ang[3] = {cd[0], cd[1], cd[2]}, cr[3];
+  cross3(cr, ang, off);
+  for (int i = 0; i < 3; ++i) col[i] = cd[3 + i] + cr[i];
+}
+
 // mj_passive + mj_fwdActuation + qfrc_smooth + qacc_smooth (lane per dof)
 template <int G>
 __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
@@ -2873,6 +2886,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         for (int i = 0; i < 3; ++i) h[8 + i] = crec[2 + i];
         h[11] = __int_as_float(b1 | (b2 << 16));
         for (int i = 0; i < 9; ++i) h[12 + i] = crec[5 + i];
+        h[21] = __int_as_float(m.body_rootid[b1] | (m.body_rootid[b2] << 16));
       } else {
         h[8] = jval;
         h[11] = __int_as_float(t == EFC_FRICTION ? id : m.jnt_dofadr[id]);
@@ -2895,7 +2909,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     const int my_end = my_start + my_n;
     int qc = my_start;
     // the item headers are read one item ahead (loads in flight while the current item is built)
-    struct Hdr { v4f a, b, c, d, e; float f; };
+    struct Hdr { v4f a, b, c, d, e, f; };
     auto load_hdr = [&](int q) {
       const gfloat* h = hdr + kHdr * q;
       Hdr o;
@@ -2904,7 +2918,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       o.c = *(const __attribute__((address_space(1))) v4f*)(h + 8);
       o.d = *(const __attribute__((address_space(1))) v4f*)(h + 12);
       o.e = *(const __attribute__((address_space(1))) v4f*)(h + 16);
-      o.f = h[20];
+      o.f = *(const __attribute__((address_space(1))) v4f*)(h + 20);
       return o;
     };
     Hdr nxt = load_hdr(qc < my_end ? qc : 0);
@@ -2915,7 +2929,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       const int q0 = act ? qc : 0;  // record 0 always starts an item
       const Hdr cur = nxt;
       const v4f h0 = cur.a, h1 = cur.b, h2 = cur.c, h3 = cur.d, h4 = cur.e;
-      const float h20 = cur.f;
+      const float h20 = cur.f.x;
+      const int roots = __float_as_int(cur.f.y);
       {
         const int nr_ = (__float_as_int(h0.z) >> 16) & 0xf;
         const int qn = qc + (act ? nr_ : 0);
@@ -2938,8 +2953,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           const float cp[3] = {h2.x, h2.y, h2.z};
           const float fr[9] = {h3.x, h3.y, h3.z, h3.w, h4.x, h4.y, h4.z, h4.w, h20};
           float c1[3], c2[3];
-          jac_col(m, s, b1, cp, d, c1);
-          jac_col(m, s, b2, cp, d, c2);
+          jac_col_blk(s, L, b1, roots & 0xffff, cp, d, c1);
+          jac_col_blk(s, L, b2, roots >> 16, cp, d, c2);
           const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
           for (int i = 0; i < 3; ++i) jc[i] = fr[3 * i] * dc[0] + fr[3 * i + 1] * dc[1] + fr[3 * i + 2] * dc[2];
         }
@@ -3929,7 +3944,19 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     }
     switch (m.pipe_w) {
       case 8: return constraints_sparse<8>(ENV_ARGS, ncon, qacc_s);
-      case 16: return constraints_sparse<16>(ENV_ARGS, ncon, qacc_s);
+      case 16: {
+        // out of line the call saves and restores ~106 callee-saved VGPRs through scratch memory
+        // every step (C5: ~2 GB per 10-step launch); inlined, the kernel's own live values spill
+        // around the solve instead and the launch was measured slower (12.0 vs 10.6 ms), so it stays
+        // out of line unless MRS_SPARSE_INLINE (A/B builds)
+        float qa;
+#ifdef MRS_SPARSE_INLINE
+        [[clang::always_inline]] qa = constraints_sparse<16>(ENV_ARGS, ncon, qacc_s);
+#else
+        qa = constraints_sparse<16>(ENV_ARGS, ncon, qacc_s);
+#endif
+        return qa;
+      }
       case 32: return constraints_sparse<32>(ENV_ARGS, ncon, qacc_s);
       default: return constraints_sparse<64>(ENV_ARGS, ncon, qacc_s);
     }
@@ -4982,6 +5009,12 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       s[L.trees + 4 * t + 1] = __int_as_float(m.tree_dofnum[t]);
       s[L.trees + 4 * t + 2] = __int_as_float(m.tree_Moff[t]);
       s[L.trees + 4 * t + 3] = 0;
+    }
+    #pragma unroll 1
+    for (int j = lane; j < m.nv; j += G) {
+      const int bj = m.dof_bodyid[j];
+      s[L.dofb + 2 * j] = __int_as_float(bj);
+      s[L.dofb + 2 * j + 1] = __int_as_float(m.body_subtree_end[bj]);
     }
   }
   double time = st.time[e];
