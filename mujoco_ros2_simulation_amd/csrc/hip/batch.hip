@@ -22,7 +22,7 @@
 namespace mrs {
 
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, hipStream_t stream);
+                       int n_steps, bool forward_only, int group, bool primal, hipStream_t stream);
 
 namespace {
 
@@ -1389,7 +1389,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
       prod.rf_mode = 1;
       DevModel* d_prod = static_cast<DevModel*>(dalloc(*b, sizeof(DevModel)));
       HIP_CHECK(hipMemcpyAsync(d_prod, &prod, sizeof(DevModel), hipMemcpyHostToDevice, b->stream));
-      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, b->stream));
+      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, false, b->stream));
       HIP_CHECK(hipStreamSynchronize(b->stream));
     }
     batch_launch(b, 1, true);  // mj_forward after load (src/mujoco_system_interface.cpp:741)
@@ -1530,7 +1530,7 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
-  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group, b->stream));
+  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group, b->model->solver != MRS_SOL_PGS, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
 }

@@ -3929,10 +3929,209 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
   return dof ? qa : 0.0f;
 }
 
-template <int G>
+// The same primal solvers (solve_primal's algorithm, step for step) for small systems on G = 16
+// groups (nv <= 16, nefc <= 16), register-resident: lane j holds column j of every row of J and dof
+// j of the vectors, lane r holds row r's scalars (R, aref, friction-loss bound, jar = J_r qacc - aref,
+// J_r p, state, force).  Row products J x are KR independent DPP row reductions, J' f and M x are
+// DPP row broadcasts and FMAs, so nothing but the Hessian's factor (LDS, as in solve_primal) leaves
+// the registers -- the generic form keeps the rows and their products in the env's global scratch,
+// one dependent global round trip per row loop, and that was half of the reference scene's step
+// under MuJoCo's default solver.  KR: rows unrolled (the wave's largest system rounded up), KV: dof
+// unroll bound (>= nv).  Rows past the group's nefc are zero rows (J = 0, aref = 0): jar = 0 keeps
+// them satisfied, so they add nothing to any cost, slope or force.
+// kUnit: every row is the unit vector of the dof in lane r's `mydof` (dof friction-loss rows), built
+// in registers instead of read from the global rows J (row forces then stored only for force sensors)
+template <bool kUnit, int KR, int KV>
+__device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfloat* ff, int nefc, float myR, float myaref,
+                                                float myfl, bool myfric, float qs, bool newton, int mydof = -1) {
+  constexpr int G = 16;
+  ENV_UNPACK;
+  const int nv = m.nv;
+  const bool dof = lane < nv;
+  const bool row = lane < nefc;
+  if (!row) { myR = 1; myaref = 0; myfl = 0; myfric = false; }
+  qs = dof ? qs : 0.0f;
+  float Jt[KR];
+  unroll<KR>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if constexpr (kUnit)
+      Jt[r] = (r < nefc && lane == __float_as_int(rowb<r>(__int_as_float(mydof)))) ? 1.0f : 0.0f;
+    else
+      Jt[r] = (r < nefc && dof) ? J[r * nv + lane] : 0.0f;
+  });
+  // row `lane` of M (LDS; zero past nv, where x is zero too)
+  auto mrow = [&](int k) { return (k < nv && dof) ? (float)s[L.M + lane * nv + k] : 0.0f; };
+  const float scale = m.pgs_scale;
+  // lane r: J_r x (KR independent row reductions)
+  auto rows_dot = [&](float x) {
+    float out = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      const float t = gsum<16>(Jt[r] * x);
+      if (lane == r) out = t;
+    });
+    return out;
+  };
+  // lane j: (M x)_j, (J' f)_j
+  auto mmul = [&](float x) {
+    float y = 0;
+    unroll<KV>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      y += mrow(k) * rowb<k>(x);
+    });
+    return y;
+  };
+  auto jtmul = [&](float f) {
+    float q = 0;
+    unroll<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      q += Jt[r] * rowb<r>(f);
+    });
+    return q;
+  };
+  float jar = 0, myf = 0;  // row lanes
+  int st = PST_SAT;
+  // mj_constraintUpdate at jar: row state and force, returns (J' f)_lane
+  auto update = [&]() {
+    st = row ? prow_state(myfric, myR, myfl, jar) : PST_SAT;
+    myf = row ? -prow_slope(st, myR, myfl, jar) : 0.0f;
+    return jtmul(myf);
+  };
+  auto cost_at = [&](float x) {
+    const float md = mmul(x - qs);
+    jar = rows_dot(x) - myaref;
+    const float c = row ? prow_cost(prow_state(myfric, myR, myfl, jar), myR, myfl, jar) : 0.0f;
+    return gsum<16>((dof ? 0.5f * md * (x - qs) : 0.0f) + c);
+  };
+  float qa = qs;
+  if (!(m.disableflags & MRS_DSBL_WARMSTART)) {
+    const float xw = dof ? s[L.qacc_ws + lane] : 0.0f;
+    const float c_ws = cost_at(xw), c_sm = cost_at(qs);
+    if (c_ws <= c_sm) qa = xw;
+  }
+  float Md = mmul(qa - qs);
+  jar = rows_dot(qa) - myaref;
+  float qfrc = update();
+  float p = 0, gold = 0, Mgold = 0;
+  bool refined = false;
+  int nit = 0;
+  lfloat* H = s + L.L;
+  #pragma unroll 1
+  for (int iter = 0;; ++iter) {
+    const float grad = dof ? Md - qfrc : 0.0f;
+    float Mg;
+    if (newton) {
+      // H = M + J' diag(D of quadratic rows) J, row `lane` in registers, then factored in the LDS
+      // factor slot (M's factor is not needed again before integrate() refactors)
+      const float Dr = (row && st == PST_QUAD) ? 1.0f / myR : 0.0f;
+      float dj[KR];
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        dj[r] = Jt[r] * rowb<r>(Dr);
+      });
+      unroll<KV>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        float h = mrow(k);
+        unroll<KR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value;
+          h += dj[r] * rowb<k>(Jt[r]);
+        });
+        if (dof && k < nv) H[lane * nv + k] = h;
+      });
+      wsync();
+      MRS_CALL(16, cholesky<16>(mp, H, H, lane));
+      MRS_CALL(16, Mg = chol_solve_lanes<16>(mp, H, grad, lane));
+    } else {
+      MRS_CALL(16, Mg = chol_solve_lanes<16>(mp, s + L.L, grad, lane));
+    }
+    if (iter == 0 || newton) {
+      p = -Mg;
+    } else {
+      const float num = gsum<16>(grad * (Mg - Mgold)), den = gsum<16>(gold * Mgold);
+      const float beta = fmaxf(0.0f, num / (den > kMinVal ? den : kMinVal));
+      p = -Mg + beta * p;
+    }
+    if (iter >= m.iterations) break;
+    const float Mv = mmul(p);
+    const float jv = rows_dot(p);
+    const float g1 = gsum<16>(p * Md), g2 = gsum<16>(p * Mv), snorm = sqrtf(gsum<16>(p * p));
+    auto ls_eval = [&](float a, float a0, float& d1, float& d2, bool& ch) {
+      float s1 = 0, s2 = 0;
+      bool c = false;
+      if (row && jv != 0) {
+        const float ja = jar + a * jv;
+        const int stt = prow_state(myfric, myR, myfl, ja);
+        c = stt != prow_state(myfric, myR, myfl, jar + a0 * jv);
+        s1 = jv * prow_slope(stt, myR, myfl, ja);
+        if (stt == PST_QUAD) s2 = jv * jv / myR;
+      }
+      d1 = g1 + a * g2 + gsum<16>(s1);
+      d2 = g2 + gsum<16>(s2);
+      ch = gany<16>(c);
+    };
+    float alpha = 0;
+    if (snorm >= kMinVal && g2 > 0) {
+      const float gtol = m.tolerance * m.ls_tolerance * snorm / scale;
+      float d1, d2;
+      bool ch;
+      ls_eval(0.0f, 0.0f, d1, d2, ch);
+      if (d1 < 0) {
+        float a = 0, lo = 0, hi = -1;
+        #pragma unroll 1
+        for (int it = 0; it < m.ls_iterations; ++it) {
+          float an = a - d1 / d2;
+          bool nstep = true;
+          if (hi >= 0 && (an <= lo || an >= hi)) { an = 0.5f * (lo + hi); nstep = false; }
+          float n1, n2;
+          ls_eval(an, a, n1, n2, ch);
+          a = an; d1 = n1; d2 = n2;
+          if (fabsf(d1) < gtol || (nstep && !ch)) break;
+          if (d1 < 0) lo = a; else hi = a;
+        }
+        alpha = a;
+      }
+    }
+    if (alpha == 0) break;
+    float dc = 0;
+    bool changed = false;
+    if (row) {
+      const float j1 = jar + alpha * jv;
+      const int s1 = prow_state(myfric, myR, myfl, j1);
+      dc = prow_dcost(st, s1, myR, myfl, jar, alpha * jv);
+      changed = st != s1;
+      jar = j1;
+    }
+    const float dcost = alpha * g1 + 0.5f * alpha * alpha * g2 + gsum<16>(dc);
+    changed = gany<16>(changed);
+    qa += alpha * p;
+    Md += alpha * Mv;
+    gold = grad;
+    Mgold = Mg;
+    qfrc = update();
+    ++nit;
+    const float gn = dof ? Md - qfrc : 0.0f;
+    const float gnorm = sqrtf(gsum<16>(gn * gn));
+    if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance) break;
+    if (newton && !changed) {
+      const bool floor = fabsf(gn) <= 64.0f * __FLT_EPSILON__ * (fabsf(Md) + fabsf(qfrc));
+      if (refined || !gany<16>(!floor)) break;
+      refined = true;
+      Md = mmul(qa - qs);
+      jar = rows_dot(qa) - myaref;
+      qfrc = update();
+    }
+  }
+  if (dof) s[L.qfrc_con + lane] = qfrc;
+  if (row && (!kUnit || (m.acc_sens & 2))) ff[lane] = myf;  // row forces (mj_rnePostConstraint, mrs_batch_get_efc)
+  if (lane == 0) s[L.niter] = __int_as_float(nit);
+  wsync();
+  return dof ? qa : 0.0f;
+}
+
+template <int G, bool kPrimal = false>
 __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s);
 
-template <int G>
+template <int G, bool kPrimal = false>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) {
@@ -3976,7 +4175,10 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
         const float q = s[L.qpos + __float_as_int(lr[0])], mg = lr[1];
         lim |= (q - lr[2] < mg) | (lr[3] - q < mg);
       }
-    if (m.solver == MRS_SOL_PGS && ncon == 0 && nf > 0 && nf <= 16 && !gany<G>(lim)) {
+    // (kPrimal: the G = 16 kernel instantiated for models whose solver is Newton or CG, so the
+    // primal form is inlined only there and the PGS kernels keep their code and registers)
+    if ((kPrimal ? m.solver != MRS_SOL_PGS : m.solver == MRS_SOL_PGS) && ncon == 0 && nf > 0 && nf <= 16 &&
+        !gany<G>(lim)) {
       if (lane == 0) scr[S.efc_n] = __int_as_float(-1);  // rows stay in registers
       int mydof = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
@@ -3990,9 +4192,20 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
         myb = s[L.qacc_smooth + j] - myaref;
         myfl = fr[3];
       }
+      float qa;
+      if constexpr (kPrimal) {
+        // Newton / CG (MuJoCo's default solver): the register-resident primal form on the same rows
+        const bool newton = m.solver == MRS_SOL_NEWTON;
+        if (nf <= 4 && m.nv <= 8)
+          qa = primal_small16<true, 4, 8>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, lane < nf, qacc_s, newton, mydof);
+        else if (nf <= 8 && m.nv <= 8)
+          qa = primal_small16<true, 8, 8>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, lane < nf, qacc_s, newton, mydof);
+        else
+          qa = primal_small16<true, 16, 16>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, lane < nf, qacc_s, newton, mydof);
+        return qa;
+      }
       // rows (and the dofs they touch) unrolled to 8 when the model has at most 8 friction dofs:
       // a quarter of the substitution code
-      float qa;
       if (nf <= 8 && m.nv <= 8)
         qa = pgs_small16_qacc<true, 8>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
       else
@@ -4004,13 +4217,13 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   // rows with contacts or active joint limits: the dense row path, out of line -- cold in C3's
   // steady state, and keeping it out of the inlined step loop keeps the hot code footprint small
   float qa;
-  [[clang::noinline]] qa = constraints_dense<G>(ENV_ARGS, ncon, qacc_s);
+  [[clang::noinline]] qa = constraints_dense<G, kPrimal>(ENV_ARGS, ncon, qacc_s);
   return qa;
 }
 
 // dense constraint rows in the env's global scratch (J, M^-1 J', row scalars), then the
 // register-resident PGS (<= 16 rows on G = 16) or the row-serial PGS with wave reductions
-template <int G>
+template <int G, bool kPrimal>
 __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) ncon = uniform_int(ncon);
@@ -4143,8 +4356,9 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   }
   // --- impedance, R, aref, M^-1 J', ARii, b (lane per row); the primal solvers need R and aref only
   const bool primal = m.solver != MRS_SOL_PGS;
-  const bool small = G == 16 && nefc <= 16 && !primal;
+  const bool small = G == 16 && nefc <= 16;  // register-resident solvers (dual PGS or primal)
   float my_R = 1, my_aref = 0, my_b = 0, my_fl = 0;
+  bool my_fric = false;
   #pragma unroll 1
   for (int r = lane; r < nefc; r += G) {
     const int code = __float_as_int(type[r]);
@@ -4192,6 +4406,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       my_aref = -B * vel - pterm;
       my_b = jqs - my_aref;
       my_fl = t == EFC_FRICTION ? floss[r] : 0.0f;
+      my_fric = t == EFC_FRICTION;
       aref[r] = my_aref;
       continue;
     }
@@ -4209,19 +4424,35 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   wsync();
   SUB_ADD(PH_CON_REC, t_sub);
   t_sub = SUB_T();
-  if (primal) {
-    float qa;
-    [[clang::noinline]] qa = solve_primal<G>(ENV_ARGS, nefc, m.solver == MRS_SOL_NEWTON);
-    return qa;
-  }
+  int rmax = 0;
   if constexpr (G == 16) {
     // rows unrolled up to the largest small system among the wave's active groups (wave-uniform
     // bound; binary search with ballots, which only see active lanes)
     const int mine = small ? nefc : 0;
-    int rmax = 0;
 #pragma unroll
     for (int bit = 16; bit >= 1; bit >>= 1)
       if (__ballot(mine >= rmax + bit) != 0) rmax += bit;
+  }
+  if (primal) {
+    float qa;
+    const bool newton = m.solver == MRS_SOL_NEWTON;
+    if constexpr (G == 16 && kPrimal) {  // (the G = 16 kernel instantiated for Newton / CG models)
+      if (small) {
+        auto solve = [&](auto kv) {
+          constexpr int KV = decltype(kv)::value;
+          if (rmax <= 4) return primal_small16<false, 4, KV>(ENV_ARGS, J, ff, nefc, my_R, my_aref, my_fl, my_fric, qacc_s, newton);
+          if (rmax <= 8) return primal_small16<false, 8, KV>(ENV_ARGS, J, ff, nefc, my_R, my_aref, my_fl, my_fric, qacc_s, newton);
+          return primal_small16<false, 16, KV>(ENV_ARGS, J, ff, nefc, my_R, my_aref, my_fl, my_fric, qacc_s, newton);
+        };
+        qa = nv <= 8 ? solve(std::integral_constant<int, 8>{}) : solve(std::integral_constant<int, 16>{});
+        SUB_ADD(PH_CON_PGS, t_sub);
+        return qa;
+      }
+    }
+    [[clang::noinline]] qa = solve_primal<G>(ENV_ARGS, nefc, newton);
+    return qa;
+  }
+  if constexpr (G == 16) {
     if (small) {
       // rows unrolled to the wave's row count, the substitutions to the model's dof count (nv can
       // exceed the row count: a free body with one contact, an arm with one active limit)
@@ -4846,7 +5077,7 @@ __device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
 }
 
 // full forward pass; returns qacc (lane per dof)
-template <int G>
+template <int G, bool kPrimal = false>
 __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
@@ -4874,7 +5105,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
     s[L.niter] = __int_as_float(0);
     scr[S.efc_n] = __int_as_float(0);  // no rows unless constraints() builds some (mrs_batch_get_efc)
   }
-  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = constraints<G>(ENV_ARGS, ncon, qacc_s));
+  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = (constraints<G, kPrimal>(ENV_ARGS, ncon, qacc_s)));
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
@@ -4977,7 +5208,7 @@ template <int G>
 #endif
 struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
-template <int G, bool kForwardOnly>
+template <int G, bool kForwardOnly, bool kPrimal = false>
 __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -5074,7 +5305,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 #else
     gfloat* sd_step = sensordata;
 #endif
-    MRS_CALL(G, ncon = forward<G>(ENV_ARGS, sd_step PH_ACC_ARG));
+    MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG)));
     if (kForwardOnly) break;
     bool redo = false;
     if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
@@ -5087,7 +5318,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     }
     // forward() is entered by the whole wave; for envs that were not reset it recomputes the
     // same outputs from the same state
-    if (__any(redo)) { [[clang::noinline]] ncon = forward<G>(ENV_ARGS, sd_step PH_ACC_ARG); }  // rare
+    if (__any(redo)) { [[clang::noinline]] ncon = forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG); }  // rare
     {
       PH_BEGIN();
       MRS_CALL(G, integrate<G>(ENV_ARGS));
@@ -5144,10 +5375,17 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 
 template <int G>
 static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                     int n_steps, bool forward_only, hipStream_t stream) {
+                     int n_steps, bool forward_only, bool primal, hipStream_t stream) {
   constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
+  if constexpr (G == 16) {
+    if (primal && !forward_only) {
+      hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st,
+                         n_envs, n_steps);
+      return;
+    }
+  }
   if (forward_only)
     hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs, 1);
   else
@@ -5174,12 +5412,12 @@ int phase_cycles(double* out, int n, bool reset) {
 }
 
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, hipStream_t stream) {
+                       int n_steps, bool forward_only, int group, bool primal, hipStream_t stream) {
   switch (group) {
-    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
-    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
-    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
-    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, stream); break;
+    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

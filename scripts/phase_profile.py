@@ -17,7 +17,13 @@ scene = sys.argv[1] if len(sys.argv) > 1 else str(ROOT / "scenes" / "arm7_lidar.
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 launches = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 period = 10
-model = sim.Model.load(scene)
+if scene == "c2":  # the C2 bench scene: the reference's scene.xml with sensors disabled
+    sys.path.insert(0, str(ROOT))
+    from bench import ref_scene_xml  # noqa: E402
+    model = sim.Model.from_string(*ref_scene_xml(sensors=False))
+    scene = "scene"
+else:
+    model = sim.Model.load(scene)
 b = sim.Batch(model, n)
 b.set(sim.FIELD_QPOS, synth.initial_qpos(model, np.arange(n)))
 table = torch.from_numpy(synth.ctrl_table(model, np.arange(n), launches + 2, period).astype(np.float32)).cuda()
