@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--render-sync", action="store_true",
                    help="C4: render each frame on the batch stream between steps instead of the camera "
                         "pipeline (pose snapshot, render concurrently with the following steps)")
+    p.add_argument("--solver", choices=["PGS", "CG", "Newton"], default=None,
+                   help="override the scene's <option solver> (e.g. c5 under MuJoCo's default Newton)")
     p.add_argument("--no-gather", action="store_true",
                    help="N>1: skip the end-of-period observation gather (on by default when N > 1)")
     return p.parse_args()
@@ -136,6 +138,18 @@ def ref_scene_xml(sensors: bool) -> tuple[str, str]:
         i = xml.index(">", xml.index("<mujoco")) + 1
         xml = xml[:i] + '\n  <option><flag sensor="disable"/></option>' + xml[i:]
     return xml, str(REF_SCENE.parent)
+
+
+def with_solver(xml: str, solver: str) -> str:
+    """the scene with <option solver=...> set (inserted when the scene has no <option>)"""
+    import re
+    m = re.search(r"<option\b[^>]*?/?>", xml)
+    if m is None:
+        i = xml.index(">", xml.index("<mujoco")) + 1
+        return xml[:i] + f'\n  <option solver="{solver}"/>' + xml[i:]
+    tag = re.sub(r'\ssolver="[^"]*"', "", m.group(0))
+    tag = tag.replace("<option", f'<option solver="{solver}"', 1)
+    return xml[:m.start()] + tag + xml[m.end():]
 
 
 # ------------------------------------------------------------------------------------------------ C1
@@ -266,15 +280,19 @@ def main():
     dev = f"cuda:{local}"
     cfg = args.config
     if args.scene:
-        model = sim.Model.load(args.scene)
-        scene_name = Path(args.scene).stem
+        path = Path(args.scene)
+        xml, base = path.read_text(), str(path.parent)
+        scene_name = path.stem
     elif cfg == "c2":
         xml, base = ref_scene_xml(sensors=False)
-        model = sim.Model.from_string(xml, base)
         scene_name = "scene"
     else:
         scene_name = {"c3": "arm7_lidar", "c3m": "arm7_mesh", "c4": "mobile_base", "c5": "arm_boxes"}[cfg]
-        model = sim.Model.load(ROOT / "scenes" / f"{scene_name}.xml")
+        path = ROOT / "scenes" / f"{scene_name}.xml"
+        xml, base = path.read_text(), str(path.parent)
+    if args.solver:
+        xml = with_solver(xml, args.solver)
+    model = sim.Model.from_string(xml, base)
     n = args.envs or {"c2": 4096, "c3": 8192, "c3m": 8192, "c4": 2048, "c5": 8192}[cfg]
     env_ids = shard.env_ids(rank, n)
     P = args.warmup + args.steps
@@ -406,7 +424,7 @@ def main():
                 "traffic": traffic_rec["traffic_bytes_per_launch"] if traffic_rec else None,
                 "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": n * args.period * roofline.bytes_per_env_step(model, args.period),
-                "kernel": "step_kernel<G, false> (fused 10-step launch)", "kernel_ms": step_ms,
+                "kernel": "step_kernel<G, false, *> (fused 10-step launch)", "kernel_ms": step_ms,
                 "flops_per_env_step": flops,
                 "flops_source": "SURVEY.md §8(d) per-unit figure x envs x steps per launch",
                 "flops_per_env_step_structural": detailed_flops,

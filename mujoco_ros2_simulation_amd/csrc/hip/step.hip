@@ -3713,6 +3713,64 @@ __device__ float chol_solve_dense(const lfloat* Lf, float x, int nv, int lane) {
   return x;
 }
 
+// Newton's Hessian in blocked mode (G = 64, one env per wave): H = M + J' diag(D) J, D_r = 1 / R_r for
+// rows in the quadratic state, as the dense nv x nv lower triangle in LDS (all chol_dense reads).
+// J' D J is a genuine contraction over the rows (nv up to 64 dofs, hundreds of rows in contact-rich
+// scenes): one v_mfma_f32_16x16x4f32 per (16 x 16 dof tile, 4 rows), the lower-triangle tiles of
+// every 4-row slice issued back to back.  Lane l feeds A[i][k] = D_r J_ri and B[k][j] = J_rj with
+// i, j = tile offset + l % 16 and r = r0 + l / 16, and holds D[4 (l / 16) + v][l % 16] of the tile in
+// result register v (scripts/probes/mfma16x16x4.hip checks this layout on the device).  Slices whose
+// four rows are all outside the quadratic state are skipped.
+__device__ __forceinline__ void hessian_mfma64(const DevModel& m, const lfloat* s, const gfloat* J, const gfloat* st,
+                                               const gfloat* Rr, int nefc, lfloat* H, int lane) {
+  const int nv = m.nv;
+  const int col = lane & 15, kq = lane >> 4;
+  v4f acc[10];
+  unroll<10>([&](auto tc) { acc[decltype(tc)::value] = v4f{0.0f, 0.0f, 0.0f, 0.0f}; });
+  #pragma unroll 1
+  for (int r0 = 0; r0 < nefc; r0 += 4) {
+    const int r = r0 + kq;
+    float D = 0;
+    if (r < nefc && __float_as_int(st[r]) == PST_QUAD) D = 1.0f / Rr[r];
+    if (!__any(D != 0)) continue;
+    float v[4];
+    unroll<4>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      const int i = 16 * b + col;
+      v[b] = (D != 0 && i < nv) ? J[r * nv + i] : 0.0f;
+    });
+    unroll<4>([&](auto ic) {
+      constexpr int I = decltype(ic)::value;
+      if (16 * I < nv) {
+        const float a = v[I] * D;
+        unroll<I + 1>([&](auto jc) {
+          constexpr int Jb = decltype(jc)::value;
+          constexpr int tt = I * (I + 1) / 2 + Jb;
+          acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, v[Jb], acc[tt], 0, 0, 0);
+        });
+      }
+    });
+  }
+  unroll<4>([&](auto ic) {
+    constexpr int I = decltype(ic)::value;
+    if (16 * I < nv)
+      unroll<I + 1>([&](auto jc) {
+        constexpr int Jb = decltype(jc)::value;
+        constexpr int tt = I * (I + 1) / 2 + Jb;
+        const int j = 16 * Jb + col;
+        unroll<4>([&](auto vc) {
+          constexpr int vv = decltype(vc)::value;
+          const int i = 16 * I + 4 * kq + vv;
+          if (i < nv && j < nv && i >= j) {
+            float h = acc[tt][vv];
+            if (m.dof_tree[i] == m.dof_tree[j]) h += s[m.L.M + midx<64>(m, i, j)];
+            H[i * nv + j] = h;
+          }
+        });
+      });
+  });
+}
+
 template <int G>
 __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
   ENV_UNPACK;
@@ -3812,16 +3870,20 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     const float grad = dof ? Md - qfrc : 0.0f;
     float Mg;
     if (newton) {
-      // H row `lane` (dense: into the factor slot L.L; blocked: L.H), then factor in place
-      if (dof)
-        #pragma unroll 1
-        for (int k = 0; k < nv; ++k) {
-          float h = mval(k);
+      // H row `lane` (dense: into the factor slot L.L; blocked: L.H, by MFMA), then factor in place
+      if constexpr (G == 64) {
+        hessian_mfma64(m, s, J, st, Rr, nefc, H, lane);
+      } else {
+        if (dof)
           #pragma unroll 1
-          for (int r = 0; r < nefc; ++r)
-            if (__float_as_int(st[r]) == PST_QUAD) h += J[r * nv + lane] * J[r * nv + k] / Rr[r];
-          H[lane * nv + k] = h;
-        }
+          for (int k = 0; k < nv; ++k) {
+            float h = mval(k);
+            #pragma unroll 1
+            for (int r = 0; r < nefc; ++r)
+              if (__float_as_int(st[r]) == PST_QUAD) h += J[r * nv + lane] * J[r * nv + k] / Rr[r];
+            H[lane * nv + k] = h;
+          }
+      }
       wsync();
       if constexpr (G == 64) {
         chol_dense<G>(H, nv, lane);

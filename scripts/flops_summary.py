@@ -15,6 +15,7 @@ Kernel time: the bench line of the same config (gpurun_out/bench_<cfg>.json, in-
 Usage: python scripts/flops_summary.py OUT.json cfg [envs] [steps_per_launch]
 """
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
@@ -27,7 +28,7 @@ STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 COUNTERS = ["SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32",
             "SQ_INSTS_VALU_FLOPS_FP32", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
 rows = [r for r in csv.DictReader(open(ROOT / f"gpurun_out/pmc_flops_{CFG}/run_counter_collection.csv"))
-        if "step_kernel" in r["Kernel_Name"] and "false>" in r["Kernel_Name"]]
+        if "step_kernel" in r["Kernel_Name"] and not re.search(r"step_kernel<\d+, true", r["Kernel_Name"])]
 per = defaultdict(lambda: defaultdict(float))
 for r in rows:
     per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])

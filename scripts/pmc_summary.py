@@ -8,6 +8,7 @@ Usage: python scripts/pmc_summary.py OUT.json [cfg]
   cfg c2 / c3 / c5: the fused multi-step launches (step_kernel<G, false>); c4 / c3m: the depth kernel.
 """
 import csv
+import re
 import json
 import sys
 from pathlib import Path
@@ -22,7 +23,7 @@ def per_launch(name: str) -> tuple[float, str, int]:
     if not d.exists():
         d = ROOT / f"gpurun_out/pmc_{name}"
     rows = [r for r in csv.DictReader(open(d / "run_counter_collection.csv"))
-            if KERNEL in r["Kernel_Name"] and (KERNEL != "step_kernel" or "false>" in r["Kernel_Name"])]
+            if KERNEL in r["Kernel_Name"] and (KERNEL != "step_kernel" or not re.search(r"step_kernel<\d+, true", r["Kernel_Name"]))]
     vals = [float(r["Counter_Value"]) for r in rows]
     steady = vals[1:] if len(vals) > 2 else vals  # drop the first (cold caches)
     return sum(steady) / len(steady), rows[0]["Kernel_Name"], len(steady)

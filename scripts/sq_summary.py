@@ -17,6 +17,7 @@ Kernel time: the bench line of the same config (gpurun_out/bench_<cfg>.json, in-
 Usage: python scripts/sq_summary.py OUT.json cfg
 """
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
@@ -26,7 +27,7 @@ ROOT = Path(__file__).resolve().parents[1]
 OUT, CFG = Path(sys.argv[1]), sys.argv[2]
 KERNEL = "step_kernel"
 rows = [r for r in csv.DictReader(open(ROOT / f"gpurun_out/pmc_sq_{CFG}/run_counter_collection.csv"))
-        if KERNEL in r["Kernel_Name"] and "false>" in r["Kernel_Name"]]
+        if KERNEL in r["Kernel_Name"] and not re.search(r"step_kernel<\d+, true", r["Kernel_Name"])]
 per = defaultdict(lambda: defaultdict(float))
 for r in rows:
     per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
