@@ -1209,6 +1209,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     // primal solvers in blocked mode: H = M + J'DJ couples the trees a contact joins, so it is
     // stored dense (dense mode builds H in the factor slot L.L instead)
     L.H = blocked && m.solver != MRS_SOL_PGS ? take(nv * nv) : 0;
+    L.rk = m.integrator == MRS_INT_RK4 ? take(std::max(1, m.nq) + 4 * nv) : 0;
     L.total = off;
   };
   lds_layout(false);

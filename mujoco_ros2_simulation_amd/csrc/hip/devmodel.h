@@ -43,6 +43,8 @@ struct LdsLayout {
       trees,   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
       dofb,    // blocked mode: per dof its body and that body's subtree end (int bits; jac_col)
       H,       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
+      rk,      // RK4 models: the step's initial qpos [nq], then qvel [nv], stage velocity, B-weighted sums of
+               // the stage velocities and accelerations [nv each]
       niter;   // constraint solver iterations of the last forward (int bits)
   int total;  // floats per env (multiple of 4)
 };

@@ -3686,6 +3686,7 @@ __device__ void chol_dense(lfloat* A, int nv, int lane) {
     float t = 0;
     if (lane >= k && lane < nv) {
       t = A[lane * nv + k];
+      #pragma unroll 8
       for (int p = 0; p < k; ++p) t -= A[lane * nv + p] * A[k * nv + p];
     }
     const float dk = gbcast<G>(t, k);
@@ -3727,18 +3728,21 @@ __device__ __forceinline__ void hessian_mfma64(const DevModel& m, const lfloat* 
   const int col = lane & 15, kq = lane >> 4;
   v4f acc[10];
   unroll<10>([&](auto tc) { acc[decltype(tc)::value] = v4f{0.0f, 0.0f, 0.0f, 0.0f}; });
-  #pragma unroll 1
+  // slices unrolled by 4 with every load of a slice independent of the others (the row's state, R
+  // and its J entries), so ~24 loads per lane are in flight instead of one dependent round trip each
+  #pragma unroll 4
   for (int r0 = 0; r0 < nefc; r0 += 4) {
     const int r = r0 + kq;
-    float D = 0;
-    if (r < nefc && __float_as_int(st[r]) == PST_QUAD) D = 1.0f / Rr[r];
-    if (!__any(D != 0)) continue;
+    const bool in = r < nefc;
+    const int sr = in ? __float_as_int(st[r]) : PST_SAT;
+    const float Rv = in ? (float)Rr[r] : 1.0f;
     float v[4];
     unroll<4>([&](auto bc) {
       constexpr int b = decltype(bc)::value;
       const int i = 16 * b + col;
-      v[b] = (D != 0 && i < nv) ? J[r * nv + i] : 0.0f;
+      v[b] = (in && i < nv) ? J[r * nv + i] : 0.0f;
     });
+    const float D = sr == PST_QUAD ? 1.0f / Rv : 0.0f;
     unroll<4>([&](auto ic) {
       constexpr int I = decltype(ic)::value;
       if (16 * I < nv) {
@@ -3816,7 +3820,8 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     for (int r = lane; r < nefc; r += G) {
       float v = -shift * aref[r];
       const gfloat* Jr = J + r * nv;
-      #pragma unroll 1
+      // unrolled: the row's loads are independent, issued together instead of one round trip each
+      #pragma unroll 8
       for (int j = 0; j < nv; ++j) v += Jr[j] * xb[j];
       out[r] = v;
     }
@@ -3834,7 +3839,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     wsync();
     float q = 0;
     if (dof)
-      #pragma unroll 1
+      #pragma unroll 8
       for (int r = 0; r < nefc; ++r) q += J[r * nv + lane] * ff[r];
     return q;
   };
@@ -5171,10 +5176,41 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
-  if (m.acc_sens && !(m.disableflags & MRS_DSBL_SENSOR)) { [[clang::noinline]] rne_post<G>(ENV_ARGS, ncon); }
-  if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
+  // sensordata == nullptr: mj_forwardSkip(skipsensor) (the RK4 stages)
+  if (sensordata) {
+    if (m.acc_sens && !(m.disableflags & MRS_DSBL_SENSOR)) { [[clang::noinline]] rne_post<G>(ENV_ARGS, ncon); }
+    if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
+  }
   PH_END(ph_acc, PH_SENS);
   return ncon;
+}
+
+// mj_integratePos: qpos (LDS) advanced by h * vel (an LDS vector of nv)
+template <int G>
+__device__ __forceinline__ void integrate_pos(const DevModel& m, lfloat* s, const lfloat* vel, float h, int lane) {
+  const LdsLayout& L = m.L;
+  #pragma unroll 1
+  for (int j = lane; j < m.njnt; j += G) {
+    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
+    const int jt = m.jnt_type[j];
+    if (jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) {
+      s[L.qpos + a] += h * vel[da];
+      continue;
+    }
+    if (jt == MRS_JNT_FREE) {
+      for (int i = 0; i < 3; ++i) s[L.qpos + a + i] += h * vel[da + i];
+      a += 3; da += 3;
+    }
+    float q[4] = {s[L.qpos + a], s[L.qpos + a + 1], s[L.qpos + a + 2], s[L.qpos + a + 3]};
+    float v[3] = {vel[da], vel[da + 1], vel[da + 2]};
+    float ang = h * normalize3(v), dq[4];
+    axis_angle_quat(dq, v, ang);
+    quat_normalize(q);
+    quat_mul(q, q, dq);
+    quat_normalize(q);
+    for (int i = 0; i < 4; ++i) s[L.qpos + a + i] = q[i];
+  }
+  wsync();
 }
 
 // mj_Euler / mj_implicit(implicitfast) + mj_advance
@@ -5235,28 +5271,66 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
     s[L.qvel + lane] += h * qacc_int;
   }
   wsync();
-  #pragma unroll 1
-  for (int j = lane; j < m.njnt; j += G) {
-    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
-    const int jt = m.jnt_type[j];
-    if (jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) {
-      s[L.qpos + a] += h * s[L.qvel + da];
-      continue;
-    }
-    if (jt == MRS_JNT_FREE) {
-      for (int i = 0; i < 3; ++i) s[L.qpos + a + i] += h * s[L.qvel + da + i];
-      a += 3; da += 3;
-    }
-    float q[4] = {s[L.qpos + a], s[L.qpos + a + 1], s[L.qpos + a + 2], s[L.qpos + a + 3]};
-    float v[3] = {s[L.qvel + da], s[L.qvel + da + 1], s[L.qvel + da + 2]};
-    float ang = h * normalize3(v), dq[4];
-    axis_angle_quat(dq, v, ang);
-    quat_normalize(q);
-    quat_mul(q, q, dq);
-    quat_normalize(q);
-    for (int i = 0; i < 4; ++i) s[L.qpos + a + i] = q[i];
+  integrate_pos<G>(m, s, s + L.qvel, h, lane);
+}
+
+// mj_RungeKutta(m, d, 4) (oracle.c rk4 states the restatement): the stages around the step loop's
+// single forward() call site.  Stage i = 1..3 (entered with F_{i-1} = (qvel, qacc) in LDS): saves X_0
+// at stage 1, accumulates B_{i-1} F_{i-1}, and sets X_i = X_0 '+' h A_i F_{i-1}; rk4_final adds F_3
+// and advances X_0 by h sum B_j F_j.  Lane per dof (nv <= G); qpos lane-strided.
+template <int G>
+__device__ void rk4_stage(ENV_PARAMS, int stage) {
+  ENV_UNPACK;
+  const int nq = m.nq, nv = m.nv;
+  const float h = m.timestep;
+  const float a = stage == 3 ? 1.0f : 0.5f;
+  const float b = stage == 1 ? 1.0f / 6 : 1.0f / 3;
+  lfloat* q0 = s + L.rk;
+  lfloat* v0 = q0 + (nq > 1 ? nq : 1);
+  lfloat *dv = v0 + nv, *sv = dv + nv, *sa = sv + nv;
+  if (stage == 1) {
+    #pragma unroll 1
+    for (int i = lane; i < nq; i += G) q0[i] = s[L.qpos + i];
   }
+  #pragma unroll 1
+  for (int j = lane; j < nv; j += G) {
+    const float vel = s[L.qvel + j], acc = s[L.qacc + j];
+    if (stage == 1) {
+      v0[j] = vel;
+      sv[j] = b * vel;
+      sa[j] = b * acc;
+    } else {
+      sv[j] += b * vel;
+      sa[j] += b * acc;
+    }
+    dv[j] = a * vel;
+    s[L.qvel + j] = v0[j] + h * (a * acc);
+  }
+  #pragma unroll 1
+  for (int i = lane; i < nq; i += G) s[L.qpos + i] = q0[i];
   wsync();
+  integrate_pos<G>(m, s, dv, h, lane);
+}
+template <int G>
+__device__ void rk4_final(ENV_PARAMS) {
+  ENV_UNPACK;
+  const int nq = m.nq, nv = m.nv;
+  const float h = m.timestep;
+  lfloat* q0 = s + L.rk;
+  lfloat* v0 = q0 + (nq > 1 ? nq : 1);
+  lfloat *sv = v0 + 2 * nv, *sa = sv + nv;
+  #pragma unroll 1
+  for (int j = lane; j < nv; j += G) {
+    const float acc = s[L.qacc + j];
+    sv[j] += (1.0f / 6) * s[L.qvel + j];
+    const float dA = sa[j] + (1.0f / 6) * acc;
+    s[L.qacc_ws + j] = acc;  // mj_advance: the last stage's qacc
+    s[L.qvel + j] = v0[j] + h * dA;
+  }
+  #pragma unroll 1
+  for (int i = lane; i < nq; i += G) s[L.qpos + i] = q0[i];
+  wsync();
+  integrate_pos<G>(m, s, sv, h, lane);
 }
 
 // waves per SIMD the register budget is sized for.  One env per wave (G = 64, blocked mode): 2 waves
@@ -5362,7 +5436,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       }
     }
 #ifdef MRS_DIAG_SENS_LAST
-    // diagnostic build: sensordata stored on the last step of the launch only (rays still computed)
+    // diagnostic build: sensors evaluated and stored on the last step of the launch only
     gfloat* sd_step = (kForwardOnly || step == n_steps - 1) ? sensordata : nullptr;
 #else
     gfloat* sd_step = sensordata;
@@ -5381,7 +5455,15 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     // forward() is entered by the whole wave; for envs that were not reset it recomputes the
     // same outputs from the same state
     if (__any(redo)) { [[clang::noinline]] ncon = forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG); }  // rare
-    {
+    if (m.integrator == MRS_INT_RK4) {
+      // stages out of line (RK4 models only), each followed by a forward without sensors
+      #pragma unroll 1
+      for (int stage = 1; stage < 4; ++stage) {
+        [[clang::noinline]] rk4_stage<G>(ENV_ARGS, stage);
+        [[clang::noinline]] ncon = forward<G, kPrimal>(ENV_ARGS, nullptr PH_ACC_ARG);
+      }
+      [[clang::noinline]] rk4_final<G>(ENV_ARGS);
+    } else {
       PH_BEGIN();
       MRS_CALL(G, integrate<G>(ENV_ARGS));
       PH_END(ph_acc, PH_INTEG);

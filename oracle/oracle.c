@@ -2160,7 +2160,8 @@ static void fwd_position(const mrs_model_view* m, orc_data* d) {
   make_constraint(m, d);
 }
 
-void orc_forward(const mrs_model_view* m, orc_data* d) {
+/* mj_forwardSkip(m, d, mjSTAGE_NONE, skip_sensor) */
+static void forward_skip(const mrs_model_view* m, orc_data* d, int skip_sensor) {
   orc_ws* w = (orc_ws*)d->ws;
   int nv = m->nv;
   fwd_position(m, d);
@@ -2173,9 +2174,36 @@ void orc_forward(const mrs_model_view* m, orc_data* d) {
   chol_solve(w->L, w->qacc_smooth, w->qfrc_smooth, nv);
   /* constraint impedance/aref need efc_vel from qvel: recompute after comVel (rows built above) */
   fwd_constraint(m, d);
-  sensors(m, d);
+  if (!skip_sensor) sensors(m, d);
   d->ncon = w->ncon;
   d->nefc = w->nefc;
+}
+
+void orc_forward(const mrs_model_view* m, orc_data* d) { forward_skip(m, d, 0); }
+
+/* mj_integratePos: qpos advanced by h * vel (free joints: position and quaternion; ball: quaternion) */
+static void integrate_pos(const mrs_model_view* m, double* qpos, const double* vel, double h) {
+  for (int j = 0; j < m->njnt; ++j) {
+    int a = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    switch (m->jnt_type[j]) {
+      case MRS_JNT_FREE:
+        for (int i = 0; i < 3; ++i) qpos[a + i] += h * vel[da + i];
+        a += 3; da += 3;
+        /* fall through */
+      case MRS_JNT_BALL: {
+        double* q = qpos + a;
+        double v[3] = {vel[da], vel[da + 1], vel[da + 2]};
+        double ang = h * normalize3(v);
+        double dq[4];
+        axis_angle_quat(dq, v, ang);
+        quat_normalize(q);
+        quat_mul(q, q, dq);
+        quat_normalize(q);
+        break;
+      }
+      default: qpos[a] += h * vel[da];
+    }
+  }
 }
 
 /* mj_Euler (implicit in joint damping) and mj_implicit(implicitfast) [upstream engine_forward.c]:
@@ -2228,29 +2256,51 @@ static void integrate(const mrs_model_view* m, orc_data* d) {
   /* mj_advance: warm start keeps the constraint solver's qacc */
   memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(double));
   for (int j = 0; j < nv; ++j) d->qvel[j] += h * qacc_int[j];
-  /* mj_integratePos */
-  for (int j = 0; j < m->njnt; ++j) {
-    int a = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
-    switch (m->jnt_type[j]) {
-      case MRS_JNT_FREE:
-        for (int i = 0; i < 3; ++i) d->qpos[a + i] += h * d->qvel[da + i];
-        a += 3; da += 3;
-        /* fall through */
-      case MRS_JNT_BALL: {
-        double* q = d->qpos + a;
-        double v[3] = {d->qvel[da], d->qvel[da + 1], d->qvel[da + 2]};
-        double ang = h * normalize3(v);
-        double dq[4];
-        axis_angle_quat(dq, v, ang);
-        quat_normalize(q);
-        quat_mul(q, q, dq);
-        quat_normalize(q);
-        break;
-      }
-      default: d->qpos[a] += h * d->qvel[da];
-    }
-  }
+  integrate_pos(m, d->qpos, d->qvel, h);
   d->time += h;
+}
+
+/* mj_RungeKutta(m, d, 4) [upstream engine_forward.c], restated: the classic tableau A = diag(1/2, 1/2,
+ * 1), B = (1/6, 1/3, 1/3, 1/6), C = (1/2, 1/2, 1).  F_0 = (qvel, qacc) of the step's mj_forward; stage
+ * i = 1..3 sets X_i = X_0 '+' h A_i F_{i-1} (positions by mj_integratePos with velocity A_i qvel_{i-1},
+ * velocities qvel_0 + h A_i qacc_{i-1}) and evaluates F_i by mj_forwardSkip without sensors; then the
+ * state returns to X_0 and mj_advance moves it by h sum_j B_j F_j (qvel += h dX_acc, positions
+ * integrated with dX_vel), qacc_warmstart = the last stage's qacc [restated; verify against upstream].
+ * Sensor data stays that of the step's first forward, the other mjData outputs are the last stage's. */
+static void rk4(const mrs_model_view* m, orc_data* d) {
+  static const double A[3] = {0.5, 0.5, 1.0}, B[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
+  const int nq = m->nq, nv = m->nv;
+  const double h = m->timestep, t0 = d->time;
+  double* q0 = (double*)malloc((size_t)(nq ? nq : 1) * sizeof(double));
+  double* buf = (double*)calloc((size_t)(4 * nv + 1), sizeof(double));
+  double *v0 = buf, *sv = buf + nv, *sa = buf + 2 * nv, *dv = buf + 3 * nv;
+  memcpy(q0, d->qpos, nq * sizeof(double));
+  memcpy(v0, d->qvel, nv * sizeof(double));
+  for (int i = 1; i < 4; ++i) {
+    for (int j = 0; j < nv; ++j) {
+      const double vel = d->qvel[j], acc = d->qacc[j];
+      sv[j] += B[i - 1] * vel;
+      sa[j] += B[i - 1] * acc;
+      dv[j] = A[i - 1] * vel;
+      d->qvel[j] = v0[j] + h * (A[i - 1] * acc);
+    }
+    memcpy(d->qpos, q0, nq * sizeof(double));
+    integrate_pos(m, d->qpos, dv, h);
+    d->time = t0 + A[i - 1] * h;
+    forward_skip(m, d, 1);
+  }
+  for (int j = 0; j < nv; ++j) {
+    sv[j] += B[3] * d->qvel[j];
+    sa[j] += B[3] * d->qacc[j];
+  }
+  memcpy(d->qpos, q0, nq * sizeof(double));
+  /* mj_advance */
+  memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(double));
+  for (int j = 0; j < nv; ++j) d->qvel[j] = v0[j] + h * sa[j];
+  integrate_pos(m, d->qpos, sv, h);
+  d->time = t0 + h;
+  free(q0);
+  free(buf);
 }
 
 /* mj_checkPos / mj_checkVel / mj_checkAcc with auto-reset [upstream engine_forward.c] */
@@ -2274,7 +2324,8 @@ void orc_step(const mrs_model_view* m, orc_data* d) {
   check(m, d, d->qvel, m->nv, 1);
   orc_forward(m, d);
   if (check(m, d, d->qacc, m->nv, 2)) orc_forward(m, d);
-  integrate(m, d);
+  if (m->integrator == MRS_INT_RK4) rk4(m, d);
+  else integrate(m, d);
 }
 
 void orc_mass_matrix(const mrs_model_view* m, orc_data* d, double* M) {

@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
       "", "<mujoco", "<mujoco><worldbody><body><geom type=\"box\"/></body></worldbody>",
       "<mujoco><worldbody><geom type=\"mesh\"/></worldbody></mujoco>",
       "<mujoco><worldbody><body><joint type=\"hinge\" range=\"1\"/><geom size=\"0.1\"/></body></worldbody></mujoco>",
-      "<mujoco><option integrator=\"RK4\"/><worldbody/></mujoco>",
+      "<mujoco><option integrator=\"implicit\"/><worldbody/></mujoco>",
       "<mujoco><worldbody><geom type=\"sphere\" size=\"-1 x\"/></worldbody></mujoco>",
       "<mujoco><worldbody><replicate count=\"-3\"><site/></replicate></worldbody></mujoco>",
       "<mujoco><asset><mesh name=\"m\" vertex=\"0 0 0 1 0\"/></asset><worldbody><geom type=\"mesh\" mesh=\"m\"/></worldbody></mujoco>",

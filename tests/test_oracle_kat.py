@@ -259,3 +259,47 @@ def test_friction_sphere_rolls_at_five_sevenths():
     d.step(500)
     assert abs(d.qvel[0] - 5 / 7) < 0.01
     assert abs(d.qvel[4] * 0.1 - d.qvel[0]) < 0.01   # rolling: omega r = v
+
+
+def _rk4_step(f, x, h):
+    k1 = f(x)
+    k2 = f(x + 0.5 * h * k1)
+    k3 = f(x + 0.5 * h * k2)
+    k4 = f(x + h * k3)
+    return x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+
+
+def test_servo_rk4_closed_form():
+    """mj_RungeKutta(4) on a damped position servo: every force is explicit under RK4 (joint damping
+    and the actuator's kv included), so each step is the classic RK4 map of q' = v,
+    v' = (kp (c - q) - (b + kv) v) / I"""
+    I, b, kp, kv, h, c = 0.5, 0.3, 40.0, 2.0, 0.002, 0.8
+    m = sim.Model.from_string(SERVO.format(integ="RK4", b=b, I=I, kp=kp, kv=kv))
+    d = binding.OracleData(m)
+    d.ctrl[:] = [c]
+    f = lambda x: np.array([x[1], (kp * (c - x[0]) - (b + kv) * x[1]) / I])  # noqa: E731
+    x = np.zeros(2)
+    for _ in range(300):
+        x = _rk4_step(f, x, h)
+        d.step()
+        assert d.qpos[0] == pytest.approx(x[0], rel=1e-12, abs=1e-14)
+        assert d.qvel[0] == pytest.approx(x[1], rel=1e-12, abs=1e-14)
+    assert d.time == pytest.approx(300 * h)
+
+
+def test_ballistic_free_body_rk4():
+    """RK4 integrates constant gravity exactly (z = z0 + v t - g t^2 / 2) and a constant spin of an
+    isotropic body exactly (no gyroscopic torque)"""
+    xml = """<mujoco><option timestep="0.01" integrator="RK4"/><worldbody><body pos="0 0 5"><freejoint/>
+    <geom type="sphere" size="0.1" contype="0" conaffinity="0"/></body></worldbody></mujoco>"""
+    m = sim.Model.from_string(xml)
+    d = binding.OracleData(m)
+    d.qvel[:] = [1.0, -0.5, 2.0, 0, 0, 3.0]
+    h, g, n = 0.01, 9.81, 100
+    d.step(n)
+    t = n * h
+    assert d.qpos[2] == pytest.approx(5 + 2.0 * t - 0.5 * g * t * t, rel=1e-12)
+    assert d.qvel[2] == pytest.approx(2.0 - g * t, rel=1e-12)
+    assert d.qpos[0] == pytest.approx(1.0 * t) and d.qpos[1] == pytest.approx(-0.5 * t)
+    ang = 3.0 * t
+    np.testing.assert_allclose(d.qpos[3:], [np.cos(ang / 2), 0, 0, np.sin(ang / 2)], atol=1e-12)
