@@ -3876,6 +3876,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     float Mg;
     if (newton) {
       // H row `lane` (dense: into the factor slot L.L; blocked: L.H, by MFMA), then factor in place
+      unsigned long long t_h = SUB_T();
       if constexpr (G == 64) {
         hessian_mfma64(m, s, J, st, Rr, nefc, H, lane);
       } else {
@@ -3890,9 +3891,12 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
           }
       }
       wsync();
+      SUB_ADD(PH_CON_DEL, t_h);
+      t_h = SUB_T();
       if constexpr (G == 64) {
         chol_dense<G>(H, nv, lane);
         Mg = chol_solve_dense<G>(H, grad, nv, lane);
+        SUB_ADD(PH_CON_WARM, t_h);
       } else {
         MRS_CALL(G, cholesky<G>(mp, H, H, lane));
         MRS_CALL(G, Mg = chol_solve_lanes<G>(mp, H, grad, lane));
@@ -4517,6 +4521,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       }
     }
     [[clang::noinline]] qa = solve_primal<G>(ENV_ARGS, nefc, newton);
+    SUB_ADD(PH_CON_PGS, t_sub);
     return qa;
   }
   if constexpr (G == 16) {

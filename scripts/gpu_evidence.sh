@@ -17,9 +17,12 @@ if [ "${PART:-A}" = A ]; then
     timeout -k 10 300 python bench.py --config $c > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit $?
   done
   timeout -k 10 300 python bench.py --config c3 --scene scenes/arm7_lidar1080.xml --no-cpu-baseline > gpurun_out/bench_c3_1080.json 2> gpurun_out/bench_c3_1080.err || exit $?
+  # MuJoCo's default solver on the contact-rich scene and the reference scene under PGS (extra lines)
+  timeout -k 10 300 python bench.py --config c5 --solver Newton --steps 40 --warmup 4 --no-cpu-baseline > gpurun_out/bench_c5_newton.json 2> gpurun_out/bench_c5_newton.err || exit $?
+  timeout -k 10 300 python bench.py --config c4 --solver Newton --no-cpu-baseline > gpurun_out/bench_c4_newton.json 2> gpurun_out/bench_c4_newton.err || exit $?
   exit 0
 fi
-for c in $CFGS; do
+[ "${SKIP_STATS:-0}" = 1 ] || for c in $CFGS; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rocprof_$c -o run -- python3 bench.py --config $c --no-cpu-baseline > gpurun_out/rocprof_$c.log 2>&1 || exit $?
 done
 [ "${SKIP_PMC:-0}" = 1 ] && exit 0

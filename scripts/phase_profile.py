@@ -1,6 +1,6 @@
 """Per-phase cycle breakdown of the step kernel with a profiling build (MRS_LIB pointing at a
 library built with -DMRS_PHASE_TIMING, e.g. scripts/build_variant.sh timing -DMRS_PHASE_TIMING).
-Usage: phase_profile.py [scene.xml] [n_envs] [launches]  (default: C3, 8192 envs, 20 launches)"""
+Usage: phase_profile.py [scene.xml|c2] [n_envs] [launches] [solver]  (default: C3, 8192 envs, 20 launches)"""
 import json
 import sys
 from pathlib import Path
@@ -23,7 +23,12 @@ if scene == "c2":  # the C2 bench scene: the reference's scene.xml with sensors 
     model = sim.Model.from_string(*ref_scene_xml(sensors=False))
     scene = "scene"
 else:
-    model = sim.Model.load(scene)
+    xml = Path(scene).read_text()
+    if len(sys.argv) > 4:  # solver override (bench.py --solver)
+        sys.path.insert(0, str(ROOT))
+        from bench import with_solver  # noqa: E402
+        xml = with_solver(xml, sys.argv[4])
+    model = sim.Model.from_string(xml, str(Path(scene).parent))
 b = sim.Batch(model, n)
 b.set(sim.FIELD_QPOS, synth.initial_qpos(model, np.arange(n)))
 table = torch.from_numpy(synth.ctrl_table(model, np.arange(n), launches + 2, period).astype(np.float32)).cuda()
