@@ -17,7 +17,7 @@ if [ "${PART:-A}" = A ]; then
     timeout -k 10 300 python bench.py --config $c > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit $?
   done
   timeout -k 10 300 python bench.py --config c3 --scene scenes/arm7_lidar1080.xml --no-cpu-baseline > gpurun_out/bench_c3_1080.json 2> gpurun_out/bench_c3_1080.err || exit $?
-  # MuJoCo's default solver on the contact-rich scene and the reference scene under PGS (extra lines)
+  # extra lines: C5 and C4 under MuJoCo's default solver (Newton)
   timeout -k 10 300 python bench.py --config c5 --solver Newton --steps 40 --warmup 4 --no-cpu-baseline > gpurun_out/bench_c5_newton.json 2> gpurun_out/bench_c5_newton.err || exit $?
   timeout -k 10 300 python bench.py --config c4 --solver Newton --no-cpu-baseline > gpurun_out/bench_c4_newton.json 2> gpurun_out/bench_c4_newton.err || exit $?
   exit 0
