@@ -4374,6 +4374,58 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       for (int r = m.nfric; r < nefc; ++r) floss[r] = 0;
   }
   // --- contact rows: lane per dof, loop over contacts
+  if constexpr (G == 64) {
+    // blocked mode (Newton / CG): every contact's record and pair data are loaded lane-parallel up
+    // front (lane = contact) and taken by readlane in the row loop, whose Jacobian columns then come
+    // from LDS alone (jac_col_blk) -- no dependent global round trip per contact
+    #pragma unroll 1
+    for (int c0 = 0; c0 < ncon; c0 += 64) {
+      const int ci = c0 + lane;
+      const bool in = ci < ncon;
+      const gfloat* rc = scr + S.con + kConRec * (in ? ci : c0);
+      const int pl = __float_as_int(rc[0]);
+      float cv[13];
+      for (int i = 0; i < 13; ++i) cv[i] = rc[1 + i];  // dist, pos[3], frame[9]
+      const int dl = m.pair_dim[pl];
+      const int b1l = m.geom_bodyid[m.pair_g1[pl]], b2l = m.geom_bodyid[m.pair_g2[pl]];
+      const int r1l = m.body_rootid[b1l], r2l = m.body_rootid[b2l];
+      const float mul = m.pair_friction[3 * pl], mgl = m.pair_margin[pl] - m.pair_gap[pl];
+      const int nc = ncon - c0 < 64 ? ncon - c0 : 64;
+      #pragma unroll 1
+      for (int k = 0; k < nc; ++k) {
+        const int c = c0 + k;
+        const int dim = __builtin_amdgcn_readlane(dl, k);
+        const int b1 = __builtin_amdgcn_readlane(b1l, k), b2 = __builtin_amdgcn_readlane(b2l, k);
+        const int r1 = __builtin_amdgcn_readlane(r1l, k), r2 = __builtin_amdgcn_readlane(r2l, k);
+        const float dist = bcast(cv[0], k), mu = bcast(mul, k), mg = bcast(mgl, k);
+        float cp[3] = {bcast(cv[1], k), bcast(cv[2], k), bcast(cv[3], k)};
+        float fr[9];
+        for (int i = 0; i < 9; ++i) fr[i] = bcast(cv[4 + i], k);
+        if (lane == 0) scr[S.con + kConRec * c + 14] = __int_as_float(nefc + (dim == 1 ? 1 : 4) <= m.max_efc ? nefc : -1);
+        float jc[3] = {0, 0, 0};
+        if (lane < nv) {
+          float c1[3], c2[3];
+          jac_col_blk(s, L, b1, r1, cp, lane, c1);
+          jac_col_blk(s, L, b2, r2, cp, lane, c2);
+          const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+          for (int r = 0; r < 3; ++r) jc[r] = fr[3 * r] * dc[0] + fr[3 * r + 1] * dc[1] + fr[3 * r + 2] * dc[2];
+        }
+        const int nrow = dim == 1 ? 1 : 4;
+        for (int q = 0; q < nrow; ++q) {
+          if (nefc >= m.max_efc) break;
+          // pyramid edges: both tangent directions use the sliding coefficient (mj_setContact)
+          const int kk = 1 + (q >> 1);
+          const float sg = (q & 1) ? -1.0f : 1.0f;
+          if (lane < nv) J[nefc * nv + lane] = dim == 1 ? jc[0] : jc[0] + sg * mu * (kk == 1 ? jc[1] : jc[2]);
+          if (lane == 0) {
+            type[nefc] = __int_as_float(EFC_CONTACT * 65536 + c);
+            pos[nefc] = dist; marg[nefc] = mg; floss[nefc] = 0;
+          }
+          ++nefc;
+        }
+      }
+    }
+  } else
   #pragma unroll 1
   for (int c = 0; c < ncon; ++c) {
     gfloat* rec = scr + S.con + kConRec * c;
