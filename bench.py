@@ -232,7 +232,7 @@ def run_c1(args):
         "paced_steps_per_s": paced, "paced_expected": speed / h, "sim_speed_factor": speed,
         "unpaced_single_step_per_s": single,
         "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None,
-                     "traffic": None, "kernel": "step_kernel<16, false> (10-step launch of 1 env)",
+                     "traffic": None, "kernel": "step_kernel<16, false, true> (10-step launch of 1 env; Newton kernel)",
                      "kernel_ms": kernel_ms,
                      "note": "one env occupies one 16-lane group of one wave: a launch- and copy-latency "
                              "measurement, not a roofline one; host overhead per cycle = ms_per_step - kernel_ms"},

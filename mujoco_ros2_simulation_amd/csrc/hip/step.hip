@@ -3828,11 +3828,15 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     wsync();
   };
   // mj_constraintUpdate at the stored jar: row states and forces; returns (J' f)_lane
+  // (chg: some row's state differs from the one stored before)
+  bool chg = false;
   auto update = [&]() {
+    chg = false;
     #pragma unroll 1
     for (int r = lane; r < nefc; r += G) {
       const float R = Rr[r], fl = floss[r], ja = jar[r];
       const int stt = prow_state(is_fric(r), R, fl, ja);
+      chg |= __float_as_int(st[r]) != stt;
       st[r] = __int_as_float(stt);
       ff[r] = -prow_slope(stt, R, fl, ja);
     }
@@ -3869,12 +3873,21 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
   float qfrc = update();
   float p = 0, gold = 0, Mgold = 0;
   bool refined = false;
+  // the Hessian's factor in H is still that of the current row states (refinement step after a step
+  // that kept the active set): H = M + J'DJ depends on the states only, so it is not rebuilt
+  bool reuse = false;
   int nit = 0;  // steps taken (mjData.solver_niter)
   #pragma unroll 1
   for (int iter = 0;; ++iter) {
     const float grad = dof ? Md - qfrc : 0.0f;
     float Mg;
-    if (newton) {
+    if (newton && reuse) {
+      if constexpr (G == 64) {
+        Mg = chol_solve_dense<G>(H, grad, nv, lane);
+      } else {
+        MRS_CALL(G, Mg = chol_solve_lanes<G>(mp, H, grad, lane));
+      }
+    } else if (newton) {
       // H row `lane` (dense: into the factor slot L.L; blocked: L.H, by MFMA), then factor in place
       unsigned long long t_h = SUB_T();
       if constexpr (G == 64) {
@@ -3992,6 +4005,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
       Md = mmul(qa - qs);
       jmul(qa, jar, 1.0f);
       qfrc = update();
+      reuse = !gany<G>(chg);
     }
   }
   if (dof) s[L.qfrc_con + lane] = qfrc;
@@ -4084,14 +4098,16 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
   jar = rows_dot(qa) - myaref;
   float qfrc = update();
   float p = 0, gold = 0, Mgold = 0;
-  bool refined = false;
+  bool refined = false, reuse = false;  // reuse: H's factor is that of the current row states
   int nit = 0;
   lfloat* H = s + L.L;
   #pragma unroll 1
   for (int iter = 0;; ++iter) {
     const float grad = dof ? Md - qfrc : 0.0f;
     float Mg;
-    if (newton) {
+    if (newton && reuse) {
+      MRS_CALL(16, Mg = chol_solve_lanes<16>(mp, H, grad, lane));
+    } else if (newton) {
       // H = M + J' diag(D of quadratic rows) J, row `lane` in registers, then factored in the LDS
       // factor slot (M's factor is not needed again before integrate() refactors)
       const float Dr = (row && st == PST_QUAD) ? 1.0f / myR : 0.0f;
@@ -4189,7 +4205,9 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
       refined = true;
       Md = mmul(qa - qs);
       jar = rows_dot(qa) - myaref;
+      const int st_old = st;
       qfrc = update();
+      reuse = !gany<16>(st != st_old);
     }
   }
   if (dof) s[L.qfrc_con + lane] = qfrc;
