@@ -1,5 +1,6 @@
 """MJCF-subset compiler against the reference's own scenes (tests/golden/ref_scenes, copied from
 test/test_resources/) and closed-form constants."""
+from pathlib import Path
 import numpy as np
 import pytest
 
@@ -195,3 +196,23 @@ def test_compiler_accepts_converter_options():
     m = _body_model('assetdir="assets" balanceinertia="true" discardvisual="false" strippath="false" angle="radian"',
                     '<inertial pos="0 0 0" mass="2" diaginertia="0.1 0.2 0.25"/>')
     assert m.nbody == 2
+
+
+def test_integrator_options():
+    """<option integrator>: Euler / implicitfast / RK4 compile (RK4 runs as mj_RungeKutta's 4 stages),
+    the full implicit integrator is rejected at load, never silently replaced"""
+    base = '<mujoco><option integrator="{}"/><worldbody><body><joint/><geom size="0.1"/></body></worldbody></mujoco>'
+    for name, code in (("Euler", 0), ("RK4", 1), ("implicitfast", 3)):
+        assert sim.Model.from_string(base.format(name)).integrator == code
+    with pytest.raises(sim.MrsError, match="not supported"):
+        sim.Model.from_string(base.format("implicit"))
+
+
+def test_bench_solver_override():
+    """bench.py --solver rewrites or inserts <option solver> (the C5-under-Newton line)"""
+    import bench
+    xml = (Path(__file__).resolve().parents[1] / "scenes" / "arm_boxes.xml").read_text()
+    out = bench.with_solver(xml, "Newton")
+    assert 'solver="Newton"' in out and 'solver="PGS"' not in out and 'iterations="50"' in out
+    bare = "<mujoco><worldbody/></mujoco>"
+    assert '<option solver="CG"/>' in bench.with_solver(bare, "CG")
