@@ -118,13 +118,26 @@ def cpu_baseline(model, period: int, target_s: float):
 
 
 # ------------------------------------------------------------------------------------------------ evidence
-def committed(kind: str, cfg: str, envs: int, period: int):
-    """newest committed rocprofv3 PMC summary `profiles/r*/<kind>_<cfg>.json` of this same bench
-    command (scripts/gpu_full.sh -> scripts/pmc_summary.py); None for other workload sizes"""
+def variant_key(cfg: str, solver: str | None, scene: str | None) -> str:
+    """file key of one bench command's counter summaries: the config, plus the solver and scene when
+    they override the config's own (e.g. c5_newton, c3_arm7_lidar1080), so a bench line never
+    carries the counters of a different kernel run (scripts/gpu_evidence.sh collects them per key)"""
+    key = cfg
+    if solver:
+        key += "_" + solver.lower()
+    if scene:
+        key += "_" + Path(scene).stem
+    return key
+
+
+def committed(kind: str, cfg: str, envs: int, period: int, key: str | None = None):
+    """newest committed rocprofv3 PMC summary `profiles/r*/<kind>_<key>.json` of this same bench
+    command (scripts/gpu_evidence.sh -> scripts/pmc_summary.py); None for other workload sizes or
+    when no summary of exactly this variant (config + solver + scene) was collected"""
     default_envs = {"c2": 4096, "c3": 8192, "c3m": 8192, "c4": 2048, "c5": 8192}
     if cfg not in default_envs or envs != default_envs[cfg] or period != 10:
         return None, None
-    found = sorted(ROOT.glob(f"profiles/r*/{kind}_{cfg}.json"))
+    found = sorted(ROOT.glob(f"profiles/r*/{kind}_{key or cfg}.json"))
     if not found:
         return None, None
     return json.loads(found[-1].read_text()), str(found[-1].relative_to(ROOT))
@@ -279,6 +292,7 @@ def main():
     torch.cuda.set_device(local)
     dev = f"cuda:{local}"
     cfg = args.config
+    vkey = variant_key(cfg, args.solver, args.scene)
     if args.scene:
         path = Path(args.scene)
         xml, base = path.read_text(), str(path.parent)
@@ -400,8 +414,8 @@ def main():
               "parallelism": f"env-sharded x{world}",
               "obs_gather": ("per period (qpos, qvel) of every env to rank 0, RCCL batch_isend_irecv"
                              if gather is not None else None)}
-    traffic_rec, traffic_src = committed("pmc", cfg, n, args.period)
-    sq_rec, sq_src = committed("sq", cfg, n, args.period)
+    traffic_rec, traffic_src = committed("pmc", cfg, n, args.period, vkey)
+    sq_rec, sq_src = committed("sq", cfg, n, args.period, vkey)
     if render:
         config["depth_every_physics_steps"] = every * args.period
         config["camera_pipeline"] = ("frames rendered on the batch stream between steps" if args.render_sync else
@@ -430,7 +444,7 @@ def main():
                 "flops_per_env_step_structural": detailed_flops,
                 "algorithmic_bytes_per_env_step": roofline.bytes_per_env_step(model, args.period),
                 "note": "fp32 vector-ALU bound path (no GEMM-shaped work at these sizes); peak = fp32 VALU rate"}
-    fl_rec, fl_src = committed("flops", cfg, n, args.period)
+    fl_rec, fl_src = committed("flops", cfg, n, args.period, vkey)
     if not render:
         roof["frac_model"] = roof["frac"]
         if fl_rec:

@@ -1268,9 +1268,16 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   b.g16_one_wg = 0;
   if (b.group > 16 && m.nv <= 16) {
     if (d.rf_common) {
+      // drop the common-frame ray table only if that is what lets the 16-lane layout fit; otherwise
+      // the model keeps its wider groups and the table (no silent slowdown of the ray pass)
       d.rf_common = 0;
       layout_shared();
-      if (lds_bytes(16) <= 80 * 1024) b.group = 16;
+      if (lds_bytes(16) <= 80 * 1024) {
+        b.group = 16;
+      } else {
+        d.rf_common = 1;
+        layout_shared();
+      }
     }
     // (one 160 KB workgroup per CU was measured slower than 32-lane groups on the mesh robot: 27 vs
     // 15 ms per 10-step launch -- a single wave per SIMD cannot hide its memory latency)

@@ -20,6 +20,8 @@ namespace mrs {
 
 namespace {
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+
 constexpr float kMinVal = 1e-15f;
 constexpr float kMaxVal = 1e10f;
 
@@ -561,8 +563,15 @@ __device__ __forceinline__ void capsule_ends(const float* pos, const float* mat,
 // The poses are read from the env's LDS and the sizes from the model here, not passed as arrays: a
 // caller array whose address escapes into a call lives in scratch, and the caller's pair loop would
 // store every pair's pose there whether or not it reaches this function.
+// row i (0..2, runtime) of a 3x3 register matrix / element i of a 3-vector, by selects: a runtime
+// index into a private array would place the array in scratch memory
+__device__ __forceinline__ void row3_sel(const float M[3][3], int i, float out[3]) {
+  for (int c = 0; c < 3; ++c) out[c] = i == 0 ? M[0][c] : (i == 1 ? M[1][c] : M[2][c]);
+}
+__device__ __forceinline__ float elt3_sel(const float v[3], int i) { return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]); }
+
 template <int G>
-__device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CPtr<float> gsize, int g1, int g2,
+__device__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CPtr<float> gsize, int g1, int g2,
                                     float margin, gCon* out) {
   float p1[3], p2[3], h1[3], h2[3], A[3][3], B[3][3];
   for (int i = 0; i < 3; ++i) {
@@ -576,31 +585,38 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
   // a later face axis must beat the best by more than `tie` (oracle.c col_box_box): resting faces have
   // equal separations along both boxes' normals, and rounding must not pick the reference face
   const float tie = 1e-5f * (h1[0] + h1[1] + h1[2] + h2[0] + h2[1] + h2[2]);
-  #pragma unroll 1
-  for (int k = 0; k < 15; ++k) {
+  // the 15 axes unrolled (every matrix index compile-time: the boxes' frames stay in registers); a
+  // separating axis is remembered and ends the test after the loop -- the same answer as leaving at it
+  bool separated = false;
+  unroll<15>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     float L[3];
-    if (k < 3) { L[0] = A[k][0]; L[1] = A[k][1]; L[2] = A[k][2]; }
-    else if (k < 6) { L[0] = B[k - 3][0]; L[1] = B[k - 3][1]; L[2] = B[k - 3][2]; }
+    if constexpr (k < 3) { L[0] = A[k][0]; L[1] = A[k][1]; L[2] = A[k][2]; }
+    else if constexpr (k < 6) { L[0] = B[k - 3][0]; L[1] = B[k - 3][1]; L[2] = B[k - 3][2]; }
     else cross3(L, A[(k - 6) / 3], B[(k - 6) % 3]);
     const float ln = sqrtf(dot3(L, L));
-    if (ln < 1e-6f) continue;
-    for (int c = 0; c < 3; ++c) L[c] /= ln;
-    float ra = 0, rb = 0;
-    for (int i = 0; i < 3; ++i) { ra += h1[i] * fabsf(dot3(A[i], L)); rb += h2[i] * fabsf(dot3(B[i], L)); }
-    const float sv = dot3(d, L);
-    const float sep = fabsf(sv) - ra - rb;
-    if (sep > margin) return 0;
-    const float sg = sv >= 0 ? 1.0f : -1.0f;
-    if (k < 6) {
-      if (sep > best_face + tie) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
-    } else if (sep > best_edge) {
-      best_edge = sep; edge_i = (k - 6) / 3; edge_j = (k - 6) % 3;
-      for (int c = 0; c < 3; ++c) ne[c] = sg * L[c];
+    if (ln >= 1e-6f) {
+      for (int c = 0; c < 3; ++c) L[c] /= ln;
+      float ra = 0, rb = 0;
+      for (int i = 0; i < 3; ++i) { ra += h1[i] * fabsf(dot3(A[i], L)); rb += h2[i] * fabsf(dot3(B[i], L)); }
+      const float sv = dot3(d, L);
+      const float sep = fabsf(sv) - ra - rb;
+      separated |= sep > margin;
+      const float sg = sv >= 0 ? 1.0f : -1.0f;
+      if constexpr (k < 6) {
+        if (sep > best_face + tie) { best_face = sep; face_axis = k; for (int c = 0; c < 3; ++c) nf[c] = sg * L[c]; }
+      } else if (sep > best_edge) {
+        best_edge = sep; edge_i = (k - 6) / 3; edge_j = (k - 6) % 3;
+        for (int c = 0; c < 3; ++c) ne[c] = sg * L[c];
+      }
     }
-  }
-  if (face_axis < 0) return 0;
+  });
+  if (separated || face_axis < 0) return 0;
   if (edge_i >= 0 && best_edge > best_face + 0.05f * fabsf(best_face) + 1e-6f) {
-    float a0[3], a1[3], b0[3], b1[3], c1[3], c2[3];
+    float a0[3], a1[3], b0[3], b1[3], c1[3], c2[3], Ae[3], Be[3];
+    row3_sel(A, edge_i, Ae);
+    row3_sel(B, edge_j, Be);
+    const float hae = elt3_sel(h1, edge_i), hbe = elt3_sel(h2, edge_j);
     for (int c = 0; c < 3; ++c) { a0[c] = p1[c]; b0[c] = p2[c]; }
     for (int i = 0; i < 3; ++i) {
       if (i != edge_i) {
@@ -613,8 +629,8 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
       }
     }
     for (int c = 0; c < 3; ++c) {
-      a1[c] = a0[c] + h1[edge_i] * A[edge_i][c]; a0[c] -= h1[edge_i] * A[edge_i][c];
-      b1[c] = b0[c] + h2[edge_j] * B[edge_j][c]; b0[c] -= h2[edge_j] * B[edge_j][c];
+      a1[c] = a0[c] + hae * Ae[c]; a0[c] -= hae * Ae[c];
+      b1[c] = b0[c] + hbe * Be[c]; b0[c] -= hbe * Be[c];
     }
     seg_seg_closest(a0, a1, b0, b1, c1, c2);
     gCon& o = out[0];
@@ -622,17 +638,17 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
     o.dist = best_edge;
     return 1;
   }
-  // face case: reference box r (normal nr pointing at the other box), incident box i
+  // face case: reference box r (normal nr pointing at the other box), incident box i (register
+  // copies chosen by selects)
   const bool refA = face_axis < 3;
   const int ir = refA ? face_axis : face_axis - 3;
-  const float* pr = refA ? p1 : p2;
-  const float* pi = refA ? p2 : p1;
-  const float* hr = refA ? h1 : h2;
-  const float* hi = refA ? h2 : h1;
-  float nr[3];
-  for (int c = 0; c < 3; ++c) nr[c] = refA ? nf[c] : -nf[c];
-  float (*Rr)[3] = refA ? A : B;
-  float (*Ri)[3] = refA ? B : A;
+  float pr[3], pi[3], hr[3], hi[3], Rr[3][3], Ri[3][3], nr[3];
+  for (int c = 0; c < 3; ++c) {
+    pr[c] = refA ? p1[c] : p2[c]; pi[c] = refA ? p2[c] : p1[c];
+    hr[c] = refA ? h1[c] : h2[c]; hi[c] = refA ? h2[c] : h1[c];
+    nr[c] = refA ? nf[c] : -nf[c];
+    for (int e = 0; e < 3; ++e) { Rr[c][e] = refA ? A[c][e] : B[c][e]; Ri[c][e] = refA ? B[c][e] : A[c][e]; }
+  }
   int j = 0;
   float bestc = -1;
   for (int k = 0; k < 3; ++k) {
@@ -640,7 +656,10 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
     if (cc > bestc) { bestc = cc; j = k; }
   }
   const int k1 = (j + 1) % 3, k2 = (j + 2) % 3;
-  const float sgn = dot3(Ri[j], nr) > 0 ? -1.0f : 1.0f;
+  float Rij[3], Rik1[3], Rik2[3];
+  row3_sel(Ri, j, Rij); row3_sel(Ri, k1, Rik1); row3_sel(Ri, k2, Rik2);
+  const float hij = elt3_sel(hi, j), hik1 = elt3_sel(hi, k1), hik2 = elt3_sel(hi, k2);
+  const float sgn = dot3(Rij, nr) > 0 ? -1.0f : 1.0f;
   // Clipping in the reference face's frame: u, v along its in-plane axes Rr[r1], Rr[r2] and w along
   // nr, measured from the face centre cr, so the four side planes are |u| <= hr[r1], |v| <= hr[r2]
   // and a vertex's separation is w.  Sutherland-Hodgman with the polygon in 8 static register slots:
@@ -648,21 +667,24 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
   // takes the candidate whose running count is o (no private-memory arrays: a scratch round trip per
   // vertex made this the slowest part of the contact-rich step).
   const int r1 = (ir + 1) % 3, r2 = (ir + 2) % 3;
+  float Rr1[3], Rr2[3];
+  row3_sel(Rr, r1, Rr1); row3_sel(Rr, r2, Rr2);
+  const float hr0 = elt3_sel(hr, ir), hr1 = elt3_sel(hr, r1), hr2 = elt3_sel(hr, r2);
   float cr[3];
-  for (int c = 0; c < 3; ++c) cr[c] = pr[c] + hr[ir] * nr[c];
+  for (int c = 0; c < 3; ++c) cr[c] = pr[c] + hr0 * nr[c];
   float pu[8], pv[8], pw[8];
   for (int vtx = 0; vtx < 4; ++vtx) {
     const float su = (vtx == 0 || vtx == 3) ? 1.0f : -1.0f, sv = (vtx < 2) ? 1.0f : -1.0f;
     float q[3];
     for (int c = 0; c < 3; ++c)
-      q[c] = pi[c] + sgn * hi[j] * Ri[j][c] + su * hi[k1] * Ri[k1][c] + sv * hi[k2] * Ri[k2][c] - cr[c];
-    pu[vtx] = dot3(q, Rr[r1]); pv[vtx] = dot3(q, Rr[r2]); pw[vtx] = dot3(q, nr);
+      q[c] = pi[c] + sgn * hij * Rij[c] + su * hik1 * Rik1[c] + sv * hik2 * Rik2[c] - cr[c];
+    pu[vtx] = dot3(q, Rr1); pv[vtx] = dot3(q, Rr2); pw[vtx] = dot3(q, nr);
   }
   for (int vtx = 4; vtx < 8; ++vtx) { pu[vtx] = 0; pv[vtx] = 0; pw[vtx] = 0; }
   int np = 4;
 #pragma unroll
   for (int side = 0; side < 4; ++side) {
-    const float lim = (side < 2) ? hr[r1] : hr[r2];
+    const float lim = (side < 2) ? hr1 : hr2;
     const float sg = (side & 1) ? -1.0f : 1.0f;
     float f[8];
 #pragma unroll
@@ -704,7 +726,7 @@ __device__ __noinline__ int box_box(const lfloat* gxpos, const lfloat* gxmat, CP
       const float bu = pu[vtx], bv = pv[vtx], bs = pw[vtx];
       gCon& o = out[n++];
       for (int c = 0; c < 3; ++c) {
-        const float pt = cr[c] + bu * Rr[r1][c] + bv * Rr[r2][c] + bs * nr[c];
+        const float pt = cr[c] + bu * Rr1[c] + bv * Rr2[c] + bs * nr[c];
         o.pos[c] = pt - nr[c] * bs / 2;
         o.nrm[c] = nf[c];
       }
@@ -1070,7 +1092,16 @@ __device__ int narrowphase(const DevModel& m, int t1, int t2, const float* p1, c
 #ifdef MRS_DIAG_NOBB
     return 0;  // diagnostic build only: no box-box contacts
 #endif
-    return box_box<G>(gxpos, gxmat, gsize, g1, g2, margin, out);
+    int n;
+#ifdef MRS_BB_INLINE
+    if constexpr (G == 64) {
+      [[clang::always_inline]] n = box_box<G>(gxpos, gxmat, gsize, g1, g2, margin, out);
+    } else
+#endif
+    {
+      [[clang::noinline]] n = box_box<G>(gxpos, gxmat, gsize, g1, g2, margin, out);
+    }
+    return n;
   }
   // every other pair has an ellipsoid, cylinder or mesh: general convex (MPR)
   return convex_convex(m, g1, g2, p1, m1, s1, p2, m2, s2, margin, out);
@@ -1107,7 +1138,7 @@ enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
 // around each phase, summed per wave and added to a device table at the end of the kernel.
 enum { PH_KIN, PH_COMPOS, PH_MAKEM, PH_CHOL, PH_COMVEL, PH_RNE, PH_SMOOTH, PH_COLL, PH_CONSTR, PH_SENS,
        PH_INTEG, PH_CHECK, PH_SENS_L1, PH_SENS_SETUP, PH_SENS_GEOMS, PH_CON_ROWS, PH_CON_REC, PH_CON_WARM,
-       PH_CON_PGS, PH_COLL_NARROW, PH_COLL_OUT, PH_CON_DEL, PH_COUNT };
+       PH_CON_PGS, PH_COLL_NARROW, PH_COLL_OUT, PH_CON_DEL, PH_REC_J, PH_REC_SOLVE, PH_REC_ROWS, PH_COUNT };
 #ifdef MRS_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[PH_COUNT];
 #define SUB_T() __builtin_amdgcn_s_memtime()
@@ -2016,17 +2047,46 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
     unsigned long long t_out = SUB_T();
     int total;
     int off = gscan_excl<G>(n, lane, total);
-    #pragma unroll 1
-    for (int k = 0; k < n; ++k) {
-      const int slot = ncon + off + k;
-      if (slot >= m.max_con) break;
-      gfloat* rec = scr + S.con + kConRec * slot;
-      float fr[9] = {c[k].nrm[0], c[k].nrm[1], c[k].nrm[2], 0, 0, 0, 0, 0, 0};
-      make_frame(fr);
-      rec[0] = __int_as_float(p);
-      rec[1] = c[k].dist;
-      for (int i = 0; i < 3; ++i) rec[2 + i] = c[k].pos[i];
-      for (int i = 0; i < 9; ++i) rec[5 + i] = fr[i];
+    if constexpr (G == 64) {
+      // the next staged contact is loaded before this one's record is stored: a staging load issued
+      // after a store would wait for it (vmcnt counts stores too), one store round trip per contact
+      // of a box-box face polygon
+      auto ld = [&](int k) {
+        Con o;
+        const gfloat* cf = (const gfloat*)(c + k);
+        o.dist = cf[0];
+        for (int i = 0; i < 3; ++i) { o.pos[i] = cf[1 + i]; o.nrm[i] = cf[4 + i]; }
+        return o;
+      };
+      Con nx = ld(0);
+      #pragma unroll 1
+      for (int k = 0; k < n; ++k) {
+        const Con cur = nx;
+        nx = ld(k + 1 < kMaxPairCon ? k + 1 : k);
+        const int slot = ncon + off + k;
+        if (slot >= m.max_con) break;
+        // (words 14, 15 are the rows phase's; written here only to make four 16-byte stores)
+        __attribute__((address_space(1))) v4f* rec = (__attribute__((address_space(1))) v4f*)(scr + S.con + kConRec * slot);
+        float fr[9] = {cur.nrm[0], cur.nrm[1], cur.nrm[2], 0, 0, 0, 0, 0, 0};
+        make_frame(fr);
+        rec[0] = (v4f){__int_as_float(p), cur.dist, cur.pos[0], cur.pos[1]};
+        rec[1] = (v4f){cur.pos[2], fr[0], fr[1], fr[2]};
+        rec[2] = (v4f){fr[3], fr[4], fr[5], fr[6]};
+        rec[3] = (v4f){fr[7], fr[8], 0.0f, 0.0f};
+      }
+    } else {
+      #pragma unroll 1
+      for (int k = 0; k < n; ++k) {
+        const int slot = ncon + off + k;
+        if (slot >= m.max_con) break;
+        gfloat* rec = scr + S.con + kConRec * slot;
+        float fr[9] = {c[k].nrm[0], c[k].nrm[1], c[k].nrm[2], 0, 0, 0, 0, 0, 0};
+        make_frame(fr);
+        rec[0] = __int_as_float(p);
+        rec[1] = c[k].dist;
+        for (int i = 0; i < 3; ++i) rec[2 + i] = c[k].pos[i];
+        for (int i = 0; i < 9; ++i) rec[5 + i] = fr[i];
+      }
     }
     ncon += total;
     SUB_ADD(PH_COLL_OUT, t_out);
@@ -2372,7 +2432,6 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
 // pipes by longest-processing-time.  Records (J, M^-1 J' and dof per slot, row scalars) sit in the
 // env's scratch in solver order, pipe p's rows at [start_p, start_p + n_p); each level k of a sweep
 // is one row per pipe, its record prefetched a level ahead; qacc and the row forces stay in LDS.
-typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr int kHdr = 24;     // item header floats (blocked mode; batch.hip sizes efc_hdr to match)
 constexpr int kRecScal = 12;  // aref, R, ARii, bound (frictionloss, -1 otherwise), b, then the coupling
                               // J_r M^-1 J_s' of row r to the earlier rows s < r of its item (3 floats),
@@ -2799,8 +2858,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       if (q == best) load[q] += c;
     });
   }
-  // solver order: pipe p's rows in row order at records [start_p, start_p + n_p); the first record
-  // of every item holds the item's first row index (itemat)
+  // solver order: pipe p's rows in row order at records [start_p, start_p + n_p)
   int start[NP], fill[NP], nlev = 0, my_n = 0, my_start = 0;
   {
     int acc = 0;
@@ -2812,8 +2870,18 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
     });
     nlev = uniform_int(nlev);
   }
-  gfloat* itemat = scr + S.efc_item;
   gfloat* hdr = scr + S.efc_hdr;
+  // item headers: everything the records phase needs that does not depend on the dof slot, computed
+  // lane-per-item (64 items at once, no dependent chain per item there).  With at most 64 items
+  // (C5: ~47) they stay in the item lane's registers and the records loop fetches its pipe's
+  // current item by lane permute: no header round trip through the env's global scratch, whose
+  // loads would wait (vmcnt counts stores too) for every record store issued before them.
+  // Otherwise they go to the scratch (efc_hdr, kHdr floats at the item's first record).
+  struct Hdr { v4f a, b, c, d, e, f; };
+  const bool hreg = nitem <= 64;
+  Hdr hv{};                       // hreg: this lane's item header (f.z: its first record)
+  unsigned long long pend[NP];    // hreg: per pipe, the lanes of its items not yet built (item order)
+  unroll<NP>([&](auto pc) { pend[decltype(pc)::value] = 0; });
   #pragma unroll 1
   for (int base = 0; base < nitem; base += 64) {
     const int i = base + lane;
@@ -2829,10 +2897,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       const int ex = gscan_excl<64>(pr == q ? nr : 0, lane, tot);
       if (pr == q) q0 = fill[q] + ex;
       fill[q] += tot;
+      if (hreg) pend[q] = __ballot(pr == q && nr > 0);
     });
     if (nr > 0) {
-      // item header: everything that does not depend on the dof slot, computed here for 64 items
-      // at once (the per-pipe build below then waits on one header load instead of a chain)
       const int code = __float_as_int(type[r0]);
       const int t = code >> 16, id = code & 0xffff;
       CPtr<float> sr, si;
@@ -2870,28 +2937,31 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       }
       const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (ps - mg);
       const float jval = t == EFC_FRICTION ? 1.0f : (t == EFC_LIMIT ? floss[r0] : 0.0f);
-      gfloat* h = hdr + kHdr * q0;
-      h[0] = __int_as_float(r0);
-      h[1] = __int_as_float(code);
-      h[2] = __int_as_float((t1 + 1) | ((t2 + 1) << 8) | (nr << 16) | (dim << 20) | ((t1 < 0 ? 0xff : il) << 24));
-      h[3] = mu;
-      h[4] = R; h[5] = B; h[6] = pterm; h[7] = bound;
-      // what the records phase reads per item, copied here where 64 items load at once: the contact's
-      // position, bodies and frame (no dependent chain contact -> pair -> geom -> body per item there),
-      // or the friction / limit row's dof and J value
+      Hdr h{};
+      h.a = (v4f){__int_as_float(r0), __int_as_float(code),
+                  __int_as_float((t1 + 1) | ((t2 + 1) << 8) | (nr << 16) | (dim << 20) | ((t1 < 0 ? 0xff : il) << 24)), mu};
+      h.b = (v4f){R, B, pterm, bound};
+      // what the records phase reads per item: the contact's position, bodies, frame and roots (no
+      // dependent chain contact -> pair -> geom -> body per item there), or the friction / limit
+      // row's J value and dof
       if (t == EFC_CONTACT) {
         const gfloat* crec = scr + S.con + kConRec * id;
         const int p = __float_as_int(crec[0]);
         const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
-        for (int i = 0; i < 3; ++i) h[8 + i] = crec[2 + i];
-        h[11] = __int_as_float(b1 | (b2 << 16));
-        for (int i = 0; i < 9; ++i) h[12 + i] = crec[5 + i];
-        h[21] = __int_as_float(m.body_rootid[b1] | (m.body_rootid[b2] << 16));
+        h.c = (v4f){crec[2], crec[3], crec[4], __int_as_float(b1 | (b2 << 16))};
+        h.d = (v4f){crec[5], crec[6], crec[7], crec[8]};
+        h.e = (v4f){crec[9], crec[10], crec[11], crec[12]};
+        h.f = (v4f){crec[13], __int_as_float(m.body_rootid[b1] | (m.body_rootid[b2] << 16)), 0.0f, 0.0f};
       } else {
-        h[8] = jval;
-        h[11] = __int_as_float(t == EFC_FRICTION ? id : m.jnt_dofadr[id]);
+        h.c = (v4f){jval, 0.0f, 0.0f, __int_as_float(t == EFC_FRICTION ? id : m.jnt_dofadr[id])};
       }
-      itemat[q0] = jval;  // J value of a friction / limit row at its dof
+      h.f.z = __int_as_float(q0);
+      if (hreg) {
+        hv = h;
+      } else {
+        __attribute__((address_space(1))) v4f* o = (__attribute__((address_space(1))) v4f*)(hdr + kHdr * q0);
+        o[0] = h.a; o[1] = h.b; o[2] = h.c; o[3] = h.d; o[4] = h.e; o[5] = h.f;
+      }
     }
   }
   wsync();
@@ -2908,8 +2978,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   {
     const int my_end = my_start + my_n;
     int qc = my_start;
-    // the item headers are read one item ahead (loads in flight while the current item is built)
-    struct Hdr { v4f a, b, c, d, e, f; };
+    // hreg: the pipe's next item is the lowest lane left in its pending mask (scalar find-first),
+    // its header is fetched from that lane by permute; otherwise headers are read from the scratch
+    // one item ahead (loads in flight while the current item is built)
     auto load_hdr = [&](int q) {
       const gfloat* h = hdr + kHdr * q;
       Hdr o;
@@ -2921,21 +2992,43 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       o.f = *(const __attribute__((address_space(1))) v4f*)(h + 20);
       return o;
     };
-    Hdr nxt = load_hdr(qc < my_end ? qc : 0);
+    auto perm4 = [](v4f v, int src) {
+      return (v4f){__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src)};
+    };
+    Hdr nxt{};
+    if (!hreg) nxt = load_hdr(qc < my_end ? qc : 0);
+    unsigned long long t_rj = 0, t_rs = 0, t_rr = 0;  // timing build: records sub-phases
+    (void)t_rj; (void)t_rs; (void)t_rr;
     #pragma unroll 1
     for (;;) {
-      const bool act = qc < my_end;
-      if (!__any(act)) break;
-      const int q0 = act ? qc : 0;  // record 0 always starts an item
-      const Hdr cur = nxt;
-      const v4f h0 = cur.a, h1 = cur.b, h2 = cur.c, h3 = cur.d, h4 = cur.e;
-      const float h20 = cur.f.x;
-      const int roots = __float_as_int(cur.f.y);
-      {
-        const int nr_ = (__float_as_int(h0.z) >> 16) & 0xf;
+      unsigned long long t_it = SUB_T();
+      Hdr cur;
+      bool act;
+      if (hreg) {
+        int src = 0;
+        act = false;
+        unroll<NP>([&](auto pc) {
+          constexpr int q = decltype(pc)::value;
+          const unsigned long long pm = pend[q];
+          const int lq = pm ? __builtin_ctzll(pm) : 0;
+          if (pipe == q) { src = lq; act = pm != 0; }
+          pend[q] = pm & (pm - 1);
+        });
+        if (!__any(act)) break;
+        cur.a = perm4(hv.a, src); cur.b = perm4(hv.b, src); cur.c = perm4(hv.c, src);
+        cur.d = perm4(hv.d, src); cur.e = perm4(hv.e, src); cur.f = perm4(hv.f, src);
+      } else {
+        act = qc < my_end;
+        if (!__any(act)) break;
+        cur = nxt;
+        const int nr_ = (__float_as_int(cur.a.z) >> 16) & 0xf;
         const int qn = qc + (act ? nr_ : 0);
         nxt = load_hdr(qn < my_end ? qn : 0);
       }
+      const int q0 = act ? (hreg ? __float_as_int(cur.f.z) : qc) : 0;  // record 0 always starts an item
+      const v4f h0 = cur.a, h1 = cur.b, h2 = cur.c, h3 = cur.d, h4 = cur.e;
+      const float h20 = cur.f.x;
+      const int roots = __float_as_int(cur.f.y);
       const int r0 = __float_as_int(h0.x), code = __float_as_int(h0.y), pk = __float_as_int(h0.z);
       const float mu = h0.w, R = h1.x, B = h1.y, pterm = h1.z, bound = h1.w;
       const int t = code >> 16, id = code & 0xffff;
@@ -2963,7 +3056,13 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         jc[0] = d == __float_as_int(h2.w) ? h2.x : 0.0f;
       }
       float yc[3];
+#ifdef MRS_PHASE_TIMING
+      { const unsigned long long t_ = SUB_T(); t_rj += t_ - t_it; t_it = t_; }
+#endif
       pipe_lsolve3(m, s + L.L, sm, pbase, jc, yc);
+#ifdef MRS_PHASE_TIMING
+      { const unsigned long long t_ = SUB_T(); t_rs += t_ - t_it; t_it = t_; }
+#endif
       const float qv = d >= 0 ? s[L.qvel + d] : 0.0f, qs = d >= 0 ? s[L.qacc_smooth + d] : 0.0f;
       const float qw = warm && d >= 0 ? s[L.qacc_ws + d] : 0.0f;
       if (act && slot == 0 && my_nq < 16) quadtab[pipe * 16 + my_nq] = __int_as_float(q0 | (nr << 16));
@@ -2999,7 +3098,17 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       });
       qc += act ? nr : 0;
       my_nq += act ? 1 : 0;
+#ifdef MRS_PHASE_TIMING
+      t_rr += SUB_T() - t_it;
+#endif
     }
+#ifdef MRS_PHASE_TIMING
+    if (__lane_id() == 0) {
+      atomicAdd(&g_phase_cycles[PH_REC_J], t_rj);
+      atomicAdd(&g_phase_cycles[PH_REC_SOLVE], t_rs);
+      atomicAdd(&g_phase_cycles[PH_REC_ROWS], t_rr);
+    }
+#endif
   }
   const int nq_max = uniform_int(wave_max(my_nq));
   wsync();
@@ -3183,20 +3292,29 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
       });
       if (lane < nv) tmp[lane] = 0;
       wsync();
-      #pragma unroll 1
-      for (int l = 0; l < nlev; ++l) {
-        const int q = l < my_n ? my_start + l : 0;
-        const gfloat* o = rec + q * RF;
-        const int d = l < my_n ? __float_as_int(o[P + slot]) : -1;
-        const float Y = o[slot];
-        float f = 0;  // the level's force, from its owner lane l % 16 of the pipe
-        unroll<NJ>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          const float fj = __shfl(fr[j], pbase + (l & 15));
-          if ((l >> 4) == j) f = fj;
-        });
-        if (d >= 0) tmp[d] += Y * f;
-      }
+      // 16 levels at a time: every record load of the chunk is in flight together (one vmcnt wait per
+      // chunk, not one per level), the level's force comes from its owner slot by a DPP row broadcast,
+      // and the per-dof sums accumulate in level order (a dof belongs to one island, so one pipe and
+      // one slot write it: no two lanes of an instruction share an address)
+      unroll<NJ>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if (j < nch) {
+          float Yl[16];
+          int dl[16];
+          unroll<16>([&](auto oc) {
+            constexpr int o = decltype(oc)::value;
+            const int l = 16 * j + o;
+            const gfloat* r = rec + (l < my_n ? my_start + l : 0) * RF;
+            Yl[o] = r[slot];
+            dl[o] = l < my_n ? __float_as_int(r[P + slot]) : -1;
+          });
+          unroll<16>([&](auto oc) {
+            constexpr int o = decltype(oc)::value;
+            const float f = rowb<o>(fr[j]);
+            if (dl[o] >= 0) tmp[dl[o]] += Yl[o] * f;
+          });
+        }
+      });
       unroll<NJ>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const int k = 16 * j + slot;

@@ -166,7 +166,8 @@ def lib() -> C.CDLL:
 PHASES = ["kinematics", "com_pos", "make_M", "cholesky", "com_vel", "rne", "smooth_forces", "collision",
           "constraints", "sensors", "integrate", "checks", "sensors.level1", "sensors.setup", "sensors.geoms",
           "constraints.rows", "constraints.records", "constraints.warmstart", "constraints.pgs",
-          "collision.narrow", "collision.out", "constraints.delassus"]
+          "collision.narrow", "collision.out", "constraints.delassus", "records.jac", "records.solve",
+          "records.rows"]
 
 
 def phase_cycles(reset: bool = False) -> dict | None:

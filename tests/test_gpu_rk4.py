@@ -50,7 +50,9 @@ def test_reseeded_rk4(scene, solver, n):
     stiff wheel velocity servos are unstable under explicit RK4 at its 2 ms step -- the oracle itself
     reaches |qvel| ~ 1e9 and auto-resets, which is the integrator's behaviour, not a parity case.)"""
     model = rk4_scene(scene, solver)
-    wq, wv, ncon, flips = _reseeded(model, n, 60)
+    # (contacts of an RK4 step are those of its last stage's forward, not of the start state that
+    # flips.explain_flip perturbs, so only the flip count is bounded here)
+    wq, wv, ncon, flips, _ = _reseeded(model, n, 60)
     print(f"{scene} RK4 {solver or 'PGS'}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; flips {flips}")
     assert flips <= 0.01 * n * 60
     assert wq <= RTOL and wv <= RTOL

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from conftest import ARM7
+from flips import explain_flip
 from mujoco_ros2_simulation_amd import sim, synth
 import binding
 
@@ -137,8 +138,10 @@ def _reseeded(model, n, steps, period=10, settle=20):
     one step of fp64 (not the scene's sensitivity to rounding its state: unconverged 50-sweep PGS on
     C5 moves qvel by up to 2e-2 when the oracle's own input is rounded).  Env-steps whose contact
     count differs are excluded and counted (a contact whose distance sits within fp32 rounding of
-    its activation threshold exists on one side only).
-    Returns (worst qpos, worst qvel, oracle contact counts [steps, n], flips)."""
+    its activation threshold exists on one side only) -- and each one must be explained
+    as such (flips.explain_flip: the GPU's contact pairs are what the fp64 oracle produces for a
+    state within 2e-5 of the step's start).
+    Returns (worst qpos, worst qvel, oracle contact counts [steps, n], flips, unexplained flips)."""
     envs = np.arange(n)
     qpos0 = synth.initial_qpos(model, envs)
     table = synth.ctrl_table(model, envs, (steps + settle) // period + 1, period)
@@ -153,7 +156,7 @@ def _reseeded(model, n, steps, period=10, settle=20):
             d.step()
     b = sim.Batch(model, n)
     worst_q = worst_v = 0.0
-    ncon, flips = [], 0
+    ncon, flips, unexplained = [], 0, []
     for t in range(settle, settle + steps):
         for e, (d, r) in enumerate(zip(orc, ref)):
             if t % period == 0:
@@ -164,6 +167,7 @@ def _reseeded(model, n, steps, period=10, settle=20):
         b.set(sim.FIELD_QVEL, np.array([r.qvel for r in ref]))
         b.set(sim.FIELD_QACC_WARMSTART, np.array([r.qacc_warmstart for r in ref]))
         b.set(sim.FIELD_CTRL, np.array([r.ctrl for r in ref]))
+        start = [(r.qpos.copy(), r.qvel.copy()) for r in ref]
         b.step(1)
         for d, r in zip(orc, ref):
             r.step()
@@ -173,11 +177,15 @@ def _reseeded(model, n, steps, period=10, settle=20):
         nc, nr = b.get(sim.FIELD_NCON)[:, 0].astype(int), np.array([r.ncon for r in ref])
         ok = nc == nr
         flips += int(np.sum(~ok))
+        for e in np.flatnonzero(~ok):
+            done, diff, eps = explain_flip(model, *start[e], b.contacts(int(e))[0])
+            if not done:
+                unexplained.append((t, int(e), diff))
         if ok.any():
             worst_q, worst_v = max(worst_q, _rel(q[ok], qr[ok])), max(worst_v, _rel(v[ok], vr[ok]))
         ncon.append(nr)
     b.close()
-    return worst_q, worst_v, np.array(ncon), flips
+    return worst_q, worst_v, np.array(ncon), flips, unexplained
 
 
 @pytest.mark.parametrize("scene, solver, n, steps, tol", [("arm_boxes", "PGS", 64, 200, None),
@@ -196,11 +204,12 @@ def test_reseeded_step_parity(scene, solver, n, steps, tol):
     deterministically.)"""
     it = (50 if solver == "PGS" else 100) if tol is None else f'50" tolerance="{tol}'
     model = with_solver(SCENES / f"{scene}.xml", solver, it)
-    wq, wv, ncon, flips = _reseeded(model, n, steps)
+    wq, wv, ncon, flips, unexplained = _reseeded(model, n, steps)
     print(f"{scene} {solver}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts per env "
           f"{ncon.mean():.1f}; contact-count flips {flips} of {n * steps} env-steps")
     assert ncon.max() > 0
     assert flips <= 0.01 * n * steps
+    assert not unexplained, unexplained[:5]
     assert wq <= RTOL and wv <= RTOL
 
 
@@ -212,10 +221,11 @@ def test_reseeded_sparse_solver_paths(off, monkeypatch):
     Y = L^-1 J' (qacc tracked as w = L' qacc); every step from the oracle's state within 1e-5."""
     monkeypatch.setenv("MRS_SPARSE_OFF", str(off))
     model = with_solver(SCENES / "arm_boxes.xml", "PGS", 50)
-    wq, wv, ncon, flips = _reseeded(model, 64, 60)
+    wq, wv, ncon, flips, unexplained = _reseeded(model, 64, 60)
     print(f"MRS_SPARSE_OFF={off}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; flips {flips}")
     assert ncon.max() > 0
     assert flips <= 0.01 * 64 * 60
+    assert not unexplained, unexplained[:5]
     assert wq <= RTOL and wv <= RTOL
 
 
@@ -269,3 +279,43 @@ def test_g16_dense_pgs_more_dofs_than_rows(xml, min_rows, monkeypatch):
     eq, ev = _rel(q, qr), _rel(v, vr)
     print(f"nv={model.nv}: qpos {eq:.2e} qvel {ev:.2e}")
     assert eq <= RTOL and ev <= RTOL
+
+
+def test_full_size_c5_batch_properties():
+    """8192 envs of C5 (arm + 8 free boxes, PGS 50: BASELINE configs[4] per GPU): envs with equal
+    inputs give bit-identical state wherever they sit in the batch (the island-dual solve, its pipes
+    and the per-env scratch do not depend on the env's position), launches are deterministic, and
+    env 0 stays within the scene's fp32 sensitivity of the oracle after 50 steps (10x + 1e-5; the
+    per-step 1e-5 pin is test_reseeded_step_parity)"""
+    model = sim.Model.load(ARM_BOXES)
+    n, reps, steps = 8192, 8, 50
+    q0 = np.tile(synth.initial_qpos(model, np.arange(reps)), (n // reps, 1))
+    ctrl = np.tile(synth.ctrl_table(model, np.arange(reps), 1, 10)[0], (n // reps, 1))
+    outs = []
+    for _ in range(2):
+        b = sim.Batch(model, n)
+        b.set(sim.FIELD_QPOS, q0)
+        b.set(sim.FIELD_CTRL, ctrl)
+        for _ in range(steps // 10):
+            b.step(10)
+        outs.append((b.get(sim.FIELD_QPOS), b.get(sim.FIELD_QVEL), b.get(sim.FIELD_NCON)))
+        b.close()
+    for a, c in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, c)
+    q, v, nc = outs[0]
+    for x in (q, v, nc):
+        assert np.all(x.reshape(n // reps, reps, -1) == x[:reps][None])
+    assert nc.min() > 0
+    ref, ref32 = (binding.OracleData(model) for _ in range(2))
+    for d, rnd in ((ref, False), (ref32, True)):
+        d.qpos[:] = q0[0]
+        d.ctrl[:] = ctrl[0]
+        for _ in range(steps):
+            d.step()
+            if rnd:
+                d.qpos[:] = d.qpos.astype(np.float32)
+                d.qvel[:] = d.qvel.astype(np.float32)
+    scale = np.maximum(np.abs(ref.qpos), 1.0)
+    err, sens = np.max(np.abs(q[0] - ref.qpos) / scale), np.max(np.abs(ref32.qpos - ref.qpos) / scale)
+    print(f"C5 env 0 after {steps} steps: qpos err {err:.2e}, fp32-state sensitivity {sens:.2e}")
+    assert err <= 10 * sens + 1e-5
