@@ -352,18 +352,12 @@ __device__ __forceinline__ float ray_box_slab(const float* s, const float lp[3],
   if (tmax < tmin || tmax < 0) return -1;
   return tmin >= 0 ? tmin : tmax;
 }
-__global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, const int* geom_group,
-                                                       const float* geom_size, const float* geom_rgba, int ngeom,
-                                                       const float* geom_xpos, const float* geom_xmat,
-                                                       const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
-                                                       int env0, int W, int H, float f, float znear, float zfar,
-                                                       float* out, unsigned char* rgb, MeshRef mesh) {
-  __shared__ DepthGeom G[kDepthGeoms];
-  const int env = env0 + blockIdx.x;
-  const size_t eo = static_cast<size_t>(env);
-  const float* cp = cam_xpos + (eo * ncam + cam) * 3;
-  const float* cm = cam_xmat + (eo * ncam + cam) * 9;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// one visible-geom record of a frame (lane g of the frame's workgroup): the camera origin and the pixel
+// ray directions in the geom frame, the geom's culling box in the camera frame, its colour and type
+__device__ __forceinline__ void stage_depth_geom(DepthGeom* G, const int* geom_type, const int* geom_group,
+                                                 const float* geom_size, const float* geom_rgba, int ngeom,
+                                                 const float* geom_xpos, const float* geom_xmat, const float* cp,
+                                                 const float* cm, size_t eo, float znear, float zfar, MeshRef mesh) {
   if (threadIdx.x < ngeom) {
     const int g = threadIdx.x;
     const float cpos[3] = {cp[0], cp[1], cp[2]};
@@ -405,6 +399,20 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       if (zc + rz < znear || zc - rz > zfar) o.vis = 0;
     }
   }
+}
+__global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, const int* geom_group,
+                                                       const float* geom_size, const float* geom_rgba, int ngeom,
+                                                       const float* geom_xpos, const float* geom_xmat,
+                                                       const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
+                                                       int env0, int W, int H, float f, float znear, float zfar,
+                                                       float* out, unsigned char* rgb, MeshRef mesh) {
+  __shared__ DepthGeom G[kDepthGeoms];
+  const int env = env0 + blockIdx.x;
+  const size_t eo = static_cast<size_t>(env);
+  const float* cp = cam_xpos + (eo * ncam + cam) * 3;
+  const float* cm = cam_xmat + (eo * ncam + cam) * 9;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  stage_depth_geom(G, geom_type, geom_group, geom_size, geom_rgba, ngeom, geom_xpos, geom_xmat, cp, cm, eo, znear, zfar, mesh);
   __syncthreads();
   const int tiles_x = (W + kDepthTileW - 1) / kDepthTileW, tiles_y = (H + kDepthTileH - 1) / kDepthTileH;
   float* img = out + static_cast<size_t>(blockIdx.x) * W * H;
@@ -510,6 +518,259 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
   }
 }
 
+// ---- frames of scenes with mesh geoms: triangle binning + per-pixel exact hits (depth_kernel_mesh).
+// A per-pixel BVH walk (depth_kernel_v2's mesh path) is a chain of dependent node loads per pixel;
+// here one workgroup renders one env frame in bands of kBandH rows:
+//  1. every triangle of every visible mesh geom is put in camera coordinates once (lane per
+//     triangle) and given its conservative pixel box (projected vertices, 1 pixel of margin);
+//     triangles off screen, wholly nearer than znear or beyond zfar are dropped;
+//  2. the kept triangles are sorted by first band (counting sort: per-band counters in LDS, the list
+//     of (triangle, box) records in the frame's global scratch);
+//  3. per band: each kept triangle overlapping the band tests the pixel rays of its box inside the
+//     band with exactly raymesh.h ray_tri's arithmetic and keeps the nearest per pixel by an LDS
+//     64-bit atomic min of (t bits, geom, triangle) -- so the depth of every pixel is bit-identical to
+//     the every-triangle loop -- then every pixel of the band adds the primitive geoms (the band's
+//     pyramid culls them as depth_kernel_v2's tile does), picks the nearest (ties to the lower geom
+//     index, as the serial loop) and writes depth and colour.
+// Triangles at or behind the camera plane, or spanning more than kMaxSpan bands, go to a side list
+// tested in every band they overlap.
+constexpr int kBandH = 8, kMaxBands = 128, kMaxSpan = 4;
+constexpr int kRasterFaceBits = 18;  // triangle index bits in a record (mesh geom slot above)
+
+// ray_tri (raymesh.h) with the triangle's vertex a and edges e1, e2 already loaded: the same
+// expressions in the same order, so t is bit-identical
+__device__ __forceinline__ float ray_tri_v(const float a[3], const float e1[3], const float e2[3], const float lp[3],
+                                           const float lv[3]) {
+  const float pv[3] = {lv[1] * e2[2] - lv[2] * e2[1], lv[2] * e2[0] - lv[0] * e2[2], lv[0] * e2[1] - lv[1] * e2[0]};
+  const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+  if (fabsf(det) < 1e-15f) return -1;
+  const float inv = 1.0f / det;
+  const float tv[3] = {lp[0] - a[0], lp[1] - a[1], lp[2] - a[2]};
+  const float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
+  if (u < 0 || u > 1) return -1;
+  const float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
+  const float v = (lv[0] * qv[0] + lv[1] * qv[1] + lv[2] * qv[2]) * inv;
+  if (v < 0 || u + v > 1) return -1;
+  const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
+  return t >= 0 ? t : -1;
+}
+
+struct TriLoad { float a[3], e1[3], e2[3]; };
+__device__ __forceinline__ TriLoad load_tri(const float* mv, const int* mf, int f) {
+  const int ia = 3 * mf[3 * f], ib = 3 * mf[3 * f + 1], ic = 3 * mf[3 * f + 2];
+  TriLoad o;
+  for (int i = 0; i < 3; ++i) {
+    o.a[i] = mv[ia + i];
+    o.e1[i] = mv[ib + i] - o.a[i];
+    o.e2[i] = mv[ic + i] - o.a[i];
+  }
+  return o;
+}
+
+// triangle f of mesh geom slot k: its conservative pixel box; 0 dropped, 1 kept, 2 side list
+__device__ __forceinline__ int tri_box(const DepthGeom& o, const float* mv, const int* mf, int f, int W, int H, float fpx,
+                                       float znear, float zfar, int& c0, int& c1, int& r0, int& r1) {
+  const int id[3] = {3 * mf[3 * f], 3 * mf[3 * f + 1], 3 * mf[3 * f + 2]};
+  float cmin = 3.0e38f, cmax = -3.0e38f, rmin = 3.0e38f, rmax = -3.0e38f, zmin = 3.0e38f, zmax = -3.0e38f;
+  bool behind = false;
+  for (int v = 0; v < 3; ++v) {
+    const float q[3] = {mv[id[v]] - o.lp[0], mv[id[v] + 1] - o.lp[1], mv[id[v] + 2] - o.lp[2]};
+    float c[3];
+    for (int j = 0; j < 3; ++j) c[j] = o.A[j] * q[0] + o.A[3 + j] * q[1] + o.A[6 + j] * q[2];
+    const float depth = -c[2];
+    zmin = fminf(zmin, depth);
+    zmax = fmaxf(zmax, depth);
+    if (depth < 1e-4f) { behind = true; continue; }
+    const float inv = fpx / depth;
+    const float col = c[0] * inv + 0.5f * W - 0.5f, row = 0.5f * H - 0.5f - c[1] * inv;
+    cmin = fminf(cmin, col); cmax = fmaxf(cmax, col);
+    rmin = fminf(rmin, row); rmax = fmaxf(rmax, row);
+  }
+  // (1e-4 relative slack on the view-depth cull: t along the pixel ray equals the eye depth)
+  if (zmax < znear * (1 - 1e-4f) || zmin > zfar * (1 + 1e-4f)) return 0;
+  if (behind) { c0 = 0; c1 = W - 1; r0 = 0; r1 = H - 1; return 2; }
+  c0 = max(0, static_cast<int>(ceilf(cmin)) - 1);
+  c1 = min(W - 1, static_cast<int>(floorf(cmax)) + 1);
+  r0 = max(0, static_cast<int>(ceilf(rmin)) - 1);
+  r1 = min(H - 1, static_cast<int>(floorf(rmax)) + 1);
+  if (c0 > c1 || r0 > r1) return 0;
+  return (r1 / kBandH - r0 / kBandH) > kMaxSpan ? 2 : 1;
+}
+
+__global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, const int* geom_group,
+                                                         const float* geom_size, const float* geom_rgba, int ngeom,
+                                                         const float* geom_xpos, const float* geom_xmat,
+                                                         const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
+                                                         int env0, int W, int H, float f, float znear, float zfar,
+                                                         float* out, unsigned char* rgb, MeshRef mesh, const int* mgeom,
+                                                         const int* mbase, int nmg, int npair,
+                                                         unsigned long long* lists) {
+  __shared__ DepthGeom G[kDepthGeoms];
+  __shared__ int cnt[kMaxBands + 1], cur[kMaxBands], mg[kDepthGeoms], mb[kDepthGeoms + 1];
+  __shared__ int nside, maxspan;
+  extern __shared__ unsigned long long band[];  // W x kBandH (t bits << 32 | geom << 24 | triangle)
+  const int env = env0 + blockIdx.x;
+  const size_t eo = static_cast<size_t>(env);
+  const float* cp = cam_xpos + (eo * ncam + cam) * 3;
+  const float* cm = cam_xmat + (eo * ncam + cam) * 9;
+  const int lane = threadIdx.x & 63, tid = threadIdx.x;
+  stage_depth_geom(G, geom_type, geom_group, geom_size, geom_rgba, ngeom, geom_xpos, geom_xmat, cp, cm, eo, znear, zfar, mesh);
+  const int nb = (H + kBandH - 1) / kBandH;
+  for (int i = tid; i <= nb; i += 256) cnt[i] = 0;
+  for (int i = tid; i < nb; i += 256) cur[i] = 0;
+  for (int i = tid; i < nmg; i += 256) { mg[i] = mgeom[i]; mb[i] = mbase[i]; }
+  if (tid == 0) { mb[nmg] = npair; nside = 0; maxspan = 0; }
+  __syncthreads();
+  unsigned long long* list = lists + static_cast<size_t>(blockIdx.x) * npair;
+  // 1-2: count, then fill the band-sorted list (the side list fills the frame's list from its end)
+  for (int pass = 0; pass < 2; ++pass) {
+    int k = 0;
+    for (int p = tid; p < npair; p += 256) {
+      while (p >= mb[k + 1]) ++k;
+      const DepthGeom& o = G[mg[k]];
+      if (!o.vis) continue;
+      const float* mv = mesh.vert + 3 * mesh.vertadr[o.dataid];
+      const int* mf = mesh.face + 3 * mesh.faceadr[o.dataid];
+      const int fi = p - mb[k];
+      int c0, c1, r0, r1;
+      const int kind = tri_box(o, mv, mf, fi, W, H, f, znear, zfar, c0, c1, r0, r1);
+      if (kind == 0) continue;
+      const int b0 = r0 / kBandH;
+      if (pass == 0) {
+        if (kind == 1) { atomicAdd(&cnt[b0], 1); atomicMax(&maxspan, r1 / kBandH - b0); }
+        else atomicAdd(&nside, 1);
+      } else {
+        // record: triangle (24 bits: slot << kRasterFaceBits | index), c0 (11), c1 - c0 (11), r0 (10),
+        // r1 - r0 (8; 255: to the last row, conservative for the side list)
+        const unsigned long long rec = static_cast<unsigned long long>((k << kRasterFaceBits) | fi) |
+                                       (static_cast<unsigned long long>(c0) << 24) |
+                                       (static_cast<unsigned long long>(c1 - c0) << 35) |
+                                       (static_cast<unsigned long long>(r0) << 46) |
+                                       (static_cast<unsigned long long>(min(r1 - r0, 255)) << 56);
+        if (kind == 1) list[cnt[b0] + atomicAdd(&cur[b0], 1)] = rec;
+        else list[npair - 1 - atomicAdd(&nside, 1)] = rec;
+      }
+    }
+    __syncthreads();
+    if (pass == 0) {
+      if (tid == 0) {  // exclusive prefix over the bands (cnt[b] becomes the band's first record)
+        int acc = 0;
+        for (int b = 0; b <= nb; ++b) { const int c = b < nb ? cnt[b] : 0; cnt[b] = acc; acc += c; }
+        nside = 0;  // refilled by the fill pass
+      }
+      __syncthreads();
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  const int ms = maxspan, ns = nside;
+  float* img = out + static_cast<size_t>(blockIdx.x) * W * H;
+  unsigned char* frame = rgb ? rgb + static_cast<size_t>(blockIdx.x) * W * H * 3 : nullptr;
+  const float x0 = (0.5f - 0.5f * W) / f, x1 = (W - 1.0f + 0.5f - 0.5f * W) / f;
+  for (int b = 0; b < nb; ++b) {
+    const int rb = b * kBandH, re = min(H, rb + kBandH);
+    const int npx = (re - rb) * W;
+    for (int i = tid; i < npx; i += 256) band[i] = ~0ull;
+    __syncthreads();
+    // 3a. triangles overlapping the band: band-sorted records of bands b - maxspan .. b, then the side list
+    const int lo = cnt[max(0, b - ms)], hi = cnt[b + 1];
+    const int nwork = hi - lo + ns;
+    for (int w = tid; w < nwork; w += 256) {
+      const unsigned long long rec = w < hi - lo ? list[lo + w] : list[npair - ns + (w - (hi - lo))];
+      const int r0 = static_cast<int>((rec >> 46) & 0x3ff), dr = static_cast<int>(rec >> 56);
+      const int r1 = dr == 255 ? H - 1 : r0 + dr;
+      const int ra = max(r0, rb), rz = min(r1, re - 1);
+      if (ra > rz) continue;
+      const int c0 = static_cast<int>((rec >> 24) & 0x7ff), c1 = c0 + static_cast<int>((rec >> 35) & 0x7ff);
+      const int kf = static_cast<int>(rec & 0xffffff), k = kf >> kRasterFaceBits, fi = kf & ((1 << kRasterFaceBits) - 1);
+      const int g = mg[k];
+      const DepthGeom& o = G[g];
+      const TriLoad tr = load_tri(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid], fi);
+      const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]};
+      float A[9];
+      for (int i = 0; i < 9; ++i) A[i] = o.A[i];
+      const unsigned low = (static_cast<unsigned>(g) << 24) | static_cast<unsigned>(fi);
+      for (int r = ra; r <= rz; ++r) {
+        const float dy = (0.5f * H - r - 0.5f) / f;
+        for (int c = c0; c <= c1; ++c) {
+          const float dx = (c + 0.5f - 0.5f * W) / f;
+          const float lv[3] = {A[0] * dx + A[1] * dy - A[2], A[3] * dx + A[4] * dy - A[5], A[6] * dx + A[7] * dy - A[8]};
+          const float t = ray_tri_v(tr.a, tr.e1, tr.e2, lp, lv);
+          if (t >= znear)
+            atomicMin(&band[(r - rb) * W + c], (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | low);
+        }
+      }
+    }
+    // 3b. primitive geoms of the band (pyramid cull as depth_kernel_v2's tile), then every pixel
+    const float y1 = (0.5f * H - rb - 0.5f) / f, y0 = (0.5f * H - (re - 1) - 0.5f) / f;
+    bool keep = false;
+    if (lane < ngeom && G[lane].vis && G[lane].type != MRS_GEOM_MESH) {
+      const DepthGeom& o = G[lane];
+      if (o.type == MRS_GEOM_PLANE) {
+        const float n[3] = {o.A[6], o.A[7], o.A[8]};
+        const float bx = fminf(x0 * n[0], x1 * n[0]), by = fminf(y0 * n[1], y1 * n[1]);
+        keep = bx + by - n[2] < 1e-6f;
+      } else {
+        auto outside = [&](float nx, float ny, float nz) {
+          const float c = nx * o.cc[0] + ny * o.cc[1] + nz * o.cc[2];
+          float r = 0;
+          for (int i = 0; i < 3; ++i) r += o.ext[i] * fabsf(nx * o.A[3 * i] + ny * o.A[3 * i + 1] + nz * o.A[3 * i + 2]);
+          return c + r < -1e-5f * (fabsf(c) + r);
+        };
+        keep = !(outside(1, 0, x0) || outside(-1, 0, -x1) || outside(0, 1, y0) || outside(0, -1, -y1));
+      }
+    }
+    const unsigned long long prim = __ballot(keep);
+    __syncthreads();
+    for (int i = tid; i < npx; i += 256) {
+      const int r = rb + i / W, c = i % W;
+      const float dx = (c + 0.5f - 0.5f * W) / f, dy = (0.5f * H - r - 0.5f) / f;
+      float best = -1;
+      int bestg = 0;
+      unsigned long long cand = prim;
+      while (cand) {
+        const int g = __builtin_ctzll(cand);
+        cand &= cand - 1;
+        const DepthGeom& o = G[g];
+        const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]}, sz[3] = {o.size[0], o.size[1], o.size[2]};
+        const float lv[3] = {o.A[0] * dx + o.A[1] * dy - o.A[2], o.A[3] * dx + o.A[4] * dy - o.A[5],
+                             o.A[6] * dx + o.A[7] * dy - o.A[8]};
+        const float t = o.type == MRS_GEOM_BOX ? ray_box_slab(sz, lp, lv) : ray_prim(o.type, sz, lp, lv);
+        if (t >= znear && (best < 0 || t < best)) { best = t; bestg = g; }
+      }
+      const unsigned long long key = band[i];
+      int tri = -1;
+      if (key != ~0ull) {
+        const float tm = __uint_as_float(static_cast<unsigned>(key >> 32));
+        const int gm = static_cast<int>((key >> 24) & 0x3f);
+        if (best < 0 || tm < best || (tm == best && gm < bestg)) {
+          best = tm; bestg = gm; tri = static_cast<int>(key & 0xffffff);
+        }
+      }
+      img[static_cast<size_t>(r) * W + c] = (best < 0 || best > zfar) ? zfar : best;
+      if (frame) {
+        unsigned char* px = frame + (static_cast<size_t>(r) * W + c) * 3;
+        if (best < 0 || best > zfar) { px[0] = px[1] = px[2] = 0; continue; }
+        const DepthGeom& o = G[bestg];
+        const float v[3] = {dx, dy, -1.0f};
+        const float lv[3] = {o.A[0] * dx + o.A[1] * dy - o.A[2], o.A[3] * dx + o.A[4] * dy - o.A[5],
+                             o.A[6] * dx + o.A[7] * dy - o.A[8]};
+        float nl[3], nc[3];
+        if (tri >= 0) {
+          mesh_tri_normal(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid], tri, lv, nl);
+        } else {
+          float q[3];
+          for (int k = 0; k < 3; ++k) q[k] = o.lp[k] + best * lv[k];
+          local_normal(o.type, o.size, q, nl);
+        }
+        for (int j = 0; j < 3; ++j) nc[j] = nl[0] * o.A[j] + nl[1] * o.A[3 + j] + nl[2] * o.A[6 + j];
+        shade(o.rgba, lambert(nc, v), px);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ packing helpers
 struct Packer {
   std::vector<float> f;
@@ -560,6 +821,9 @@ struct BatchImpl {
   hipEvent_t snap_ev = nullptr, rend_ev = nullptr;
   bool rend_pending = false;
   float *snap_gpos = nullptr, *snap_gmat = nullptr, *snap_cpos = nullptr, *snap_cmat = nullptr;
+  // depth_kernel_mesh: per-frame lists of (triangle, pixel box) records, sized for rast_frames frames
+  unsigned long long* rast_list = nullptr;
+  int rast_frames = 0;
 };
 
 namespace {
@@ -857,6 +1121,26 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.mesh_hulladr, m.mesh_hulladr); P.addi(&d.mesh_hullnum, m.mesh_hullnum); P.addi(&d.mesh_face, bvh_face);
   P.addi(&d.mesh_bvhadr, bvh_adr); P.addi(&d.mesh_bvhnum, bvh_num); P.addf(&d.mesh_bvh, bvh_node);
   P.addi(&d.mesh_hull, m.mesh_hull); P.addf(&d.mesh_vert, m.mesh_vert);
+  {
+    // mesh geoms a camera can see (groups 0-2, alpha > 0), for the binning frame kernel; limits of its
+    // records: 64 geom slots, 2^18 triangles per mesh, pairs within an int
+    std::vector<int> rg, rb;
+    long long np = 0;
+    bool ok = true;
+    for (int g = 0; g < m.ngeom; ++g) {
+      if (m.geom_type[g] != MRS_GEOM_MESH || m.geom_group[g] < 0 || m.geom_group[g] > 2 || m.geom_rgba[4 * g + 3] == 0) continue;
+      const int fn = m.mesh_facenum[m.geom_dataid[g]];
+      ok &= fn < (1 << 18);
+      rg.push_back(g);
+      rb.push_back(static_cast<int>(np));
+      np += fn;
+    }
+    ok &= rg.size() <= 64 && np < (1ll << 30) && m.ngeom <= kDepthGeoms;
+    if (!ok) { rg.clear(); rb.clear(); np = 0; }
+    d.nrast = static_cast<int>(rg.size());
+    d.nrast_pair = static_cast<int>(np);
+    P.addi(&d.rast_geom, rg); P.addi(&d.rast_base, rb);
+  }
   P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
   P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
   P.addi(&d.pair_g1, pg1); P.addi(&d.pair_g2, pg2); P.addi(&d.pair_dim, pdim);
@@ -1209,6 +1493,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     // primal solvers in blocked mode: H = M + J'DJ couples the trees a contact joins, so it is
     // stored dense (dense mode builds H in the factor slot L.L instead)
     L.H = blocked && m.solver != MRS_SOL_PGS ? take(nv * nv) : 0;
+    L.Li = blocked && m.solver == MRS_SOL_PGS ? take(std::max(1, d.nMblk)) : 0;
     L.rk = m.integrator == MRS_INT_RK4 ? take(std::max(1, m.nq) + 4 * nv) : 0;
     L.total = off;
   };
@@ -1415,6 +1700,7 @@ void batch_free(BatchImpl* b) {
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   if (b->rstream) (void)hipStreamSynchronize(b->rstream);
   for (void* p : b->allocs) (void)hipFree(p);
+  if (b->rast_list) (void)hipFree(b->rast_list);
   if (b->snap_ev) (void)hipEventDestroy(b->snap_ev);
   if (b->rend_ev) (void)hipEventDestroy(b->rend_ev);
   if (b->rstream) (void)hipStreamDestroy(b->rstream);
@@ -1564,8 +1850,25 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
   const DevModel& d = b->dm;
   const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p,
                      d.mesh_facenum.p, d.mesh_bvh.p, d.mesh_bvhadr.p, d.mesh_bvhnum.p};
+  const bool raster = d.nrast > 0 && W <= 2048 && H <= kBandH * kMaxBands && !std::getenv("MRS_DEPTH_V2") &&
+                     !std::getenv("MRS_DEPTH_V1");
+  if (raster && b->rast_frames < n) {
+    // (one render at a time per batch: the lists are reused by every later frame batch)
+    if (b->rast_list) {
+      HIP_CHECK(hipStreamSynchronize(b->stream));
+      if (b->rstream) HIP_CHECK(hipStreamSynchronize(b->rstream));
+      HIP_CHECK(hipFree(b->rast_list));
+    }
+    HIP_CHECK(hipMalloc(&b->rast_list, static_cast<size_t>(n) * d.nrast_pair * sizeof(unsigned long long)));
+    b->rast_frames = n;
+  }
   HIP_CHECK(hipEventRecord(b->ev0[1], stream));
-  if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
+  if (raster) {
+    const size_t lds = static_cast<size_t>(W) * kBandH * sizeof(unsigned long long);
+    hipLaunchKernelGGL(depth_kernel_mesh, dim3(n), dim3(256), lds, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
+                       d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam, cam, env0, W, H, f, znear,
+                       zfar, dout, drgb, mesh, d.rast_geom.p, d.rast_base.p, d.nrast, d.nrast_pair, b->rast_list);
+  } else if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
     hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
                        cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);

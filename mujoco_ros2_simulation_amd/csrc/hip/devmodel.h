@@ -43,6 +43,7 @@ struct LdsLayout {
       trees,   // blocked mode: per tree dofadr, dofnum, M block offset, pad (int bits)
       dofb,    // blocked mode: per dof its body and that body's subtree end (int bits; jac_col)
       H,       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
+      Li,      // blocked mode with PGS: L^-1 per tree block (same offsets as L): the records' Y = L^-1 J'
       rk,      // RK4 models: the step's initial qpos [nq], then qvel [nv], stage velocity, B-weighted sums of
                // the stage velocities and accelerations [nv each]
       niter;   // constraint solver iterations of the last forward (int bits)
@@ -127,6 +128,10 @@ struct DevModel {
   CPtr<int> body_tree, dof_tree, tree_dofadr, tree_dofnum, tree_Moff;  // tree -1: world / no dofs
   // geoms
   CPtr<int> geom_type, geom_bodyid, geom_group, geom_dataid;
+  // mesh frames by triangle binning (batch.hip depth_kernel_mesh): the visible mesh geoms and the
+  // first (geom, triangle) pair of each; nrast = 0 when the model has none (or exceeds its limits)
+  CPtr<int> rast_geom, rast_base;
+  int nrast, nrast_pair;
   CPtr<float> geom_size, geom_pos, geom_quat, geom_rbound, geom_rgba;
   // meshes (mrs_model.h): vertices in the mesh frame, triangles and convex-hull vertex ids (both
   // relative to the mesh's first vertex)

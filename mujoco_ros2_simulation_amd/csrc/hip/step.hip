@@ -2595,6 +2595,43 @@ __device__ __forceinline__ void pipe_lsolve3(const DevModel& m, const lfloat* Lf
     }
   }
 }
+// Li = L^-1 per tree block (lane per dof d: column li(d) of its tree's inverse factor, forward
+// substitution down the column; each lane reads only L and writes only its own column)
+__device__ __forceinline__ void tree_linv(const DevModel& m, lfloat* s, const LdsLayout& L, int lane) {
+  if (lane < m.nv) {
+    const TreeInfo ti = tree_lds(s, L, m.dof_tree[lane]);
+    const int n = ti.num, c = lane - ti.adr;
+    const lfloat* Lb = s + L.L + ti.off;
+    lfloat* Ib = s + L.Li + ti.off;
+    Ib[c * n + c] = 1.0f / Lb[c * n + c];
+    #pragma unroll 1
+    for (int i = c + 1; i < n; ++i) {
+      float acc = 0;
+      #pragma unroll 1
+      for (int k = c; k < i; ++k) acc += Lb[i * n + k] * Ib[k * n + c];
+      Ib[i * n + c] = -acc / Lb[i * n + i];
+    }
+  }
+  wsync();
+}
+// y = L^-1 v by the inverse factor (tree_linv): y_li = sum_k Li[li][k] v_k over the slot's tree
+// segment, the v_k fetched from the segment's lanes by independent permutes (pipe_lsolve3's
+// substitution is a dependent chain of one permute round trip per dof).  Segments of at most 8 dofs.
+__device__ __forceinline__ void pipe_linv3(const lfloat* Li, const SlotMap& sm, int pbase, const float v[3], float x[3]) {
+  const int li = sm.li, n = sm.n;
+  const lfloat* Ib = Li + sm.off + li * n;
+  const int src = pbase + sm.sb;
+  float vv[3];
+  for (int i = 0; i < 3; ++i) { vv[i] = sm.d >= 0 ? v[i] : 0.0f; x[i] = 0.0f; }
+  unroll<8>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int sl = min(src + k, 63);
+    float xs[3];
+    for (int i = 0; i < 3; ++i) xs[i] = __shfl(vv[i], sl);
+    const float lik = (sm.d >= 0 && k <= li) ? Ib[k] : 0.0f;
+    for (int i = 0; i < 3; ++i) x[i] += lik * xs[i];
+  });
+}
 // lane per dof (blocked mode, nv <= 64): the dof's tree segment in the LDS factor
 struct DofTree { int adr, li, n; const lfloat* Lb; };
 __device__ __forceinline__ DofTree dof_tree_lds(const DevModel& m, const lfloat* s, const LdsLayout& L, int lane) {
@@ -2647,6 +2684,26 @@ __device__ __forceinline__ int wave_max(int v) {
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mask), 0));
+}
+// acc + a * (v of lane K of the row): one v_fmac_f32 with the row broadcast as its DPP source
+// operand (the compiler keeps a separate v_mov_dpp).  The s_nop covers the two wait states a DPP read
+// of a VGPR needs after the VALU write that produced it (the hazard recognizer does not see inside
+// inline asm).
+template <int K>
+__device__ __forceinline__ float fmac_rowb(float acc, float a, float v) {
+  asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "+v"(acc) : "v"(v), "v"(a), "n"(K));
+  return acc;
+}
+// three held rows at once, the chain's own first: a += x * b, c += x * d, e += x * f with x lane K's
+// v (every update a v_fmac_f32 with the broadcast as its DPP operand, one wait for all three)
+template <int K>
+__device__ __forceinline__ void fmac3_rowb(float& g0, float& g1, float& g2, float v, float a0, float a1, float a2) {
+  asm("s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %3, %4 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %1, %3, %5 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %2, %3, %6 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(g0), "+v"(g1), "+v"(g2) : "v"(v), "v"(a0), "v"(a1), "v"(a2), "n"(K));
 }
 // v = own on lanes O, O + 16, O + 32, O + 48 (slot O of every 16-lane pipe), other elsewhere: one
 // v_cndmask with a constant lane mask (no per-use compare)
@@ -2974,6 +3031,9 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
   // need J itself (J qvel, J qacc_smooth, J qacc_warmstart) are taken here, so records hold Y only
   gfloat* quadtab = scr + S.efc_quad;  // per pipe, its first 16 items in order: record | rows << 16
   int my_nq = 0;                        // items of this lane's pipe
+  // Y through the inverse factor when the layout holds one and every tree fits the 8-term product
+  const bool use_linv = L.Li != 0 && m.tree_nmax <= 8 && !(m.sparse_off & 8);
+  if (use_linv) tree_linv(m, s, L, lane);
   const bool warm = !(m.disableflags & MRS_DSBL_WARMSTART);
   {
     const int my_end = my_start + my_n;
@@ -3059,7 +3119,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
 #ifdef MRS_PHASE_TIMING
       { const unsigned long long t_ = SUB_T(); t_rj += t_ - t_it; t_it = t_; }
 #endif
-      pipe_lsolve3(m, s + L.L, sm, pbase, jc, yc);
+      if (use_linv) pipe_linv3(s + L.Li, sm, pbase, jc, yc);
+      else pipe_lsolve3(m, s + L.L, sm, pbase, jc, yc);
 #ifdef MRS_PHASE_TIMING
       { const unsigned long long t_ = SUB_T(); t_rs += t_ - t_it; t_it = t_; }
 #endif
@@ -3265,8 +3326,20 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
               constexpr int o = decltype(oc)::value, k = 16 * j + o;
               const float cand = __builtin_amdgcn_fmed3f(gn[j], lh[j].x, lh[j].y);
               gb[j] = sel_slot16<o>(gn[j], gb[j]);
-              const float dl = rowb<o>(cand);
-              unroll<NJ>([&](auto jc2) { gn[decltype(jc2)::value] += ARn[decltype(jc2)::value][k] * dl; });
+              // the chain to the next level's step runs through held block j only: its update takes
+              // the broadcast as the FMA's DPP operand (med3 -> fmac_dpp -> med3); the other blocks
+              // use a separate broadcast off that chain
+              if constexpr (NJ == 3) {
+                constexpr int ja = (j + 1) % 3, jb = (j + 2) % 3;
+                fmac3_rowb<o>(gn[j], gn[ja], gn[jb], cand, ARn[j][k], ARn[ja][k], ARn[jb][k]);
+              } else {
+                gn[j] = fmac_rowb<o>(gn[j], ARn[j][k], cand);
+                const float dl = rowb<o>(cand);
+                unroll<NJ>([&](auto jc2) {
+                  constexpr int j2 = decltype(jc2)::value;
+                  if constexpr (j2 != j) gn[j2] += ARn[j2][k] * dl;
+                });
+              }
             });
           }
         });
