@@ -17,17 +17,23 @@ Usage: python scripts/flops_summary.py OUT.json cfg [envs] [steps_per_launch]
 import csv
 import re
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-OUT, CFG = Path(sys.argv[1]), sys.argv[2]
-ENVS = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 4096, "c3": 8192, "c4": 2048, "c5": 8192}[CFG]
+OUT = Path(sys.argv[1])
+# variant key (bench.py variant_key): "<cfg>[_<solver>][_<scene>]"; directories and bench lines use
+# the key, the kernel and defaults its config; extra bench arguments (--solver / --scene) from $BENCH_ARGS
+KEY = sys.argv[2]
+CFG = KEY.split("_")[0]
+EXTRA = os.environ.get("BENCH_ARGS", "")
+ENVS = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 4096, "c3": 8192, "c3m": 8192, "c4": 2048, "c5": 8192}[CFG]
 STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 COUNTERS = ["SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32",
             "SQ_INSTS_VALU_FLOPS_FP32", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
-rows = [r for r in csv.DictReader(open(ROOT / f"gpurun_out/pmc_flops_{CFG}/run_counter_collection.csv"))
+rows = [r for r in csv.DictReader(open(ROOT / f"gpurun_out/pmc_flops_{KEY}/run_counter_collection.csv"))
         if "step_kernel" in r["Kernel_Name"] and not re.search(r"step_kernel<\d+, true", r["Kernel_Name"])]
 per = defaultdict(lambda: defaultdict(float))
 for r in rows:
@@ -35,7 +41,7 @@ for r in rows:
 disp = sorted(per, key=int)
 steady = disp[1:] if len(disp) > 2 else disp
 avg = {k: sum(per[d][k] for d in steady) / len(steady) for k in per[steady[0]]}
-bench = json.loads((ROOT / f"gpurun_out/bench_{CFG}.json").read_text().strip().splitlines()[-1])
+bench = json.loads((ROOT / f"gpurun_out/bench_{KEY}.json").read_text().strip().splitlines()[-1])
 kms = bench["roofline"].get("step_kernel_ms") or bench["roofline"]["kernel_ms"]
 full = 64 * (2 * avg["SQ_INSTS_VALU_FMA_F32"] + avg["SQ_INSTS_VALU_ADD_F32"] + avg["SQ_INSTS_VALU_MUL_F32"]
              + avg["SQ_INSTS_VALU_TRANS_F32"])
@@ -44,14 +50,14 @@ executed = full
 units = ENVS * STEPS
 tf = executed / (kms * 1e-3) / 1e12
 rec = {
-    "kernel": rows[0]["Kernel_Name"], "config": CFG, "launches_averaged": len(steady),
+    "kernel": rows[0]["Kernel_Name"], "config": KEY, "launches_averaged": len(steady),
     "counters_per_launch": avg, "kernel_ms": kms, "env_steps_per_launch": units,
     "flops_fullwave_per_launch": full, "flops_counter_per_launch": cnt,
     "flops_executed_per_launch": executed, "flops_executed_per_env_step": executed / units,
     "flops_counter_over_fullwave": cnt / full if full else None,
     "executed_tflops": tf, "frac_executed": tf / 157.3,
     "command": f"rocprofv3 --pmc {' '.join(COUNTERS)} --kernel-trace -- "
-               f"python3 bench.py --config {CFG} --steps 5 --warmup 1 --no-cpu-baseline",
+               f"python3 bench.py --config {CFG} {EXTRA} --steps 5 --warmup 1 --no-cpu-baseline",
 }
 OUT.write_text(json.dumps(rec, indent=1) + "\n")
 print(json.dumps({k: v for k, v in rec.items() if k != "counters_per_launch"}))

@@ -10,16 +10,21 @@ Usage: python scripts/pmc_summary.py OUT.json [cfg]
 import csv
 import re
 import json
+import os
 import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-CFG = sys.argv[2] if len(sys.argv) > 2 else "c3"
+# variant key (bench.py variant_key): "<cfg>[_<solver>][_<scene>]"; directories and bench lines use
+# the key, the kernel and defaults its config; extra bench arguments (--solver / --scene) from $BENCH_ARGS
+KEY = (sys.argv[2] if len(sys.argv) > 2 else "c3")
+CFG = KEY.split("_")[0]
+EXTRA = os.environ.get("BENCH_ARGS", "")
 KERNEL = "depth_kernel" if CFG in ("c4", "c3m") else "step_kernel"
 
 
 def per_launch(name: str) -> tuple[float, str, int]:
-    d = ROOT / f"gpurun_out/pmc_{name}_{CFG}"
+    d = ROOT / f"gpurun_out/pmc_{name}_{KEY}"
     if not d.exists():
         d = ROOT / f"gpurun_out/pmc_{name}"
     rows = [r for r in csv.DictReader(open(d / "run_counter_collection.csv"))
@@ -34,7 +39,7 @@ write_kib, _, n2 = per_launch("write")
 steps = {"c4": 200, "c3m": 20}.get(CFG, 5)  # C4: 20 depth frames, C3m: 2
 rec = {
     "kernel": kname,
-    "config": CFG,
+    "config": KEY,
     "launches_averaged": min(n1, n2),
     "fetch_size_kib_raw": fetch_kib,
     "write_size_kib": write_kib,
@@ -42,7 +47,7 @@ rec = {
     "write_bytes": write_kib * 1024,
     "traffic_bytes_per_launch": 2 * fetch_kib * 1024 + write_kib * 1024,
     "correction": "FETCH_SIZE x2 (gfx950 half-count, MI355X_MICROARCH.md HBM section); WRITE_SIZE as is",
-    "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- python3 bench.py --config {CFG} "
+    "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace -- python3 bench.py --config {CFG} {EXTRA} "
                f"--steps {steps} --warmup 1 --no-cpu-baseline",
 }
 out = Path(sys.argv[1])
