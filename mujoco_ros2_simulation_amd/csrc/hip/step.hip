@@ -5501,10 +5501,17 @@ __device__ __forceinline__ void integrate_pos(const DevModel& m, lfloat* s, cons
   wsync();
 }
 
+template <int G>
+__device__ void integrate_implicit(ENV_PARAMS);
+
 // mj_Euler / mj_implicit(implicitfast) + mj_advance
 template <int G>
 __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   ENV_UNPACK;
+  if (m.integrator == MRS_INT_IMPLICIT) {
+    [[clang::noinline]] integrate_implicit<G>(ENV_ARGS);
+    return;
+  }
   const int nv = m.nv;
   const float h = m.timestep;
   const float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
@@ -5557,6 +5564,118 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
   if (lane < nv) {
     s[L.qacc_ws + lane] = qacc;
     s[L.qvel + lane] += h * qacc_int;
+  }
+  wsync();
+  integrate_pos<G>(m, s, s + L.qvel, h, lane);
+}
+
+// the velocity derivative of the actuators and passive forces on lane j's dof, as integrate()'s
+// implicitfast path (minus the derivative of qfrc_passive + qfrc_actuator)
+template <int G>
+__device__ __forceinline__ float implicit_dg(const DevModel& m, const lfloat* s, int lane) {
+  const LdsLayout& L = m.L;
+  const auto dr = dof_tab<G>(m, lane);
+  float dg = (m.disableflags & MRS_DSBL_PASSIVE) ? 0.0f : dr[9];
+  if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
+    auto act_dv = [&](int a) {
+      const auto ar = act_tab<G>(m, a);
+      if (__float_as_int(ar[14])) {
+        const float f = s[L.act_force + a];
+        if (f <= ar[15] || f >= ar[16]) return;
+      }
+      const float bv = __float_as_int(ar[10]) == MRS_BIAS_AFFINE ? ar[13] : 0.0f;
+      const float gv = __float_as_int(ar[6]) == MRS_GAIN_AFFINE ? ar[9] : 0.0f;
+      float ctrl = s[L.ctrl + a];
+      if (__float_as_int(ar[3]) && !(m.disableflags & MRS_DSBL_CLAMPCTRL)) ctrl = clampf(ctrl, ar[4], ar[5]);
+      const float g = ar[2];
+      dg -= g * g * (bv + gv * ctrl);
+    };
+    const int da = __float_as_int(dr[0]);
+    if (da >= 0) {
+      act_dv(da);
+    } else if (da == -2) {
+      #pragma unroll 1
+      for (int a = 0; a < m.nu; ++a)
+        if (__float_as_int(act_tab<G>(m, a)[1]) == lane) act_dv(a);
+    }
+  }
+  return dg;
+}
+
+// mj_implicit with the full velocity derivative (oracle.c integrate / orc_bias_vel): the matrix
+// M + h (diag(dg) + d qfrc_bias / d qvel) is not symmetric (Coriolis, centrifugal and gyroscopic
+// terms), so it is factored by LU without pivoting.  Column j of the RNE derivative is
+// (bias(qvel + e_j) - bias(qvel - e_j)) / 2 -- exact for qfrc_bias, which is quadratic in qvel -- from
+// two com_vel + rne passes of the env's own phases; the derivative couples only dofs of one kinematic
+// tree, so blocked mode keeps M's tree blocks and factors each in place (lane = row of its tree).
+// Out of line: only models with integrator="implicit" reach it.
+template <int G>
+__device__ void integrate_implicit(ENV_PARAMS) {
+  ENV_UNPACK;
+  const int nv = m.nv;
+  const float h = m.timestep;
+  const float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
+  const float dg = lane < nv ? implicit_dg<G>(m, s, lane) : 0.0f;
+  const float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
+  int ta = 0, tn = nv, tmax = nv;
+  if constexpr (G == 64) {
+    tmax = m.tree_nmax;
+    if (lane < nv) {
+      const int t = m.dof_tree[lane];
+      ta = m.tree_dofadr[t];
+      tn = m.tree_dofnum[t];
+    }
+  }
+  if (lane < nv) s[L.M + midx<G>(m, lane, lane)] += h * dg;
+  #pragma unroll 1
+  for (int j = 0; j < nv; ++j) {
+    const float vj = s[L.qvel + j];
+    float bias[2];
+    for (int sg = 0; sg < 2; ++sg) {
+      wsync();
+      if (lane == 0) s[L.qvel + j] = sg == 0 ? vj + 1.0f : vj - 1.0f;
+      wsync();
+      com_vel<G>(ENV_ARGS);
+      rne<G>(ENV_ARGS);
+      bias[sg] = lane < nv ? s[L.qfrc_bias + lane] : 0.0f;
+    }
+    wsync();
+    if (lane == 0) s[L.qvel + j] = vj;
+    if (lane < nv && j >= ta && j < ta + tn) s[L.M + midx<G>(m, lane, j)] += h * (0.5f * (bias[0] - bias[1]));
+  }
+  wsync();
+  auto from = [&](float v, int src) {  // the value of lane src of this env's group
+    if constexpr (G == 64) return __shfl(v, src);
+    else return gbcast<G>(v, src);
+  };
+  // LU of every tree block in place (unit lower L below the diagonal, U on and above)
+  #pragma unroll 1
+  for (int k = 0; k < tmax; ++k) {
+    const int piv = ta + k;
+    if (lane < nv && k < tn && lane - ta > k) {
+      const float l = s[L.M + midx<G>(m, lane, piv)] / s[L.M + midx<G>(m, piv, piv)];
+      s[L.M + midx<G>(m, lane, piv)] = l;
+      #pragma unroll 1
+      for (int c = k + 1; c < tn; ++c) s[L.M + midx<G>(m, lane, ta + c)] -= l * s[L.M + midx<G>(m, piv, ta + c)];
+    }
+    wsync();
+  }
+  float y = rhs;
+  #pragma unroll 1
+  for (int k = 0; k < tmax; ++k) {
+    const float yk = from(y, min(ta + k, G - 1));
+    if (lane < nv && k < tn && lane - ta > k) y -= s[L.M + midx<G>(m, lane, ta + k)] * yk;
+  }
+  float x = 0;
+  #pragma unroll 1
+  for (int k = tmax - 1; k >= 0; --k) {
+    if (lane < nv && lane - ta == k) x = y / s[L.M + midx<G>(m, lane, lane)];
+    const float xk = from(x, min(ta + k, G - 1));
+    if (lane < nv && k < tn && lane - ta < k) y -= s[L.M + midx<G>(m, lane, ta + k)] * xk;
+  }
+  if (lane < nv) {
+    s[L.qacc_ws + lane] = qacc;
+    s[L.qvel + lane] += h * x;
   }
   wsync();
   integrate_pos<G>(m, s, s + L.qvel, h, lane);

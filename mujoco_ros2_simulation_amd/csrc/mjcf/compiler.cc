@@ -579,8 +579,6 @@ struct Compiler {
       else if (*s == "implicit") m.integrator = MRS_INT_IMPLICIT;
       else if (*s == "implicitfast") m.integrator = MRS_INT_IMPLICITFAST;
       else fail(e, "unknown integrator " + *s);
-      if (m.integrator == MRS_INT_IMPLICIT)
-        fail(e, "integrator '" + *s + "' is not supported (Euler, RK4 and implicitfast are)");
     }
     if (auto* s = e->attr("solver")) {
       if (*s == "PGS") m.solver = MRS_SOL_PGS;

@@ -42,6 +42,7 @@ def lib():
         L.orc_step.argtypes = [C.c_void_p, C.POINTER(OrcData)]
         L.orc_forward.argtypes = [C.c_void_p, C.POINTER(OrcData)]
         L.orc_mass_matrix.argtypes = [C.c_void_p, C.POINTER(OrcData), P]
+        L.orc_bias_vel.argtypes = [C.c_void_p, C.POINTER(OrcData), P]
         L.orc_kinematics.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P, P, P]
         L.orc_ray.restype = C.c_double
         L.orc_ray.argtypes = [C.c_void_p, C.POINTER(OrcData), P, P, C.c_int, C.POINTER(C.c_int)]
@@ -114,6 +115,12 @@ class OracleData:
         M = np.zeros(self.model.nv * self.model.nv)
         lib().orc_mass_matrix(self._mv, self._d, _dp(M))
         return M.reshape(self.model.nv, self.model.nv)
+
+    def bias_vel(self) -> np.ndarray:
+        """d qfrc_bias / d qvel at the current state (after forward), [nv, nv]"""
+        dB = np.zeros(self.model.nv * self.model.nv)
+        lib().orc_bias_vel(self._mv, self._d, _dp(dB))
+        return dB.reshape(self.model.nv, self.model.nv)
 
     def kinematics(self):
         m = self.model

@@ -186,7 +186,7 @@ void orc_free_data(orc_data* d) {
 
 /* mj_resetData / mj_resetDataKeyframe [upstream engine_io.c] */
 void orc_reset(const mrs_model_view* m, orc_data* d, int key) {
-  memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
+  if (m->nq > 0) memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);  /* (an empty model has no arrays) */
   memset(d->qvel, 0, sizeof(double) * m->nv);
   memset(d->ctrl, 0, sizeof(double) * m->nu);
   memset(d->qfrc_applied, 0, sizeof(double) * m->nv);
@@ -197,9 +197,9 @@ void orc_reset(const mrs_model_view* m, orc_data* d, int key) {
   d->time = 0;
   if (key >= 0 && key < m->nkey) {
     d->time = m->key_time[key];
-    memcpy(d->qpos, m->key_qpos + (size_t)key * m->nq, sizeof(double) * m->nq);
-    memcpy(d->qvel, m->key_qvel + (size_t)key * m->nv, sizeof(double) * m->nv);
-    memcpy(d->ctrl, m->key_ctrl + (size_t)key * m->nu, sizeof(double) * m->nu);
+    if (m->nq > 0) memcpy(d->qpos, m->key_qpos + (size_t)key * m->nq, sizeof(double) * m->nq);
+    if (m->nv > 0) memcpy(d->qvel, m->key_qvel + (size_t)key * m->nv, sizeof(double) * m->nv);
+    if (m->nu > 0) memcpy(d->ctrl, m->key_ctrl + (size_t)key * m->nu, sizeof(double) * m->nu);
   }
 }
 
@@ -2206,10 +2206,80 @@ static void integrate_pos(const mrs_model_view* m, double* qpos, const double* v
   }
 }
 
-/* mj_Euler (implicit in joint damping) and mj_implicit(implicitfast) [upstream engine_forward.c]:
- *   (M + h*diag(B_eff)) qacc_int = qfrc_smooth + qfrc_constraint
+/* mj_Euler (implicit in joint damping) and mj_implicit (implicitfast / implicit) [upstream
+ * engine_forward.c]:
+ *   (M + h*diag(B_eff) [+ h dB]) qacc_int = qfrc_smooth + qfrc_constraint
  * with B_eff = dof damping (Euler) or dof damping - d(actuator force)/d(qvel) (implicitfast; joint
- * transmissions make it diagonal), then qvel += h qacc_int, integrate qpos, time += h. */
+ * transmissions make it diagonal), dB = d qfrc_bias / d qvel for the full implicit integrator
+ * (orc_bias_vel), then qvel += h qacc_int, integrate qpos, time += h. */
+/* qfrc_bias (mj_rne, flg_acc = 0) at velocity v with the current positions: com_vel + rne on v, the
+ * velocity-dependent work arrays and qvel restored after */
+static void bias_at(const mrs_model_view* m, orc_data* d, const double* v, double* out) {
+  orc_ws* w = (orc_ws*)d->ws;
+  const int nb = m->nbody, nv = m->nv;
+  double* save = (double*)malloc(sizeof(double) * (size_t)(24 * nb + 6 * nv + 2 * nv + 1));
+  double* p = save;
+  memcpy(p, w->cvel, 6 * nb * sizeof(double)); p += 6 * nb;
+  memcpy(p, w->cacc, 6 * nb * sizeof(double)); p += 6 * nb;
+  memcpy(p, w->cfrc, 6 * nb * sizeof(double)); p += 6 * nb;
+  memcpy(p, w->cdof_dot, 6 * nv * sizeof(double)); p += 6 * nv;
+  memcpy(p, w->qfrc_bias, nv * sizeof(double)); p += nv;
+  memcpy(p, d->qvel, nv * sizeof(double));
+  memcpy(d->qvel, v, nv * sizeof(double));
+  com_vel(m, d);
+  rne(m, d);
+  memcpy(out, w->qfrc_bias, nv * sizeof(double));
+  p = save;
+  memcpy(w->cvel, p, 6 * nb * sizeof(double)); p += 6 * nb;
+  memcpy(w->cacc, p, 6 * nb * sizeof(double)); p += 6 * nb;
+  memcpy(w->cfrc, p, 6 * nb * sizeof(double)); p += 6 * nb;
+  memcpy(w->cdof_dot, p, 6 * nv * sizeof(double)); p += 6 * nv;
+  memcpy(w->qfrc_bias, p, nv * sizeof(double)); p += nv;
+  memcpy(d->qvel, p, nv * sizeof(double));
+  free(save);
+}
+
+/* mjd_rne_vel restated: dB[i * nv + j] = d qfrc_bias_i / d qvel_j.  qfrc_bias = C(q, v) v + g(q) is
+ * exactly quadratic in v for fixed positions (Coriolis, centrifugal and gyroscopic terms; gravity is
+ * constant), so the central difference (B(v + e_j) - B(v - e_j)) / 2 is its derivative with no
+ * truncation error, only rounding -- the same matrix upstream's analytic recursion forms
+ * [restated; verify]. */
+void orc_bias_vel(const mrs_model_view* m, orc_data* d, double* dB) {
+  const int nv = m->nv;
+  double* v = (double*)malloc(sizeof(double) * (size_t)(3 * nv + 1));
+  double *bp = v + nv, *bm = bp + nv;
+  for (int j = 0; j < nv; ++j) {
+    memcpy(v, d->qvel, nv * sizeof(double));
+    v[j] += 1;
+    bias_at(m, d, v, bp);
+    v[j] -= 2;
+    bias_at(m, d, v, bm);
+    for (int i = 0; i < nv; ++i) dB[i * nv + j] = 0.5 * (bp[i] - bm[i]);
+  }
+  free(v);
+}
+
+/* dense LU without pivoting (mj_factorLU restated densely: the implicit matrix is M plus small h-scaled
+ * derivative terms, so it stays diagonally dominated like M) and the solve A x = b, in place */
+static void lu_solve(double* A, double* x, const double* b, int n) {
+  for (int k = 0; k < n; ++k)
+    for (int i = k + 1; i < n; ++i) {
+      const double l = A[i * n + k] / A[k * n + k];
+      A[i * n + k] = l;
+      for (int j = k + 1; j < n; ++j) A[i * n + j] -= l * A[k * n + j];
+    }
+  for (int i = 0; i < n; ++i) {
+    double v = b[i];
+    for (int k = 0; k < i; ++k) v -= A[i * n + k] * x[k];
+    x[i] = v;
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double v = x[i];
+    for (int k = i + 1; k < n; ++k) v -= A[i * n + k] * x[k];
+    x[i] = v / A[i * n + i];
+  }
+}
+
 static void integrate(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   int nv = m->nv;
@@ -2220,7 +2290,7 @@ static void integrate(const mrs_model_view* m, orc_data* d) {
   if (m->integrator == MRS_INT_EULER) {
     if (!(m->disableflags & MRS_DSBL_EULERDAMP))
       for (int j = 0; j < nv; ++j) if (m->dof_damping[j] > 0) { Dg[j] = m->dof_damping[j]; need_solve = 1; }
-  } else { /* implicitfast */
+  } else { /* implicitfast, implicit */
     need_solve = 1;
     if (!(m->disableflags & MRS_DSBL_PASSIVE))
       for (int j = 0; j < nv; ++j) Dg[j] = m->dof_damping[j];
@@ -2243,7 +2313,18 @@ static void integrate(const mrs_model_view* m, orc_data* d) {
         Dg[m->jnt_dofadr[m->actuator_trnid[2 * a]]] -= gear * gear * v;
       }
   }
-  if (need_solve) {
+  if (need_solve && m->integrator == MRS_INT_IMPLICIT) {
+    /* mj_implicit: (M - h qDeriv) qacc_int = qfrc_smooth + qfrc_constraint with the full velocity
+     * derivative qDeriv = d(qfrc_passive + qfrc_actuator - qfrc_bias)/d qvel: the diagonal terms of
+     * implicitfast plus the RNE (Coriolis / centrifugal / gyroscopic) derivative, non-symmetric, so LU */
+    memcpy(w->Mi, w->M, (size_t)nv * nv * sizeof(double));
+    orc_bias_vel(m, d, w->Li);
+    for (int i = 0; i < nv; ++i)
+      for (int j = 0; j < nv; ++j) w->Mi[i * nv + j] += h * w->Li[i * nv + j];
+    for (int j = 0; j < nv; ++j) w->Mi[j * nv + j] += h * Dg[j];
+    for (int j = 0; j < nv; ++j) w->tmp2[j] = w->qfrc_smooth[j] + w->qfrc_constraint[j];
+    lu_solve(w->Mi, qacc_int, w->tmp2, nv);
+  } else if (need_solve) {
     memcpy(w->Mi, w->M, (size_t)nv * nv * sizeof(double));
     for (int j = 0; j < nv; ++j) w->Mi[j * nv + j] += h * Dg[j];
     cholesky(w->Mi, w->Li, nv);

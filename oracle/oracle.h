@@ -41,6 +41,9 @@ void orc_forward(const mrs_model_view* m, orc_data* d);
 
 /* introspection for tests: dense joint-space inertia at the current qpos (nv*nv) */
 void orc_mass_matrix(const mrs_model_view* m, orc_data* d, double* M);
+/* d qfrc_bias / d qvel at the current state after a forward (nv*nv, row i = bias component i): the
+ * RNE velocity derivative the full implicit integrator adds to its matrix */
+void orc_bias_vel(const mrs_model_view* m, orc_data* d, double* dB);
 /* kinematics at the current qpos: body xpos (nbody*3), xquat (nbody*4), geom xpos (ngeom*3),
  * geom xmat (ngeom*9); any pointer may be NULL */
 void orc_kinematics(const mrs_model_view* m, orc_data* d, double* xpos, double* xquat,

@@ -199,13 +199,13 @@ def test_compiler_accepts_converter_options():
 
 
 def test_integrator_options():
-    """<option integrator>: Euler / implicitfast / RK4 compile (RK4 runs as mj_RungeKutta's 4 stages),
-    the full implicit integrator is rejected at load, never silently replaced"""
+    """<option integrator>: Euler / RK4 / implicit / implicitfast compile to mjtIntegrator's codes (RK4
+    runs as mj_RungeKutta's 4 stages, implicit with the RNE velocity derivative); unknown names fail"""
     base = '<mujoco><option integrator="{}"/><worldbody><body><joint/><geom size="0.1"/></body></worldbody></mujoco>'
-    for name, code in (("Euler", 0), ("RK4", 1), ("implicitfast", 3)):
+    for name, code in (("Euler", 0), ("RK4", 1), ("implicit", 2), ("implicitfast", 3)):
         assert sim.Model.from_string(base.format(name)).integrator == code
-    with pytest.raises(sim.MrsError, match="not supported"):
-        sim.Model.from_string(base.format("implicit"))
+    with pytest.raises(sim.MrsError, match="unknown integrator"):
+        sim.Model.from_string(base.format("Verlet"))
 
 
 def test_bench_solver_override():

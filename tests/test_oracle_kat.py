@@ -303,3 +303,68 @@ def test_ballistic_free_body_rk4():
     assert d.qpos[0] == pytest.approx(1.0 * t) and d.qpos[1] == pytest.approx(-0.5 * t)
     ang = 3.0 * t
     np.testing.assert_allclose(d.qpos[3:], [np.cos(ang / 2), 0, 0, np.sin(ang / 2)], atol=1e-12)
+
+
+@pytest.mark.parametrize("q2, v", [(0.4, (1.3, -0.7)), (-1.1, (0.2, 2.5)), (2.0, (-3.0, 0.5))])
+def test_bias_velocity_derivative_closed_form(s2_model, q2, v):
+    """the full implicit integrator's RNE derivative (orc_bias_vel, mjd_rne_vel restated) on the
+    reference's 2-link arm: its hinges are parallel to gravity, so qfrc_bias is the planar Coriolis /
+    centrifugal force of link 2 (mass m2 = 27, com lc2 = 0.5 from the elbow, link 1 l1 = 1):
+    bias = h (-(2 v1 v2 + v2^2), v1^2), h = m2 l1 lc2 sin q2 -- independent of the link inertias -- so
+    d bias / d v = h [[-2 v2, -2 (v1 + v2)], [2 v1, 0]]"""
+    d = binding.OracleData(s2_model)
+    d.qpos[:] = [0.3, q2]
+    d.qvel[:] = v
+    d.forward()
+    hh = 27 * 1.0 * 0.5 * np.sin(q2)
+    v1, v2 = v
+    expect = hh * np.array([[-2 * v2, -2 * (v1 + v2)], [2 * v1, 0.0]])
+    np.testing.assert_allclose(d.bias_vel(), expect, atol=1e-9)
+
+
+def test_servo_recurrence_implicit():
+    """a single hinge about its own principal axis has no velocity-dependent bias force, so the full
+    implicit integrator reduces to implicitfast's recurrence (a = f / (I + h (b + kv)))"""
+    I, b, kp, kv, h, c = 0.5, 0.3, 40.0, 2.0, 0.002, 0.8
+    m = sim.Model.from_string(SERVO.format(integ="implicit", b=b, I=I, kp=kp, kv=kv))
+    d = binding.OracleData(m)
+    d.ctrl[:] = [c]
+    q, v = 0.0, 0.0
+    for _ in range(300):
+        f = kp * (c - q) - (b + kv) * v
+        v = v + h * f / (I + h * (b + kv))
+        q = q + h * v
+        d.step()
+        assert d.qpos[0] == pytest.approx(q, rel=1e-12, abs=1e-14)
+        assert d.qvel[0] == pytest.approx(v, rel=1e-12, abs=1e-14)
+
+
+def test_implicit_two_link_step(s2_model):
+    """one implicit step of the free-swinging 2-link arm (no actuation) in closed form: the velocity
+    update solves (M + h (diag(damping) + d bias / d v)) a = qfrc_smooth + qfrc_constraint with the
+    closed-form mass matrix and Coriolis derivative, the joints' damping and the position servos' kv
+    (no joint limit is active; the friction-loss row of joint 1 enters through the oracle's own
+    qfrc_constraint)"""
+    xml = (Path(__file__).resolve().parent / "golden" / "ref_scenes" / "scene.xml").read_text()
+    xml = xml.replace('<include file="test_robot.xml"/>', '<include file="test_robot.xml"/><option integrator="implicit"/>')
+    m = sim.Model.from_string(xml, str(Path(__file__).resolve().parent / "golden" / "ref_scenes"))
+    assert m.integrator == 2
+    d = binding.OracleData(m)
+    q, v = np.array([0.2, 0.9]), np.array([1.5, -2.0])
+    d.qpos[:] = q
+    d.qvel[:] = v
+    d.forward()
+    qacc = d.qacc.copy()
+    a_s, f_s = d.smooth()
+    M = d.mass_matrix()
+    hh = 27 * 0.5 * np.sin(q[1])
+    dB = hh * np.array([[-2 * v[1], -2 * (v[0] + v[1])], [2 * v[0], 0.0]])
+    damp = np.array([m.dof_damping[0], m.dof_damping[1]], dtype=float)
+    bias = np.asarray(m.actuator_biasprm).reshape(m.nu, -1)
+    for a in range(m.nu):  # position servos: d(actuator force)/d(qvel) = biasprm[2] = -kv
+        damp[m.jnt_dofadr[m.actuator_trnid[a][0]]] -= bias[a, 2]
+    h = m.timestep
+    qfrc_con = M @ (qacc - a_s)   # the constraint force from mj_fwdConstraint's qacc
+    a_int = np.linalg.solve(M + h * (np.diag(damp) + dB), f_s + qfrc_con)
+    d.step()
+    np.testing.assert_allclose(d.qvel, v + h * a_int, rtol=1e-10, atol=1e-12)
