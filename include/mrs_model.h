@@ -31,6 +31,7 @@ enum { MRS_GEOM_PLANE = 0, MRS_GEOM_HFIELD = 1, MRS_GEOM_SPHERE = 2, MRS_GEOM_CA
 enum { MRS_JNT_FREE = 0, MRS_JNT_BALL = 1, MRS_JNT_SLIDE = 2, MRS_JNT_HINGE = 3 };
 enum { MRS_INT_EULER = 0, MRS_INT_RK4 = 1, MRS_INT_IMPLICIT = 2, MRS_INT_IMPLICITFAST = 3 };
 enum { MRS_SOL_PGS = 0, MRS_SOL_CG = 1, MRS_SOL_NEWTON = 2 };
+enum { MRS_CONE_PYRAMIDAL = 0, MRS_CONE_ELLIPTIC = 1 };  /* mjtCone */
 enum { MRS_TRN_JOINT = 0 };
 enum { MRS_DYN_NONE = 0 };
 enum { MRS_GAIN_FIXED = 0, MRS_GAIN_AFFINE = 1 };

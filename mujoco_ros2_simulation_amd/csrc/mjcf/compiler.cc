@@ -596,7 +596,9 @@ struct Compiler {
     if (auto* s = e->attr("ls_iterations"))
       m.ls_iterations = static_cast<int>(parse_reals(*s, e, "ls_iterations").at(0));
     if (auto* s = e->attr("cone")) {
-      if (*s != "pyramidal") fail(e, "only cone=\"pyramidal\" is supported");
+      if (*s == "pyramidal") m.cone = MRS_CONE_PYRAMIDAL;
+      else if (*s == "elliptic") m.cone = MRS_CONE_ELLIPTIC;
+      else fail(e, "unknown cone " + *s);
     }
     for (auto& c : e->children) {
       if (c->tag != "flag") continue;

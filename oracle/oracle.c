@@ -47,11 +47,17 @@ typedef struct {
       efc_vel[MAXEFC], efc_solref[MAXEFC][2], efc_solimp[MAXEFC][5], efc_KBIP[MAXEFC][4],
       efc_rscale[MAXEFC], efc_jar[MAXEFC], efc_jv[MAXEFC];
   int efc_state[MAXEFC];
+  /* elliptic cones: row k of its contact's block (0 normal, 1-2 tangents; -1 for every other row),
+   * the block's regularised cone mu = friction / sqrt(impratio) and the tangents' friction coefficient */
+  int efc_sub[MAXEFC];
+  double efc_mu[MAXEFC], efc_fr[MAXEFC];
   double* AR;
   orc_contact con[MAXCON];
 } orc_ws;
 
 enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
+/* an elliptic contact block starts at row r (its normal) */
+#define ELL_BLOCK(w, r) ((w)->efc_sub[r] == 0)
 
 /* ------------------------------------------------------------------------ small math */
 static void quat_mul(double r[4], const double a[4], const double b[4]) {
@@ -1396,6 +1402,7 @@ static void add_row(orc_ws* w, int nv, int type, int id, const double* J, double
   w->efc_pos[r] = pos; w->efc_margin[r] = margin; w->efc_frictionloss[r] = floss;
   w->efc_diag[r] = diag;
   w->efc_rscale[r] = 1;
+  w->efc_sub[r] = -1;
   memcpy(w->efc_solref[r], solref, 2 * sizeof(double));
   memcpy(w->efc_solimp[r], solimp, 5 * sizeof(double));
 }
@@ -1445,7 +1452,21 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
       for (int r = 0; r < 3; ++r) Jc[r * nv + j] = dot3(con->frame + 3 * r, dc);
     }
     w->efc_con_first[c] = w->nefc;
-    if (con->dim == 1) {
+    if (con->dim == 3 && m->cone == MRS_CONE_ELLIPTIC) {
+      /* elliptic cone [upstream mj_instantiateContact / mj_makeImpedance, restated; verify]: rows J_n,
+       * J_t1, J_t2 of the contact frame, diagApprox tran for each; the impedance of the normal for all
+       * three; the tangents' regulariser R_n mu_1^2 / (mu_j^2 impratio) = R_n / impratio (both tangents
+       * use the sliding coefficient); the cone's regularised mu = mu_1 / sqrt(impratio) */
+      if (w->nefc + 3 <= MAXEFC)
+        for (int k = 0; k < 3; ++k) {
+          add_row(w, nv, EFC_CONTACT, c, Jc + (size_t)k * nv, con->dist, con->includemargin, 0, tran, con->solref,
+                  con->solimp);
+          w->efc_sub[w->nefc - 1] = k;
+          w->efc_rscale[w->nefc - 1] = k == 0 ? 1 : 1 / m->impratio;
+          w->efc_fr[w->nefc - 1] = con->friction[0];
+          w->efc_mu[w->nefc - 1] = con->friction[0] / sqrt(m->impratio);
+        }
+    } else if (con->dim == 1) {
       add_row(w, nv, EFC_CONTACT, c, Jc, con->dist, con->includemargin, 0, tran, con->solref, con->solimp);
     } else {
       /* pyramid edges J_n +/- mu J_tk.  diagApprox of an edge is tran (1 + mu^2) [upstream
@@ -1489,10 +1510,141 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
     double vel = 0;
     for (int j = 0; j < nv; ++j) vel += w->efc_J[(size_t)r * nv + j] * d->qvel[j];
     w->efc_vel[r] = vel;
-    double pterm = w->efc_type[r] == EFC_FRICTION ? 0 : K * imp * (w->efc_pos[r] - w->efc_margin[r]);
+    /* (friction loss rows and the tangent rows of an elliptic cone carry no position term) */
+    double pterm = (w->efc_type[r] == EFC_FRICTION || w->efc_sub[r] > 0) ? 0 : K * imp * (w->efc_pos[r] - w->efc_margin[r]);
     w->efc_aref[r] = -B * vel - pterm;
     w->efc_KBIP[r][0] = K; w->efc_KBIP[r][1] = B; w->efc_KBIP[r][2] = imp; w->efc_KBIP[r][3] = 0;
   }
+}
+
+/* ---- elliptic cones [upstream mj_constraintUpdate elliptic branch, restated; verify].  In the
+ * regularised cone space U = (mu jar_n, mu_t jar_t1, mu_t jar_t2) (mu = the block's efc_mu, mu_t = its
+ * friction coefficient), N = U_0, T = |U_t|:
+ *   top zone    N >= mu T:         no force, no cost;
+ *   bottom zone mu N + T <= 0:     every row quadratic, f_j = -D_j jar_j, cost 1/2 sum D_j jar_j^2;
+ *   middle zone otherwise:         cost 1/2 Dm (N - mu T)^2 with Dm = D_n / (mu^2 (1 + mu^2)),
+ *                                  f = -d cost / d jar, Hessian S H_U S (S = diag(mu, mu_t, mu_t)),
+ *                                  H_U = Dm [[1, -mu U_t'/T], [-mu U_t/T, mu N/T^3 U_t U_t' + (mu^2 - mu N/T) I]].
+ * Returns the zone as a row state (ST_SAT, ST_QUAD, ST_CONE); f, cost and H (3x3, jar space) may be
+ * NULL. */
+enum { ST_CONE = 4 };
+static int ell_block(const orc_ws* w, int r, const double jar[3], double f[3], double* cost, double H[9]) {
+  const double mu = w->efc_mu[r], ft = w->efc_fr[r];
+  const double U[3] = {mu * jar[0], ft * jar[1], ft * jar[2]};
+  const double N = U[0], T = sqrt(U[1] * U[1] + U[2] * U[2]);
+  if (N >= mu * T || (T <= 0 && N >= 0)) {
+    if (f) f[0] = f[1] = f[2] = 0;
+    if (cost) *cost = 0;
+    if (H) memset(H, 0, 9 * sizeof(double));
+    return 0; /* ST_SAT */
+  }
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+    double c = 0;
+    for (int j = 0; j < 3; ++j) {
+      if (f) f[j] = -w->efc_D[r + j] * jar[j];
+      c += 0.5 * w->efc_D[r + j] * jar[j] * jar[j];
+    }
+    if (cost) *cost = c;
+    if (H) {
+      memset(H, 0, 9 * sizeof(double));
+      for (int j = 0; j < 3; ++j) H[4 * j] = w->efc_D[r + j];
+    }
+    return 1; /* ST_QUAD */
+  }
+  const double Dm = w->efc_D[r] / (mu * mu * (1 + mu * mu)), NT = N - mu * T;
+  if (cost) *cost = 0.5 * Dm * NT * NT;
+  if (f) {
+    f[0] = -Dm * NT * mu;
+    for (int j = 1; j < 3; ++j) f[j] = Dm * NT * mu / T * U[j] * ft;
+  }
+  if (H) {
+    const double S[3] = {mu, ft, ft};
+    double HU[9];
+    HU[0] = 1;
+    for (int j = 1; j < 3; ++j) HU[j] = HU[3 * j] = -mu * U[j] / T;
+    for (int j = 1; j < 3; ++j)
+      for (int k = 1; k < 3; ++k)
+        HU[3 * j + k] = mu * N / (T * T * T) * U[j] * U[k] + (j == k ? mu * mu - mu * N / T : 0);
+    for (int j = 0; j < 3; ++j)
+      for (int k = 0; k < 3; ++k) H[3 * j + k] = Dm * S[j] * HU[3 * j + k] * S[k];
+  }
+  return ST_CONE;
+}
+
+/* mju_QCQP2 [upstream engine_util_solve.c, restated]: min 1/2 x'Ax + x'b s.t. sum (x_i / d_i)^2 <= r^2
+ * over 2 variables: scaled to the unit-coefficient ball, Newton on the multiplier la of the active
+ * constraint (A + la I) y = -b, |y| = r, at most 20 iterations, stopping when |y|^2 - r^2 < 1e-10 or the
+ * step < 1e-10; returns 1 when the constraint is active */
+static double qcqp2_la(double res[2], const double A[4], const double b[2], const double d[2], double r);
+static int qcqp2(double res[2], const double A[4], const double b[2], const double d[2], double r) {
+  return qcqp2_la(res, A, b, d, r) != 0;
+}
+/* ... and its multiplier: la of (A_s + la I) y = -b_s in the scaled variables y = x / d */
+static double qcqp2_la(double res[2], const double A[4], const double b[2], const double d[2], double r) {
+  const double b1 = b[0] * d[0], b2 = b[1] * d[1];
+  const double A11 = A[0] * d[0] * d[0], A22 = A[3] * d[1] * d[1], A12 = A[1] * d[0] * d[1];
+  double la = 0, v1 = 0, v2 = 0;
+  for (int it = 0; it < 20; ++it) {
+    const double det = (A11 + la) * (A22 + la) - A12 * A12;
+    if (det < 1e-10) { res[0] = res[1] = 0; return 0; }
+    const double di = 1 / det, P11 = (A22 + la) * di, P22 = (A11 + la) * di, P12 = -A12 * di;
+    v1 = -P11 * b1 - P12 * b2;
+    v2 = -P12 * b1 - P22 * b2;
+    const double val = v1 * v1 + v2 * v2 - r * r;
+    if (val < 1e-10) break;
+    const double deriv = -2.0 * (P11 * v1 * v1 + 2.0 * P12 * v1 * v2 + P22 * v2 * v2);
+    const double delta = -val / deriv;
+    if (delta < 1e-10) break;
+    la += delta;
+  }
+  res[0] = v1 * d[0];
+  res[1] = v2 * d[1];
+  return la;
+}
+
+/* the exact minimiser of 1/2 y'Ay + y'c over the elliptic cone K = {|y_t| <= mu y_n} (3x3 block):
+ * g(s) = min over |x| <= mu s of the block cost at y = (s, x) (mju_QCQP2) is convex in s, with
+ * g'(s) = (A y + c)_n - la s (envelope theorem; la the QCQP's multiplier), so s is found by a safeguarded
+ * secant / bisection on g' over s >= 0 (s = 0, i.e. y = 0, when g'(0+) = c_n - mu |c_t| >= 0). */
+static void ell_block_min(const double A[9], const double c[3], double mu, double y[3]) {
+  const double At[4] = {A[4], A[5], A[7], A[8]}, dd[2] = {mu, mu};
+  /* y(s) and g'(s) */
+  double x[2];
+  /* g'(0+) = c_n - mu |c_t| (the friction takes the boundary at once): the apex y = 0 is optimal
+   * when c lies in the dual cone */
+  double gp_lo = c[0] - mu * sqrt(c[1] * c[1] + c[2] * c[2]), s_lo = 0, s_hi, gp_hi;
+  if (gp_lo >= 0) { y[0] = y[1] = y[2] = 0; return; }
+  #define ELL_EVAL(S, GP)                                                                  \
+    do {                                                                                   \
+      const double s_ = (S);                                                               \
+      const double bc_[2] = {c[1] + A[3] * s_, c[2] + A[6] * s_};                          \
+      const double la_ = qcqp2_la(x, At, bc_, dd, s_);                                     \
+      (GP) = A[0] * s_ + A[1] * x[0] + A[2] * x[1] + c[0] - la_ * s_;                      \
+    } while (0)
+  s_hi = -c[0] / A[0];
+  if (s_hi <= 0) s_hi = 1;
+  for (int k = 0; k < 60; ++k) {
+    ELL_EVAL(s_hi, gp_hi);
+    if (gp_hi >= 0) break;
+    s_lo = s_hi; gp_lo = gp_hi;
+    s_hi *= 2;
+  }
+  double s_ = s_hi;
+  for (int it = 0; it < 100 && s_hi - s_lo > 1e-14 * (1 + s_hi); ++it) {
+    /* secant step inside the bracket, bisection when it stalls near an end */
+    double sn = s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo);
+    if (!(sn > s_lo + 0.01 * (s_hi - s_lo) && sn < s_hi - 0.01 * (s_hi - s_lo))) sn = 0.5 * (s_lo + s_hi);
+    double gp;
+    ELL_EVAL(sn, gp);
+    s_ = sn;
+    if (gp == 0) { s_lo = s_hi = sn; break; }
+    if (gp < 0) { s_lo = sn; gp_lo = gp; } else { s_hi = sn; gp_hi = gp; }
+  }
+  #undef ELL_EVAL
+  s_ = 0.5 * (s_lo + s_hi);
+  const double bc[2] = {c[1] + A[3] * s_, c[2] + A[6] * s_};
+  qcqp2_la(x, At, bc, dd, s_);
+  y[0] = s_; y[1] = x[0]; y[2] = x[1];
 }
 
 /* force of one row for a given jar = J qacc - aref (mj_constraintUpdate primal states) */
@@ -1568,6 +1720,14 @@ static double primal_update(const mrs_model_view* m, orc_ws* w) {
   int nv = m->nv, nefc = w->nefc;
   double cost = 0;
   for (int r = 0; r < nefc; ++r) {
+    if (ELL_BLOCK(w, r)) {
+      double c;
+      const int st = ell_block(w, r, w->efc_jar + r, w->efc_force + r, &c, NULL);
+      w->efc_state[r] = w->efc_state[r + 1] = w->efc_state[r + 2] = st;
+      cost += c;
+      r += 2;
+      continue;
+    }
     int st = row_state(w, r, w->efc_jar[r]);
     w->efc_state[r] = st;
     cost += row_cost(w, r, w->efc_jar[r], st);
@@ -1589,9 +1749,20 @@ static double primal_cost_at(const mrs_model_view* m, orc_ws* w, const double* x
   for (int j = 0; j < nv; ++j) gauss += 0.5 * (Mx[j] - w->qfrc_smooth[j]) * (x[j] - w->qacc_smooth[j]);
   double c = 0;
   for (int r = 0; r < w->nefc; ++r) {
-    double jar = -w->efc_aref[r];
-    for (int j = 0; j < nv; ++j) jar += w->efc_J[(size_t)r * nv + j] * x[j];
-    c += row_cost(w, r, jar, row_state(w, r, jar));
+    const int nb = ELL_BLOCK(w, r) ? 3 : 1;
+    double jar[3];
+    for (int k = 0; k < nb; ++k) {
+      jar[k] = -w->efc_aref[r + k];
+      for (int j = 0; j < nv; ++j) jar[k] += w->efc_J[(size_t)(r + k) * nv + j] * x[j];
+    }
+    if (nb == 3) {
+      double cb;
+      ell_block(w, r, jar, NULL, &cb, NULL);
+      c += cb;
+      r += 2;
+      continue;
+    }
+    c += row_cost(w, r, jar[0], row_state(w, r, jar[0]));
   }
   return gauss + c;
 }
@@ -1602,6 +1773,33 @@ static void ls_eval(const orc_ws* w, double g1, double g2, double a, double a0, 
   double s1 = g1 + a * g2, s2 = g2;
   int ch = 0;
   for (int r = 0; r < w->nefc; ++r) {
+    if (ELL_BLOCK(w, r)) {
+      /* elliptic block: 1-D derivatives of its zone's cost along the line; the middle zone is not
+       * quadratic in a, so a step that ends in it is never taken as exact (ch) */
+      double jar[3], jv3[3];
+      for (int k = 0; k < 3; ++k) { jar[k] = w->efc_jar[r + k] + a * w->efc_jv[r + k]; jv3[k] = w->efc_jv[r + k]; }
+      double j0[3];
+      for (int k = 0; k < 3; ++k) j0[k] = w->efc_jar[r + k] + a0 * w->efc_jv[r + k];
+      const int st = ell_block(w, r, jar, NULL, NULL, NULL), st0 = ell_block(w, r, j0, NULL, NULL, NULL);
+      ch |= st != st0 || st == ST_CONE;
+      if (st == ST_QUAD) {
+        for (int k = 0; k < 3; ++k) {
+          s1 += jv3[k] * w->efc_D[r + k] * jar[k];
+          s2 += w->efc_D[r + k] * jv3[k] * jv3[k];
+        }
+      } else if (st == ST_CONE) {
+        const double mu = w->efc_mu[r], ft = w->efc_fr[r];
+        const double N = mu * jar[0], dN = mu * jv3[0];
+        const double U1 = ft * jar[1], U2 = ft * jar[2], dU1 = ft * jv3[1], dU2 = ft * jv3[2];
+        const double T = sqrt(U1 * U1 + U2 * U2), dT = (U1 * dU1 + U2 * dU2) / T;
+        const double Dm = w->efc_D[r] / (mu * mu * (1 + mu * mu)), NT = N - mu * T;
+        const double g = dN - mu * dT;
+        s1 += Dm * NT * g;
+        s2 += Dm * (g * g - NT * mu * ((dU1 * dU1 + dU2 * dU2) - dT * dT) / T);
+      }
+      r += 2;
+      continue;
+    }
     double jv = w->efc_jv[r];
     if (jv == 0) continue;
     double jar = w->efc_jar[r] + a * jv;
@@ -1673,6 +1871,21 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
     if (newton) {
       memcpy(H, w->M, (size_t)nv * nv * sizeof(double));
       for (int r = 0; r < nefc; ++r) {
+        if (ELL_BLOCK(w, r)) {
+          /* elliptic block: J_b' H_b J_b with the zone's 3x3 jar-space Hessian */
+          double Hb[9];
+          ell_block(w, r, w->efc_jar + r, NULL, NULL, Hb);
+          const double* Jb = w->efc_J + (size_t)r * nv;
+          for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) {
+              const double h = Hb[3 * a + c];
+              if (h == 0) continue;
+              for (int i = 0; i < nv; ++i)
+                for (int k = 0; k < nv; ++k) H[i * nv + k] += h * Jb[(size_t)a * nv + i] * Jb[(size_t)c * nv + k];
+            }
+          r += 2;
+          continue;
+        }
         if (w->efc_state[r] != ST_QUAD) continue;
         const double* Jr = w->efc_J + (size_t)r * nv;
         for (int i = 0; i < nv; ++i)
@@ -1710,6 +1923,17 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
     double dcost = alpha * g1 + 0.5 * alpha * alpha * g2;
     int changed = 0;
     for (int r = 0; r < nefc; ++r) {
+      if (ELL_BLOCK(w, r)) {
+        double j1[3], c0, c1;
+        for (int k = 0; k < 3; ++k) j1[k] = w->efc_jar[r + k] + alpha * w->efc_jv[r + k];
+        ell_block(w, r, w->efc_jar + r, NULL, &c0, NULL);
+        const int s1 = ell_block(w, r, j1, NULL, &c1, NULL);
+        dcost += c1 - c0;
+        changed |= s1 != w->efc_state[r] || s1 == ST_CONE;
+        for (int k = 0; k < 3; ++k) w->efc_jar[r + k] = j1[k];
+        r += 2;
+        continue;
+      }
       double j0 = w->efc_jar[r], j1 = j0 + alpha * w->efc_jv[r];
       int s0 = w->efc_state[r], s1 = row_state(w, r, j1);
       dcost += row_dcost(w, r, s0, s1, j0, alpha * w->efc_jv[r]);
@@ -1791,7 +2015,15 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
     for (int r = 0; r < nefc; ++r) {
       double jar = -w->efc_aref[r];
       for (int j = 0; j < nv; ++j) jar += w->efc_J[(size_t)r * nv + j] * d->qacc_warmstart[j];
-      f[r] = row_force(w, r, jar);
+      w->efc_jar[r] = jar;
+    }
+    for (int r = 0; r < nefc; ++r) {
+      if (ELL_BLOCK(w, r)) {  /* elliptic block: the zone forces of mj_constraintUpdate */
+        ell_block(w, r, w->efc_jar + r, f + r, NULL, NULL);
+        r += 2;
+        continue;
+      }
+      f[r] = row_force(w, r, w->efc_jar[r]);
     }
     double cost = 0;
     for (int r = 0; r < nefc; ++r) {
@@ -1806,6 +2038,32 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
   for (int it = 0; it < m->iterations; ++it) {
     double improvement = 0;
     for (int r = 0; r < nefc; ++r) {
+      if (ELL_BLOCK(w, r)) {
+        /* elliptic block: the block's forces minimise its local cost 1/2 y'Ay + y'(res - A f_old) over
+         * the cone |y_t| <= mu y_n exactly (ell_block_min), so the sweeps are block Gauss-Seidel on the
+         * dual and reach the optimum Newton / CG reach.  (Upstream mj_solPGS updates the normal force
+         * by its own 1-D step and then the friction by mju_QCQP2 with the normal fixed; that split
+         * stops short of the optimum when the contact slides -- the cone multiplier couples the two --
+         * so it is not restated: documented deviation, verify.) */
+        double res[3], A[9], old[3], nw[3], cb[3];
+        for (int k = 0; k < 3; ++k) {
+          const double* ar = w->AR + (size_t)(r + k) * nefc;
+          res[k] = w->efc_b[r + k];
+          for (int s = 0; s < nefc; ++s) res[k] += ar[s] * f[s];
+          for (int c = 0; c < 3; ++c) A[3 * k + c] = ar[r + c];
+          old[k] = f[r + k];
+        }
+        for (int k = 0; k < 3; ++k) cb[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
+        ell_block_min(A, cb, w->efc_fr[r], nw);
+        double delta[3], quad = 0;
+        for (int k = 0; k < 3; ++k) delta[k] = nw[k] - old[k];
+        for (int k = 0; k < 3; ++k)
+          for (int c = 0; c < 3; ++c) quad += delta[k] * A[3 * k + c] * delta[c];
+        improvement -= delta[0] * res[0] + delta[1] * res[1] + delta[2] * res[2] + 0.5 * quad;
+        for (int k = 0; k < 3; ++k) f[r + k] = nw[k];
+        r += 2;
+        continue;
+      }
       const double* ar = w->AR + (size_t)r * nefc;
       double res = w->efc_b[r];
       for (int s = 0; s < nefc; ++s) res += ar[s] * f[s];
@@ -2029,6 +2287,8 @@ static void rne_post_constraint(const mrs_model_view* m, orc_data* d) {
     double lfrc[3] = {0, 0, 0};
     if (con->dim == 1) {
       lfrc[0] = f[0];
+    } else if (m->cone == MRS_CONE_ELLIPTIC) {
+      for (int i = 0; i < 3; ++i) lfrc[i] = f[i];  /* (normal, tangent 1, tangent 2) in the contact frame */
     } else {
       for (int i = 0; i < con->dim - 1; ++i) {
         lfrc[0] += f[2 * i] + f[2 * i + 1];

@@ -79,3 +79,84 @@ def test_pyramid_edge_regulariser(impratio):
     imp = 0.9 + y * (0.95 - 0.9)
     want = 2 * mu * mu / impratio * (1 - imp) / imp * tran * (1 + mu * mu)
     np.testing.assert_allclose(efc["R"], want, rtol=1e-9)
+
+
+def test_three_solvers_one_optimum_elliptic():
+    """elliptic cones (cone="elliptic", impratio 3): the same C5 state (~30 contacts as 3-row blocks)
+    through the PGS block update (normal step + mju_QCQP2 friction), Newton's cone zones and CG reaches
+    one optimum -- the dual and primal restatements of the elliptic cone are the same convex problem"""
+    m0 = sim.Model.load(ARM_BOXES)
+    d = binding.OracleData(m0)
+    d.qpos[:] = synth.initial_qpos(m0, np.arange(1))[0]
+    d.step(60)
+    q, v = d.qpos.copy(), d.qvel.copy()
+    qacc = {}
+    for name, opt in [("PGS", 'solver="PGS" iterations="20000" tolerance="1e-15"'),
+                      ("Newton", 'solver="Newton" iterations="100"'),
+                      ("CG", 'solver="CG" iterations="2000" tolerance="1e-15"')]:
+        m = with_option(ARM_BOXES, opt + ' cone="elliptic" impratio="3"')
+        e = binding.OracleData(m)
+        e.qpos[:] = q
+        e.qvel[:] = v
+        e.forward()
+        assert e.nefc > 60
+        qacc[name] = e.qacc.copy()
+    scale = np.maximum(np.abs(qacc["Newton"]), 1.0)
+    print({k: float(np.max(np.abs(qacc[k] - qacc["Newton"]) / scale)) for k in qacc})
+    assert np.max(np.abs(qacc["PGS"] - qacc["Newton"]) / scale) < 1e-4
+    assert np.max(np.abs(qacc["CG"] - qacc["Newton"]) / scale) < 1e-4
+
+
+_BOX = """<mujoco><option timestep="0.002" cone="elliptic" impratio="{imp}" solver="{solver}"/><worldbody>
+<geom type="plane" size="0 0 1" friction="0.6 0.005 0.0001"/><body pos="0 0 0.1"><freejoint/>
+<geom type="box" size="0.1 0.08 0.06" mass="1" friction="0.6 0.005 0.0001"/></body></worldbody></mujoco>"""
+
+
+@pytest.mark.parametrize("imp", [1.0, 4.0])
+def test_elliptic_forces_solve_the_cone_program(imp):
+    """the elliptic-cone contact forces of the oracle's Newton solve are the minimiser of MuJoCo's
+    dual problem 1/2 f'(A + R) f + f'b over the friction cones |f_t| <= mu f_n -- computed here by an
+    independent solver (scipy SLSQP) from the oracle's own rows -- in resting, sliding and tumbling
+    states of a box; PGS's block updates reach the same forces"""
+    from scipy.optimize import minimize
+    rng = np.random.default_rng(5)
+    m = sim.Model.from_string(_BOX.format(imp=imp, solver="Newton"))
+    mp = sim.Model.from_string(_BOX.format(imp=imp, solver="PGS").replace('solver="PGS"', 'solver="PGS" iterations="500" tolerance="1e-14"'))
+    d = binding.OracleData(m)
+    d.step(100)
+    checked = 0
+    for trial in range(12):
+        d.qvel[:] = rng.normal(0, [0.8, 0.8, 0.05, 1.5, 1.5, 2.0])
+        for _ in range(40):
+            d.step()
+            if d.ncon > 0:
+                break
+        if d.ncon == 0:
+            continue
+        e = binding.OracleData(m)
+        e.qpos[:] = d.qpos
+        e.qvel[:] = d.qvel
+        e.forward()
+        efc = e.efc()
+        J, R, aref, f = efc["J"], efc["R"], efc["aref"], efc["force"]
+        a0, _ = e.smooth()
+        M = e.mass_matrix()
+        A = J @ np.linalg.solve(M, J.T)
+        b = J @ a0 - aref
+        n = len(f)
+        assert n % 3 == 0 and np.all(efc["type"] == 3)
+        cons = [{"type": "ineq", "fun": (lambda x, k=k: 0.6 * x[k] - np.hypot(x[k + 1], x[k + 2]))} for k in range(0, n, 3)]
+        cons += [{"type": "ineq", "fun": (lambda x, k=k: x[k])} for k in range(0, n, 3)]
+        obj = lambda x: 0.5 * x @ (A + np.diag(R)) @ x + x @ b  # noqa: E731
+        best = minimize(obj, np.maximum(f, 0), constraints=cons, method="SLSQP",
+                        options={"ftol": 1e-15, "maxiter": 2000})
+        scale = max(1.0, np.max(np.abs(best.x)))
+        assert obj(f) <= best.fun + 1e-9 * max(1.0, abs(best.fun))
+        np.testing.assert_allclose(f, best.x, atol=2e-4 * scale)
+        p = binding.OracleData(mp)
+        p.qpos[:] = d.qpos
+        p.qvel[:] = d.qvel
+        p.forward()
+        np.testing.assert_allclose(p.efc()["force"], f, atol=1e-5 * scale)
+        checked += 1
+    assert checked >= 6
