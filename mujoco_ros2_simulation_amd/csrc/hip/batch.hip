@@ -921,7 +921,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nsite = m.nsite; d.ncam = m.ncam; d.nsensor = m.nsensor; d.nsensordata = m.nsensordata;
   d.max_depth = m.max_depth;
   d.integrator = m.integrator; d.iterations = m.iterations; d.disableflags = m.disableflags;
-  d.solver = m.solver; d.ls_iterations = m.ls_iterations;
+  d.solver = m.solver; d.ls_iterations = m.ls_iterations; d.cone = m.cone;
   d.impratio = static_cast<float>(m.impratio); d.ls_tolerance = static_cast<float>(m.ls_tolerance);
   // diagnostic phase ablation for profiling only (bit 0 sensors, 1 collision, 2 constraints)
   d.diag_skip = std::getenv("MRS_DIAG_SKIP") ? std::atoi(std::getenv("MRS_DIAG_SKIP")) : 0;
@@ -1585,7 +1585,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   off = 0;
   const int ne = std::max(1, d.max_efc);
   // dense rows: dense mode, and blocked mode with a primal solver (the sparse records are PGS's)
-  const int dn = d.blocked && m.solver == MRS_SOL_PGS ? 0 : ne;
+  const int dn = d.blocked && m.solver == MRS_SOL_PGS && m.cone != MRS_CONE_ELLIPTIC ? 0 : ne;
   S.efc_J = take(dn * nv); S.efc_MJ = take(dn * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(dn); S.efc_aref = take(dn);
   S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));

@@ -111,6 +111,7 @@ struct DevModel {
   float* rf_static;
   // options
   int integrator, iterations, disableflags, solver, ls_iterations;
+  int cone;  // MRS_CONE_*: elliptic models take the dense row path (3-row contact blocks)
   int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run
   float timestep, tolerance, pgs_scale, gravity[3], impratio, ls_tolerance;

@@ -3860,6 +3860,118 @@ __device__ __forceinline__ float prow_cost(int st, float R, float fl, float jar)
 __device__ __forceinline__ float prow_slope(int st, float R, float fl, float jar) {
   return st == PST_QUAD ? jar / R : (st == PST_LINNEG ? -fl : (st == PST_LINPOS ? fl : 0.0f));
 }
+// ---- elliptic friction cones (oracle.c ell_block / qcqp2_la / ell_block_min restate them; same
+// formulas in fp32).  A contact of condim 3 under cone="elliptic" is a 3-row block (normal, tangent 1,
+// tangent 2); its rows carry k + 1 in the efc_floss slot (k = 0, 1, 2; 0 for every other contact row),
+// so a block starts where that slot holds 1.
+enum { PST_CONE = 4 };
+__device__ __forceinline__ bool ell_start(const DevModel& m, const gfloat* type, const gfloat* floss, int r) {
+  return m.cone == MRS_CONE_ELLIPTIC && (__float_as_int(type[r]) >> 16) == EFC_CONTACT && floss[r] == 1.0f;
+}
+// the block's friction coefficient (both tangents: sliding) and regularised cone mu = mu_1 / sqrt(impratio)
+__device__ __forceinline__ float ell_friction(const DevModel& m, const gfloat* scr, const gfloat* type, int r) {
+  const int c = __float_as_int(type[r]) & 0xffff;
+  return m.pair_friction[3 * __float_as_int(scr[m.S.con + kConRec * c])];
+}
+// zone (PST_SAT top, PST_QUAD bottom, PST_CONE middle) at jar; f, cost and the jar-space Hessian H may
+// be null
+__device__ __forceinline__ int ell_zone(float ft, float imp, const float D[3], const float jar[3], float* f, float* cost,
+                                        float* H) {
+  const float mu = ft * rsqrtf(imp);
+  const float U[3] = {mu * jar[0], ft * jar[1], ft * jar[2]};
+  const float N = U[0], T = sqrtf(U[1] * U[1] + U[2] * U[2]);
+  if (N >= mu * T || (T <= 0 && N >= 0)) {
+    if (f) { f[0] = f[1] = f[2] = 0; }
+    if (cost) *cost = 0;
+    if (H) for (int i = 0; i < 9; ++i) H[i] = 0;
+    return PST_SAT;
+  }
+  if (mu * N + T <= 0 || (T <= 0 && N < 0)) {
+    float c = 0;
+    for (int j = 0; j < 3; ++j) {
+      if (f) f[j] = -D[j] * jar[j];
+      c += 0.5f * D[j] * jar[j] * jar[j];
+    }
+    if (cost) *cost = c;
+    if (H) for (int i = 0; i < 9; ++i) H[i] = (i % 4 == 0) ? D[i / 4] : 0.0f;
+    return PST_QUAD;
+  }
+  const float Dm = D[0] / (mu * mu * (1 + mu * mu)), NT = N - mu * T;
+  if (cost) *cost = 0.5f * Dm * NT * NT;
+  if (f) {
+    f[0] = -Dm * NT * mu;
+    for (int j = 1; j < 3; ++j) f[j] = Dm * NT * mu / T * U[j] * ft;
+  }
+  if (H) {
+    const float S[3] = {mu, ft, ft};
+    float HU[9];
+    HU[0] = 1;
+    for (int j = 1; j < 3; ++j) HU[j] = HU[3 * j] = -mu * U[j] / T;
+    for (int j = 1; j < 3; ++j)
+      for (int k = 1; k < 3; ++k) HU[3 * j + k] = mu * N / (T * T * T) * U[j] * U[k] + (j == k ? mu * mu - mu * N / T : 0.0f);
+    for (int j = 0; j < 3; ++j)
+      for (int k = 0; k < 3; ++k) H[3 * j + k] = Dm * S[j] * HU[3 * j + k] * S[k];
+  }
+  return PST_CONE;
+}
+// mju_QCQP2 with its multiplier (oracle.c qcqp2_la)
+__device__ __forceinline__ float qcqp2_la(float res[2], const float A[4], const float b[2], float d, float r) {
+  const float b1 = b[0] * d, b2 = b[1] * d;
+  const float A11 = A[0] * d * d, A22 = A[3] * d * d, A12 = A[1] * d * d;
+  float la = 0, v1 = 0, v2 = 0;
+  #pragma unroll 1
+  for (int it = 0; it < 20; ++it) {
+    const float det = (A11 + la) * (A22 + la) - A12 * A12;
+    if (det < 1e-10f) { res[0] = res[1] = 0; return 0; }
+    const float di = 1 / det, P11 = (A22 + la) * di, P22 = (A11 + la) * di, P12 = -A12 * di;
+    v1 = -P11 * b1 - P12 * b2;
+    v2 = -P12 * b1 - P22 * b2;
+    const float val = v1 * v1 + v2 * v2 - r * r;
+    if (val < 1e-10f) break;
+    const float deriv = -2.0f * (P11 * v1 * v1 + 2.0f * P12 * v1 * v2 + P22 * v2 * v2);
+    const float delta = -val / deriv;
+    if (delta < 1e-10f) break;
+    la += delta;
+  }
+  res[0] = v1 * d;
+  res[1] = v2 * d;
+  return la;
+}
+// the exact minimiser of 1/2 y'Ay + y'c over |y_t| <= mu y_n (oracle.c ell_block_min): secant /
+// bisection on g'(s) = (A y + c)_n - la s with the QCQP inside; the bracket stops at fp32 resolution
+__device__ __forceinline__ void ell_block_min(const float A[9], const float c[3], float mu, float y[3]) {
+  const float At[4] = {A[4], A[5], A[7], A[8]};
+  float x[2];
+  float gp_lo = c[0] - mu * sqrtf(c[1] * c[1] + c[2] * c[2]), s_lo = 0, gp_hi = 0;
+  if (gp_lo >= 0) { y[0] = y[1] = y[2] = 0; return; }
+  auto eval = [&](float s) {
+    const float bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
+    const float la = qcqp2_la(x, At, bc, mu, s);
+    return A[0] * s + A[1] * x[0] + A[2] * x[1] + c[0] - la * s;
+  };
+  float s_hi = -c[0] / A[0];
+  if (!(s_hi > 0)) s_hi = 1;
+  #pragma unroll 1
+  for (int k = 0; k < 60; ++k) {
+    gp_hi = eval(s_hi);
+    if (gp_hi >= 0) break;
+    s_lo = s_hi; gp_lo = gp_hi;
+    s_hi *= 2;
+  }
+  #pragma unroll 1
+  for (int it = 0; it < 60 && s_hi - s_lo > 1e-6f * (1 + s_hi); ++it) {
+    float sn = s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo);
+    if (!(sn > s_lo + 0.01f * (s_hi - s_lo) && sn < s_hi - 0.01f * (s_hi - s_lo))) sn = 0.5f * (s_lo + s_hi);
+    const float gp = eval(sn);
+    if (gp == 0) { s_lo = s_hi = sn; break; }
+    if (gp < 0) { s_lo = sn; gp_lo = gp; } else { s_hi = sn; gp_hi = gp; }
+  }
+  const float s = 0.5f * (s_lo + s_hi);
+  const float bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
+  qcqp2_la(x, At, bc, mu, s);
+  y[0] = s; y[1] = x[0]; y[2] = x[1];
+}
+
 // cost change of a row moved from jar j0 (state s0) by dj to state s1, in factored form when the
 // state is kept (no cancellation of two nearly equal costs in fp32)
 __device__ __forceinline__ float prow_dcost(int s0, int s1, float R, float fl, float j0, float dj) {
@@ -3993,6 +4105,31 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
   const float qs = dof ? s[L.qacc_smooth + lane] : 0.0f;
   const float fs = dof ? s[L.qfrc_smooth + lane] : 0.0f;
   auto is_fric = [&](int r) { return (__float_as_int(type[r]) >> 16) == EFC_FRICTION; };
+  auto is_con = [&](int r) { return (__float_as_int(type[r]) >> 16) == EFC_CONTACT; };
+  const bool ell = m.cone == MRS_CONE_ELLIPTIC;  // 3-row contact blocks (floss slot: k + 1)
+  // an elliptic block's zone cost at jar0 + a dj (dj null: at jar0) and its 1-D slope / curvature
+  auto ell_line = [&](int r, float a, const float* dj, float& cost, float& d1, float& d2) {
+    float ja[3], D[3], v[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k) {
+      if (dj) v[k] = dj[k];
+      ja[k] = jar[r + k] + a * v[k];
+      D[k] = 1.0f / Rr[r + k];
+    }
+    const float ft = ell_friction(m, scr, type, r), mu = ft * rsqrtf(m.impratio);
+    const int z = ell_zone(ft, m.impratio, D, ja, nullptr, &cost, nullptr);
+    d1 = d2 = 0;
+    if (z == PST_QUAD) {
+      for (int k = 0; k < 3; ++k) { d1 += v[k] * D[k] * ja[k]; d2 += D[k] * v[k] * v[k]; }
+    } else if (z == PST_CONE) {
+      const float N = mu * ja[0], dN = mu * v[0];
+      const float U1 = ft * ja[1], U2 = ft * ja[2], dU1 = ft * v[1], dU2 = ft * v[2];
+      const float T = sqrtf(U1 * U1 + U2 * U2), dT = (U1 * dU1 + U2 * dU2) / T;
+      const float Dm = D[0] / (mu * mu * (1 + mu * mu)), NT = N - mu * T, g = dN - mu * dT;
+      d1 = Dm * NT * g;
+      d2 = Dm * (g * g - NT * mu * ((dU1 * dU1 + dU2 * dU2) - dT * dT) / T);
+    }
+    return z;
+  };
   // M[lane][k]: dense, or per kinematic tree in blocked mode (zero across trees)
   const int mytree = G == 64 && dof ? m.dof_tree[lane] : 0;
   auto mval = [&](int k) {
@@ -4039,6 +4176,17 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     chg = false;
     #pragma unroll 1
     for (int r = lane; r < nefc; r += G) {
+      if (ell && is_con(r) && floss[r] > 0.5f) {
+        // elliptic block: the first row's lane sets the zone and the forces of all three rows (the
+        // middle zone's Hessian depends on jar, so a block in it always counts as changed)
+        if (floss[r] != 1.0f) continue;
+        float ja3[3], D[3], f3[3];
+        for (int k = 0; k < 3; ++k) { ja3[k] = jar[r + k]; D[k] = 1.0f / Rr[r + k]; }
+        const int z = ell_zone(ell_friction(m, scr, type, r), m.impratio, D, ja3, f3, nullptr, nullptr);
+        chg |= __float_as_int(st[r]) != z || z == PST_CONE;
+        for (int k = 0; k < 3; ++k) { st[r + k] = __int_as_float(z); ff[r + k] = f3[k]; }
+        continue;
+      }
       const float R = Rr[r], fl = floss[r], ja = jar[r];
       const int stt = prow_state(is_fric(r), R, fl, ja);
       chg |= __float_as_int(st[r]) != stt;
@@ -4068,6 +4216,14 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     float c = 0;
     #pragma unroll 1
     for (int r = lane; r < nefc; r += G) {
+      if (ell && is_con(r) && floss[r] > 0.5f) {
+        if (floss[r] == 1.0f) {
+          float cb, d1, d2;
+          ell_line(r, 0.0f, nullptr, cb, d1, d2);
+          c += cb;
+        }
+        continue;
+      }
       const float R = Rr[r], fl = floss[r], ja = jar[r];
       c += prow_cost(prow_state(is_fric(r), R, fl, ja), R, fl, ja);
     }
@@ -4117,6 +4273,26 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
           }
       }
       wsync();
+      if (ell) {
+        // elliptic blocks in the middle zone: J_b' H_b J_b with the zone's 3x3 jar-space Hessian
+        // (bottom-zone blocks are quadratic rows, already in); lower triangle, lane per H row
+        #pragma unroll 1
+        for (int r = 0; r < nefc; ++r) {
+          if (!(is_con(r) && floss[r] == 1.0f) || __float_as_int(st[r]) != PST_CONE) continue;
+          float ja3[3], D[3], Hb[9];
+          for (int k = 0; k < 3; ++k) { ja3[k] = jar[r + k]; D[k] = 1.0f / Rr[r + k]; }
+          ell_zone(ell_friction(m, scr, type, r), m.impratio, D, ja3, nullptr, nullptr, Hb);
+          if (dof) {
+            float u[3];  // (H_b J_b)[:, lane]
+            for (int a = 0; a < 3; ++a)
+              u[a] = Hb[3 * a] * J[r * nv + lane] + Hb[3 * a + 1] * J[(r + 1) * nv + lane] + Hb[3 * a + 2] * J[(r + 2) * nv + lane];
+            #pragma unroll 1
+            for (int k = 0; k <= (G == 64 ? lane : nv - 1); ++k)
+              H[lane * nv + k] += u[0] * J[r * nv + k] + u[1] * J[(r + 1) * nv + k] + u[2] * J[(r + 2) * nv + k];
+          }
+          wsync();
+        }
+      }
       SUB_ADD(PH_CON_DEL, t_h);
       t_h = SUB_T();
       if constexpr (G == 64) {
@@ -4148,6 +4324,20 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
       bool c = false;
       #pragma unroll 1
       for (int r = lane; r < nefc; r += G) {
+        if (ell && is_con(r) && floss[r] > 0.5f) {
+          // elliptic block: the middle zone is not quadratic in a, so a step ending in it is never
+          // taken as exact
+          if (floss[r] == 1.0f) {
+            const float dj[3] = {jv[r], jv[r + 1], jv[r + 2]};
+            float cb, e1, e2, x1, x2;
+            const int z = ell_line(r, a, dj, cb, e1, e2);
+            const int z0 = ell_line(r, a0, dj, cb, x1, x2);
+            c |= z != z0 || z == PST_CONE;
+            s1 += e1;
+            s2 += e2;
+          }
+          continue;
+        }
         const float v = jv[r];
         if (v == 0) continue;
         const bool fr = is_fric(r);
@@ -4189,6 +4379,18 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     bool changed = false;
     #pragma unroll 1
     for (int r = lane; r < nefc; r += G) {
+      if (ell && is_con(r) && floss[r] > 0.5f) {
+        if (floss[r] == 1.0f) {
+          const float dj[3] = {jv[r], jv[r + 1], jv[r + 2]};
+          float c0, c1, d1, d2;
+          ell_line(r, 0.0f, nullptr, c0, d1, d2);
+          const int z1 = ell_line(r, alpha, dj, c1, d1, d2);
+          dc += c1 - c0;
+          changed |= z1 != __float_as_int(st[r]) || z1 == PST_CONE;
+          for (int k = 0; k < 3; ++k) jar[r + k] = jar[r + k] + alpha * dj[k];
+        }
+        continue;
+      }
       const bool fr = is_fric(r);
       const float R = Rr[r], fl = floss[r], j0 = jar[r], j1 = j0 + alpha * jv[r];
       const int s0 = __float_as_int(st[r]), s1 = prow_state(fr, R, fl, j1);
@@ -4437,8 +4639,9 @@ template <int G, bool kPrimal = false>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) {
-    if (m.solver != MRS_SOL_PGS) {
-      // Newton / CG in blocked mode: dense rows, dense Hessian (solve_primal)
+    if (m.solver != MRS_SOL_PGS || m.cone == MRS_CONE_ELLIPTIC) {
+      // Newton / CG in blocked mode, and elliptic cones under every solver: dense rows (solve_primal,
+      // or the row-serial PGS with its 3-row contact blocks)
       float qa;
       [[clang::noinline]] qa = constraints_dense<G>(ENV_ARGS, ncon, qacc_s);
       return qa;
@@ -4632,7 +4835,9 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
         float cp[3] = {bcast(cv[1], k), bcast(cv[2], k), bcast(cv[3], k)};
         float fr[9];
         for (int i = 0; i < 9; ++i) fr[i] = bcast(cv[4 + i], k);
-        if (lane == 0) scr[S.con + kConRec * c + 14] = __int_as_float(nefc + (dim == 1 ? 1 : 4) <= m.max_efc ? nefc : -1);
+        const bool ell = dim == 3 && m.cone == MRS_CONE_ELLIPTIC;
+        const int nrow = dim == 1 ? 1 : (ell ? 3 : 4);
+        if (lane == 0) scr[S.con + kConRec * c + 14] = __int_as_float(nefc + nrow <= m.max_efc ? nefc : -1);
         float jc[3] = {0, 0, 0};
         if (lane < nv) {
           float c1[3], c2[3];
@@ -4641,16 +4846,19 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
           const float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
           for (int r = 0; r < 3; ++r) jc[r] = fr[3 * r] * dc[0] + fr[3 * r + 1] * dc[1] + fr[3 * r + 2] * dc[2];
         }
-        const int nrow = dim == 1 ? 1 : 4;
+        if (ell && nefc + nrow > m.max_efc) continue;  // (an elliptic block is kept whole)
         for (int q = 0; q < nrow; ++q) {
           if (nefc >= m.max_efc) break;
-          // pyramid edges: both tangent directions use the sliding coefficient (mj_setContact)
+          // pyramid edges: both tangent directions use the sliding coefficient (mj_setContact);
+          // elliptic: the frame rows themselves, k + 1 in the floss slot
           const int kk = 1 + (q >> 1);
           const float sg = (q & 1) ? -1.0f : 1.0f;
-          if (lane < nv) J[nefc * nv + lane] = dim == 1 ? jc[0] : jc[0] + sg * mu * (kk == 1 ? jc[1] : jc[2]);
+          if (lane < nv)
+            J[nefc * nv + lane] = (dim == 1 || (ell && q == 0)) ? jc[0]
+                                  : (ell ? (q == 1 ? jc[1] : jc[2]) : jc[0] + sg * mu * (kk == 1 ? jc[1] : jc[2]));
           if (lane == 0) {
             type[nefc] = __int_as_float(EFC_CONTACT * 65536 + c);
-            pos[nefc] = dist; marg[nefc] = mg; floss[nefc] = 0;
+            pos[nefc] = dist; marg[nefc] = mg; floss[nefc] = ell ? (float)(q + 1) : 0.0f;
           }
           ++nefc;
         }
@@ -4665,7 +4873,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
     float cp[3] = {rec[2], rec[3], rec[4]};
     // first efc row of this contact (rec[14]; -1 if the row cap cut its rows), for cfrc_ext
-    if (lane == 0) rec[14] = __int_as_float(nefc + (dim == 1 ? 1 : 4) <= m.max_efc ? nefc : -1);
+    const bool ell = dim == 3 && m.cone == MRS_CONE_ELLIPTIC;
+    if (lane == 0) rec[14] = __int_as_float(nefc + (dim == 1 ? 1 : (ell ? 3 : 4)) <= m.max_efc ? nefc : -1);
     float jc[3] = {0, 0, 0};
     if (lane < nv) {
       float c1[3], c2[3];
@@ -4674,7 +4883,18 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       float dc[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
       for (int r = 0; r < 3; ++r) jc[r] = rec[5 + 3 * r] * dc[0] + rec[6 + 3 * r] * dc[1] + rec[7 + 3 * r] * dc[2];
     }
-    if (dim == 1) {
+    if (ell) {
+      // elliptic cone: the frame rows (normal, tangent 1, tangent 2), kept whole, k + 1 in floss
+      if (nefc + 3 <= m.max_efc)
+        for (int k = 0; k < 3; ++k) {
+          if (lane < nv) J[nefc * nv + lane] = jc[k];
+          if (lane == 0) {
+            type[nefc] = __int_as_float(EFC_CONTACT * 65536 + c);
+            pos[nefc] = rec[1]; marg[nefc] = m.pair_margin[p] - m.pair_gap[p]; floss[nefc] = (float)(k + 1);
+          }
+          ++nefc;
+        }
+    } else if (dim == 1) {
       if (nefc < m.max_efc) {
         if (lane < nv) J[nefc * nv + lane] = jc[0];
         if (lane == 0) {
@@ -4710,7 +4930,9 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   }
   // --- impedance, R, aref, M^-1 J', ARii, b (lane per row); the primal solvers need R and aref only
   const bool primal = m.solver != MRS_SOL_PGS;
-  const bool small = G == 16 && nefc <= 16;  // register-resident solvers (dual PGS or primal)
+  // register-resident solvers (dual PGS or primal) for small systems; elliptic blocks take the
+  // generic paths below
+  const bool small = G == 16 && nefc <= 16 && !(m.cone == MRS_CONE_ELLIPTIC && ncon > 0);
   float my_R = 1, my_aref = 0, my_b = 0, my_fl = 0;
   bool my_fric = false;
   #pragma unroll 1
@@ -4728,7 +4950,10 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
       float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
       diag = tran;
-      if (m.pair_dim[p] == 3) {
+      if (m.pair_dim[p] == 3 && m.cone == MRS_CONE_ELLIPTIC) {
+        // elliptic: diagApprox tran for every row of the block, the tangents' regulariser / impratio
+        if (floss[r] > 1.5f) diag = tran / m.impratio;
+      } else if (m.pair_dim[p] == 3) {
         // pyramid edge: diagApprox tran (1 + mu^2) (mu sliding, for both tangent directions);
         // mj_makeImpedance scales the edges' regulariser by 2 mu^2 / impratio
         const float mu = m.pair_friction[3 * p];
@@ -4754,7 +4979,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     const gfloat* Jr = J + r * nv;
     #pragma unroll 4
     for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
-    const float pterm = t == EFC_FRICTION ? 0.0f : K * imp * (pos[r] - marg[r]);
+    // (friction-loss rows and the tangent rows of an elliptic block carry no position term)
+    const float pterm = (t == EFC_FRICTION || (t == EFC_CONTACT && floss[r] > 1.5f)) ? 0.0f : K * imp * (pos[r] - marg[r]);
     if (small) {
       my_R = R;
       my_aref = -B * vel - pterm;
@@ -4831,6 +5057,26 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     #pragma unroll 1
     for (int r = lane; r < nefc; r += G) {
       float f = 0;
+      if (m.cone == MRS_CONE_ELLIPTIC && (__float_as_int(type[r]) >> 16) == EFC_CONTACT && floss[r] > 0.5f) {
+        // elliptic block: its first row's lane writes the three forces (the zone forces of
+        // mj_constraintUpdate at qacc_warmstart)
+        if (floss[r] != 1.0f) continue;
+        float f3[3] = {0, 0, 0};
+        if (warm) {
+          float jar3[3], D[3];
+          for (int k = 0; k < 3; ++k) {
+            const gfloat* Jr = J + (r + k) * nv;
+            float jar = -aref[r + k];
+            #pragma unroll 1
+            for (int j = 0; j < nv; ++j) jar += Jr[j] * s[L.qacc_ws + j];
+            jar3[k] = jar;
+            D[k] = 1.0f / Rr[r + k];
+          }
+          ell_zone(ell_friction(m, scr, type, r), m.impratio, D, jar3, f3, nullptr, nullptr);
+        }
+        for (int k = 0; k < 3; ++k) ff[r + k] = f3[k];
+        continue;
+      }
       if (warm) {
         const gfloat* Jr = J + r * nv;
         float jar = -aref[r];
@@ -4876,6 +5122,31 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     float improvement = 0;
     #pragma unroll 1
     for (int r = 0; r < nefc; ++r) {
+      if (ell_start(m, type, floss, r)) {
+        // elliptic block: its forces minimise the block's local cost over the cone exactly
+        // (ell_block_min; oracle.c fwd_constraint states the deviation from upstream's split update)
+        float res[3], A[9], old[3], c[3], y[3];
+        for (int k = 0; k < 3; ++k) {
+          old[k] = ff[r + k];
+          res[k] = gsum<G>(lane < nv ? J[(r + k) * nv + lane] * qa : 0.0f) - aref[r + k] + Rr[r + k] * old[k];
+          A[4 * k] = ARii[r + k];
+        }
+        for (int a = 0; a < 3; ++a)
+          for (int b = a + 1; b < 3; ++b)
+            A[3 * a + b] = A[3 * b + a] = gsum<G>(lane < nv ? J[(r + a) * nv + lane] * MJ[(r + b) * nv + lane] : 0.0f);
+        for (int k = 0; k < 3; ++k) c[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
+        ell_block_min(A, c, ell_friction(m, scr, type, r), y);
+        float dl[3], quad = 0;
+        for (int k = 0; k < 3; ++k) dl[k] = y[k] - old[k];
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) quad += dl[a] * A[3 * a + b] * dl[b];
+        if (lane < nv) qa += MJ[r * nv + lane] * dl[0] + MJ[(r + 1) * nv + lane] * dl[1] + MJ[(r + 2) * nv + lane] * dl[2];
+        if (lane == 0) { ff[r] = y[0]; ff[r + 1] = y[1]; ff[r + 2] = y[2]; }
+        improvement -= dl[0] * res[0] + dl[1] * res[1] + dl[2] * res[2] + 0.5f * quad;
+        wsync();
+        r += 2;
+        continue;
+      }
       const float jq = gsum<G>(lane < nv ? J[r * nv + lane] * qa : 0.0f);
       const float f0 = ff[r];
       const float res = jq - aref[r] + Rr[r] * f0;
@@ -4972,6 +5243,8 @@ __device__ MRS_PHASE void rne_post(ENV_PARAMS, int ncon) {
         float lf[3] = {0, 0, 0};
         if (m.pair_dim[p] == 1) {
           lf[0] = ff[r0];
+        } else if (m.cone == MRS_CONE_ELLIPTIC) {
+          for (int i = 0; i < 3; ++i) lf[i] = ff[r0 + i];  // (normal, tangent 1, tangent 2)
         } else {
           for (int k = 0; k < 2; ++k) {
             const float fp = ff[r0 + 2 * k], fm = ff[r0 + 2 * k + 1];

@@ -1,0 +1,65 @@
+"""GPU parity of elliptic friction cones (cone="elliptic": 3-row contact blocks; oracle.c ell_block /
+ell_block_min / the primal cone zones state the restatement, pinned on the CPU by an independent
+cone-program solve, tests/test_oracle_solvers.py).  On the device every elliptic model takes the
+dense row path: the row-serial PGS with exact block updates, or solve_primal with the cone zones'
+costs, forces and Hessian blocks.  Tolerance: 1e-5 of scale per re-seeded step (north_star)."""
+import numpy as np
+import pytest
+
+from conftest import ARM7
+from mujoco_ros2_simulation_amd import sim
+from test_gpu_solvers import _reseeded
+import binding
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+SCENES = ARM7.parent
+
+
+def elliptic_scene(name: str, solver: str, impratio: float = 1.0) -> "sim.Model":
+    path = SCENES / f"{name}.xml"
+    xml = path.read_text().replace('solver="PGS" iterations="50"',
+                                   f'solver="{solver}" iterations="{50 if solver == "PGS" else 100}" '
+                                   f'cone="elliptic" impratio="{impratio}"')
+    m = sim.Model.from_string(xml, str(path.parent))
+    assert m.solver == {"PGS": 0, "CG": 1, "Newton": 2}[solver]
+    return m
+
+
+@pytest.mark.parametrize("scene, solver, imp, n", [("arm_boxes", "PGS", 1.0, 16), ("arm_boxes", "Newton", 3.0, 8),
+                                                   ("arm_boxes", "CG", 1.0, 8), ("mobile_base", "PGS", 1.0, 32),
+                                                   ("mobile_base", "Newton", 10.0, 32)])
+def test_reseeded_elliptic(scene, solver, imp, n):
+    """contact scenes under cone="elliptic" (blocked mode for the arm + boxes, 16-lane groups for the
+    mobile base), every step from the oracle's state, qpos / qvel within 1e-5 of scale"""
+    model = elliptic_scene(scene, solver, imp)
+    wq, wv, ncon, flips, unexplained = _reseeded(model, n, 40)
+    print(f"{scene} elliptic {solver} impratio {imp}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; "
+          f"contacts per env {ncon.mean():.1f}; flips {flips}")
+    assert ncon.max() > 0
+    assert flips <= max(1, 0.01 * n * 40)
+    assert not unexplained, unexplained[:5]
+    assert wq <= RTOL and wv <= RTOL
+
+
+def test_elliptic_forces_match_oracle():
+    """the elliptic block forces themselves (mjData.efc_force by mrs_batch_get_efc) against the oracle's
+    from the same state, Newton and PGS: within 1e-4 of the block's normal force"""
+    for solver in ("Newton", "PGS"):
+        model = elliptic_scene("arm_boxes", solver)
+        b = sim.Batch(model, 4)
+        ref = binding.OracleData(model)
+        q0 = ref.qpos.copy()
+        ref.step(40)
+        b.set(sim.FIELD_QPOS, np.tile(ref.qpos, (4, 1)))
+        b.set(sim.FIELD_QVEL, np.tile(ref.qvel, (4, 1)))
+        b.set(sim.FIELD_QACC_WARMSTART, np.tile(ref.qacc_warmstart, (4, 1)))
+        b.forward()
+        ref.forward()
+        e, r = b.efc(0), ref.efc()
+        assert len(e["force"]) == len(r["force"]) > 30
+        scale = max(1.0, float(np.max(np.abs(r["force"]))))
+        np.testing.assert_allclose(e["force"], r["force"], atol=1e-4 * scale)
+        b.close()
+        del q0
