@@ -427,7 +427,8 @@ def main():
                 "frac": achieved / roofline.PEAK_HBM_GBS,
                 "traffic": traffic_rec["traffic_bytes_per_launch"] if traffic_rec else None,
                 "traffic_source": traffic_src, "traffic_unit": "bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
-                "kernel": "depth_kernel_v2 (one 640x480 frame of every env)", "kernel_ms": rend_ms,
+                "kernel": (("depth_kernel_mesh (triangle-binned" if model.nmesh > 0 else "depth_kernel_v2 (tiled") +
+                           f", one {W}x{H} frame of every env)"), "kernel_ms": rend_ms,
                 "algorithmic_bytes_per_launch": bytes_frame, "step_kernel_ms": step_ms}
     else:
         detailed_flops = roofline.flops_per_env_step(model)

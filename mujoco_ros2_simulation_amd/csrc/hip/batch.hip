@@ -465,8 +465,8 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       const int type = o.type;
 #pragma unroll
       for (int k = 0; k < kDepthTileH; ++k) {
-        const float lv[3] = {A[0] * dx + A[1] * dy[k] - A[2], A[3] * dx + A[4] * dy[k] - A[5],
-                             A[6] * dx + A[7] * dy[k] - A[8]};
+        float lv[3];
+        pixel_ray(A, dx, dy[k], lv);
         float t;
         if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
         else if (type == MRS_GEOM_MESH)
@@ -501,8 +501,8 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
           if (o.type == MRS_GEOM_MESH) {  // the hit triangle's normal, facing the ray
             const float* mv = mesh.vert + 3 * mesh.vertadr[o.dataid];
             const int* mf = mesh.face + 3 * mesh.faceadr[o.dataid];
-            const float lv[3] = {o.A[0] * dx + o.A[1] * dy[k] - o.A[2], o.A[3] * dx + o.A[4] * dy[k] - o.A[5],
-                                 o.A[6] * dx + o.A[7] * dy[k] - o.A[8]};
+            float lv[3];
+        pixel_ray(o.A, dx, dy[k], lv);
             int tri = 0;
             ray_mesh(mv, mf, mesh.facenum[o.dataid], o.size, o.lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
                           mesh.bvhnum[o.dataid], &tri);
@@ -541,6 +541,7 @@ constexpr int kRasterFaceBits = 18;  // triangle index bits in a record (mesh ge
 // expressions in the same order, so t is bit-identical
 __device__ __forceinline__ float ray_tri_v(const float a[3], const float e1[3], const float e2[3], const float lp[3],
                                            const float lv[3]) {
+#pragma clang fp contract(off)
   const float pv[3] = {lv[1] * e2[2] - lv[2] * e2[1], lv[2] * e2[0] - lv[0] * e2[2], lv[0] * e2[1] - lv[1] * e2[0]};
   const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
   if (fabsf(det) < 1e-15f) return -1;
@@ -694,7 +695,8 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
         const float dy = (0.5f * H - r - 0.5f) / f;
         for (int c = c0; c <= c1; ++c) {
           const float dx = (c + 0.5f - 0.5f * W) / f;
-          const float lv[3] = {A[0] * dx + A[1] * dy - A[2], A[3] * dx + A[4] * dy - A[5], A[6] * dx + A[7] * dy - A[8]};
+          float lv[3];
+        pixel_ray(A, dx, dy, lv);
           const float t = ray_tri_v(tr.a, tr.e1, tr.e2, lp, lv);
           if (t >= znear)
             atomicMin(&band[(r - rb) * W + c], (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | low);
@@ -733,8 +735,8 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
         cand &= cand - 1;
         const DepthGeom& o = G[g];
         const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]}, sz[3] = {o.size[0], o.size[1], o.size[2]};
-        const float lv[3] = {o.A[0] * dx + o.A[1] * dy - o.A[2], o.A[3] * dx + o.A[4] * dy - o.A[5],
-                             o.A[6] * dx + o.A[7] * dy - o.A[8]};
+        float lv[3];
+        pixel_ray(o.A, dx, dy, lv);
         const float t = o.type == MRS_GEOM_BOX ? ray_box_slab(sz, lp, lv) : ray_prim(o.type, sz, lp, lv);
         if (t >= znear && (best < 0 || t < best)) { best = t; bestg = g; }
       }
@@ -753,8 +755,8 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
         if (best < 0 || best > zfar) { px[0] = px[1] = px[2] = 0; continue; }
         const DepthGeom& o = G[bestg];
         const float v[3] = {dx, dy, -1.0f};
-        const float lv[3] = {o.A[0] * dx + o.A[1] * dy - o.A[2], o.A[3] * dx + o.A[4] * dy - o.A[5],
-                             o.A[6] * dx + o.A[7] * dy - o.A[8]};
+        float lv[3];
+        pixel_ray(o.A, dx, dy, lv);
         float nl[3], nc[3];
         if (tri >= 0) {
           mesh_tri_normal(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid], tri, lv, nl);
@@ -1951,7 +1953,7 @@ void batch_render_wait(BatchImpl* b) {
 int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force) {
   if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
   if (max < 0) throw std::invalid_argument("negative capacity");
-  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS)
+  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS && b->model->cone != MRS_CONE_ELLIPTIC)
     throw UnsupportedError("blocked-mode PGS keeps its constraint rows in sparse records");
   HIP_CHECK(hipSetDevice(b->device));
   const ScratchLayout& S = b->S;

@@ -10,6 +10,9 @@
 // one triangle, both faces (Moller-Trumbore); t >= 0 of the hit or -1
 template <class PV, class PF>
 __device__ __forceinline__ float ray_tri(PV vert, PF face, int f, const float lp[3], const float lv[3]) {
+  // (no FMA contraction here nor in pixel_ray: the binned frame kernel (batch.hip ray_tri_v) and
+  // the per-pixel kernels then give bit-identical t whatever the compiler fuses around them)
+#pragma clang fp contract(off)
   const int ia = 3 * face[3 * f], ib = 3 * face[3 * f + 1], ic = 3 * face[3 * f + 2];
   const float a[3] = {vert[ia], vert[ia + 1], vert[ia + 2]};
   const float e1[3] = {vert[ib] - a[0], vert[ib + 1] - a[1], vert[ib + 2] - a[2]};
@@ -26,6 +29,15 @@ __device__ __forceinline__ float ray_tri(PV vert, PF face, int f, const float lp
   if (v < 0 || u + v > 1) return -1;
   const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
   return t >= 0 ? t : -1;
+}
+
+// a pixel ray (camera-frame slopes dx, dy; direction (dx, dy, -1)) in a geom frame: rows of A
+template <class PA>
+__device__ __forceinline__ void pixel_ray(const PA A, float dx, float dy, float lv[3]) {
+#pragma clang fp contract(off)
+  lv[0] = A[0] * dx + A[1] * dy - A[2];
+  lv[1] = A[3] * dx + A[4] * dy - A[5];
+  lv[2] = A[6] * dx + A[7] * dy - A[8];
 }
 
 // slab test of the ray against an axis-aligned box [lo, hi]: the entry parameter, or 3e38 on a miss

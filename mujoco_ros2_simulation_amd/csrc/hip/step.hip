@@ -3959,14 +3959,16 @@ __device__ __forceinline__ void ell_block_min(const float A[9], const float c[3]
     s_hi *= 2;
   }
   #pragma unroll 1
-  for (int it = 0; it < 60 && s_hi - s_lo > 1e-6f * (1 + s_hi); ++it) {
+  for (int it = 0; it < 60 && s_hi - s_lo > 4e-7f * s_hi; ++it) {
     float sn = s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo);
     if (!(sn > s_lo + 0.01f * (s_hi - s_lo) && sn < s_hi - 0.01f * (s_hi - s_lo))) sn = 0.5f * (s_lo + s_hi);
     const float gp = eval(sn);
-    if (gp == 0) { s_lo = s_hi = sn; break; }
+    if (gp == 0) { s_lo = s_hi = sn; gp_lo = gp_hi = 0; break; }
     if (gp < 0) { s_lo = sn; gp_lo = gp; } else { s_hi = sn; gp_hi = gp; }
   }
-  const float s = 0.5f * (s_lo + s_hi);
+  // the root of the final bracket's secant (the bracket itself stops at a few ulps of s)
+  float s = gp_hi > gp_lo ? s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo) : 0.5f * (s_lo + s_hi);
+  s = fminf(fmaxf(s, s_lo), s_hi);
   const float bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
   qcqp2_la(x, At, bc, mu, s);
   y[0] = s; y[1] = x[0]; y[2] = x[1];
@@ -4992,7 +4994,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     }
     aref[r] = -B * vel - pterm;
     bb[r] = jqs - aref[r];
-    if (primal) continue;
+    if (primal || G == 64) continue;
     // M^-1 J_r'
     gfloat* MJr = MJ + r * nv;
     chol_solve_serial(s + L.L, nv, Jr, MJr);
@@ -5002,6 +5004,22 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     ARii[r] = d + R;
   }
   wsync();
+  if constexpr (G == 64) {
+    // blocked mode (elliptic PGS): L.L holds the per-tree block factor, so M^-1 J_r' is the
+    // wave's lane-per-dof block solve, one row at a time
+    if (!primal) {
+      #pragma unroll 1
+      for (int r = 0; r < nefc; ++r) {
+        const float jr = lane < nv ? J[r * nv + lane] : 0.0f;
+        float y;
+        MRS_CALL(G, y = chol_solve_lanes<G>(mp, s + L.L, jr, lane));
+        if (lane < nv) MJ[r * nv + lane] = y;
+        const float d = gsum<G>(lane < nv ? jr * y : 0.0f);
+        if (lane == 0) ARii[r] = d + Rr[r];
+      }
+      wsync();
+    }
+  }
   SUB_ADD(PH_CON_REC, t_sub);
   t_sub = SUB_T();
   int rmax = 0;

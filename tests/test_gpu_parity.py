@@ -876,6 +876,9 @@ def test_full_size_c4_batch_properties():
         b.set(sim.FIELD_CTRL, ctrl)
         for _ in range(steps // 10):
             b.step(10)
+        # (after mj_step the poses are those of the step's start; forward() brings them to the final
+        # qpos, the state the oracle renders below)
+        b.forward()
         frames = torch.empty((n, H, W), dtype=torch.float32, device="cuda")
         b.render_depth_device(0, 0, n, frames.data_ptr())
         b.sync()
