@@ -1480,8 +1480,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     off = 0;
     L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
     L.xanchor = take(3 * nj); L.xaxis = take(3 * nj); L.gxpos = take(3 * ng); L.gxmat = take(9 * ng);
-    L.scom = take(3 * nb); L.cinert = take(10 * nb); L.crb = take(10 * nb); L.cdof = take(6 * nv);
+    L.scom = take(3 * nb); L.cinert = take(10 * nb); L.crb = d.acc_sens ? take(10 * nb) : 0; L.cdof = take(6 * nv);
     L.cdofdot = take(6 * nv); L.cvel = take(6 * nb); L.cacc = take(6 * nb); L.cfrc = take(6 * nb);
+    // without accelerometer / force / torque sensors (no rne_post), crb shares cacc + cfrc (12 nb):
+    // CRBA's composite inertias are dead before mj_rne starts, and mj_rne's subtree force sums
+    // (6 per body at crb) overwrite only cacc, which is dead once cfrc is built
+    if (!d.acc_sens) L.crb = L.cacc;
     const int msize = blocked ? std::max(1, d.nMblk) : nv * nv;
     L.M = take(msize); L.L = take(msize); L.qpos = take(std::max(1, m.nq)); L.qvel = take(nv);
     L.ctrl = take(std::max(1, m.nu)); L.qfrc_applied = take(nv); L.qacc_ws = take(nv); L.qfrc_bias = take(nv);

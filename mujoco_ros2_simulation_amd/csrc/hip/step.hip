@@ -4132,6 +4132,26 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     }
     return z;
   };
+  // a block's cost change from jar0 to jar0 + a dj within one zone, in factored form (the plain
+  // difference of two nearly equal fp32 costs can come out positive on a descent step, which the
+  // solver's improvement test would take for convergence)
+  auto ell_dcost = [&](int r, int z, float a, const float* dj) {
+    float D[3], d[3];
+    for (int k = 0; k < 3; ++k) { D[k] = 1.0f / Rr[r + k]; d[k] = a * dj[k]; }
+    if (z == PST_QUAD) {
+      float c = 0;
+      for (int k = 0; k < 3; ++k) c += 0.5f * D[k] * d[k] * (2.0f * jar[r + k] + d[k]);
+      return c;
+    }
+    if (z != PST_CONE) return 0.0f;
+    const float ft = ell_friction(m, scr, type, r), mu = ft * rsqrtf(m.impratio);
+    const float U1 = ft * jar[r + 1], U2 = ft * jar[r + 2], dU1 = ft * d[1], dU2 = ft * d[2];
+    const float T0 = sqrtf(U1 * U1 + U2 * U2), T1 = sqrtf((U1 + dU1) * (U1 + dU1) + (U2 + dU2) * (U2 + dU2));
+    const float dT = T0 + T1 > 0 ? (dU1 * (2.0f * U1 + dU1) + dU2 * (2.0f * U2 + dU2)) / (T0 + T1) : 0.0f;
+    const float NT0 = mu * jar[r] - mu * T0, dNT = mu * d[0] - mu * dT;
+    const float Dm = D[0] / (mu * mu * (1 + mu * mu));
+    return 0.5f * Dm * dNT * (2.0f * NT0 + dNT);
+  };
   // M[lane][k]: dense, or per kinematic tree in blocked mode (zero across trees)
   const int mytree = G == 64 && dof ? m.dof_tree[lane] : 0;
   auto mval = [&](int k) {
@@ -4385,9 +4405,9 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
         if (floss[r] == 1.0f) {
           const float dj[3] = {jv[r], jv[r + 1], jv[r + 2]};
           float c0, c1, d1, d2;
-          ell_line(r, 0.0f, nullptr, c0, d1, d2);
+          const int z0 = ell_line(r, 0.0f, nullptr, c0, d1, d2);
           const int z1 = ell_line(r, alpha, dj, c1, d1, d2);
-          dc += c1 - c0;
+          dc += z0 == z1 ? ell_dcost(r, z0, alpha, dj) : c1 - c0;
           changed |= z1 != __float_as_int(st[r]) || z1 == PST_CONE;
           for (int k = 0; k < 3; ++k) jar[r + k] = jar[r + k] + alpha * dj[k];
         }

@@ -1,7 +1,7 @@
 """binned vs per-pixel mesh frames: the differing pixels against the oracle's render (diagnostic)"""
 import os
 import sys
-sys.path[:0] = ["tests", "oracle"]
+sys.path[:0] = [".", "tests", "oracle"]
 import numpy as np
 from mujoco_ros2_simulation_amd import sim
 from test_gpu_mesh import _mesh_robot, _mesh_robot_states
