@@ -5407,6 +5407,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
   constexpr int kMaxSlots = 64 / R;
   unsigned long long mneed = 0;  // bit slot * R + j: ray j is a candidate of the slot-th mesh geom
   unsigned mslot = 0, mover = 0;  // ray-geom indices of the recorded mesh geoms, and of the rest
+  unsigned long long slot_geom = 0;  // ray-geom index of slot s in bits 5 s .. 5 s + 4 (nrgeom <= 32)
   int nms = 0;
   #pragma unroll 1
   while (wmask) {
@@ -5437,6 +5438,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       if (nms < kMaxSlots) {
         mneed |= static_cast<unsigned long long>(cmask) << (nms * R);
         mslot |= 1u << i;
+        slot_geom |= static_cast<unsigned long long>(i) << (5 * nms);
         ++nms;
       } else {
         mover |= 1u << i;
@@ -5467,83 +5469,96 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     }
   }
   if (mslot | mover) {
-    // mesh walks: each round every lane walks its next candidate ray (lowest j) -- a lane's rays lie
-    // `stride` rays apart, so a mesh holds one or two of them -- so the wave runs max-over-lanes
-    // walks per mesh rather than one per ray slot any lane needs.  The ray is rebuilt from the table
-    // (the pass's pnt / vec arrays are dead here, which keeps the walk out of their registers)
+    // mesh walks.  Each round every lane walks its next candidate (mesh slot, ray j) -- lowest bit of
+    // its own record, whichever mesh that is -- so the wave runs max-over-lanes(candidates) walks
+    // rather than one per (mesh, ray slot) any lane needs; geoms past kMaxSlots are walked one at a
+    // time with every ray.  The ray is rebuilt from the table (the pass's pnt / vec arrays are dead
+    // here, which keeps the walk out of their registers)
+    auto ray_of = [&](int k, float p[3], float v[3]) {
+      int rb;
+      if (common_body >= 0) {
+        rb = common_body;
+        float dl[3];
+        if (m.rf_common) {
+          const lfloat* rr = shared_lds(m) + m.shr_rf + 4 * k;
+          dl[0] = rr[0]; dl[1] = rr[1]; dl[2] = rr[2];
+        } else {
+          const CPtr<float> rr = m.rfray + 8 * k;
+          dl[0] = rr[0]; dl[1] = rr[1]; dl[2] = rr[2];
+        }
+        p[0] = common_o[0]; p[1] = common_o[1]; p[2] = common_o[2];
+        if (m.rf_static_frame) {
+          v[0] = dl[0]; v[1] = dl[1]; v[2] = dl[2];
+        } else {
+          float bq[4] = {se[L.xquat + 4 * rb], se[L.xquat + 4 * rb + 1], se[L.xquat + 4 * rb + 2], se[L.xquat + 4 * rb + 3]};
+          float bm[9];
+          quat2mat(bm, bq);
+          mat_vec(v, bm, dl);
+          mat_vec(p, bm, common_o);
+          for (int q = 0; q < 3; ++q) p[q] += se[L.xpos + 3 * rb + q];
+        }
+      } else {
+        const CPtr<float> rr = m.rfray + 8 * k;
+        const float dl[3] = {rr[0], rr[1], rr[2]}, ol[3] = {rr[5], rr[6], rr[7]};
+        rb = __float_as_int(rr[4]);
+        if (m.rf_static_frame) {
+          for (int q = 0; q < 3; ++q) { p[q] = ol[q]; v[q] = dl[q]; }
+        } else {
+          float bq[4] = {se[L.xquat + 4 * rb], se[L.xquat + 4 * rb + 1], se[L.xquat + 4 * rb + 2], se[L.xquat + 4 * rb + 3]};
+          float bm[9];
+          quat2mat(bm, bq);
+          mat_vec(p, bm, ol);
+          for (int q = 0; q < 3; ++q) p[q] += se[L.xpos + 3 * rb + q];
+          mat_vec(v, bm, dl);
+        }
+      }
+      return rb;
+    };
+    // one walk: ray j of this lane against ray geom i (lane-varying), nearest hit into dist[j]
+    auto walk = [&](bool has, int i, int js) {
+      const int k = k0 + js * stride;
+      float p[3], v[3];
+      const int rb = ray_of(k, p, v);
+      const CPtr<float> rec = m.rgeom + 8 * i;
+      const int g = __float_as_int(rec[0]), gb = __float_as_int(rec[2]), id = __float_as_int(rec[7]);
+      float t = -1;
+      if (has && rb != gb) {
+        const float dv[3] = {p[0] - se[L.gxpos + 3 * g], p[1] - se[L.gxpos + 3 * g + 1], p[2] - se[L.gxpos + 3 * g + 2]};
+        float gm[9], lp[3], lv[3];
+        for (int q = 0; q < 9; ++q) gm[q] = se[L.gxmat + 9 * g + q];
+        matT_vec(lp, gm, dv);
+        matT_vec(lv, gm, v);
+        t = ray_mesh(m.mesh_vert + 3 * m.mesh_vertadr[id], m.mesh_face + 3 * m.mesh_faceadr[id], m.mesh_facenum[id],
+                     rec + 4, lp, lv, m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id]);
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (has && j == js && t >= 0 && (dist[j] < 0 || t < dist[j])) dist[j] = t;
+    };
+    unsigned long long need = mneed;
+    #pragma unroll 1
+    while (__any(need != 0)) {
+      const bool has = need != 0;
+      const int bit = has ? __builtin_ctzll(need) : 0;
+      need &= need - 1;
+      const int sl = bit / R;
+      walk(has, static_cast<int>((slot_geom >> (5 * sl)) & 31u), bit - sl * R);
+    }
     unsigned actm = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) actm |= static_cast<unsigned>(act[j]) << j;
-    unsigned todo = mslot | mover;
-    int slot = 0;
+    unsigned over = mover;
     #pragma unroll 1
-    while (todo) {
-      const int i = __builtin_ctz(todo);
-      todo &= todo - 1;
+    while (over) {
+      const int i = __builtin_ctz(over);
+      over &= over - 1;
       unsigned bits = actm;
-      if ((mslot >> i) & 1u) { bits = static_cast<unsigned>(mneed >> (slot * R)) & ((1u << R) - 1u); ++slot; }
-      if (!__any(bits != 0)) continue;
-      const CPtr<float> rec = m.rgeom + 8 * i;
-      const int g = __float_as_int(rec[0]), gb = __float_as_int(rec[2]), id = __float_as_int(rec[7]);
-      const float gp[3] = {se[L.gxpos + 3 * g], se[L.gxpos + 3 * g + 1], se[L.gxpos + 3 * g + 2]};
-      float gm[9];
-      for (int k = 0; k < 9; ++k) gm[k] = se[L.gxmat + 9 * g + k];
       #pragma unroll 1
       while (__any(bits != 0)) {
         const bool has = bits != 0;
         const int js = has ? __builtin_ctz(bits) : 0;
         bits &= bits - 1;
-        const int k = k0 + js * stride;
-        float p[3], v[3];
-        int rb;
-        if (common_body >= 0) {
-          rb = common_body;
-          float dl[3];
-          if (m.rf_common) {
-            const lfloat* rr = shared_lds(m) + m.shr_rf + 4 * k;
-            dl[0] = rr[0]; dl[1] = rr[1]; dl[2] = rr[2];
-          } else {
-            const CPtr<float> rr = m.rfray + 8 * k;
-            dl[0] = rr[0]; dl[1] = rr[1]; dl[2] = rr[2];
-          }
-          p[0] = common_o[0]; p[1] = common_o[1]; p[2] = common_o[2];
-          if (m.rf_static_frame) {
-            v[0] = dl[0]; v[1] = dl[1]; v[2] = dl[2];
-          } else {
-            float bq[4] = {se[L.xquat + 4 * rb], se[L.xquat + 4 * rb + 1], se[L.xquat + 4 * rb + 2], se[L.xquat + 4 * rb + 3]};
-            float bm[9];
-            quat2mat(bm, bq);
-            mat_vec(v, bm, dl);
-            mat_vec(p, bm, common_o);
-            for (int q = 0; q < 3; ++q) p[q] += se[L.xpos + 3 * rb + q];
-          }
-        } else {
-          const CPtr<float> rr = m.rfray + 8 * k;
-          const float dl[3] = {rr[0], rr[1], rr[2]}, ol[3] = {rr[5], rr[6], rr[7]};
-          rb = __float_as_int(rr[4]);
-          if (m.rf_static_frame) {
-            for (int q = 0; q < 3; ++q) { p[q] = ol[q]; v[q] = dl[q]; }
-          } else {
-            float bq[4] = {se[L.xquat + 4 * rb], se[L.xquat + 4 * rb + 1], se[L.xquat + 4 * rb + 2], se[L.xquat + 4 * rb + 3]};
-            float bm[9];
-            quat2mat(bm, bq);
-            mat_vec(p, bm, ol);
-            for (int q = 0; q < 3; ++q) p[q] += se[L.xpos + 3 * rb + q];
-            mat_vec(v, bm, dl);
-          }
-        }
-        float t = -1;
-        if (has && rb != gb) {
-          const float dv[3] = {p[0] - gp[0], p[1] - gp[1], p[2] - gp[2]};
-          float lp[3], lv[3];
-          matT_vec(lp, gm, dv);
-          matT_vec(lv, gm, v);
-          t = ray_mesh(m.mesh_vert + 3 * m.mesh_vertadr[id], m.mesh_face + 3 * m.mesh_faceadr[id], m.mesh_facenum[id],
-                       rec + 4, lp, lv, m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id]);
-        }
-#pragma unroll
-        for (int j = 0; j < R; ++j)
-          if (has && j == js && t >= 0 && (dist[j] < 0 || t < dist[j])) dist[j] = t;
+        walk(has, i, js);
       }
     }
   }

@@ -300,3 +300,44 @@ def test_binned_frames_match_per_pixel_kernel(resolution, monkeypatch):
     print(f"{resolution}: colour equal on {same.mean():.6f} of pixels")
     assert same.mean() >= 0.9995
     assert np.sum(db < db.max()) > 1000  # the meshes are in view
+
+
+# ---------------------------------------------------------------- MPR pairs, re-seeded per step
+MPR_SCENE = f"""<mujoco><option timestep="0.002" solver="PGS" iterations="50"/>
+  <asset><mesh name="rock" vertex="{_rock(40, 7)}" scale="3 3 3"/></asset>
+  <worldbody><geom type="plane" size="0 0 1"/>
+    <geom name="rock" type="mesh" mesh="rock" pos="0 0 0.12" euler="10 20 30"/>
+    <body name="e1" pos="0.02 0.01 0.36"><freejoint/><geom type="ellipsoid" size="0.06 0.05 0.04"/></body>
+    <body name="e2" pos="-0.05 0.08 0.48"><freejoint/><geom type="ellipsoid" size="0.05 0.04 0.05"/></body>
+    <body name="s1" pos="0.1 -0.06 0.42"><freejoint/><geom type="sphere" size="0.04"/></body>
+    <body name="c1" pos="-0.12 -0.08 0.40"><freejoint/><geom type="capsule" size="0.03 0.04"/></body>
+  </worldbody></mujoco>"""
+
+
+def test_reseeded_mpr_pairs():
+    """one step at a time from the oracle's state (test_gpu_solvers._reseeded): bodies with curved
+    surfaces (ellipsoids, a sphere, a capsule) tumbling over a static mesh rock and each other, so the
+    contacts are MPR pairs (ellipsoid-mesh, sphere-mesh, capsule-mesh, ellipsoid-ellipsoid) -- qpos /
+    qvel within 1e-5 of scale per step (north_star), contact-count flips explained as threshold cases.
+    Curved-on-flat and curved-on-curved pairs have one contact point, to which MPR converges within
+    its 1e-6 tolerance on both sides; flat-on-flat pairs (a box face on a mesh face) do not -- MPR may
+    stop on either of two neighbouring portals of the face, which moves the single contact along it
+    (test_mesh_convex_contact_lists bounds those at 2e-3)"""
+    from test_gpu_solvers import _reseeded
+    model = sim.Model.from_string(MPR_SCENE)
+    settle, steps = 75, 100
+    d = binding.OracleData(model)
+    d.qpos[:] = synth.initial_qpos(model, np.arange(1))[0]
+    kinds = set()
+    for t in range(settle + steps):
+        d.step()
+        if t >= settle:
+            kinds |= {tuple(int(model.geom_type[x]) for x in p) for p in d.contacts()[0]}
+    assert {(4, 7), (2, 7)} <= kinds, kinds  # ellipsoid-mesh and sphere-mesh MPR pairs occur
+    wq, wv, ncon, flips, unexplained = _reseeded(model, 16, steps, settle=settle)
+    print(f"MPR scene: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts {ncon.mean():.2f}; "
+          f"flips {flips}; pair kinds {sorted(kinds)}")
+    assert ncon.max() > 0
+    assert flips <= max(1, 0.01 * 16 * steps)
+    assert not unexplained, unexplained[:5]
+    assert wq <= 1e-5 and wv <= 1e-5
