@@ -17,11 +17,14 @@ RTOL = 1e-5
 SCENES = ARM7.parent
 
 
-def elliptic_scene(name: str, solver: str, impratio: float = 1.0) -> "sim.Model":
+def elliptic_scene(name: str, solver: str, impratio: float = 1.0, tol: str = "") -> "sim.Model":
     path = SCENES / f"{name}.xml"
     # (CG at tolerance 1e-12, as test_gpu_solvers.test_primal_solver_mobile_base: at the default 1e-8
     # MuJoCo's CG stops short of the optimum, at an iterate fp32 arithmetic cannot reproduce)
     it = {"PGS": '50', "Newton": '100', "CG": '200" tolerance="1e-12'}[solver]
+    if tol:
+        it += f'" tolerance="{tol}'
+
     xml = path.read_text().replace('solver="PGS" iterations="50"',
                                    f'solver="{solver}" iterations="{it}" cone="elliptic" impratio="{impratio}"')
     m = sim.Model.from_string(xml, str(path.parent))
@@ -29,13 +32,17 @@ def elliptic_scene(name: str, solver: str, impratio: float = 1.0) -> "sim.Model"
     return m
 
 
-@pytest.mark.parametrize("scene, solver, imp, n", [("arm_boxes", "PGS", 1.0, 16), ("arm_boxes", "Newton", 3.0, 8),
-                                                   ("arm_boxes", "CG", 1.0, 8), ("mobile_base", "PGS", 1.0, 32),
-                                                   ("mobile_base", "Newton", 10.0, 32)])
-def test_reseeded_elliptic(scene, solver, imp, n):
+@pytest.mark.parametrize("scene, solver, imp, n, tol", [("arm_boxes", "PGS", 1.0, 16, ""), ("arm_boxes", "Newton", 3.0, 8, ""),
+                                                        ("arm_boxes", "CG", 1.0, 8, ""), ("mobile_base", "PGS", 1.0, 32, "0"),
+                                                        ("mobile_base", "Newton", 10.0, 32, "")])
+def test_reseeded_elliptic(scene, solver, imp, n, tol):
     """contact scenes under cone="elliptic" (blocked mode for the arm + boxes, 16-lane groups for the
-    mobile base), every step from the oracle's state, qpos / qvel within 1e-5 of scale"""
-    model = elliptic_scene(scene, solver, imp)
+    mobile base), every step from the oracle's state, qpos / qvel within 1e-5 of scale.  The mobile
+    base's PGS converges within its 50 sweeps, so MuJoCo's improvement test (1e-8) ends it, and fp32 /
+    fp64 can cross that threshold one sweep apart (measured 1.5e-5 in qvel at the default tolerance):
+    tolerance 0 runs all 50 sweeps on both sides, separating the arithmetic from the stop rule (as
+    test_gpu_solvers.test_reseeded_step_parity does for C5)"""
+    model = elliptic_scene(scene, solver, imp, tol)
     wq, wv, ncon, flips, unexplained = _reseeded(model, n, 40)
     print(f"{scene} elliptic {solver} impratio {imp}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; "
           f"contacts per env {ncon.mean():.1f}; flips {flips}")
