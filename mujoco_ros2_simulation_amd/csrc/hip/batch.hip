@@ -890,12 +890,62 @@ void build_mesh_bvh(const Model& m, std::vector<int>& face_out, std::vector<floa
       if (e - b <= 4) {
         nodes[8 * me + 7] = fbits((b << 8) | (e - b));
       } else {
-        int ax = 0;
-        for (int c = 1; c < 3; ++c)
-          if (chi[c] - clo[c] > chi[ax] - clo[ax]) ax = c;
-        const int mid = (b + e) / 2;
-        std::nth_element(tris.begin() + b, tris.begin() + mid, tris.begin() + e,
-                         [ax](const Tri& x, const Tri& y) { return x.c[ax] < y.c[ax]; });
+        // binned surface-area heuristic (16 centroid bins per axis): the split minimising
+        // N_left A_left + N_right A_right, i.e. the expected triangle tests of a ray that enters the
+        // node; the median of the longest axis when no bin boundary separates the centroids
+        constexpr int kBins = 16;
+        auto area = [](const double* l, const double* h) {
+          const double dx = h[0] - l[0], dy = h[1] - l[1], dz = h[2] - l[2];
+          return dx * dy + dy * dz + dz * dx;
+        };
+        int best_ax = -1, best_s = 0;
+        double best_cost = 1e300;
+        for (int ax = 0; ax < 3; ++ax) {
+          const double ext = chi[ax] - clo[ax];
+          if (ext <= 1e-12) continue;
+          int cnt[kBins] = {};
+          double blo[kBins][3], bhi[kBins][3];
+          for (int q = 0; q < kBins; ++q)
+            for (int c = 0; c < 3; ++c) { blo[q][c] = 1e300; bhi[q][c] = -1e300; }
+          for (int i = b; i < e; ++i) {
+            const int q = std::min(kBins - 1, static_cast<int>((tris[i].c[ax] - clo[ax]) / ext * kBins));
+            ++cnt[q];
+            for (int c = 0; c < 3; ++c) { blo[q][c] = std::min(blo[q][c], tris[i].lo[c]); bhi[q][c] = std::max(bhi[q][c], tris[i].hi[c]); }
+          }
+          double rl[kBins][3], rh[kBins][3];
+          int rn[kBins];
+          for (int c = 0; c < 3; ++c) { rl[kBins - 1][c] = blo[kBins - 1][c]; rh[kBins - 1][c] = bhi[kBins - 1][c]; }
+          rn[kBins - 1] = cnt[kBins - 1];
+          for (int q = kBins - 2; q >= 0; --q) {
+            rn[q] = rn[q + 1] + cnt[q];
+            for (int c = 0; c < 3; ++c) { rl[q][c] = std::min(rl[q + 1][c], blo[q][c]); rh[q][c] = std::max(rh[q + 1][c], bhi[q][c]); }
+          }
+          double ll[3] = {1e300, 1e300, 1e300}, lh[3] = {-1e300, -1e300, -1e300};
+          int ln = 0;
+          for (int q = 1; q < kBins; ++q) {
+            ln += cnt[q - 1];
+            for (int c = 0; c < 3; ++c) { ll[c] = std::min(ll[c], blo[q - 1][c]); lh[c] = std::max(lh[c], bhi[q - 1][c]); }
+            if (ln == 0 || rn[q] == 0) continue;
+            const double cost = ln * area(ll, lh) + rn[q] * area(rl[q], rh[q]);
+            if (cost < best_cost) { best_cost = cost; best_ax = ax; best_s = q; }
+          }
+        }
+        int mid = (b + e) / 2;
+        if (best_ax >= 0 && !std::getenv("MRS_BVH_MEDIAN")) {
+          const double ext = chi[best_ax] - clo[best_ax];
+          const int ax = best_ax, sp = best_s;
+          const double lo0 = clo[ax];
+          auto it = std::partition(tris.begin() + b, tris.begin() + e, [&](const Tri& t) {
+            return std::min(kBins - 1, static_cast<int>((t.c[ax] - lo0) / ext * kBins)) < sp;
+          });
+          mid = static_cast<int>(it - tris.begin());
+        } else {
+          int ax = 0;
+          for (int c = 1; c < 3; ++c)
+            if (chi[c] - clo[c] > chi[ax] - clo[ax]) ax = c;
+          std::nth_element(tris.begin() + b, tris.begin() + mid, tris.begin() + e,
+                           [ax](const Tri& x, const Tri& y) { return x.c[ax] < y.c[ax]; });
+        }
         build(b, mid);
         build(mid, e);
       }
