@@ -45,6 +45,7 @@ struct MeshRef {
   const int *face, *dataid, *vertadr, *faceadr, *facenum;
   const float* bvh;           // bounding volume hierarchies (8 floats per node, build_mesh_bvh)
   const int *bvhadr, *bvhnum;  // per mesh: first node, node count (0: no hierarchy, every triangle)
+  const float* tri;            // pre-gathered triangle records (DevModel::mesh_tri)
 };
 
 // analytic ray primitive (same restatement of engine_ray as the step kernel's rangefinder)
@@ -274,8 +275,8 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
     if (t == MRS_GEOM_MESH) {
       const int id = mesh.dataid[g];
       int tri;
-      tt = ray_mesh(mesh.vert + 3 * mesh.vertadr[id], mesh.face + 3 * mesh.faceadr[id], mesh.facenum[id],
-                         geom_size + 3 * g, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id], &tri);
+      tt = ray_mesh(mesh.tri + 9 * mesh.faceadr[id], mesh.facenum[id], geom_size + 3 * g, lp, lv,
+                    mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id], &tri);
     } else {
       tt = ray_prim(t, geom_size + 3 * g, lp, lv);
     }
@@ -303,8 +304,8 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
         lv[i] = mm[i] * vec[0] + mm[3 + i] * vec[1] + mm[6 + i] * vec[2];
       }
       int tri = 0;
-      ray_mesh(mv, mf, mesh.facenum[id], geom_size + 3 * bestg, lp, lv, mesh.bvh + 8 * mesh.bvhadr[id],
-                    mesh.bvhnum[id], &tri);
+      ray_mesh(mesh.tri + 9 * mesh.faceadr[id], mesh.facenum[id], geom_size + 3 * bestg, lp, lv,
+               mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id], &tri);
       mesh_tri_normal(mv, mf, tri, lv, nl);
     } else {
       local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
@@ -472,9 +473,8 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         else if (type == MRS_GEOM_MESH)
         {
           int tri;
-          t = ray_mesh(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid],
-                       mesh.facenum[o.dataid], sz, lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
-                       mesh.bvhnum[o.dataid], &tri);
+          t = ray_mesh(mesh.tri + 9 * mesh.faceadr[o.dataid], mesh.facenum[o.dataid], sz, lp, lv,
+                       mesh.bvh + 8 * mesh.bvhadr[o.dataid], mesh.bvhnum[o.dataid], &tri);
         }
         else t = ray_prim(type, sz, lp, lv);
         if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
@@ -504,8 +504,8 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
             float lv[3];
         pixel_ray(o.A, dx, dy[k], lv);
             int tri = 0;
-            ray_mesh(mv, mf, mesh.facenum[o.dataid], o.size, o.lp, lv, mesh.bvh + 8 * mesh.bvhadr[o.dataid],
-                          mesh.bvhnum[o.dataid], &tri);
+            ray_mesh(mesh.tri + 9 * mesh.faceadr[o.dataid], mesh.facenum[o.dataid], o.size, o.lp, lv,
+                     mesh.bvh + 8 * mesh.bvhadr[o.dataid], mesh.bvhnum[o.dataid], &tri);
             mesh_tri_normal(mv, mf, tri, lv, nl);
           } else {
             local_normal(o.type, o.size, q, nl);
@@ -541,29 +541,16 @@ constexpr int kRasterFaceBits = 18;  // triangle index bits in a record (mesh ge
 // expressions in the same order, so t is bit-identical
 __device__ __forceinline__ float ray_tri_v(const float a[3], const float e1[3], const float e2[3], const float lp[3],
                                            const float lv[3]) {
-#pragma clang fp contract(off)
-  const float pv[3] = {lv[1] * e2[2] - lv[2] * e2[1], lv[2] * e2[0] - lv[0] * e2[2], lv[0] * e2[1] - lv[1] * e2[0]};
-  const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
-  if (fabsf(det) < 1e-15f) return -1;
-  const float inv = 1.0f / det;
-  const float tv[3] = {lp[0] - a[0], lp[1] - a[1], lp[2] - a[2]};
-  const float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
-  if (u < 0 || u > 1) return -1;
-  const float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
-  const float v = (lv[0] * qv[0] + lv[1] * qv[1] + lv[2] * qv[2]) * inv;
-  if (v < 0 || u + v > 1) return -1;
-  const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
-  return t >= 0 ? t : -1;
+  return mt_core(a, e1, e2, lp, lv);
 }
 
 struct TriLoad { float a[3], e1[3], e2[3]; };
-__device__ __forceinline__ TriLoad load_tri(const float* mv, const int* mf, int f) {
-  const int ia = 3 * mf[3 * f], ib = 3 * mf[3 * f + 1], ic = 3 * mf[3 * f + 2];
+__device__ __forceinline__ TriLoad load_tri(const float* rec, int f) {
   TriLoad o;
   for (int i = 0; i < 3; ++i) {
-    o.a[i] = mv[ia + i];
-    o.e1[i] = mv[ib + i] - o.a[i];
-    o.e2[i] = mv[ic + i] - o.a[i];
+    o.a[i] = rec[9 * f + i];
+    o.e1[i] = rec[9 * f + 3 + i];
+    o.e2[i] = rec[9 * f + 6 + i];
   }
   return o;
 }
@@ -686,7 +673,7 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
       const int kf = static_cast<int>(rec & 0xffffff), k = kf >> kRasterFaceBits, fi = kf & ((1 << kRasterFaceBits) - 1);
       const int g = mg[k];
       const DepthGeom& o = G[g];
-      const TriLoad tr = load_tri(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid], fi);
+      const TriLoad tr = load_tri(mesh.tri + 9 * mesh.faceadr[o.dataid], fi);
       const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]};
       float A[9];
       for (int i = 0; i < 9; ++i) A[i] = o.A[i];
@@ -1173,6 +1160,24 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.mesh_hulladr, m.mesh_hulladr); P.addi(&d.mesh_hullnum, m.mesh_hullnum); P.addi(&d.mesh_face, bvh_face);
   P.addi(&d.mesh_bvhadr, bvh_adr); P.addi(&d.mesh_bvhnum, bvh_num); P.addf(&d.mesh_bvh, bvh_node);
   P.addi(&d.mesh_hull, m.mesh_hull); P.addf(&d.mesh_vert, m.mesh_vert);
+  {
+    // pre-gathered triangle records in device face order: vertex a, b - a, c - a, formed in fp32 from
+    // the fp32 vertices exactly as ray_tri forms them on the device (bit-identical t)
+    std::vector<float> tri(9 * bvh_face.size() / 3);
+    const int nmesh = static_cast<int>(m.mesh_faceadr.size());
+    for (int k = 0; k < nmesh; ++k)
+      for (int f = m.mesh_faceadr[k]; f < m.mesh_faceadr[k] + m.mesh_facenum[k]; ++f) {
+        float v[3][3];
+        for (int c = 0; c < 3; ++c)
+          for (int i = 0; i < 3; ++i) v[c][i] = static_cast<float>(m.mesh_vert[3 * (m.mesh_vertadr[k] + bvh_face[3 * f + c]) + i]);
+        for (int i = 0; i < 3; ++i) {
+          tri[9 * f + i] = v[0][i];
+          tri[9 * f + 3 + i] = v[1][i] - v[0][i];
+          tri[9 * f + 6 + i] = v[2][i] - v[0][i];
+        }
+      }
+    P.addf(&d.mesh_tri, tri);
+  }
   {
     // mesh geoms a camera can see (groups 0-2, alpha > 0), for the binning frame kernel; limits of its
     // records: 64 geom slots, 2^18 triangles per mesh, pairs within an int
@@ -1905,7 +1910,7 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
   const float znear = static_cast<float>(m.vis_znear * m.stat_extent), zfar = static_cast<float>(m.vis_zfar * m.stat_extent);
   const DevModel& d = b->dm;
   const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p,
-                     d.mesh_facenum.p, d.mesh_bvh.p, d.mesh_bvhadr.p, d.mesh_bvhnum.p};
+                     d.mesh_facenum.p, d.mesh_bvh.p, d.mesh_bvhadr.p, d.mesh_bvhnum.p, d.mesh_tri.p};
   const bool raster = d.nrast > 0 && W <= 2048 && H <= kBandH * kMaxBands && !std::getenv("MRS_DEPTH_V2") &&
                      !std::getenv("MRS_DEPTH_V1");
   if (raster && b->rast_frames < n) {

@@ -142,6 +142,9 @@ struct DevModel {
   // first node and the node count (0: none), 8 floats per node
   CPtr<int> mesh_bvhadr, mesh_bvhnum;
   CPtr<float> mesh_bvh;
+  // the triangles pre-gathered in device face order (same index as mesh_face): vertex a and the edges
+  // b - a, c - a in fp32, 9 floats each -- one load per triangle instead of face -> vertex chains
+  CPtr<float> mesh_tri;
   // candidate collision pairs (static filters applied; g1 has the smaller geom type)
   CPtr<int> pair_g1, pair_g2, pair_dim;
   CPtr<float> pair_margin, pair_gap, pair_friction /*3*/, pair_solref /*2*/, pair_solimp /*5*/;

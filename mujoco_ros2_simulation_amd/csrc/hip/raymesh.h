@@ -2,42 +2,59 @@
 // (batch.hip).  mj_rayMesh restated (oracle.c ray_mesh): the ray in the geom frame (origin lp,
 // direction lv) is first tested against the geom's bounding box (half extents s, slab test), then
 // against the triangles, both faces (Moller-Trumbore) -- the ones the mesh's bounding volume
-// hierarchy does not rule out.  `vert` / `face` point at the mesh's own vertices and triangles (face
-// ids relative to vert).  Returns the nearest t >= 0, or -1; *tri gets the nearest triangle when tri
-// is not null.
+// hierarchy does not rule out.  `trirec` points at the mesh's first pre-gathered triangle record
+// (DevModel::mesh_tri, 9 floats per triangle in device face order).  Returns the nearest t >= 0, or
+// -1; *tri gets the nearest triangle when tri is not null.
 #pragma once
+
+// Moller-Trumbore core with explicit fmaf chains: the result does not depend on how the compiler
+// contracts the surrounding code (the backend fuses multiply-adds freely), so every call site -- the
+// every-triangle loop, the hierarchy walk, the binned frame kernel -- gets the same t bit for bit
+__device__ __forceinline__ float mt_core(const float a[3], const float e1[3], const float e2[3], const float lp[3],
+                                         const float lv[3]) {
+  const float pv[3] = {fmaf(lv[1], e2[2], -(lv[2] * e2[1])), fmaf(lv[2], e2[0], -(lv[0] * e2[2])),
+                       fmaf(lv[0], e2[1], -(lv[1] * e2[0]))};
+  const float det = fmaf(e1[0], pv[0], fmaf(e1[1], pv[1], e1[2] * pv[2]));
+  if (fabsf(det) < 1e-15f) return -1;
+  const float inv = 1.0f / det;
+  const float tv[3] = {lp[0] - a[0], lp[1] - a[1], lp[2] - a[2]};
+  const float u = fmaf(tv[0], pv[0], fmaf(tv[1], pv[1], tv[2] * pv[2])) * inv;
+  if (u < 0 || u > 1) return -1;
+  const float qv[3] = {fmaf(tv[1], e1[2], -(tv[2] * e1[1])), fmaf(tv[2], e1[0], -(tv[0] * e1[2])),
+                       fmaf(tv[0], e1[1], -(tv[1] * e1[0]))};
+  const float v = fmaf(lv[0], qv[0], fmaf(lv[1], qv[1], lv[2] * qv[2])) * inv;
+  if (v < 0 || u + v > 1) return -1;
+  const float t = fmaf(e2[0], qv[0], fmaf(e2[1], qv[1], e2[2] * qv[2])) * inv;
+  return t >= 0 ? t : -1;
+}
 
 // one triangle, both faces (Moller-Trumbore); t >= 0 of the hit or -1
 template <class PV, class PF>
 __device__ __forceinline__ float ray_tri(PV vert, PF face, int f, const float lp[3], const float lv[3]) {
-  // (no FMA contraction here nor in pixel_ray: the binned frame kernel (batch.hip ray_tri_v) and
-  // the per-pixel kernels then give bit-identical t whatever the compiler fuses around them)
-#pragma clang fp contract(off)
   const int ia = 3 * face[3 * f], ib = 3 * face[3 * f + 1], ic = 3 * face[3 * f + 2];
   const float a[3] = {vert[ia], vert[ia + 1], vert[ia + 2]};
   const float e1[3] = {vert[ib] - a[0], vert[ib + 1] - a[1], vert[ib + 2] - a[2]};
   const float e2[3] = {vert[ic] - a[0], vert[ic + 1] - a[1], vert[ic + 2] - a[2]};
-  const float pv[3] = {lv[1] * e2[2] - lv[2] * e2[1], lv[2] * e2[0] - lv[0] * e2[2], lv[0] * e2[1] - lv[1] * e2[0]};
-  const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
-  if (fabsf(det) < 1e-15f) return -1;
-  const float inv = 1.0f / det;
-  const float tv[3] = {lp[0] - a[0], lp[1] - a[1], lp[2] - a[2]};
-  const float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
-  if (u < 0 || u > 1) return -1;
-  const float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
-  const float v = (lv[0] * qv[0] + lv[1] * qv[1] + lv[2] * qv[2]) * inv;
-  if (v < 0 || u + v > 1) return -1;
-  const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
-  return t >= 0 ? t : -1;
+  return mt_core(a, e1, e2, lp, lv);
 }
 
 // a pixel ray (camera-frame slopes dx, dy; direction (dx, dy, -1)) in a geom frame: rows of A
 template <class PA>
 __device__ __forceinline__ void pixel_ray(const PA A, float dx, float dy, float lv[3]) {
-#pragma clang fp contract(off)
-  lv[0] = A[0] * dx + A[1] * dy - A[2];
-  lv[1] = A[3] * dx + A[4] * dy - A[5];
-  lv[2] = A[6] * dx + A[7] * dy - A[8];
+  lv[0] = fmaf(A[0], dx, fmaf(A[1], dy, -A[2]));
+  lv[1] = fmaf(A[3], dx, fmaf(A[4], dy, -A[5]));
+  lv[2] = fmaf(A[6], dx, fmaf(A[7], dy, -A[8]));
+}
+
+// one pre-gathered triangle record (vertex a, edges e1 = b - a, e2 = c - a: DevModel::mesh_tri), both
+// faces; the expressions of ray_tri in the same order, so t is bit-identical to it
+template <class PT>
+__device__ __forceinline__ float ray_tri_rec(PT tri, int f, const float lp[3], const float lv[3]) {
+  const int o = 9 * f;
+  const float a[3] = {tri[o], tri[o + 1], tri[o + 2]};
+  const float e1[3] = {tri[o + 3], tri[o + 4], tri[o + 5]};
+  const float e2[3] = {tri[o + 6], tri[o + 7], tri[o + 8]};
+  return mt_core(a, e1, e2, lp, lv);
 }
 
 // slab test of the ray against an axis-aligned box [lo, hi]: the entry parameter, or 3e38 on a miss
@@ -68,8 +85,8 @@ __device__ __forceinline__ float ray_aabb(const float lo[3], const float hi[3], 
 // (A wave-coherent packet walk -- node index by ballot, scalar loads -- measured slower at both call
 // sites on the mesh robot: step 26.7 vs 12.8 ms, depth 501 vs 442 ms: the union of 64 rays' paths
 // visits far more nodes than one ray's.)
-template <class PV, class PF, class PS, class PN>
-__device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS s, const float lp[3],
+template <class PT, class PS, class PN>
+__device__ __forceinline__ float ray_mesh(PT trirec, int nface, const PS s, const float lp[3],
                                           const float lv[3], PN bvh, int nnode, int* tri = nullptr) {
   {
     const float lo[3] = {-s[0], -s[1], -s[2]}, hi[3] = {s[0], s[1], s[2]};
@@ -79,7 +96,7 @@ __device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS 
   float best = -1;
   if (nnode <= 0) {
     for (int f = 0; f < nface; ++f) {
-      const float t = ray_tri(vert, face, f, lp, lv);
+      const float t = ray_tri_rec(trirec, f, lp, lv);
       if (t >= 0 && (best < 0 || t < best)) { best = t; if (tri) *tri = f; }
     }
     return best;
@@ -103,7 +120,7 @@ __device__ __forceinline__ float ray_mesh(PV vert, PF face, int nface, const PS 
     if (hit && cur.leaf >= 0) {
       const int f0 = cur.leaf >> 8, nf = cur.leaf & 0xff;
       for (int f = f0; f < f0 + nf; ++f) {
-        const float t = ray_tri(vert, face, f, lp, lv);
+        const float t = ray_tri_rec(trirec, f, lp, lv);
         if (t >= 0 && (best < 0 || t < best)) { best = t; if (tri) *tri = f; }
       }
     }

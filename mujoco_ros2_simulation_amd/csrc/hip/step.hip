@@ -5528,8 +5528,8 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
         for (int q = 0; q < 9; ++q) gm[q] = se[L.gxmat + 9 * g + q];
         matT_vec(lp, gm, dv);
         matT_vec(lv, gm, v);
-        t = ray_mesh(m.mesh_vert + 3 * m.mesh_vertadr[id], m.mesh_face + 3 * m.mesh_faceadr[id], m.mesh_facenum[id],
-                     rec + 4, lp, lv, m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id]);
+        t = ray_mesh(m.mesh_tri + 9 * m.mesh_faceadr[id], m.mesh_facenum[id], rec + 4, lp, lv,
+                     m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id]);
       }
 #pragma unroll
       for (int j = 0; j < R; ++j)
