@@ -85,15 +85,20 @@ __device__ __forceinline__ float ray_aabb(const float lo[3], const float hi[3], 
 // (A wave-coherent packet walk -- node index by ballot, scalar loads -- measured slower at both call
 // sites on the mesh robot: step 26.7 vs 12.8 ms, depth 501 vs 442 ms: the union of 64 rays' paths
 // visits far more nodes than one ray's.)
+// bound >= 0: a hit already known along the ray (the caller's nearest so far); only nearer triangles
+// count, boxes entered beyond it are skipped (a ray through a closed shell whose inside hit is known
+// never walks the far side), and the result is bound itself when nothing nearer is found
 template <class PT, class PS, class PN>
 __device__ __forceinline__ float ray_mesh(PT trirec, int nface, const PS s, const float lp[3],
-                                          const float lv[3], PN bvh, int nnode, int* tri = nullptr) {
+                                          const float lv[3], PN bvh, int nnode, int* tri = nullptr,
+                                          float bound = -1.0f) {
   {
     const float lo[3] = {-s[0], -s[1], -s[2]}, hi[3] = {s[0], s[1], s[2]};
     const float iv[3] = {1.0f / lv[0], 1.0f / lv[1], 1.0f / lv[2]};
-    if (ray_aabb(lo, hi, lp, lv, iv) == 3.0e38f) return -1;
+    const float te = ray_aabb(lo, hi, lp, lv, iv);
+    if (te == 3.0e38f || (bound >= 0 && te > bound)) return -1;
   }
-  float best = -1;
+  float best = bound;
   if (nnode <= 0) {
     for (int f = 0; f < nface; ++f) {
       const float t = ray_tri_rec(trirec, f, lp, lv);

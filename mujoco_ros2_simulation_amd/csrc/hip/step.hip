@@ -5514,26 +5514,43 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       }
       return rb;
     };
-    // one walk: ray j of this lane against ray geom i (lane-varying), nearest hit into dist[j]
+    // the pass's results go to their output slots first (sensordata, or the static-hit table in the
+    // producer pass); each walk then reads its ray's nearest hit so far from there as the walk's
+    // bound and writes a nearer hit back -- the R results leave the registers for the walks
+    auto out_of = [&](int k) -> gfloat* {
+      if (m.rf_mode == 1) return (gfloat*)(m.rf_static + k);
+      const int a = m.rf_common ? __float_as_int(shared_lds(m)[m.shr_rf + 4 * k + 3]) : __float_as_int(m.rfray[8 * k + 3]);
+      return sd + a;
+    };
+    const bool sd_ok = m.rf_mode == 1 || MRS_SD_OK(sd);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (m.rf_mode == 1) {
+        if (act[j]) m.rf_static[k0 + j * stride] = dist[j];
+      } else if (act[j] && sd_ok) {
+        sd[adr[j]] = dist[j];
+      }
+    }
+    // one walk: ray js of this lane against ray geom i (lane-varying)
     auto walk = [&](bool has, int i, int js) {
       const int k = k0 + js * stride;
       float p[3], v[3];
       const int rb = ray_of(k, p, v);
       const CPtr<float> rec = m.rgeom + 8 * i;
       const int g = __float_as_int(rec[0]), gb = __float_as_int(rec[2]), id = __float_as_int(rec[7]);
-      float t = -1;
-      if (has && rb != gb) {
+      if (has && rb != gb && sd_ok) {
+        gfloat* o = out_of(k);
+        const float dcur = *o;
         const float dv[3] = {p[0] - se[L.gxpos + 3 * g], p[1] - se[L.gxpos + 3 * g + 1], p[2] - se[L.gxpos + 3 * g + 2]};
         float gm[9], lp[3], lv[3];
         for (int q = 0; q < 9; ++q) gm[q] = se[L.gxmat + 9 * g + q];
         matT_vec(lp, gm, dv);
         matT_vec(lv, gm, v);
-        t = ray_mesh(m.mesh_tri + 9 * m.mesh_faceadr[id], m.mesh_facenum[id], rec + 4, lp, lv,
-                     m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id]);
+        const float t = ray_mesh(m.mesh_tri + 9 * m.mesh_faceadr[id], m.mesh_facenum[id], rec + 4, lp, lv,
+                                 m.mesh_bvh + 8 * m.mesh_bvhadr[id], m.mesh_bvhnum[id], nullptr, dcur);
+        // (t is dcur itself when the walk found nothing nearer)
+        if (t >= 0 && (dcur < 0 || t < dcur)) *o = t;
       }
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-        if (has && j == js && t >= 0 && (dist[j] < 0 || t < dist[j])) dist[j] = t;
     };
     unsigned long long need = mneed;
     #pragma unroll 1
@@ -5561,6 +5578,8 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
         walk(has, i, js);
       }
     }
+    SUB_ADD(PH_SENS_GEOMS, t_geoms);
+    return;
   }
 #pragma unroll
   for (int j = 0; j < R; ++j) {
