@@ -7,7 +7,7 @@ from mujoco_ros2_simulation_amd import sim
 from test_gpu_mesh import _mesh_robot, _mesh_robot_states
 import binding
 
-model = _mesh_robot((640, 480))
+model = _mesh_robot("640 480")
 q = _mesh_robot_states(model, n=8)
 out = {}
 for key in ("bin", "v2"):
