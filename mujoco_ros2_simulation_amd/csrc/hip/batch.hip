@@ -1088,7 +1088,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     d.pipe_w = 8;
     while (d.pipe_w < widest) d.pipe_w *= 2;
   }
-  d.sparse_off = std::getenv("MRS_SPARSE_OFF") ? std::atoi(std::getenv("MRS_SPARSE_OFF")) & 7 : 0;
+  d.sparse_off = std::getenv("MRS_SPARSE_OFF") ? std::atoi(std::getenv("MRS_SPARSE_OFF")) & 15 : 0;
   std::vector<int> fric, lim, rf;
   for (int j = 0; j < m.nv; ++j) if (m.dof_frictionloss[j] > 0) fric.push_back(j);
   for (int j = 0; j < m.njnt; ++j)
