@@ -213,12 +213,14 @@ def test_reseeded_step_parity(scene, solver, n, steps, tol):
     assert wq <= RTOL and wv <= RTOL
 
 
-@pytest.mark.parametrize("off", [1, 3, 7], ids=["item-blocked", "register", "global-records"])
+@pytest.mark.parametrize("off", [1, 3, 7, 8], ids=["item-blocked", "register", "global-records", "substitution"])
 def test_reseeded_sparse_solver_paths(off, monkeypatch):
     """C5 through each of the blocked-mode PGS paths the island-dual solve falls back to (models
     whose islands outgrow a 16-slot pipe, or with more rows per pipe than the register paths hold):
     MRS_SPARSE_OFF switches the earlier paths off.  All of them run on records holding only
-    Y = L^-1 J' (qacc tracked as w = L' qacc); every step from the oracle's state within 1e-5."""
+    Y = L^-1 J' (qacc tracked as w = L' qacc); every step from the oracle's state within 1e-5.
+    Bit 8 builds the records by forward substitution instead of the per-tree inverse factors (the
+    path of trees over 8 dofs)."""
     monkeypatch.setenv("MRS_SPARSE_OFF", str(off))
     model = with_solver(SCENES / "arm_boxes.xml", "PGS", 50)
     wq, wv, ncon, flips, unexplained = _reseeded(model, 64, 60)
