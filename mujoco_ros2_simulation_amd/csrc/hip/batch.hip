@@ -860,6 +860,7 @@ void build_mesh_bvh(const Model& m, std::vector<int>& face_out, std::vector<floa
       }
     }
     const double pad = 1e-5 * std::max(1e-9, std::max(mhi[0] - mlo[0], std::max(mhi[1] - mlo[1], mhi[2] - mlo[2])));
+    const int leaf = std::getenv("MRS_BVH_LEAF") ? std::max(1, std::min(64, std::atoi(std::getenv("MRS_BVH_LEAF")))) : 4;
     std::vector<float> nodes;
     std::function<void(int, int)> build = [&](int b, int e) {
       const int me = static_cast<int>(nodes.size() / 8);
@@ -874,7 +875,7 @@ void build_mesh_bvh(const Model& m, std::vector<int>& face_out, std::vector<floa
       nodes.push_back(0);
       for (int c = 0; c < 3; ++c) nodes.push_back(static_cast<float>(hi[c] + pad));
       nodes.push_back(fbits(-1));
-      if (e - b <= 4) {
+      if (e - b <= leaf) {
         nodes[8 * me + 7] = fbits((b << 8) | (e - b));
       } else {
         // binned surface-area heuristic (16 centroid bins per axis): the split minimising
