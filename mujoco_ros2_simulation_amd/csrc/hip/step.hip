@@ -3228,12 +3228,21 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           hisl[j] = act ? __float_as_int(o[P]) : -1;
         });
         // AR[j][l] = Y_(16j+slot) . Y_l: each level's Y (lane = slot) read once and broadcast slot
-        // by slot into the FMAs of the three held rows
+        // by slot into the FMAs of the three held rows.  The level loads run kPre levels ahead
+        // (a rotating register buffer): one at a time, each level waited a full L2 round trip
+        constexpr int kPre = 4;
+        float ypre[kPre];
+        unroll<kPre>([&](auto pc) {
+          constexpr int q = decltype(pc)::value;
+          ypre[q] = q < nlev && q < my_n ? rec[(my_start + q) * RF + slot] : 0.0f;
+        });
         unroll<NL>([&](auto lc) {
           constexpr int l = decltype(lc)::value;
           unroll<NJ>([&](auto jc) { ARn[decltype(jc)::value][l] = 0.0f; });
+          const float mj = ypre[l % kPre];
+          if constexpr (l + kPre < NL)
+            ypre[l % kPre] = l + kPre < nlev && l + kPre < my_n ? rec[(my_start + l + kPre) * RF + slot] : 0.0f;
           if (l < nlev) {
-            const float mj = l < my_n ? rec[(my_start + l) * RF + slot] : 0.0f;
             const int il = __float_as_int(rowb<l % 16>(__int_as_float(hisl[l / 16])));
             unroll<NJ>([&](auto jc) {
               constexpr int j = decltype(jc)::value;
