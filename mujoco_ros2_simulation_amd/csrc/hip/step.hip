@@ -3230,7 +3230,7 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
         // AR[j][l] = Y_(16j+slot) . Y_l: each level's Y (lane = slot) read once and broadcast slot
         // by slot into the FMAs of the three held rows.  The level loads run kPre levels ahead
         // (a rotating register buffer): one at a time, each level waited a full L2 round trip
-        constexpr int kPre = 4;
+        constexpr int kPre = 8;
         float ypre[kPre];
         unroll<kPre>([&](auto pc) {
           constexpr int q = decltype(pc)::value;
