@@ -18,6 +18,9 @@ LIB = PKG / "libmrs.so"
 ARCH = os.environ.get("MRS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
+# step.hip is compiled once per part (-DMRS_STEP_PART=n), in parallel: part 0 is the dispatcher, the
+# others each instantiate one group width's kernels (17: the G = 16 primal-solver kernel)
+STEP_PARTS = [0, 8, 16, 17, 32, 64]
 # fp32 division/sqrt via v_rcp/v_sqrt (<= 2.5 ulp) instead of the correctly-rounded sequences:
 # the parity tolerance is 1e-5 relative, and the ray/contact math is division-heavy
 HIP_FLAGS = ["-fno-hip-fp32-correctly-rounded-divide-sqrt"]
@@ -39,19 +42,31 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("build failed: " + " ".join(cmd))
 
 
+def _up_to_date(lib: Path, inputs: list[Path]) -> bool:
+    """the library exists and is newer than every input: nothing to compile (the GPU box receives the
+    in-tree .so but not build/, so without this check it would recompile every object)"""
+    return lib.exists() and all(p.stat().st_mtime <= lib.stat().st_mtime for p in inputs)
+
+
 def build_lib(verbose: bool = False) -> Path:
-    OBJ.mkdir(parents=True, exist_ok=True)
     deps = [CSRC / h for h in HEADERS] + [ROOT / "include" / "mrs.h", ROOT / "include" / "mrs_model.h"]
+    if _up_to_date(LIB, deps + [CSRC / rel for rel in HIP_SOURCES + CXX_SOURCES] + [Path(__file__)]):
+        return LIB
+    OBJ.mkdir(parents=True, exist_ok=True)
     objs = []
     jobs = []
-    for rel in HIP_SOURCES + CXX_SOURCES:
+    units = [(rel, None) for rel in HIP_SOURCES + CXX_SOURCES if rel != "hip/step.hip"]
+    units += [("hip/step.hip", part) for part in STEP_PARTS]
+    for rel, part in units:
         src = CSRC / rel
-        obj = OBJ / (rel.replace("/", "_") + ".o")
+        obj = OBJ / (rel.replace("/", "_") + (f".part{part}" if part is not None else "") + ".o")
         objs.append(obj)
         if not _newer(src, obj, deps):
             continue
         if rel.endswith(".hip"):
-            cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *HIP_FLAGS, "-c", str(src), "-o", str(obj)]
+            extra = [f"-DMRS_STEP_PART={part}"] if part is not None else []
+            cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *HIP_FLAGS, *extra, "-c", str(src),
+                   "-o", str(obj)]
         else:
             cmd = ["hipcc", "-O2", "-std=c++17", "-fPIC", "-Wall", "-c", str(src), "-o", str(obj)]
         jobs.append(cmd)
@@ -80,6 +95,9 @@ def build_plugin(verbose: bool = False) -> Path:
     """The MujocoSystemInterface plugin host against the ROS API shim (csrc/plugin/ros_shim) and
     libmrs.so; host C++ only (no device code), linked with rpath $ORIGIN."""
     lib = build_lib(verbose)
+    srcs = [CSRC / rel for rel in PLUGIN_SOURCES] + [p for p in (CSRC / "plugin").rglob("*.hpp")]
+    if _up_to_date(PLUGIN_LIB, srcs + [lib, ROOT / "include" / "mrs_plugin.h"]):
+        return PLUGIN_LIB
     inc = [f"-I{CSRC / 'plugin' / 'include'}", f"-I{CSRC / 'plugin' / 'ros_shim'}", f"-I{ROOT / 'include'}"]
     deps = [p for p in (CSRC / "plugin").rglob("*.hpp")] + [ROOT / "include" / "mrs.h", ROOT / "include" / "mrs_model.h",
                                                           ROOT / "include" / "mrs_plugin.h", CSRC / "mjcf" / "xml.h"]

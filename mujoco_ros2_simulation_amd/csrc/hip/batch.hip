@@ -813,6 +813,7 @@ struct BatchImpl {
   // depth_kernel_mesh: per-frame lists of (triangle, pixel box) records, sized for rast_frames frames
   unsigned long long* rast_list = nullptr;
   int rast_frames = 0;
+  int max_lds = 0;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the batch's device
 };
 
 namespace {
@@ -1912,24 +1913,42 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
   const DevModel& d = b->dm;
   const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p,
                      d.mesh_facenum.p, d.mesh_bvh.p, d.mesh_bvhadr.p, d.mesh_bvhnum.p, d.mesh_tri.p};
-  const bool raster = d.nrast > 0 && W <= 2048 && H <= kBandH * kMaxBands && !std::getenv("MRS_DEPTH_V2") &&
-                     !std::getenv("MRS_DEPTH_V1");
-  if (raster && b->rast_frames < n) {
+  // the binned kernel needs its band of W x kBandH 64-bit keys in LDS (within the device's per-block
+  // limit) and a per-frame triangle list in global memory: frames go in chunks whose lists fit a
+  // budget (MRS_RAST_BUDGET_MB, default 2048 MB), so a large mesh over many envs renders in several
+  // launches instead of failing the allocation
+  const size_t band_lds = static_cast<size_t>(W) * kBandH * sizeof(unsigned long long);
+  if (b->max_lds == 0) {
+    int v = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, b->device));
+    b->max_lds = v > 0 ? v : 65536;
+  }
+  const bool raster = d.nrast > 0 && W <= 2048 && H <= kBandH * kMaxBands && band_lds <= static_cast<size_t>(b->max_lds) &&
+                     !std::getenv("MRS_DEPTH_V2") && !std::getenv("MRS_DEPTH_V1");
+  const size_t per_frame = static_cast<size_t>(std::max(d.nrast_pair, 1)) * sizeof(unsigned long long);
+  const char* bud = std::getenv("MRS_RAST_BUDGET_MB");
+  const size_t budget = (bud ? static_cast<size_t>(std::max(1L, std::atol(bud))) : 2048) << 20;
+  const int chunk = static_cast<int>(std::max<size_t>(1, std::min<size_t>(n, budget / per_frame)));
+  if (raster && b->rast_frames < chunk) {
     // (one render at a time per batch: the lists are reused by every later frame batch)
     if (b->rast_list) {
       HIP_CHECK(hipStreamSynchronize(b->stream));
       if (b->rstream) HIP_CHECK(hipStreamSynchronize(b->rstream));
       HIP_CHECK(hipFree(b->rast_list));
     }
-    HIP_CHECK(hipMalloc(&b->rast_list, static_cast<size_t>(n) * d.nrast_pair * sizeof(unsigned long long)));
-    b->rast_frames = n;
+    HIP_CHECK(hipMalloc(&b->rast_list, static_cast<size_t>(chunk) * per_frame));
+    b->rast_frames = chunk;
   }
   HIP_CHECK(hipEventRecord(b->ev0[1], stream));
   if (raster) {
-    const size_t lds = static_cast<size_t>(W) * kBandH * sizeof(unsigned long long);
-    hipLaunchKernelGGL(depth_kernel_mesh, dim3(n), dim3(256), lds, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
-                       d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam, cam, env0, W, H, f, znear,
-                       zfar, dout, drgb, mesh, d.rast_geom.p, d.rast_base.p, d.nrast, d.nrast_pair, b->rast_list);
+    for (int c0 = 0; c0 < n; c0 += chunk) {
+      const int nc = std::min(chunk, n - c0);
+      const size_t px = static_cast<size_t>(c0) * W * H;
+      hipLaunchKernelGGL(depth_kernel_mesh, dim3(nc), dim3(256), band_lds, stream, d.geom_type.p, d.geom_group.p,
+                         d.geom_size.p, d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam, cam,
+                         env0 + c0, W, H, f, znear, zfar, dout + px, drgb ? drgb + 3 * px : nullptr, mesh,
+                         d.rast_geom.p, d.rast_base.p, d.nrast, d.nrast_pair, b->rast_list);
+    }
   } else if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
     hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,

@@ -5336,9 +5336,12 @@ struct RayBatch { static constexpr int value = G == 64 ? 2 : 4; };
 // R rangefinders per lane in one pass over the geoms (mj_ray per sensor: nearest hit along the
 // site's +z over all visible geoms not on the site's body).  Each geom's pose is read from LDS once
 // for the R rays, and the R independent rays give the scheduler parallel work.  Rays k0 + j*stride.
-template <int G, int R>
+// kChunk: the pass covers ray geoms goff .. goff + 31 of a model with more than 32 (rays_chunked);
+// otherwise goff is 0 and the code is the <= 32-geom pass
+template <int G, int R, bool kChunk = false>
 __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se, gfloat* sd, int k0, int stride,
-                                             unsigned gmask, int common_body, const float* common_o) {
+                                             unsigned gmask, int common_body, const float* common_o, int goff_ = 0) {
+  const int goff = kChunk ? goff_ : 0;
   const LdsLayout& L = m.L;
   float pnt[R][3], vec[R][3], dist[R];
   int bod[R], adr[R];
@@ -5375,8 +5378,10 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       if (m.rf_static_frame) { vec[j][0] = dl[0]; vec[j][1] = dl[1]; vec[j][2] = dl[2]; }
       else mat_vec(vec[j], bm, dl);
       for (int i = 0; i < 3; ++i) pnt[j][i] = o[i];
-      // static split: start from the ray's hit on the world-welded geoms (never beaten: -1)
+      // static split: start from the ray's hit on the world-welded geoms (never beaten: -1); later
+      // chunks of ray geoms start from the earlier chunks' nearest hit in the output slot
       dist[j] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + (act[j] ? k : 0)] : -1.0f;
+      if (kChunk && goff > 0) dist[j] = act[j] && MRS_SD_OK(sd) ? (float)sd[adr[j]] : -1.0f;
     }
   } else {
 #pragma unroll
@@ -5399,6 +5404,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
         mat_vec(vec[j], bm, dl);
       }
       dist[j] = m.rf_mode == 2 ? (float)shared_lds(m)[m.shr_rfst + (act[j] ? k : 0)] : -1.0f;
+      if (kChunk && goff > 0) dist[j] = act[j] && MRS_SD_OK(sd) ? (float)sd[adr[j]] : -1.0f;
     }
   }
   SUB_ADD(PH_SENS_SETUP, t_setup);
@@ -5415,15 +5421,16 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
   wmask = __builtin_amdgcn_readfirstlane(wmask);
   constexpr int kMaxSlots = 64 / R;
   unsigned long long mneed = 0;  // bit slot * R + j: ray j is a candidate of the slot-th mesh geom
-  unsigned mslot = 0, mover = 0;  // ray-geom indices of the recorded mesh geoms, and of the rest
-  unsigned long long slot_geom = 0;  // ray-geom index of slot s in bits 5 s .. 5 s + 4 (nrgeom <= 32)
+  // chunk-local ray-geom indices of the recorded mesh geoms, and of the rest; slots are taken in
+  // ascending index order, so slot s is the s-th set bit of mslot
+  unsigned mslot = 0, mover = 0;
   int nms = 0;
   #pragma unroll 1
   while (wmask) {
     const int i = __builtin_ctz(wmask);
     wmask &= wmask - 1;
     const bool gsel = (gmask >> i) & 1u;
-    const CPtr<float> rec = m.rgeom + 8 * i;
+    const CPtr<float> rec = m.rgeom + 8 * (goff + i);
     const int g = __float_as_int(rec[0]), type = __float_as_int(rec[1]), gb = __float_as_int(rec[2]);
     const float rb = rec[3] * 1.0001f + 1e-6f;
     const float gp[3] = {se[L.gxpos + 3 * g], se[L.gxpos + 3 * g + 1], se[L.gxpos + 3 * g + 2]};
@@ -5447,7 +5454,6 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       if (nms < kMaxSlots) {
         mneed |= static_cast<unsigned long long>(cmask) << (nms * R);
         mslot |= 1u << i;
-        slot_geom |= static_cast<unsigned long long>(i) << (5 * nms);
         ++nms;
       } else {
         mover |= 1u << i;
@@ -5545,7 +5551,7 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       const int k = k0 + js * stride;
       float p[3], v[3];
       const int rb = ray_of(k, p, v);
-      const CPtr<float> rec = m.rgeom + 8 * i;
+      const CPtr<float> rec = m.rgeom + 8 * (goff + i);
       const int g = __float_as_int(rec[0]), gb = __float_as_int(rec[2]), id = __float_as_int(rec[7]);
       if (has && rb != gb && sd_ok) {
         gfloat* o = out_of(k);
@@ -5568,7 +5574,10 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
       const int bit = has ? __builtin_ctzll(need) : 0;
       need &= need - 1;
       const int sl = bit / R;
-      walk(has, static_cast<int>((slot_geom >> (5 * sl)) & 31u), bit - sl * R);
+      unsigned ms = mslot;  // the sl-th set bit of mslot: slot sl's ray geom
+      #pragma unroll 1
+      for (int q = 0; q < sl; ++q) ms &= ms - 1;
+      walk(has, __builtin_ctz(ms | 0x80000000u), bit - sl * R);
     }
     unsigned actm = 0;
 #pragma unroll
@@ -5599,6 +5608,25 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     }
   }
   SUB_ADD(PH_SENS_GEOMS, t_geoms);
+}
+
+// the rangefinder passes of a model with more than 32 ray geoms: geoms in chunks of 32 (one mask bit
+// each), every geom of a chunk a candidate (the level-1 blocks and the static split are built only
+// for <= 32 ray geoms), each chunk continuing from the nearest hit so far in the ray's output slot
+template <int G>
+__device__ void rays_chunked(ENV_PARAMS, gfloat* sensordata) {
+  ENV_UNPACK;
+  constexpr int R = RayBatch<G>::value;
+  const float zero[3] = {0, 0, 0};
+  #pragma unroll 1
+  for (int base = 0; base < m.nrf; base += G * R) {
+    #pragma unroll 1
+    for (int goff = 0; goff < m.nrgeom; goff += 32) {
+      const int nc = m.nrgeom - goff;
+      rangefinders<G, R, true>(m, s, sensordata, base + lane, G, nc >= 32 ? 0xffffffffu : ((1u << nc) - 1u), -1,
+                               zero, goff);
+    }
+  }
 }
 
 // mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel within the group,
@@ -5743,6 +5771,12 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask, common_body, common_o);
     }
   };
+#ifndef MRS_XX_NOCHUNK
+  if (m.nrgeom > 32) {
+    // more ray geoms than mask bits: the chunked pass (rare; out of line)
+    [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sensordata);
+  } else
+#endif
 #ifdef MRS_RAY_BATCH
   passes(std::integral_constant<int, MRS_RAY_BATCH>{});
 #else
@@ -6054,6 +6088,10 @@ __device__ __forceinline__ float implicit_dg(const DevModel& m, const lfloat* s,
 // two com_vel + rne passes of the env's own phases; the derivative couples only dofs of one kinematic
 // tree, so blocked mode keeps M's tree blocks and factors each in place (lane = row of its tree).
 // Out of line: only models with integrator="implicit" reach it.
+// After it returns, qvel is restored but the velocity-dependent LDS fields of the last perturbed
+// pass (cvel, cdofdot, cacc, cfrc / crb and qfrc_bias) hold the state at qvel - e_j: nothing reads
+// them before the next step's forward() recomputes them; a post-integrate consumer would have to
+// rerun com_vel + rne first.
 template <int G>
 __device__ void integrate_implicit(ENV_PARAMS) {
   ENV_UNPACK;
@@ -6369,26 +6407,36 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 
 }  // namespace
 
-template <int G>
+// kernel selection bits of launch_g (the split build compiles each part in its own translation unit)
+constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelAll = 7;
+
+template <int G, int kSel = kSelAll>
 static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
                      int n_steps, bool forward_only, bool primal, hipStream_t stream) {
   constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
-  if constexpr (G == 16) {
+  if constexpr (G == 16 && (kSel & kSelPrimal)) {
     if (primal && !forward_only) {
       hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st,
                          n_envs, n_steps);
       return;
     }
   }
-  if (forward_only)
-    hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs, 1);
-  else
-    hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs,
-                       n_steps);
+  if constexpr ((kSel & kSelForward) != 0) {
+    if (forward_only) {
+      hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs, 1);
+      return;
+    }
+  }
+  if constexpr ((kSel & kSelStep) != 0) {
+    if (!forward_only)
+      hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs,
+                         n_steps);
+  }
 }
 
+#if !defined(MRS_STEP_PART) || MRS_STEP_PART == 0
 // profiling variant only: per-phase wave-cycle totals since the last reset (s_memtime ticks summed
 // over waves); returns the number of phases, 0 in normal builds
 int phase_cycles(double* out, int n, bool reset) {
@@ -6407,6 +6455,10 @@ int phase_cycles(double* out, int n, bool reset) {
 #endif
 }
 
+#endif
+
+#ifndef MRS_STEP_PART
+// single translation unit: every instantiation (the variant builds, scripts/build_variant.sh)
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
                        int n_steps, bool forward_only, int group, bool primal, hipStream_t stream) {
   switch (group) {
@@ -6418,5 +6470,42 @@ hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_float
   }
   return hipGetLastError();
 }
+#else
+// split build (build.py): step.hip is compiled once per part, in parallel, each part instantiating
+// only its own kernels; part 0 holds the dispatcher, parts 8 / 16 / 17 (G = 16 primal) / 32 / 64
+// define launch_part_<n>
+#define MRS_LAUNCH_ARGS const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs, \
+                        int n_steps, bool forward_only, bool primal, hipStream_t stream
+#define MRS_LAUNCH_PASS d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream
+void launch_part_8(MRS_LAUNCH_ARGS);
+void launch_part_16(MRS_LAUNCH_ARGS);
+void launch_part_17(MRS_LAUNCH_ARGS);
+void launch_part_32(MRS_LAUNCH_ARGS);
+void launch_part_64(MRS_LAUNCH_ARGS);
+#if MRS_STEP_PART == 0
+hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
+                       int n_steps, bool forward_only, int group, bool primal, hipStream_t stream) {
+  switch (group) {
+    case 8: launch_part_8(MRS_LAUNCH_PASS); break;
+    case 16:
+      if (primal && !forward_only) launch_part_17(MRS_LAUNCH_PASS);
+      else launch_part_16(MRS_LAUNCH_PASS);
+      break;
+    case 32: launch_part_32(MRS_LAUNCH_PASS); break;
+    case 64: launch_part_64(MRS_LAUNCH_PASS); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+#elif MRS_STEP_PART == 17
+void launch_part_17(MRS_LAUNCH_ARGS) { launch_g<16, kSelPrimal>(MRS_LAUNCH_PASS); }
+#elif MRS_STEP_PART == 16
+void launch_part_16(MRS_LAUNCH_ARGS) { launch_g<16, kSelForward | kSelStep>(MRS_LAUNCH_PASS); }
+#else
+#define MRS_PART_FN2(n) launch_part_##n
+#define MRS_PART_FN(n) MRS_PART_FN2(n)
+void MRS_PART_FN(MRS_STEP_PART)(MRS_LAUNCH_ARGS) { launch_g<MRS_STEP_PART>(MRS_LAUNCH_PASS); }
+#endif
+#endif
 
 }  // namespace mrs

@@ -342,3 +342,77 @@ def test_reseeded_mpr_pairs():
     assert flips <= max(1, 0.01 * 16 * steps)
     assert not unexplained, unexplained[:5]
     assert wq <= 5e-4 and wv <= 0.2
+
+
+# ---------------------------------------------------------------- many ray geoms (mesh slots, > 32 geoms)
+def _ring_scene(n_mesh, n_small, static, nray=30):
+    """a lidar of `nray` rays (every third pitched 4 deg down onto the floor) inside a ring of
+    `n_mesh` mesh rocks at radius 1 and `n_small` spheres / boxes at radius 1.8; the lidar sits on a
+    spinning body, or in the world (the static ray split)"""
+    assets = "".join(f'<mesh name="r{k}" vertex="{_rock(30, 11 + k)}" scale="3 3 3"/>' for k in range(n_mesh))
+    rocks = "".join(
+        f'<geom type="mesh" mesh="r{k}" pos="{np.cos(2 * np.pi * k / n_mesh):.5f} {np.sin(2 * np.pi * k / n_mesh):.5f} 0.3" '
+        f'euler="{7 * k} {11 * k} {13 * k}"/>' for k in range(n_mesh))
+    smalls = ""
+    for k in range(n_small):
+        a = 2 * np.pi * (k + 0.5) / max(n_small, 1)
+        pos = f'{1.8 * np.cos(a):.5f} {1.8 * np.sin(a):.5f} 0.3'
+        smalls += (f'<geom type="sphere" size="0.09" pos="{pos}"/>' if k % 2 else
+                   f'<geom type="box" size="0.07 0.08 0.09" pos="{pos}" euler="0 0 {17 * k}"/>')
+    sites = ""
+    for i in range(nray):
+        a, p = 2 * np.pi * i / nray + 0.013, np.radians(94.0 if i % 3 == 0 else 90.3)
+        z = (np.cos(a) * np.sin(p), np.sin(a) * np.sin(p), np.cos(p))
+        sites += f'<site name="s{i}" zaxis="{z[0]:.6f} {z[1]:.6f} {z[2]:.6f}"/>'
+    lidar = (f'<body name="post" pos="0 0 0.3">{sites}</body>' if static else
+             f'<body name="spin" pos="0 0 0.3"><joint name="yaw" axis="0 0 1"/>'
+             f'<geom type="cylinder" size="0.03 0.02" mass="1"/>{sites}</body>')
+    sens = "".join(f'<rangefinder name="lidar-{i}" site="s{i}"/>' for i in range(nray))
+    return (f'<mujoco><asset>{assets}</asset><worldbody><geom type="plane" size="0 0 1"/>{rocks}{smalls}'
+            f'{lidar}</worldbody><sensor>{sens}</sensor></mujoco>')
+
+
+@pytest.mark.parametrize("n_mesh,n_small,static", [(14, 0, False), (14, 0, True), (14, 24, False), (6, 40, True)])
+def test_rangefinders_many_ray_geoms(n_mesh, n_small, static):
+    """more mesh ray geoms than a 64-bit slot table of 5-bit indices can name (14 meshes with 2 rays
+    per lane: 32 slots) and more than 32 ray geoms in all (the ray pass in chunks of 32): GPU
+    sensordata equals the oracle's brute-force mj_ray within 2e-5 x range, hit / miss identical, and
+    the rock ring is what most rays see"""
+    model = sim.Model.from_string(_ring_scene(n_mesh, n_small, static))
+    nrg = sum(1 for g in range(model.ngeom) if model.geom_rgba[g, 3] > 0)
+    assert (nrg > 32) == (n_small > 0)
+    n = 1 if static else 6
+    q = np.tile(model.qpos0, (n, 1))
+    if not static:
+        q[:, 0] = np.linspace(-0.4, 0.4, n)
+    b = sim.Batch(model, n)
+    b.set(sim.FIELD_QPOS, q)
+    b.forward()
+    sd = b.get(sim.FIELD_SENSORDATA)
+    b.close()
+    for e in range(n):
+        d = binding.OracleData(model)
+        d.qpos[:] = q[e]
+        d.forward()
+        ref = d.sensordata.copy()
+        hit = ref >= 0
+        assert np.array_equal(sd[e] >= 0, hit), e
+        np.testing.assert_allclose(sd[e][hit], ref[hit], rtol=2e-5, atol=2e-5)
+        assert np.sum((ref > 0.6) & (ref < 1.2)) >= n_mesh  # rays end on the rock ring
+
+
+def test_binned_frames_in_chunks(monkeypatch):
+    """the binned kernel's per-frame triangle lists under a small memory budget (MRS_RAST_BUDGET_MB=1:
+    frames rendered in several launches over a reused list) give the same frames bit for bit"""
+    model = _mesh_robot("160 120")
+    q = _mesh_robot_states(model, n=8)
+    out = []
+    for budget in (None, "1"):
+        if budget:
+            monkeypatch.setenv("MRS_RAST_BUDGET_MB", budget)
+        b = sim.Batch(model, 8)
+        b.set(sim.FIELD_QPOS, q)
+        b.forward()
+        out.append(b.render_rgbd(0, 0, 8))
+        b.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])

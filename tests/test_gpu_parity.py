@@ -903,3 +903,42 @@ def test_full_size_c4_batch_properties():
     img = d.render_depth(0)
     close = np.abs(f[0].cpu().numpy() - img) <= 1e-5 * np.maximum(img, 1)
     assert close.mean() >= 0.999, close.mean()
+
+
+def test_c2_bench_variant():
+    """the exact workload `bench.py --config c2` times: the reference scene with <flag
+    sensor="disable"/> (bench.ref_scene_xml), its default solver (Newton), 4096 envs, ctrl from the
+    bench's Philox table changed every 10-step period.  Identical envs identical wherever they sit,
+    deterministic across launches, sensordata never written (sensors disabled), and the four distinct
+    envs against the oracle after 1000 steps within 1e-5 (qpos / qvel, relative to max(|x|, 1))."""
+    import bench
+    xml, base = bench.ref_scene_xml(sensors=False)
+    model = sim.Model.from_string(xml, base)
+    assert model.solver == 2 and model.disableflags & (1 << 12)  # Newton; mjDSBL_SENSOR
+    n, period, steps, k = 4096, 10, 1000, 4
+    ids = np.arange(k)
+    q0 = synth.initial_qpos(model, ids)
+    tab = synth.ctrl_table(model, ids, steps // period, period)
+    outs = []
+    for _ in range(2):
+        b = sim.Batch(model, n)
+        b.set(sim.FIELD_QPOS, np.tile(q0, (n // k, 1)))
+        for p in range(steps // period):
+            b.set(sim.FIELD_CTRL, np.tile(tab[p], (n // k, 1)))
+            b.step(period)
+        outs.append((b.get(sim.FIELD_QPOS), b.get(sim.FIELD_QVEL), b.get(sim.FIELD_SENSORDATA)))
+        b.close()
+    for a, c in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, c)
+    q, v, sd = outs[0]
+    assert np.all(q.reshape(n // k, k, -1) == q[None, :k]) and np.all(v.reshape(n // k, k, -1) == v[None, :k])
+    assert np.all(sd == 0)
+    for e in range(k):
+        d = binding.OracleData(model)
+        d.qpos[:] = q0[e]
+        for p in range(steps // period):
+            d.ctrl[:] = tab[p, e]
+            d.step(period)
+        for got, ref in ((q[e], d.qpos), (v[e], d.qvel)):
+            err = np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1.0))
+            assert err <= RTOL, (e, err)
