@@ -66,6 +66,9 @@ mrs_model* mrs_model_copy(const mrs_model* m);
 /* read-only view of the compiled arrays (mjModel field access throughout the plugin, e.g.
  * jnt_qposadr at src/mujoco_system_interface.cpp:1224); valid while `m` lives */
 int mrs_model_view_get(const mrs_model* m, mrs_model_view* out);
+/* opt into this restatement's own solver variants (MRS_RESTATE_* bits of mrs_model.h; 0, the
+ * default, follows the upstream rules); batches created afterwards use them */
+int mrs_model_set_restate(mrs_model* m, int flags);
 /* replaces mj_name2id (src/mujoco_system_interface.cpp:1193,1213,1496-1497,1527-1529);
  * objtype is MRS_OBJ_*; returns -1 if not found */
 int mrs_name2id(const mrs_model* m, int objtype, const char* name);

@@ -41,6 +41,13 @@ enum { MRS_OBJ_UNKNOWN = 0, MRS_OBJ_BODY = 1, MRS_OBJ_JOINT = 3, MRS_OBJ_GEOM = 
 enum { MRS_SENS_ACCELEROMETER = 1, MRS_SENS_GYRO = 3, MRS_SENS_FORCE = 4, MRS_SENS_TORQUE = 5,
        MRS_SENS_RANGEFINDER = 7, MRS_SENS_JOINTPOS = 9, MRS_SENS_JOINTVEL = 10,
        MRS_SENS_ACTUATORFRC = 15, MRS_SENS_FRAMEPOS = 25, MRS_SENS_FRAMEQUAT = 26 };
+/* restate bits (not MuJoCo options; mrs_model_set_restate): opt-in variants of this restatement that
+ * upstream does not have.  NEWTON_REFINE: after a Newton step that kept every row's state, one more
+ * step from freshly formed residuals with the same factor, then stop (mj_solNewton instead keeps
+ * iterating until its improvement / gradient tests stop it).  PGS_ELLIPTIC_BLOCK: PGS solves each
+ * elliptic contact block exactly over its cone (mj_solPGS takes a normal / ray step, then the friction
+ * by mju_QCQP2 with the normal fixed). */
+enum { MRS_RESTATE_NEWTON_REFINE = 1 << 0, MRS_RESTATE_PGS_ELLIPTIC_BLOCK = 1 << 1 };
 /* disable flags (mjtDisableBit subset) */
 enum { MRS_DSBL_CONSTRAINT = 1 << 0, MRS_DSBL_EQUALITY = 1 << 1, MRS_DSBL_FRICTIONLOSS = 1 << 2,
        MRS_DSBL_LIMIT = 1 << 3, MRS_DSBL_CONTACT = 1 << 4, MRS_DSBL_PASSIVE = 1 << 5,
@@ -63,6 +70,7 @@ typedef struct mrs_model_view {
   /* options (mjOption subset) */
   double timestep, gravity[3], tolerance, impratio, ls_tolerance;
   int integrator, solver, iterations, disableflags, cone, ls_iterations;
+  int restate;       /* MRS_RESTATE_* bits: this build's own solver variants (0 = the upstream rules) */
 
   /* statistic / visual (for the depth camera) */
   double stat_extent, stat_center[3], stat_meaninertia, vis_znear, vis_zfar;

@@ -19,8 +19,9 @@ ARCH = os.environ.get("MRS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
 # step.hip is compiled once per part (-DMRS_STEP_PART=n), in parallel: part 0 is the dispatcher, the
-# others each instantiate one group width's kernels (17: the G = 16 primal-solver kernel)
-STEP_PARTS = [0, 8, 16, 17, 32, 64]
+# others each instantiate one group width's kernels (17: the G = 16 primal-solver kernel; 18: the
+# G = 16 kernels of models with more than 32 ray geoms)
+STEP_PARTS = [0, 8, 16, 17, 18, 32, 64]
 # fp32 division/sqrt via v_rcp/v_sqrt (<= 2.5 ulp) instead of the correctly-rounded sequences:
 # the parity tolerance is 1e-5 relative, and the ray/contact math is division-heavy
 HIP_FLAGS = ["-fno-hip-fp32-correctly-rounded-divide-sqrt"]

@@ -22,7 +22,7 @@
 namespace mrs {
 
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, bool primal, hipStream_t stream);
+                       int n_steps, bool forward_only, int group, bool primal, bool wide_rays, hipStream_t stream);
 
 namespace {
 
@@ -962,7 +962,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.nsite = m.nsite; d.ncam = m.ncam; d.nsensor = m.nsensor; d.nsensordata = m.nsensordata;
   d.max_depth = m.max_depth;
   d.integrator = m.integrator; d.iterations = m.iterations; d.disableflags = m.disableflags;
-  d.solver = m.solver; d.ls_iterations = m.ls_iterations; d.cone = m.cone;
+  d.solver = m.solver; d.ls_iterations = m.ls_iterations; d.cone = m.cone; d.restate = m.restate;
   d.impratio = static_cast<float>(m.impratio); d.ls_tolerance = static_cast<float>(m.ls_tolerance);
   // diagnostic phase ablation for profiling only (bit 0 sensors, 1 collision, 2 constraints)
   d.diag_skip = std::getenv("MRS_DIAG_SKIP") ? std::atoi(std::getenv("MRS_DIAG_SKIP")) : 0;
@@ -1745,7 +1745,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
       prod.rf_mode = 1;
       DevModel* d_prod = static_cast<DevModel*>(dalloc(*b, sizeof(DevModel)));
       HIP_CHECK(hipMemcpyAsync(d_prod, &prod, sizeof(DevModel), hipMemcpyHostToDevice, b->stream));
-      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, false, b->stream));
+      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, false, false, b->stream));
       HIP_CHECK(hipStreamSynchronize(b->stream));
     }
     batch_launch(b, 1, true);  // mj_forward after load (src/mujoco_system_interface.cpp:741)
@@ -1887,7 +1887,8 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
-  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group, b->model->solver != MRS_SOL_PGS, b->stream));
+  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group,
+                        b->model->solver != MRS_SOL_PGS, b->dm.nrgeom > 32 && b->dm.nrf > 0, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
 }

@@ -111,6 +111,7 @@ struct DevModel {
   float* rf_static;
   // options
   int integrator, iterations, disableflags, solver, ls_iterations;
+  int restate;  // MRS_RESTATE_* (mrs_model.h): opt-in solver variants, 0 = upstream rules
   int cone;  // MRS_CONE_*: elliptic models take the dense row path (3-row contact blocks)
   int acc_sens;   // bit 0: accelerometer, bit 1: force/torque sensors present (mj_rnePostConstraint)
   int diag_skip;  // profiling ablation only (MRS_DIAG_SKIP); 0 in every measured/parity run

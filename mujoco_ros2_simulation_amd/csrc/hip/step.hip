@@ -450,11 +450,12 @@ __device__ int sphere_box(const float p[3], float r, const float* bp, const floa
 // capsule (segment a-b, radius r) vs box: oracle.c col_capsule_box in fp32.  Exact closest point of the
 // segment to the box (F(t), the squared box distance of the segment point, is convex and piecewise
 // quadratic between the slab-crossing breakpoints: the best clamped stationary point of the pieces);
-// contacts at the two ends of the segment piece inside the slabs of the axes where that point is
-// inside the box's extent (a capsule lying on a face rests on two points, where the single closest
-// point would be arbitrary along the face and ill-conditioned between fp32 and fp64), plus the closest
-// point itself when clearly nearer than both (a capsule across an edge); a segment through the box:
-// the point of deepest penetration.  Breakpoints sorted by a 19-comparator network (static registers).
+// at most 2 contacts (mjc_CapsuleBox's count): the closest point alone when it lies strictly inside
+// the segment piece within the slabs of the axes where it is inside the box's extent and is clearly
+// nearer than both ends of that piece (a capsule across an edge), otherwise the two ends of the piece
+// (a capsule lying on a face rests on two points, where the single closest point would be arbitrary
+// along the face and ill-conditioned between fp32 and fp64); a segment through the box: the point of
+// deepest penetration.  Breakpoints sorted by a 19-comparator network (static registers).
 __device__ __forceinline__ float seg_box_F(const float la[3], const float d[3], const float* s, float t) {
   float f = 0;
   for (int i = 0; i < 3; ++i) {
@@ -538,14 +539,15 @@ __device__ int capsule_box(const float a[3], const float b[3], float r, const fl
   tc0 = fminf(tc0, tb);
   tc1 = fmaxf(tc1, tb);
   const float F0 = seg_box_F(la, d, size, tc0), F1 = seg_box_F(la, d, size, tc1);
+  if (tb > tc0 && tb < tc1 && sqrtf(Fb) < sqrtf(fminf(F0, F1)) - (1e-6f + 1e-4f * r)) {
+    // across an edge: the closest point alone
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + tb * (b[i] - a[i]);
+    return sphere_box(p, r, bp, bm, size, margin, out, n);
+  }
   for (int i = 0; i < 3; ++i) p[i] = a[i] + tc0 * (b[i] - a[i]);
   n = sphere_box(p, r, bp, bm, size, margin, out, n);
   if (tc1 > tc0) {
     for (int i = 0; i < 3; ++i) p[i] = a[i] + tc1 * (b[i] - a[i]);
-    n = sphere_box(p, r, bp, bm, size, margin, out, n);
-  }
-  if (tb > tc0 && tb < tc1 && sqrtf(Fb) < sqrtf(fminf(F0, F1)) - (1e-6f + 1e-4f * r)) {
-    for (int i = 0; i < 3; ++i) p[i] = a[i] + tb * (b[i] - a[i]);
     n = sphere_box(p, r, bp, bm, size, margin, out, n);
   }
   return n;
@@ -3983,6 +3985,38 @@ __device__ __forceinline__ void ell_block_min(const float A[9], const float c[3]
   y[0] = s; y[1] = x[0]; y[2] = x[1];
 }
 
+// mj_solPGS's split update of one elliptic block (oracle.c ell_pgs_split): a normal step (old normal
+// force 0) or the exact step along the ray of the old force (normal kept >= 0), then the friction by
+// mju_QCQP2 with the normal fixed
+__device__ __forceinline__ void ell_pgs_split(const float A[9], const float res[3], const float old[3], float mu,
+                                              float y[3]) {
+  y[0] = old[0]; y[1] = old[1]; y[2] = old[2];
+  if (A[0] < kMinVal) return;
+  if (old[0] < kMinVal) {
+    y[0] = fmaxf(old[0] - res[0] / A[0], 0.0f);
+  } else {
+    float vAv = 0, vr = 0;
+    for (int k = 0; k < 3; ++k) {
+      const float Av = A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2];
+      vAv += old[k] * Av;
+      vr += old[k] * res[k];
+    }
+    if (vAv >= kMinVal) {
+      float x = -vr / vAv;
+      if (old[0] + x * old[0] < 0) x = -1.0f;
+      for (int k = 0; k < 3; ++k) y[k] = old[k] + x * old[k];
+    }
+  }
+  if (y[0] < kMinVal) { y[0] = fmaxf(y[0], 0.0f); y[1] = y[2] = 0; return; }
+  const float At[4] = {A[4], A[5], A[7], A[8]};
+  const float dn = y[0] - old[0];
+  const float bt[2] = {res[1] + A[3] * dn - (A[4] * old[1] + A[5] * old[2]),
+                       res[2] + A[6] * dn - (A[7] * old[1] + A[8] * old[2])};
+  float x[2];
+  qcqp2_la(x, At, bt, mu, y[0]);
+  y[1] = x[0]; y[2] = x[1];
+}
+
 // cost change of a row moved from jar j0 (state s0) by dj to state s1, in factored form when the
 // state is kept (no cancellation of two nearly equal costs in fp32)
 __device__ __forceinline__ float prow_dcost(int s0, int s1, float R, float fl, float j0, float dj) {
@@ -4441,8 +4475,11 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
     const float gn = dof ? Md - qfrc : 0.0f;
     const float gnorm = sqrtf(gsum<G>(gn * gn));
     if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance) break;
-    if (newton && !changed) {
-      // active set held: the step solved the quadratic model up to the fp32 factor's rounding
+    // H = M + J'DJ depends on the row states only: after a step that kept them, the next Newton step
+    // reuses its factor (mj_solNewton keeps iterating until the tests above stop it)
+    reuse = newton && !changed;
+    if (newton && !changed && (m.restate & MRS_RESTATE_NEWTON_REFINE)) {
+      // opt-in (not upstream): the step solved the quadratic model up to the fp32 factor's rounding
       // (cond(H) eps |grad|); one refinement step from fresh residuals, then stop (oracle.c) -- unless
       // the residual is already at the rounding level of the gradient's own terms
       const bool floor = fabsf(gn) <= 64.0f * __FLT_EPSILON__ * (fabsf(Md) + fabsf(qfrc));
@@ -4645,7 +4682,8 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
     const float gn = dof ? Md - qfrc : 0.0f;
     const float gnorm = sqrtf(gsum<16>(gn * gn));
     if (scale * -dcost < m.tolerance || scale * gnorm < m.tolerance) break;
-    if (newton && !changed) {
+    reuse = newton && !changed;  // (solve_primal)
+    if (newton && !changed && (m.restate & MRS_RESTATE_NEWTON_REFINE)) {
       const bool floor = fabsf(gn) <= 64.0f * __FLT_EPSILON__ * (fabsf(Md) + fabsf(qfrc));
       if (refined || !gany<16>(!floor)) break;
       refined = true;
@@ -5170,8 +5208,9 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     #pragma unroll 1
     for (int r = 0; r < nefc; ++r) {
       if (ell_start(m, type, floss, r)) {
-        // elliptic block: its forces minimise the block's local cost over the cone exactly
-        // (ell_block_min; oracle.c fwd_constraint states the deviation from upstream's split update)
+        // elliptic block: mj_solPGS's split update (ell_pgs_split), or with the opt-in
+        // MRS_RESTATE_PGS_ELLIPTIC_BLOCK the exact minimiser of the block's local cost over the cone
+        // (ell_block_min; oracle.c fwd_constraint)
         float res[3], A[9], old[3], c[3], y[3];
         for (int k = 0; k < 3; ++k) {
           old[k] = ff[r + k];
@@ -5182,7 +5221,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
           for (int b = a + 1; b < 3; ++b)
             A[3 * a + b] = A[3 * b + a] = gsum<G>(lane < nv ? J[(r + a) * nv + lane] * MJ[(r + b) * nv + lane] : 0.0f);
         for (int k = 0; k < 3; ++k) c[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
-        ell_block_min(A, c, ell_friction(m, scr, type, r), y);
+        if (m.restate & MRS_RESTATE_PGS_ELLIPTIC_BLOCK) ell_block_min(A, c, ell_friction(m, scr, type, r), y);
+        else ell_pgs_split(A, res, old, ell_friction(m, scr, type, r), y);
         float dl[3], quad = 0;
         for (int k = 0; k < 3; ++k) dl[k] = y[k] - old[k];
         for (int a = 0; a < 3; ++a)
@@ -5771,12 +5811,11 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
       rangefinders<G, R>(m, s, sensordata, base + lane, G, gmask, common_body, common_o);
     }
   };
-#ifndef MRS_XX_NOCHUNK
   if (m.nrgeom > 32) {
-    // more ray geoms than mask bits: the chunked pass (rare; out of line)
-    [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sensordata);
+    // more ray geoms than mask bits: the chunked pass (rays_chunked) is called by the step loop
+    // right after forward() returns, in the kernels instantiated for such models (step_kernel
+    // kWideRays)
   } else
-#endif
 #ifdef MRS_RAY_BATCH
   passes(std::integral_constant<int, MRS_RAY_BATCH>{});
 #else
@@ -6234,7 +6273,10 @@ template <int G>
 #endif
 struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
-template <int G, bool kForwardOnly, bool kPrimal = false>
+// kWideRays (G = 16 only): the instantiation for models with more than 32 ray geoms, which carries
+// the chunked ray pass; the other G = 16 kernels have no call to it (its call site alone cost the
+// inlined phases registers: C3 -1.3% in an A/B).  Other widths always carry it.
+template <int G, bool kForwardOnly, bool kPrimal = false, bool kWideRays = false>
 __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -6332,6 +6374,11 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     gfloat* sd_step = sensordata;
 #endif
     MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG)));
+    // rangefinders of a model with more than 32 ray geoms (sensors() leaves them to this call)
+    if constexpr (G != 16 || kWideRays || kForwardOnly) {
+      if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
+        [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sd_step);
+    }
     if (kForwardOnly) break;
     bool redo = false;
     if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
@@ -6344,7 +6391,13 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     }
     // forward() is entered by the whole wave; for envs that were not reset it recomputes the
     // same outputs from the same state
-    if (__any(redo)) { [[clang::noinline]] ncon = forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG); }  // rare
+    if (__any(redo)) {  // rare
+      [[clang::noinline]] ncon = forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG);
+      if constexpr (G != 16 || kWideRays) {
+        if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
+          [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sd_step);
+      }
+    }
     if (m.integrator == MRS_INT_RK4) {
       // stages out of line (RK4 models only), each followed by a forward without sensors
       #pragma unroll 1
@@ -6408,14 +6461,25 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 }  // namespace
 
 // kernel selection bits of launch_g (the split build compiles each part in its own translation unit)
-constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelAll = 7;
+constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelWide = 8, kSelAll = 15;
 
 template <int G, int kSel = kSelAll>
 static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                     int n_steps, bool forward_only, bool primal, hipStream_t stream) {
+                     int n_steps, bool forward_only, bool primal, bool wide, hipStream_t stream) {
   constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
   const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
+  if constexpr (G == 16 && (kSel & kSelWide)) {
+    if (wide && !forward_only) {
+      if (primal)
+        hipLaunchKernelGGL((step_kernel<G, false, true, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream,
+                           d_model, st, n_envs, n_steps);
+      else
+        hipLaunchKernelGGL((step_kernel<G, false, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream,
+                           d_model, st, n_envs, n_steps);
+      return;
+    }
+  }
   if constexpr (G == 16 && (kSel & kSelPrimal)) {
     if (primal && !forward_only) {
       hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st,
@@ -6460,35 +6524,37 @@ int phase_cycles(double* out, int n, bool reset) {
 #ifndef MRS_STEP_PART
 // single translation unit: every instantiation (the variant builds, scripts/build_variant.sh)
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, bool primal, hipStream_t stream) {
+                       int n_steps, bool forward_only, int group, bool primal, bool wide, hipStream_t stream) {
   switch (group) {
-    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
-    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
-    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
-    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
+    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
+    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
+    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 #else
 // split build (build.py): step.hip is compiled once per part, in parallel, each part instantiating
-// only its own kernels; part 0 holds the dispatcher, parts 8 / 16 / 17 (G = 16 primal) / 32 / 64
-// define launch_part_<n>
+// only its own kernels; part 0 holds the dispatcher, parts 8 / 16 / 17 (G = 16 primal) / 18 (G = 16,
+// more than 32 ray geoms) / 32 / 64 define launch_part_<n>
 #define MRS_LAUNCH_ARGS const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs, \
-                        int n_steps, bool forward_only, bool primal, hipStream_t stream
-#define MRS_LAUNCH_PASS d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream
+                        int n_steps, bool forward_only, bool primal, bool wide, hipStream_t stream
+#define MRS_LAUNCH_PASS d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream
 void launch_part_8(MRS_LAUNCH_ARGS);
 void launch_part_16(MRS_LAUNCH_ARGS);
 void launch_part_17(MRS_LAUNCH_ARGS);
+void launch_part_18(MRS_LAUNCH_ARGS);
 void launch_part_32(MRS_LAUNCH_ARGS);
 void launch_part_64(MRS_LAUNCH_ARGS);
 #if MRS_STEP_PART == 0
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, bool primal, hipStream_t stream) {
+                       int n_steps, bool forward_only, int group, bool primal, bool wide, hipStream_t stream) {
   switch (group) {
     case 8: launch_part_8(MRS_LAUNCH_PASS); break;
     case 16:
-      if (primal && !forward_only) launch_part_17(MRS_LAUNCH_PASS);
+      if (wide && !forward_only) launch_part_18(MRS_LAUNCH_PASS);
+      else if (primal && !forward_only) launch_part_17(MRS_LAUNCH_PASS);
       else launch_part_16(MRS_LAUNCH_PASS);
       break;
     case 32: launch_part_32(MRS_LAUNCH_PASS); break;
@@ -6499,6 +6565,8 @@ hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_float
 }
 #elif MRS_STEP_PART == 17
 void launch_part_17(MRS_LAUNCH_ARGS) { launch_g<16, kSelPrimal>(MRS_LAUNCH_PASS); }
+#elif MRS_STEP_PART == 18
+void launch_part_18(MRS_LAUNCH_ARGS) { launch_g<16, kSelWide>(MRS_LAUNCH_PASS); }
 #elif MRS_STEP_PART == 16
 void launch_part_16(MRS_LAUNCH_ARGS) { launch_g<16, kSelForward | kSelStep>(MRS_LAUNCH_PASS); }
 #else

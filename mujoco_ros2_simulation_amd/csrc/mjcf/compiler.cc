@@ -1794,7 +1794,7 @@ mrs_model_view Model::view() const {
   for (int i = 0; i < 3; ++i) { v.gravity[i] = gravity[i]; v.stat_center[i] = stat_center[i]; }
   v.tolerance = tolerance; v.impratio = impratio; v.integrator = integrator; v.solver = solver;
   v.iterations = iterations; v.disableflags = disableflags; v.cone = cone;
-  v.ls_tolerance = ls_tolerance; v.ls_iterations = ls_iterations;
+  v.ls_tolerance = ls_tolerance; v.ls_iterations = ls_iterations; v.restate = restate;
   v.stat_extent = stat_extent; v.stat_meaninertia = stat_meaninertia;
   v.vis_znear = vis_znear; v.vis_zfar = vis_zfar;
 #define MRS_V(f) v.f = f.empty() ? nullptr : f.data()

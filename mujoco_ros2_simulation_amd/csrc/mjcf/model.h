@@ -17,7 +17,7 @@ struct Model {
   double timestep = 0.002, gravity[3] = {0, 0, -9.81}, tolerance = 1e-8, impratio = 1,
          ls_tolerance = 0.01;
   int integrator = MRS_INT_EULER, solver = MRS_SOL_NEWTON, iterations = 100, disableflags = 0,
-      cone = 0, ls_iterations = 50;
+      cone = 0, ls_iterations = 50, restate = 0;
 
   double stat_extent = 0, stat_center[3] = {0, 0, 0}, stat_meaninertia = 1, vis_znear = 0.01,
          vis_zfar = 50;

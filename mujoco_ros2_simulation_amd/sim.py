@@ -29,6 +29,7 @@ OBJ_BODY, OBJ_JOINT, OBJ_GEOM, OBJ_SITE, OBJ_CAMERA, OBJ_ACTUATOR, OBJ_SENSOR = 
 SENS_ACCELEROMETER, SENS_GYRO, SENS_FORCE, SENS_TORQUE, SENS_RANGEFINDER = 1, 3, 4, 5, 7
 SENS_JOINTPOS, SENS_JOINTVEL, SENS_ACTUATORFRC, SENS_FRAMEPOS, SENS_FRAMEQUAT = 9, 10, 15, 25, 26
 BIAS_NONE, BIAS_AFFINE = 0, 1
+RESTATE_NEWTON_REFINE, RESTATE_PGS_ELLIPTIC_BLOCK = 1, 2
 (FIELD_QPOS, FIELD_QVEL, FIELD_CTRL, FIELD_QFRC_APPLIED, FIELD_QACC_WARMSTART, FIELD_QACC,
  FIELD_QFRC_ACTUATOR, FIELD_SENSORDATA, FIELD_TIME, FIELD_WARNING, FIELD_NCON, FIELD_SOLVER_NITER) = range(12)
 # ActuatorType (include/mujoco_ros2_control/data.hpp:43-51 numbering)
@@ -101,7 +102,7 @@ class ModelView(C.Structure):
                 [("timestep", C.c_double), ("gravity", C.c_double * 3), ("tolerance", C.c_double),
                  ("impratio", C.c_double), ("ls_tolerance", C.c_double),
                  ("integrator", C.c_int), ("solver", C.c_int), ("iterations", C.c_int), ("disableflags", C.c_int),
-                 ("cone", C.c_int), ("ls_iterations", C.c_int),
+                 ("cone", C.c_int), ("ls_iterations", C.c_int), ("restate", C.c_int),
                  ("stat_extent", C.c_double), ("stat_center", C.c_double * 3), ("stat_meaninertia", C.c_double),
                  ("vis_znear", C.c_double), ("vis_zfar", C.c_double)] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _ARRAYS] +
@@ -126,6 +127,7 @@ def lib() -> C.CDLL:
         L.mrs_model_load_xml_string.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
         L.mrs_model_free.argtypes = [C.c_void_p]
         L.mrs_model_view_get.argtypes = [C.c_void_p, C.POINTER(ModelView)]
+        L.mrs_model_set_restate.argtypes = [C.c_void_p, C.c_int]
         L.mrs_name2id.argtypes = [C.c_void_p, C.c_int, C.c_char_p]
         L.mrs_id2name.restype = C.c_char_p
         L.mrs_id2name.argtypes = [C.c_void_p, C.c_int, C.c_int]
@@ -194,7 +196,7 @@ class Model:
         v = self.view
         for n in _SIZES + _MESH_SIZES:
             setattr(self, n, getattr(v, n))
-        for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "integrator", "solver",
+        for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "restate", "integrator", "solver",
                   "iterations", "disableflags",
                   "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
             setattr(self, n, getattr(v, n))
@@ -228,6 +230,13 @@ class Model:
         if not h:
             raise MrsError(-2, err.value.decode())
         return cls(h)
+
+    def set_restate(self, flags: int) -> None:
+        """opt into this restatement's own solver variants (RESTATE_* bits; 0 = upstream rules);
+        batches and oracle data created afterwards use them"""
+        _check(lib().mrs_model_set_restate(self._h, int(flags)))
+        _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
+        self.restate = self.view.restate
 
     def name2id(self, objtype: int, name: str) -> int:
         return lib().mrs_name2id(self._h, objtype, name.encode())

@@ -700,15 +700,17 @@ static int col_sphere_box(const double p[3], double r, const double* bpos, const
  * minimiser t* is the best of the pieces' clamped stationary points.  Contacts (restated primitive,
  * well conditioned in fp32 and fp64 alike):
  *   - the segment is clipped to the slabs |l_j| <= s_j of the axes on which the closest point t* lies
- *     inside the box's extent (the face or edge it is closest to); the two ends of that piece, where
- *     within margin, are contacts -- a capsule lying on a face rests on two points whatever its
- *     overhang, where the single closest point would be arbitrary along the face;
- *   - the closest point t* itself when it is clearly nearer than both ends (a capsule across an
- *     edge), by more than 1e-6 + 1e-4 r;
+ *     inside the box's extent (the face or edge it is closest to);
+ *   - when t* lies strictly inside that piece and is clearly nearer than both its ends (a capsule
+ *     across an edge), by more than 1e-6 + 1e-4 r, the closest point alone is the contact;
+ *   - otherwise the two ends of the piece, where within margin, are the contacts -- a capsule lying on
+ *     a face rests on two points whatever its overhang, where the single closest point would be
+ *     arbitrary along the face;
  *   - a segment that passes through the box (F(t*) = 0): the point of deepest penetration, found by
  *     ternary search on the concave min_i (s_i - |l_i(t)|).
- * Order: piece start, piece end, interior.  (MuJoCo's mjc_CapsuleBox also gives two contacts for flat
- * poses; its exact selection is not restated.)  Same algorithm as step.hip capsule_box. */
+ * At most 2 contacts, as MuJoCo's mjc_CapsuleBox (the closest point, plus a second one for a capsule
+ * parallel to a face); which points its selection takes in the flat case is not restated [verify].
+ * Same algorithm as step.hip capsule_box. */
 static double seg_box_F(const double la[3], const double d[3], const double* s, double t) {
   double f = 0;
   for (int i = 0; i < 3; ++i) {
@@ -792,15 +794,15 @@ static int col_capsule_box(const double a[3], const double b[3], double r, const
   if (tc0 > t) tc0 = t;
   if (tc1 < t) tc1 = t;
   double F0 = seg_box_F(la, d, size, tc0), F1 = seg_box_F(la, d, size, tc1);
+  double dmin = sqrt(F0 < F1 ? F0 : F1);
+  if (t > tc0 && t < tc1 && sqrt(Fbest) < dmin - (1e-6 + 1e-4 * r)) {
+    for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
+    return col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
+  }
   for (int i = 0; i < 3; ++i) p[i] = a[i] + tc0 * (b[i] - a[i]);
   n = col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
   if (tc1 > tc0) {
     for (int i = 0; i < 3; ++i) p[i] = a[i] + tc1 * (b[i] - a[i]);
-    n = col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
-  }
-  double dmin = sqrt(F0 < F1 ? F0 : F1);
-  if (t > tc0 && t < tc1 && sqrt(Fbest) < dmin - (1e-6 + 1e-4 * r)) {
-    for (int i = 0; i < 3; ++i) p[i] = a[i] + t * (b[i] - a[i]);
     n = col_sphere_box(p, r, bpos, bmat, size, margin, out, n);
   }
   return n;
@@ -1647,6 +1649,41 @@ static void ell_block_min(const double A[9], const double c[3], double mu, doubl
   y[0] = s_; y[1] = x[0]; y[2] = x[1];
 }
 
+/* mj_solPGS's update of one elliptic contact block [upstream engine_solver.c; restated from the
+ * published engine, verify]: with res = AR f + b at the old forces f_old and A the block of AR,
+ *   1. normal or ray step: when the old normal force is 0, the normal's own 1-D step
+ *      f_n -= res_n / A_nn, clamped at 0; otherwise the exact minimiser along the ray of the old force
+ *      v = f_old, x = -(v'res) / (v'A v), shortened so the normal stays >= 0;
+ *   2. friction with the normal fixed: min over f_t of the block cost, |f_t| <= mu f_n, by mju_QCQP2
+ *      (zero friction when f_n is 0).
+ * A block whose normal diagonal is below MINVAL keeps its forces. */
+static void ell_pgs_split(const double A[9], const double res[3], const double old[3], double mu, double y[3]) {
+  y[0] = old[0]; y[1] = old[1]; y[2] = old[2];
+  if (A[0] < MINVAL) return;
+  if (old[0] < MINVAL) {
+    y[0] = old[0] - res[0] / A[0];
+    if (y[0] < 0) y[0] = 0;
+  } else {
+    double Av[3], vAv = 0, vr = 0;
+    for (int k = 0; k < 3; ++k) Av[k] = A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2];
+    for (int k = 0; k < 3; ++k) { vAv += old[k] * Av[k]; vr += old[k] * res[k]; }
+    if (vAv >= MINVAL) {
+      double x = -vr / vAv;
+      if (old[0] + x * old[0] < 0) x = -1;
+      for (int k = 0; k < 3; ++k) y[k] = old[k] + x * old[k];
+    }
+  }
+  if (y[0] < MINVAL) { y[0] = y[0] < 0 ? 0 : y[0]; y[1] = y[2] = 0; return; }
+  /* friction: 1/2 x'A_tt x + x'(res_t + A_tn (y_n - f_old,n) - A_tt f_old,t) over |x| <= mu y_n */
+  const double At[4] = {A[4], A[5], A[7], A[8]}, dd[2] = {mu, mu};
+  const double dn = y[0] - old[0];
+  const double bt[2] = {res[1] + A[3] * dn - (A[4] * old[1] + A[5] * old[2]),
+                        res[2] + A[6] * dn - (A[7] * old[1] + A[8] * old[2])};
+  double x[2];
+  qcqp2(x, At, bt, dd, y[0]);
+  y[1] = x[0]; y[2] = x[1];
+}
+
 /* force of one row for a given jar = J qacc - aref (mj_constraintUpdate primal states) */
 static double row_force(orc_ws* w, int r, double jar) {
   double D = w->efc_D[r];
@@ -1951,7 +1988,9 @@ static void solve_primal(const mrs_model_view* m, orc_data* d, int newton) {
       gnorm += g * g;
     }
     if (scale * -dcost < m->tolerance || scale * sqrt(gnorm) < m->tolerance) break;
-    if (newton && !changed) {
+    /* mj_solNewton keeps iterating until the tests above (or the iteration count) stop it.  Opt-in
+     * variant (MRS_RESTATE_NEWTON_REFINE, not upstream): */
+    if (newton && !changed && (m->restate & MRS_RESTATE_NEWTON_REFINE)) {
       /* the active set held, so the step solved the quadratic model exactly up to the rounding of the
        * Hessian factor: one more step from freshly formed residuals (iterative refinement), then stop.
        * In fp64 it changes nothing measurable; in the fp32 kernel it removes the factor's rounding
@@ -2039,12 +2078,12 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
     double improvement = 0;
     for (int r = 0; r < nefc; ++r) {
       if (ELL_BLOCK(w, r)) {
-        /* elliptic block: the block's forces minimise its local cost 1/2 y'Ay + y'(res - A f_old) over
-         * the cone |y_t| <= mu y_n exactly (ell_block_min), so the sweeps are block Gauss-Seidel on the
-         * dual and reach the optimum Newton / CG reach.  (Upstream mj_solPGS updates the normal force
-         * by its own 1-D step and then the friction by mju_QCQP2 with the normal fixed; that split
-         * stops short of the optimum when the contact slides -- the cone multiplier couples the two --
-         * so it is not restated: documented deviation, verify.) */
+        /* elliptic block: mj_solPGS's split update (ell_pgs_split: a normal or ray step, then the
+         * friction by mju_QCQP2 with the normal fixed); opt-in MRS_RESTATE_PGS_ELLIPTIC_BLOCK instead
+         * minimises the block's local cost 1/2 y'Ay + y'(res - A f_old) over the cone |y_t| <= mu y_n
+         * exactly (ell_block_min) -- block Gauss-Seidel on the dual, which reaches the optimum Newton /
+         * CG reach where the split update can stall on a sliding contact (the cone multiplier couples
+         * normal and friction). */
         double res[3], A[9], old[3], nw[3], cb[3];
         for (int k = 0; k < 3; ++k) {
           const double* ar = w->AR + (size_t)(r + k) * nefc;
@@ -2054,7 +2093,8 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
           old[k] = f[r + k];
         }
         for (int k = 0; k < 3; ++k) cb[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
-        ell_block_min(A, cb, w->efc_fr[r], nw);
+        if (m->restate & MRS_RESTATE_PGS_ELLIPTIC_BLOCK) ell_block_min(A, cb, w->efc_fr[r], nw);
+        else ell_pgs_split(A, res, old, w->efc_fr[r], nw);
         double delta[3], quad = 0;
         for (int k = 0; k < 3; ++k) delta[k] = nw[k] - old[k];
         for (int k = 0; k < 3; ++k)

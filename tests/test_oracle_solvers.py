@@ -117,11 +117,20 @@ def test_elliptic_forces_solve_the_cone_program(imp):
     """the elliptic-cone contact forces of the oracle's Newton solve are the minimiser of MuJoCo's
     dual problem 1/2 f'(A + R) f + f'b over the friction cones |f_t| <= mu f_n -- computed here by an
     independent solver (scipy SLSQP) from the oracle's own rows -- in resting, sliding and tumbling
-    states of a box; PGS's block updates reach the same forces"""
+    states of a box.  PGS with the exact block step (opt-in MRS_RESTATE_PGS_ELLIPTIC_BLOCK) reaches the
+    same forces.  PGS's default split update (mj_solPGS: normal / ray step, then mju_QCQP2 friction
+    with the normal fixed) never does worse than the cone program allows and keeps every block inside
+    its cone, but it cannot leave the apex of a block whose normal alone would not push (residual
+    c_n > 0) while friction and normal together would (c_n < mu |c_t|): there it stays at zero force,
+    short of the optimum -- a property of the split update, recorded here with the count of states
+    where it reaches the optimum"""
     from scipy.optimize import minimize
     rng = np.random.default_rng(5)
     m = sim.Model.from_string(_BOX.format(imp=imp, solver="Newton"))
     mp = sim.Model.from_string(_BOX.format(imp=imp, solver="PGS").replace('solver="PGS"', 'solver="PGS" iterations="500" tolerance="1e-14"'))
+    mb = sim.Model.from_string(_BOX.format(imp=imp, solver="PGS").replace('solver="PGS"', 'solver="PGS" iterations="500" tolerance="1e-14"'))
+    mb.set_restate(sim.RESTATE_PGS_ELLIPTIC_BLOCK)
+    split_at_optimum = 0
     d = binding.OracleData(m)
     d.step(100)
     checked = 0
@@ -153,10 +162,23 @@ def test_elliptic_forces_solve_the_cone_program(imp):
         scale = max(1.0, np.max(np.abs(best.x)))
         assert obj(f) <= best.fun + 1e-9 * max(1.0, abs(best.fun))
         np.testing.assert_allclose(f, best.x, atol=2e-4 * scale)
-        p = binding.OracleData(mp)
+        p = binding.OracleData(mb)
         p.qpos[:] = d.qpos
         p.qvel[:] = d.qvel
         p.forward()
         np.testing.assert_allclose(p.efc()["force"], f, atol=1e-5 * scale)
+        p = binding.OracleData(mp)
+        p.qpos[:] = d.qpos
+        p.qvel[:] = d.qvel
+        p.forward()
+        fs = p.efc()["force"]
+        assert obj(fs) >= best.fun - 1e-9 * max(1.0, abs(best.fun))
+        for k in range(0, n, 3):
+            assert fs[k] >= 0 and np.hypot(fs[k + 1], fs[k + 2]) <= 0.6 * fs[k] * (1 + 1e-9) + 1e-12
+        at_opt = np.allclose(fs, f, atol=1e-5 * scale)
+        if not at_opt:  # explained only by a block stalled at the apex where the optimum pushes
+            assert any(np.all(fs[k:k + 3] == 0) and f[k] > 1e-6 * scale for k in range(0, n, 3)), (fs, f)
+        split_at_optimum += int(at_opt)
         checked += 1
-    assert checked >= 6
+    print(f"impratio {imp}: split update at the optimum in {split_at_optimum} of {checked} states")
+    assert checked >= 6 and split_at_optimum >= checked // 2
