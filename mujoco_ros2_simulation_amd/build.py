@@ -19,9 +19,11 @@ ARCH = os.environ.get("MRS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
 # step.hip is compiled once per part (-DMRS_STEP_PART=n), in parallel: part 0 is the dispatcher, the
-# others each instantiate one group width's kernels (17: the G = 16 primal-solver kernel; 18: the
-# G = 16 kernels of models with more than 32 ray geoms)
-STEP_PARTS = [0, 8, 16, 17, 18, 32, 64]
+# others each instantiate one group width's kernels (17: the G = 16 primal-solver kernel; 18 / 65: the
+# G = 16 / 64 kernels with the extended code, MRS_EXT -- MPR contact polish, > 32 ray geoms -- which
+# parts 16, 17 and 64 leave out)
+STEP_PARTS = [0, 8, 16, 17, 18, 32, 64, 65]
+STEP_NO_EXT = {16, 17, 64}
 # fp32 division/sqrt via v_rcp/v_sqrt (<= 2.5 ulp) instead of the correctly-rounded sequences:
 # the parity tolerance is 1e-5 relative, and the ray/contact math is division-heavy
 HIP_FLAGS = ["-fno-hip-fp32-correctly-rounded-divide-sqrt"]
@@ -65,7 +67,7 @@ def build_lib(verbose: bool = False) -> Path:
         if not _newer(src, obj, deps):
             continue
         if rel.endswith(".hip"):
-            extra = [f"-DMRS_STEP_PART={part}"] if part is not None else []
+            extra = [f"-DMRS_STEP_PART={part}", f"-DMRS_EXT={0 if part in STEP_NO_EXT else 1}"] if part is not None else []
             cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *HIP_FLAGS, *extra, "-c", str(src),
                    "-o", str(obj)]
         else:
@@ -85,6 +87,31 @@ def build_lib(verbose: bool = False) -> Path:
     if jobs or not LIB.exists():
         _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB)] + [str(o) for o in objs])
     return LIB
+
+
+def build_variant(name: str, flags: list[str]) -> Path:
+    """an A/B variant libmrs_<name>.so: every step.hip part compiled with extra flags (e.g.
+    -DMRS_PHASE_TIMING), linked with the product's other objects (scripts/build_variant.sh)"""
+    build_lib()
+    vdir = OBJ / f"variant_{name}"
+    vdir.mkdir(parents=True, exist_ok=True)
+    src = CSRC / "hip" / "step.hip"
+    objs, procs = [], []
+    for part in STEP_PARTS:
+        obj = vdir / f"step.part{part}.o"
+        objs.append(obj)
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *HIP_FLAGS, f"-DMRS_STEP_PART={part}",
+               f"-DMRS_EXT={0 if part in STEP_NO_EXT else 1}", *flags, "-c", str(src), "-o", str(obj)]
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out)
+            raise RuntimeError("variant build failed: " + " ".join(cmd))
+    others = [OBJ / (rel.replace("/", "_") + ".o") for rel in HIP_SOURCES + CXX_SOURCES if rel != "hip/step.hip"]
+    lib = PKG / f"libmrs_{name}.so"
+    _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib)] + [str(o) for o in objs + others])
+    return lib
 
 
 PLUGIN_LIB = PKG / "libmrs_plugin.so"
@@ -133,6 +160,9 @@ def build_oracle() -> Path:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "variant":
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+        sys.exit(0)
     print(build_lib(verbose=True))
     print(build_plugin(verbose=True))
     print(build_oracle())

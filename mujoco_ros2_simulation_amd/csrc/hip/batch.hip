@@ -22,7 +22,7 @@
 namespace mrs {
 
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, bool primal, bool wide_rays, hipStream_t stream);
+                       int n_steps, bool forward_only, int group, bool primal, bool ext, hipStream_t stream);
 
 namespace {
 
@@ -814,6 +814,9 @@ struct BatchImpl {
   unsigned long long* rast_list = nullptr;
   int rast_frames = 0;
   int max_lds = 0;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the batch's device
+  // the model needs the extended step kernels (step.hip MRS_EXT): general convex (MPR) collision
+  // pairs, or rangefinders with more than 32 ray geoms
+  bool ext = false;
 };
 
 namespace {
@@ -1637,6 +1640,15 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.blocked = b.group == 64 ? 1 : 0;
   if (b.group == 64) d.shr_total = shr_small;
+  // extended step kernels (step.hip MRS_EXT) for models with general convex (MPR) pairs -- a pair
+  // that is not plane-* and has an ellipsoid, cylinder or mesh (narrowphase's analytic routines cover
+  // the rest) -- or rangefinders over more than 32 ray geoms
+  b.ext = d.nrgeom > 32 && d.nrf > 0;
+  for (size_t p = 0; p < m.pair_geom1.size() && !b.ext; ++p) {
+    const int t1 = m.geom_type[m.pair_geom1[p]], t2 = m.geom_type[m.pair_geom2[p]];
+    auto conv = [](int t) { return t == MRS_GEOM_ELLIPSOID || t == MRS_GEOM_CYLINDER || t == MRS_GEOM_MESH; };
+    if (t1 != MRS_GEOM_PLANE && t2 != MRS_GEOM_PLANE && (conv(t1) || conv(t2))) b.ext = true;
+  }
 
   if (d.blocked) lds_layout(true);
   d.shr_off = L.total * envs_per_block(b.group);
@@ -1733,7 +1745,20 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     // padded to whole workgroups of the chosen group width: idle groups use it
     const size_t epb = static_cast<size_t>(envs_per_block(b->group));
     const size_t n_pad = (static_cast<size_t>(n) + epb - 1) / epb * epb;
-    b->st.scratch = static_cast<float*>(dalloc(*b, n_pad * b->S.total * sizeof(float)));
+    // env spread: lane groups per env so that a small batch still fills two waves per SIMD (the
+    // resident limit of the 256-VGPR step kernels); MRS_SPREAD=<shift> overrides (0: off)
+    int shift = 0;
+    if (b->group < 64) {
+      int cus = 0;
+      HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device));
+      const long waves = (static_cast<long>(n) * b->group + 63) / 64, target = 2L * 4 * std::max(cus, 1);
+      while (shift < 2 && (waves << (shift + 1)) <= target) ++shift;
+    }
+    if (const char* e = std::getenv("MRS_SPREAD")) shift = std::max(0, std::min(3, std::atoi(e)));
+    const size_t n_virt = ((static_cast<size_t>(n) << shift) + epb - 1) / epb * epb;
+    b->st.spread_shift = shift;
+    b->st.scr_mirror = static_cast<int>(n_pad);
+    b->st.scratch = static_cast<float*>(dalloc(*b, (n_pad + (shift ? n_virt : 0)) * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));
     b->st.geom_xmat = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 9 * sizeof(float)));
     b->st.cam_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ncam) * 3 * sizeof(float)));
@@ -1745,7 +1770,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
       prod.rf_mode = 1;
       DevModel* d_prod = static_cast<DevModel*>(dalloc(*b, sizeof(DevModel)));
       HIP_CHECK(hipMemcpyAsync(d_prod, &prod, sizeof(DevModel), hipMemcpyHostToDevice, b->stream));
-      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, false, false, b->stream));
+      HIP_CHECK(launch_step(d_prod, b->L.total, b->dm.shr_total, b->st, 1, 1, true, b->group, false, b->ext, b->stream));
       HIP_CHECK(hipStreamSynchronize(b->stream));
     }
     batch_launch(b, 1, true);  // mj_forward after load (src/mujoco_system_interface.cpp:741)
@@ -1888,7 +1913,7 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
   HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group,
-                        b->model->solver != MRS_SOL_PGS, b->dm.nrgeom > 32 && b->dm.nrf > 0, b->stream));
+                        b->model->solver != MRS_SOL_PGS, b->ext, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
 }

@@ -210,6 +210,10 @@ struct DevState {
   float* geom_xmat;  // [n_envs][ngeom][9]
   float* cam_xpos;   // [n_envs][ncam][3]
   float* cam_xmat;   // [n_envs][ncam][9]
+  // env spread (occupancy for small batches): 2^spread_shift lane groups step each env, the first
+  // (primary) writes the results, the others mirror it in their own scratch (slot scr_mirror + group);
+  // a batch of few envs then spreads over more waves / SIMDs.  0 = one group per env.
+  int spread_shift, scr_mirror;
 };
 
 }  // namespace mrs

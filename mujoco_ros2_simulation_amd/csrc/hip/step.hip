@@ -16,6 +16,12 @@
 #include "devmodel.h"
 #include "raymesh.h"
 
+// MRS_EXT: compile the extended code paths (MPR contact polish, chunked ray pass for more than 32
+// ray geoms).  The split build sets it per part (build.py); one translation unit carries them.
+#ifndef MRS_EXT
+#define MRS_EXT 1
+#endif
+
 namespace mrs {
 
 namespace {
@@ -956,6 +962,359 @@ __device__ __forceinline__ bool mpr_penetration(const MeshTab m, const Shape A, 
     mpr_expand(p, v4);
   }
 }
+// MPR contact polish (oracle.c mpr_polish, same steps in fp32): the minimiser over unit n of the
+// support function of A - B next to MPR's normal, by active-set Newton over the shapes' polyhedral
+// features (vertex / edge / face) with the smooth parts' curvature; MPR's contact is kept for pairs
+// without a curved shape, cylinders, and iterations that do not settle.
+constexpr int kPolMaxV = 4, kPolPasses = 12, kPolNewton = 12;
+struct PolPart {
+  int nv, mesh, ell, vadr, hadr;
+  float v[8][3];
+  float pos[3], mat[9];
+  float sgn, R, M[9];
+};
+__device__ __forceinline__ bool pol_part_of(const Shape& s, float sgn, PolPart& p) {
+  p.sgn = sgn; p.R = s.inflate; p.mesh = 0; p.ell = 0; p.nv = 0; p.vadr = s.vadr; p.hadr = s.hadr;
+  for (int i = 0; i < 3; ++i) p.pos[i] = s.pos[i];
+  for (int i = 0; i < 9; ++i) { p.mat[i] = s.mat[i]; p.M[i] = 0; }
+  const float* z = s.size;
+  switch (s.type) {
+    case MRS_GEOM_SPHERE:
+      p.nv = 1; p.R += z[0];
+      for (int i = 0; i < 3; ++i) p.v[0][i] = sgn * s.pos[i];
+      return true;
+    case MRS_GEOM_CAPSULE:
+      p.nv = 2; p.R += z[0];
+      for (int i = 0; i < 3; ++i) {
+        p.v[0][i] = sgn * (s.pos[i] - s.mat[3 * i + 2] * z[1]);
+        p.v[1][i] = sgn * (s.pos[i] + s.mat[3 * i + 2] * z[1]);
+      }
+      return true;
+    case MRS_GEOM_ELLIPSOID:
+      p.nv = 1; p.ell = 1;
+      for (int i = 0; i < 3; ++i) p.v[0][i] = sgn * s.pos[i];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          float v = 0;
+          for (int k = 0; k < 3; ++k) v += s.mat[3 * i + k] * z[k] * z[k] * s.mat[3 * j + k];
+          p.M[3 * i + j] = v;
+        }
+      return true;
+    case MRS_GEOM_BOX:
+      p.nv = 8;
+      for (int k = 0; k < 8; ++k) {
+        const float l[3] = {(k & 1) ? z[0] : -z[0], (k & 2) ? z[1] : -z[1], (k & 4) ? z[2] : -z[2]};
+        float x[3];
+        mat_vec(x, s.mat, l);
+        for (int i = 0; i < 3; ++i) p.v[k][i] = sgn * (s.pos[i] + x[i]);
+      }
+      return true;
+    case MRS_GEOM_MESH:
+      p.nv = s.nhull; p.mesh = 1;
+      return true;
+    default:
+      return false;
+  }
+}
+__device__ __forceinline__ void pol_vertex(const MeshTab mt, const PolPart& p, int k, float out[3]) {
+  if (!p.mesh) { for (int i = 0; i < 3; ++i) out[i] = p.v[k][i]; return; }
+  const int v = 3 * (p.vadr + mt.hull[p.hadr + k]);
+  const float l[3] = {mt.vert[v], mt.vert[v + 1], mt.vert[v + 2]};
+  float x[3];
+  mat_vec(x, p.mat, l);
+  for (int i = 0; i < 3; ++i) out[i] = p.sgn * (p.pos[i] + x[i]);
+}
+__device__ __forceinline__ void pol_smooth(const PolPart& p, const float n[3], float s[3], float H[9]) {
+  for (int i = 0; i < 3; ++i) s[i] = p.R * n[i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) H[3 * i + j] += p.R * ((i == j ? 1.0f : 0.0f) - n[i] * n[j]);
+  if (p.ell) {
+    float Mn[3];
+    mat_vec(Mn, p.M, n);
+    const float h = sqrtf(dot3(n, Mn));
+    if (h < kMinVal) return;
+    for (int i = 0; i < 3; ++i) s[i] += Mn[i] / h;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) H[3 * i + j] += (p.M[3 * i + j] - Mn[i] * Mn[j] / (h * h)) / h;
+  }
+}
+struct PolState { int F[2][kPolMaxV], nf[2]; };
+__device__ __forceinline__ void pol_grad(const MeshTab mt, const PolPart* P, const PolState& st, const float n[3], float G[3],
+                                         float H[9], float sS[2][3]) {
+  for (int i = 0; i < 9; ++i) H[i] = 0;
+  for (int i = 0; i < 3; ++i) G[i] = 0;
+  for (int q = 0; q < 2; ++q) {
+    float v0[3];
+    pol_smooth(P[q], n, sS[q], H);
+    pol_vertex(mt, P[q], st.F[q][0], v0);
+    for (int i = 0; i < 3; ++i) G[i] += sS[q][i] + v0[i];
+  }
+}
+__device__ __forceinline__ int pol_basis(const MeshTab mt, const PolPart* P, const PolState& st, float Q[3][3]) {
+  int r = 0;
+  for (int q = 0; q < 2; ++q) {
+    float v0[3];
+    pol_vertex(mt, P[q], st.F[q][0], v0);
+    for (int k = 1; k < st.nf[q]; ++k) {
+      float e[3];
+      pol_vertex(mt, P[q], st.F[q][k], e);
+      for (int i = 0; i < 3; ++i) e[i] -= v0[i];
+      const float len = sqrtf(dot3(e, e));
+      for (int j = 0; j < r; ++j) {
+        const float d = dot3(e, Q[j]);
+        for (int i = 0; i < 3; ++i) e[i] -= d * Q[j][i];
+      }
+      const float el = sqrtf(dot3(e, e));
+      if (el <= 1e-5f * len || len < kMinVal) continue;
+      if (r == 3) return 4;
+      for (int i = 0; i < 3; ++i) Q[r][i] = e[i] / el;
+      ++r;
+    }
+  }
+  return r;
+}
+__device__ __forceinline__ void pol_tangent(const float n[3], float t1[3], float t2[3]) {
+  float a[3] = {0, 0, 0};
+  a[fabsf(n[0]) < 0.6f ? 0 : (fabsf(n[1]) < 0.6f ? 1 : 2)] = 1;
+  const float d = dot3(a, n);
+  for (int i = 0; i < 3; ++i) t1[i] = a[i] - d * n[i];
+  normalize3(t1);
+  cross3(t2, n, t1);
+}
+__device__ __forceinline__ int pol_move(const MeshTab mt, const PolPart* P, PolState& st, float n[3], const float dl[3]) {
+  float tmin = 1;
+  int qmin = -1, kmin = -1;
+  for (int q = 0; q < 2; ++q) {
+    float v0[3];
+    pol_vertex(mt, P[q], st.F[q][0], v0);
+    const float c0 = dot3(v0, n), d0 = dot3(v0, dl);
+    for (int k = 0; k < P[q].nv; ++k) {
+      bool in = false;
+      for (int f = 0; f < st.nf[q]; ++f) in |= st.F[q][f] == k;
+      if (in) continue;
+      float v[3];
+      pol_vertex(mt, P[q], k, v);
+      const float c = dot3(v, n) - c0, d = dot3(v, dl) - d0;
+      if (c + d <= 0 || d <= 0) continue;
+      const float t = fmaxf(-c / d, 0.0f);
+      if (t < tmin) { tmin = t; qmin = q; kmin = k; }
+    }
+  }
+  for (int i = 0; i < 3; ++i) n[i] += tmin * dl[i];
+  normalize3(n);
+  if (qmin < 0) return 0;
+  if (st.nf[qmin] >= kPolMaxV) return -1;
+  st.F[qmin][st.nf[qmin]++] = kmin;
+  return 1;
+}
+__device__ __forceinline__ void pol_drop(PolState& st, int q, int f) {
+  for (int k = f; k + 1 < st.nf[q]; ++k) st.F[q][k] = st.F[q][k + 1];
+  --st.nf[q];
+}
+__device__ __forceinline__ float det3(const float A[9]) {
+  return A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) + A[2] * (A[3] * A[7] - A[4] * A[6]);
+}
+__device__ int pol_kkt(const MeshTab mt, const PolPart* P, PolState& st, const float n[3], const float G[3],
+                       float w[2][kPolMaxV]) {
+  float t1[3], t2[3];
+  pol_tangent(n, t1, t2);
+  const int m = st.nf[0] + st.nf[1] - 2;
+  for (int q = 0; q < 2; ++q)
+    for (int f = 0; f < kPolMaxV; ++f) w[q][f] = 0;
+  if (m == 0) return 1;
+  float E[6][2];
+  int cq[6], cf[6], nc = 0;
+  for (int q = 0; q < 2; ++q) {
+    float v0[3];
+    pol_vertex(mt, P[q], st.F[q][0], v0);
+    for (int f = 1; f < st.nf[q]; ++f) {
+      float e[3];
+      pol_vertex(mt, P[q], st.F[q][f], e);
+      for (int i = 0; i < 3; ++i) e[i] -= v0[i];
+      E[nc][0] = dot3(e, t1); E[nc][1] = dot3(e, t2);
+      cq[nc] = q; cf[nc] = f; ++nc;
+    }
+  }
+  const float g1 = dot3(G, t1), g2 = dot3(G, t2);
+  if (m == 1) {
+    const float el2 = E[0][0] * E[0][0] + E[0][1] * E[0][1];
+    if (el2 < kMinVal) return -1;
+    const float x = -(g1 * E[0][0] + g2 * E[0][1]) / el2;
+    if (x < 0) { pol_drop(st, cq[0], cf[0]); return 0; }
+    if (x > 1) { pol_drop(st, cq[0], 0); return 0; }
+    w[cq[0]][cf[0]] = x;
+    return 1;
+  }
+  if (m == 2) {
+    const float det = E[0][0] * E[1][1] - E[1][0] * E[0][1];
+    if (fabsf(det) < kMinVal) return -1;
+    const float x0 = (-g1 * E[1][1] + g2 * E[1][0]) / det, x1 = (-g2 * E[0][0] + g1 * E[0][1]) / det;
+    if (cq[0] == cq[1]) {
+      const float x2 = 1 - x0 - x1, worst = fminf(x2, fminf(x0, x1));
+      if (worst < 0) { pol_drop(st, cq[0], worst == x0 ? cf[0] : (worst == x1 ? cf[1] : 0)); return 0; }
+    } else {
+      const float v0 = fminf(x0, 1 - x0), v1 = fminf(x1, 1 - x1);
+      if (v0 < 0 || v1 < 0) {
+        const int c = v0 <= v1 ? 0 : 1;
+        const float x = c == 0 ? x0 : x1;
+        pol_drop(st, cq[c], x < 0 ? cf[c] : 0);
+        return 0;
+      }
+    }
+    w[cq[0]][cf[0]] = x0;
+    w[cq[1]][cf[1]] = x1;
+    return 1;
+  }
+  if (m == 3 && (st.nf[0] == 1 || st.nf[1] == 1)) {
+    const int q = cq[0];
+    for (int a = 0; a < 3; ++a)
+      for (int b = a + 1; b < 3; ++b) {
+        const float det = E[a][0] * E[b][1] - E[b][0] * E[a][1];
+        if (fabsf(det) < kMinVal) continue;
+        const float x0 = (-g1 * E[b][1] + g2 * E[b][0]) / det, x1 = (-g2 * E[a][0] + g1 * E[a][1]) / det;
+        if (x0 >= 0 && x1 >= 0 && x0 + x1 <= 1) { w[q][cf[a]] = x0; w[q][cf[b]] = x1; return 1; }
+      }
+    const float A3[9] = {E[0][0], E[1][0], E[2][0], E[0][1], E[1][1], E[2][1], 1, 1, 1}, rhs[3] = {-g1, -g2, 1};
+    const float dA = det3(A3);
+    if (fabsf(dA) > kMinVal) {
+      float x[3];
+      for (int c = 0; c < 3; ++c) {
+        float B3[9];
+        for (int i = 0; i < 9; ++i) B3[i] = A3[i];
+        for (int r = 0; r < 3; ++r) B3[3 * r + c] = rhs[r];
+        x[c] = det3(B3) / dA;
+      }
+      if (x[0] >= 0 && x[1] >= 0 && x[2] >= 0) {
+        w[q][cf[0]] = x[0]; w[q][cf[1]] = x[1]; w[q][cf[2]] = x[2];
+        return 1;
+      }
+    }
+    return -1;
+  }
+  return -1;
+}
+// returns true with the polished depth / normal / position, false to keep MPR's
+__device__ bool mpr_polish(const MeshTab mt, const Shape& A, const Shape& B, const float n0[3], float mpr_depth,
+                           float& depth, float nrm[3], float pos[3]) {
+  if (A.type == MRS_GEOM_CYLINDER || B.type == MRS_GEOM_CYLINDER) return false;
+  const bool curvedA = A.type == MRS_GEOM_SPHERE || A.type == MRS_GEOM_CAPSULE || A.type == MRS_GEOM_ELLIPSOID;
+  const bool curvedB = B.type == MRS_GEOM_SPHERE || B.type == MRS_GEOM_CAPSULE || B.type == MRS_GEOM_ELLIPSOID;
+  if (!curvedA && !curvedB) return false;
+  PolPart P[2];
+  if (!pol_part_of(A, 1.0f, P[0]) || !pol_part_of(B, -1.0f, P[1])) return false;
+  PolState st;
+  float n[3] = {n0[0], n0[1], n0[2]};
+  for (int q = 0; q < 2; ++q) {
+    float best = -3.0e38f;
+    st.nf[q] = 1;
+    st.F[q][0] = 0;
+    for (int k = 0; k < P[q].nv; ++k) {
+      float v[3];
+      pol_vertex(mt, P[q], k, v);
+      const float d = dot3(v, n);
+      if (d > best) { best = d; st.F[q][0] = k; }
+    }
+  }
+  float G[3], H[9], sS[2][3], w[2][kPolMaxV];
+  bool done = false;
+  for (int pass = 0; pass < kPolPasses && !done; ++pass) {
+    float Q[3][3];
+    const int rank = pol_basis(mt, P, st, Q);
+    if (rank > 2) {
+      pol_grad(mt, P, st, n, G, H, sS);
+      bool found = false;
+      for (int q = 0; q < 2 && !found; ++q)
+        for (int f = 0; f < st.nf[q] && !found; ++f) {
+          PolState t = st;
+          pol_drop(t, q, f);
+          float Qt[3][3];
+          if (pol_basis(mt, P, t, Qt) != 2) continue;
+          float Gt[3], Ht[9], sSt[2][3];
+          pol_grad(mt, P, t, n, Gt, Ht, sSt);
+          if (pol_kkt(mt, P, t, n, Gt, w) == 1) {
+            st = t;
+            found = true;
+            for (int i = 0; i < 3; ++i) { G[i] = Gt[i]; sS[0][i] = sSt[0][i]; sS[1][i] = sSt[1][i]; }
+          }
+        }
+      if (!found) return false;
+      done = true;
+      break;
+    }
+    bool moved = false, conv = false;
+    if (rank == 2) {
+      float t[3], dl[3];
+      cross3(t, Q[0], Q[1]);
+      normalize3(t);
+      if (dot3(t, n) < 0) for (int i = 0; i < 3; ++i) t[i] = -t[i];
+      for (int i = 0; i < 3; ++i) dl[i] = t[i] - n[i];
+      const int r = pol_move(mt, P, st, n, dl);
+      if (r < 0) return false;
+      moved = r > 0;
+      conv = r == 0;
+    } else {
+      for (int it = 0; it < kPolNewton; ++it) {
+        float dl[3];
+        if (rank == 0) {
+          pol_grad(mt, P, st, n, G, H, sS);
+          const float lam = dot3(G, n);
+          float t1[3], t2[3], Ht1[3], Ht2[3];
+          pol_tangent(n, t1, t2);
+          mat_vec(Ht1, H, t1);
+          mat_vec(Ht2, H, t2);
+          const float a11 = dot3(t1, Ht1) - lam, a22 = dot3(t2, Ht2) - lam, a12 = dot3(t1, Ht2);
+          const float det = a11 * a22 - a12 * a12;
+          if (!(a11 > 0 && det > 0)) return false;
+          const float b1 = -dot3(G, t1), b2 = -dot3(G, t2);
+          const float x1 = (b1 * a22 - b2 * a12) / det, x2 = (b2 * a11 - b1 * a12) / det;
+          for (int i = 0; i < 3; ++i) dl[i] = x1 * t1[i] + x2 * t2[i];
+        } else {
+          const float d = dot3(n, Q[0]);
+          for (int i = 0; i < 3; ++i) n[i] -= d * Q[0][i];
+          normalize3(n);
+          pol_grad(mt, P, st, n, G, H, sS);
+          const float lm = dot3(G, n);
+          float t[3], Ht[3];
+          cross3(t, Q[0], n);
+          mat_vec(Ht, H, t);
+          const float f2 = dot3(t, Ht) - lm;
+          if (!(f2 > 0)) return false;
+          const float th = -dot3(G, t) / f2;
+          for (int i = 0; i < 3; ++i) dl[i] = th * t[i];
+        }
+        const float step = sqrtf(dot3(dl, dl));
+        const int r = pol_move(mt, P, st, n, dl);
+        if (r < 0) return false;
+        if (r > 0) { moved = true; break; }
+        if (step < 2e-7f) { conv = true; break; }
+      }
+    }
+    if (moved) continue;
+    if (!conv) return false;
+    pol_grad(mt, P, st, n, G, H, sS);
+    const int k = pol_kkt(mt, P, st, n, G, w);
+    if (k < 0) return false;
+    done = k == 1;
+  }
+  if (!done) return false;
+  const float dp = dot3(G, n);
+  if (dot3(n, n0) < 0.8f || !(dp > 0) || dp > mpr_depth + kMprTol) return false;
+  float pA[3], pB[3];
+  for (int q = 0; q < 2; ++q) {
+    float* pt = q ? pB : pA;
+    float v0[3];
+    pol_vertex(mt, P[q], st.F[q][0], v0);
+    for (int i = 0; i < 3; ++i) pt[i] = v0[i] + sS[q][i];
+    for (int f = 1; f < st.nf[q]; ++f) {
+      float e[3];
+      pol_vertex(mt, P[q], st.F[q][f], e);
+      for (int i = 0; i < 3; ++i) pt[i] += w[q][f] * (e[i] - v0[i]);
+    }
+  }
+  depth = dp;
+  for (int i = 0; i < 3; ++i) { nrm[i] = n[i]; pos[i] = 0.5f * (pA[i] - pB[i]); }
+  return true;
+}
 __device__ __forceinline__ void shape_of(const DevModel& m, int g, const float* p, const float* mat, const float* size,
                                          float inflate, Shape& s) {
   s.type = m.geom_type[g];
@@ -977,6 +1336,12 @@ __device__ __forceinline__ int convex_convex(const DevModel& m, int g1, int g2, 
   shape_of(m, g2, p2, m2, s2, 0.5f * margin, B);
   float depth, nrm[3], pos[3];
   if (!mpr_penetration(MeshTab{m.mesh_vert, m.mesh_hull}, A, B, depth, nrm, pos)) return 0;
+#if MRS_EXT
+  {
+    const float n0[3] = {nrm[0], nrm[1], nrm[2]};
+    [[clang::noinline]] mpr_polish(MeshTab{m.mesh_vert, m.mesh_hull}, A, B, n0, depth, depth, nrm, pos);
+  }
+#endif
   gCon& o = out[0];
   for (int i = 0; i < 3; ++i) { o.pos[i] = pos[i]; o.nrm[i] = nrm[i]; }
   o.dist = margin - depth;
@@ -5813,8 +6178,7 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
   };
   if (m.nrgeom > 32) {
     // more ray geoms than mask bits: the chunked pass (rays_chunked) is called by the step loop
-    // right after forward() returns, in the kernels instantiated for such models (step_kernel
-    // kWideRays)
+    // right after forward() returns, in the extended kernels (MRS_EXT)
   } else
 #ifdef MRS_RAY_BATCH
   passes(std::integral_constant<int, MRS_RAY_BATCH>{});
@@ -6273,10 +6637,7 @@ template <int G>
 #endif
 struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
-// kWideRays (G = 16 only): the instantiation for models with more than 32 ray geoms, which carries
-// the chunked ray pass; the other G = 16 kernels have no call to it (its call site alone cost the
-// inlined phases registers: C3 -1.3% in an A/B).  Other widths always carry it.
-template <int G, bool kForwardOnly, bool kPrimal = false, bool kWideRays = false>
+template <int G, bool kForwardOnly, bool kPrimal = false>
 __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -6284,13 +6645,18 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
   const DevModel& m = *mp;
   const LdsLayout& L = m.L;
   const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
-  const int env = blockIdx.x * kEnvsPerBlock + slot;
-  // groups past n_envs stay alive (the wave-cooperative ray phase needs every lane) and mirror the
-  // last env with their own scratch (allocated for the padded count); they write nothing back
-  const bool valid = env < n_envs;
+  // group -> env: with spread 2^k (DevState::spread_shift), 2^k consecutive groups step one env and
+  // only the first writes back (the others mirror it: same state, same arithmetic, own scratch), so
+  // a small batch occupies 2^k times the waves (C4's 2048 envs: 512 waves on 1024 SIMDs otherwise)
+  const int vgroup = blockIdx.x * kEnvsPerBlock + slot;
+  const int env = vgroup >> st.spread_shift;
+  const bool primary = (vgroup & ((1 << st.spread_shift) - 1)) == 0;
+  // groups past n_envs (and mirrors) stay alive (the wave-cooperative ray phase needs every lane) and
+  // step a valid env with their own scratch; they write nothing back
+  const bool valid = env < n_envs && primary;
   lfloat* s = (lfloat*)(smem + slot * L.total);
-  gfloat* scr = (gfloat*)(st.scratch + (size_t)env * m.S.total);
-  const size_t e = (size_t)(valid ? env : n_envs - 1);
+  gfloat* scr = (gfloat*)(st.scratch + (size_t)(valid || st.spread_shift == 0 ? env : st.scr_mirror + vgroup) * m.S.total);
+  const size_t e = (size_t)(env < n_envs ? env : n_envs - 1);
   #pragma unroll 1
   for (int i = lane; i < m.nq; i += G) s[L.qpos + i] = st.qpos[e * m.nq + i];
   #pragma unroll 1
@@ -6374,11 +6740,11 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     gfloat* sd_step = sensordata;
 #endif
     MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG)));
+#if MRS_EXT
     // rangefinders of a model with more than 32 ray geoms (sensors() leaves them to this call)
-    if constexpr (G != 16 || kWideRays || kForwardOnly) {
-      if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
-        [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sd_step);
-    }
+    if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
+      [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sd_step);
+#endif
     if (kForwardOnly) break;
     bool redo = false;
     if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
@@ -6393,10 +6759,10 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     // same outputs from the same state
     if (__any(redo)) {  // rare
       [[clang::noinline]] ncon = forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG);
-      if constexpr (G != 16 || kWideRays) {
-        if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
-          [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sd_step);
-      }
+#if MRS_EXT
+      if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
+        [[clang::noinline]] rays_chunked<G>(ENV_ARGS, sd_step);
+#endif
     }
     if (m.integrator == MRS_INT_RK4) {
       // stages out of line (RK4 models only), each followed by a forward without sensors
@@ -6461,25 +6827,14 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 }  // namespace
 
 // kernel selection bits of launch_g (the split build compiles each part in its own translation unit)
-constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelWide = 8, kSelAll = 15;
+constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelAll = 7;
 
 template <int G, int kSel = kSelAll>
 static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                     int n_steps, bool forward_only, bool primal, bool wide, hipStream_t stream) {
+                     int n_steps, bool forward_only, bool primal, hipStream_t stream) {
   constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
-  const int blocks = (n_envs + kEnvsPerBlock - 1) / kEnvsPerBlock;
+  const int blocks = ((n_envs << st.spread_shift) + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
-  if constexpr (G == 16 && (kSel & kSelWide)) {
-    if (wide && !forward_only) {
-      if (primal)
-        hipLaunchKernelGGL((step_kernel<G, false, true, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream,
-                           d_model, st, n_envs, n_steps);
-      else
-        hipLaunchKernelGGL((step_kernel<G, false, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream,
-                           d_model, st, n_envs, n_steps);
-      return;
-    }
-  }
   if constexpr (G == 16 && (kSel & kSelPrimal)) {
     if (primal && !forward_only) {
       hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st,
@@ -6524,51 +6879,61 @@ int phase_cycles(double* out, int n, bool reset) {
 #ifndef MRS_STEP_PART
 // single translation unit: every instantiation (the variant builds, scripts/build_variant.sh)
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, bool primal, bool wide, hipStream_t stream) {
+                       int n_steps, bool forward_only, int group, bool primal, bool ext, hipStream_t stream) {
+  (void)ext;  // (one translation unit: MRS_EXT as compiled)
   switch (group) {
-    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
-    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
-    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
-    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream); break;
+    case 8: launch_g<8>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 16: launch_g<16>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 32: launch_g<32>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
+    case 64: launch_g<64>(d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 #else
 // split build (build.py): step.hip is compiled once per part, in parallel, each part instantiating
-// only its own kernels; part 0 holds the dispatcher, parts 8 / 16 / 17 (G = 16 primal) / 18 (G = 16,
-// more than 32 ray geoms) / 32 / 64 define launch_part_<n>
+// only its own kernels; part 0 holds the dispatcher.  Parts 16 / 17 (G = 16 primal) / 64 are compiled
+// without the extended code (MRS_EXT 0: the MPR contact polish and the chunked pass of more than 32
+// ray geoms -- their call sites alone cost the inlined G = 16 / 64 phases registers and scratch: C3
+// -1.3% for the ray call site); models that need it run parts 18 (G = 16) / 65 (G = 64), and the
+// G = 8 / 32 parts always carry it
 #define MRS_LAUNCH_ARGS const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs, \
-                        int n_steps, bool forward_only, bool primal, bool wide, hipStream_t stream
-#define MRS_LAUNCH_PASS d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, wide, stream
+                        int n_steps, bool forward_only, bool primal, hipStream_t stream
+#define MRS_LAUNCH_PASS d_model, lds_floats, shared_floats, st, n_envs, n_steps, forward_only, primal, stream
 void launch_part_8(MRS_LAUNCH_ARGS);
 void launch_part_16(MRS_LAUNCH_ARGS);
 void launch_part_17(MRS_LAUNCH_ARGS);
 void launch_part_18(MRS_LAUNCH_ARGS);
 void launch_part_32(MRS_LAUNCH_ARGS);
 void launch_part_64(MRS_LAUNCH_ARGS);
+void launch_part_65(MRS_LAUNCH_ARGS);
 #if MRS_STEP_PART == 0
 hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
-                       int n_steps, bool forward_only, int group, bool primal, bool wide, hipStream_t stream) {
+                       int n_steps, bool forward_only, int group, bool primal, bool ext, hipStream_t stream) {
   switch (group) {
     case 8: launch_part_8(MRS_LAUNCH_PASS); break;
     case 16:
-      if (wide && !forward_only) launch_part_18(MRS_LAUNCH_PASS);
+      if (ext) launch_part_18(MRS_LAUNCH_PASS);
       else if (primal && !forward_only) launch_part_17(MRS_LAUNCH_PASS);
       else launch_part_16(MRS_LAUNCH_PASS);
       break;
     case 32: launch_part_32(MRS_LAUNCH_PASS); break;
-    case 64: launch_part_64(MRS_LAUNCH_PASS); break;
+    case 64:
+      if (ext) launch_part_65(MRS_LAUNCH_PASS);
+      else launch_part_64(MRS_LAUNCH_PASS);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
+#elif MRS_STEP_PART == 16
+void launch_part_16(MRS_LAUNCH_ARGS) { launch_g<16, kSelForward | kSelStep>(MRS_LAUNCH_PASS); }
 #elif MRS_STEP_PART == 17
 void launch_part_17(MRS_LAUNCH_ARGS) { launch_g<16, kSelPrimal>(MRS_LAUNCH_PASS); }
 #elif MRS_STEP_PART == 18
-void launch_part_18(MRS_LAUNCH_ARGS) { launch_g<16, kSelWide>(MRS_LAUNCH_PASS); }
-#elif MRS_STEP_PART == 16
-void launch_part_16(MRS_LAUNCH_ARGS) { launch_g<16, kSelForward | kSelStep>(MRS_LAUNCH_PASS); }
+void launch_part_18(MRS_LAUNCH_ARGS) { launch_g<16>(MRS_LAUNCH_PASS); }
+#elif MRS_STEP_PART == 65
+void launch_part_65(MRS_LAUNCH_ARGS) { launch_g<64>(MRS_LAUNCH_PASS); }
 #else
 #define MRS_PART_FN2(n) launch_part_##n
 #define MRS_PART_FN(n) MRS_PART_FN2(n)

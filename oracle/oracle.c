@@ -15,6 +15,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #include <time.h>
 
@@ -1189,12 +1190,416 @@ static int mpr_penetration(const orc_shape* A, const orc_shape* B, double* depth
     mpr_expand(p, &v4);
   }
 }
+/* ---- MPR contact polish: the exact penetration direction next to MPR's answer (the minimum
+ * translation that EPA, MuJoCo 3.3's native convex collision, converges to; libccd's MPR measures the
+ * depth along its portal direction, which on elongated shapes can be millimetres deeper).
+ * MPR stops once the portal is within mpr_tolerance of the surface of A - B; on a curved surface the
+ * portal's normal is then fixed only to ~sqrt(2 tol / r) (7e-3 rad at r = 4 cm), and which portal fp32
+ * and fp64 stop on differs.  The penetration direction itself is well defined: the minimiser over unit
+ * n of the support function of A - B, h(n) = h_A(n) + h_B(-n) (its minimum is the depth), a convex
+ * problem on the sphere whose solution lies next to MPR's normal.  Each shape is split into a
+ * polyhedral part (vertices: mesh hull, box corners, capsule segment ends, sphere / ellipsoid centre;
+ * for B the vertices of -B) and a smooth part (sphere radius and margin/2 inflation, ellipsoid), so
+ *   h(n) = max_i a_i.n + max_j b'_j.n + h_S(n),  b' = -b,  h_S = (R_A + R_B)|n| + h_EA(n) + h_EB(n).
+ * Active-set Newton from MPR's normal: the active vertices of each polyhedral part (vertex, edge, face)
+ * give the constraints (v_k - v_0).n = 0, Newton on the sphere within them uses the smooth part's
+ * curvature (2-D in the tangent plane; 1-D on the great circle of an edge; none for a face or two skew
+ * edges, whose normal n then is); a step stops where another vertex becomes active (added), and at the
+ * solution the multipliers -- the convex weights of the feature's vertices that make the tangential
+ * gradient vanish -- must be feasible, else the vertex with the negative weight is dropped.  Pairs
+ * without a curved shape (polytope pairs: MPR's portal lies on a face), cylinders (a disk rim is not
+ * smooth), and any iteration that does not settle keep MPR's contact.  Position: midway between the
+ * shapes' contact points (smooth support + the feature point of the weights).  Same steps in fp32 on
+ * the device (csrc/hip/step.hip mpr_polish). */
+#define POL_MAXV 4
+#define POL_PASSES 12
+#define POL_NEWTON 12
+typedef struct {
+  int nv, mesh, ell;
+  double v[8][3];                       /* vertices of the part (non-mesh), world, sign applied */
+  const double *vert, *pos, *mat;       /* mesh hull vertices (local) */
+  const int* hull;
+  double sgn, R, M[9];                  /* sign (+1 A, -1 B), sphere radius, ellipsoid R diag(a^2) R' */
+} pol_part;
+
+static int pol_part_of(const orc_shape* s, double sgn, pol_part* p) {
+  memset(p, 0, sizeof *p);
+  p->sgn = sgn;
+  p->R = s->inflate;
+  const double* z = s->size;
+  double c[3] = {s->pos[0], s->pos[1], s->pos[2]};
+  switch (s->type) {
+    case MRS_GEOM_SPHERE:
+      p->nv = 1; p->R += z[0];
+      for (int i = 0; i < 3; ++i) p->v[0][i] = sgn * c[i];
+      return 1;
+    case MRS_GEOM_CAPSULE:
+      p->nv = 2; p->R += z[0];
+      for (int i = 0; i < 3; ++i) {
+        p->v[0][i] = sgn * (c[i] - s->mat[3 * i + 2] * z[1]);
+        p->v[1][i] = sgn * (c[i] + s->mat[3 * i + 2] * z[1]);
+      }
+      return 1;
+    case MRS_GEOM_ELLIPSOID:
+      p->nv = 1; p->ell = 1;
+      for (int i = 0; i < 3; ++i) p->v[0][i] = sgn * c[i];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          double v = 0;
+          for (int k = 0; k < 3; ++k) v += s->mat[3 * i + k] * z[k] * z[k] * s->mat[3 * j + k];
+          p->M[3 * i + j] = v;
+        }
+      return 1;
+    case MRS_GEOM_BOX:
+      p->nv = 8;
+      for (int k = 0; k < 8; ++k) {
+        double l[3] = {(k & 1) ? z[0] : -z[0], (k & 2) ? z[1] : -z[1], (k & 4) ? z[2] : -z[2]}, x[3];
+        mat_vec(x, s->mat, l);
+        for (int i = 0; i < 3; ++i) p->v[k][i] = sgn * (c[i] + x[i]);
+      }
+      return 1;
+    case MRS_GEOM_MESH:
+      p->nv = s->nhull; p->mesh = 1;
+      p->vert = s->vert; p->hull = s->hull; p->pos = s->pos; p->mat = s->mat;
+      return 1;
+    default:
+      return 0;  /* cylinder: not polished */
+  }
+}
+static void pol_vertex(const pol_part* p, int k, double out[3]) {
+  if (!p->mesh) { for (int i = 0; i < 3; ++i) out[i] = p->v[k][i]; return; }
+  double x[3];
+  mat_vec(x, p->mat, p->vert + 3 * p->hull[k]);
+  for (int i = 0; i < 3; ++i) out[i] = p->sgn * (p->pos[i] + x[i]);
+}
+/* smooth part of one shape (of -B for B): support along n and curvature Hessian (added into H) */
+static void pol_smooth(const pol_part* p, const double n[3], double s[3], double H[9]) {
+  for (int i = 0; i < 3; ++i) s[i] = p->R * n[i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) H[3 * i + j] += p->R * ((i == j) - n[i] * n[j]);
+  if (p->ell) {
+    double Mn[3];
+    mat_vec(Mn, p->M, n);
+    double h = sqrt(dot3(n, Mn));
+    if (h < MINVAL) return;
+    for (int i = 0; i < 3; ++i) s[i] += Mn[i] / h;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) H[3 * i + j] += (p->M[3 * i + j] - Mn[i] * Mn[j] / (h * h)) / h;
+  }
+}
+typedef struct { const pol_part* P[2]; int F[2][POL_MAXV], nf[2]; } pol_state;
+
+/* gradient G = s_S(n) + v_A0 + v_B0 and Hessian of the smooth part at n */
+static void pol_grad(const pol_state* st, const double n[3], double G[3], double H[9], double sS[2][3]) {
+  memset(H, 0, 9 * sizeof(double));
+  for (int i = 0; i < 3; ++i) G[i] = 0;
+  for (int q = 0; q < 2; ++q) {
+    double v0[3];
+    pol_smooth(st->P[q], n, sS[q], H);
+    pol_vertex(st->P[q], st->F[q][0], v0);
+    for (int i = 0; i < 3; ++i) G[i] += sS[q][i] + v0[i];
+  }
+}
+/* orthonormal basis of the feature constraint vectors (v_k - v_0); returns the rank (<= 3) */
+static int pol_basis(const pol_state* st, double Q[3][3]) {
+  int r = 0;
+  for (int q = 0; q < 2; ++q) {
+    double v0[3];
+    pol_vertex(st->P[q], st->F[q][0], v0);
+    for (int k = 1; k < st->nf[q]; ++k) {
+      double e[3];
+      pol_vertex(st->P[q], st->F[q][k], e);
+      for (int i = 0; i < 3; ++i) e[i] -= v0[i];
+      double len = norm3(e);
+      for (int j = 0; j < r; ++j) {
+        double d = dot3(e, Q[j]);
+        for (int i = 0; i < 3; ++i) e[i] -= d * Q[j][i];
+      }
+      double el = norm3(e);
+      if (el <= 1e-9 * len || len < MINVAL) continue;
+      if (r == 3) return 4;
+      for (int i = 0; i < 3; ++i) Q[r][i] = e[i] / el;
+      ++r;
+    }
+  }
+  return r;
+}
+static void pol_tangent(const double n[3], double t1[3], double t2[3]) {
+  double a[3] = {0, 0, 0};
+  a[fabs(n[0]) < 0.6 ? 0 : (fabs(n[1]) < 0.6 ? 1 : 2)] = 1;
+  double d = dot3(a, n);
+  for (int i = 0; i < 3; ++i) t1[i] = a[i] - d * n[i];
+  normalize3(t1);
+  cross3(t2, n, t1);
+}
+/* move n -> normalize(n + dl), stopping at the first vertex that ties with its part's active
+ * vertices; returns 1 when a vertex was added (n moved to the tie), 0 when the full step was taken,
+ * -1 when a feature is full */
+static int pol_move(pol_state* st, double n[3], const double dl[3]) {
+  double tmin = 1;
+  int qmin = -1, kmin = -1;
+  for (int q = 0; q < 2; ++q) {
+    const pol_part* P = st->P[q];
+    double v0[3];
+    pol_vertex(P, st->F[q][0], v0);
+    const double c0 = dot3(v0, n), d0 = dot3(v0, dl);
+    for (int k = 0; k < P->nv; ++k) {
+      int in = 0;
+      for (int f = 0; f < st->nf[q]; ++f) in |= st->F[q][f] == k;
+      if (in) continue;
+      double v[3];
+      pol_vertex(P, k, v);
+      const double c = dot3(v, n) - c0, d = dot3(v, dl) - d0;
+      if (c + d <= 0 || d <= 0) continue;
+      double t = -c / d;
+      if (t < 0) t = 0;
+      if (t < tmin) { tmin = t; qmin = q; kmin = k; }
+    }
+  }
+  for (int i = 0; i < 3; ++i) n[i] += tmin * dl[i];
+  normalize3(n);
+  if (qmin < 0) return 0;
+  if (st->nf[qmin] >= POL_MAXV) return -1;
+  st->F[qmin][st->nf[qmin]++] = kmin;
+  return 1;
+}
+static void pol_drop(pol_state* st, int q, int f) {
+  for (int k = f; k + 1 < st->nf[q]; ++k) st->F[q][k] = st->F[q][k + 1];
+  --st->nf[q];
+}
+/* convex weights of the feature vertices (beyond each part's anchor) that make the tangential
+ * gradient vanish; returns 1 feasible (w filled, per part, for vertices 1..nf-1), 0 after dropping a
+ * vertex, -1 when the case is not handled */
+static int pol_kkt(pol_state* st, const double n[3], const double G[3], double w[2][POL_MAXV]) {
+  double t1[3], t2[3];
+  pol_tangent(n, t1, t2);
+  int m = st->nf[0] + st->nf[1] - 2;
+  memset(w, 0, 2 * POL_MAXV * sizeof(double));
+  if (m == 0) return 1;
+  /* columns: the constraint vectors, tangential components */
+  double E[6][2];
+  int cq[6], cf[6], nc = 0;
+  for (int q = 0; q < 2; ++q) {
+    double v0[3];
+    pol_vertex(st->P[q], st->F[q][0], v0);
+    for (int f = 1; f < st->nf[q]; ++f) {
+      double e[3];
+      pol_vertex(st->P[q], st->F[q][f], e);
+      for (int i = 0; i < 3; ++i) e[i] -= v0[i];
+      E[nc][0] = dot3(e, t1); E[nc][1] = dot3(e, t2);
+      cq[nc] = q; cf[nc] = f; ++nc;
+    }
+  }
+  const double g1 = dot3(G, t1), g2 = dot3(G, t2);
+  if (m == 1) {
+    const double el = sqrt(E[0][0] * E[0][0] + E[0][1] * E[0][1]);
+    if (el < MINVAL) return -1;
+    const double x = -(g1 * E[0][0] + g2 * E[0][1]) / (el * el);
+    if (x < 0) { pol_drop(st, cq[0], cf[0]); return 0; }
+    if (x > 1) { pol_drop(st, cq[0], 0); return 0; }
+    w[cq[0]][cf[0]] = x;
+    return 1;
+  }
+  if (m == 2) {
+    const double det = E[0][0] * E[1][1] - E[1][0] * E[0][1];
+    if (fabs(det) < MINVAL) return -1;
+    const double x0 = (-g1 * E[1][1] + g2 * E[1][0]) / det, x1 = (-g2 * E[0][0] + g1 * E[0][1]) / det;
+    if (cq[0] == cq[1]) {  /* a triangle of one part: barycentric (1 - x0 - x1, x0, x1) */
+      const double x2 = 1 - x0 - x1;
+      const double worst = fmin(x2, fmin(x0, x1));
+      if (worst < 0) {
+        pol_drop(st, cq[0], worst == x0 ? cf[0] : (worst == x1 ? cf[1] : 0));
+        return 0;
+      }
+    } else {               /* an edge of each part */
+      const double v0 = fmin(x0, 1 - x0), v1 = fmin(x1, 1 - x1);
+      if (v0 < 0 || v1 < 0) {
+        const int c = v0 <= v1 ? 0 : 1;
+        const double x = c == 0 ? x0 : x1;
+        pol_drop(st, cq[c], x < 0 ? cf[c] : 0);
+        return 0;
+      }
+    }
+    w[cq[0]][cf[0]] = x0;
+    w[cq[1]][cf[1]] = x1;
+    return 1;
+  }
+  if (m == 3 && (st->nf[0] == 1 || st->nf[1] == 1)) {
+    /* a coplanar quad of one part: the point lies in one of its triangles (Caratheodory) */
+    const int q = cq[0];
+    for (int a = 0; a < 3; ++a)
+      for (int b = a + 1; b < 3; ++b) {
+        /* triangle (anchor, a, b) */
+        const double det = E[a][0] * E[b][1] - E[b][0] * E[a][1];
+        if (fabs(det) < MINVAL) continue;
+        const double x0 = (-g1 * E[b][1] + g2 * E[b][0]) / det, x1 = (-g2 * E[a][0] + g1 * E[a][1]) / det;
+        if (x0 >= 0 && x1 >= 0 && x0 + x1 <= 1) { w[q][cf[a]] = x0; w[q][cf[b]] = x1; return 1; }
+      }
+    /* triangle (a, b, c) without the anchor: x_a + x_b + x_c = 1 */
+    {
+      const double det = E[1][0] * E[2][1] - E[2][0] * E[1][1] - (E[0][0] * E[2][1] - E[2][0] * E[0][1]) +
+                         (E[0][0] * E[1][1] - E[1][0] * E[0][1]);
+      if (fabs(det) > MINVAL) {
+        /* solve [E0 E1 E2; 1 1 1] x = [-g; 1] by Cramer */
+        double A3[9] = {E[0][0], E[1][0], E[2][0], E[0][1], E[1][1], E[2][1], 1, 1, 1}, rhs[3] = {-g1, -g2, 1}, x[3];
+        for (int c = 0; c < 3; ++c) {
+          double B3[9];
+          memcpy(B3, A3, sizeof B3);
+          for (int r = 0; r < 3; ++r) B3[3 * r + c] = rhs[r];
+          x[c] = (B3[0] * (B3[4] * B3[8] - B3[5] * B3[7]) - B3[1] * (B3[3] * B3[8] - B3[5] * B3[6]) +
+                  B3[2] * (B3[3] * B3[7] - B3[4] * B3[6])) /
+                 (A3[0] * (A3[4] * A3[8] - A3[5] * A3[7]) - A3[1] * (A3[3] * A3[8] - A3[5] * A3[6]) +
+                  A3[2] * (A3[3] * A3[7] - A3[4] * A3[6]));
+        }
+        if (x[0] >= 0 && x[1] >= 0 && x[2] >= 0) {
+          w[q][cf[0]] = x[0]; w[q][cf[1]] = x[1]; w[q][cf[2]] = x[2];
+          return 1;
+        }
+      }
+    }
+    return -1;
+  }
+  return -1;
+}
+/* returns 1 with the polished depth / normal / position, 0 to keep MPR's */
+static int pol_debug = -1;
+#define POL_FAIL(c)                                                                        \
+  do {                                                                                     \
+    if (pol_debug < 0) pol_debug = getenv("ORC_POLISH_DEBUG") != NULL;                     \
+    if (pol_debug) fprintf(stderr, "polish fallback %d (types %d %d)\n", c, A->type, B->type); \
+    return 0;                                                                              \
+  } while (0)
+static int mpr_polish(const orc_shape* A, const orc_shape* B, const double n0[3], double mpr_depth, double* depth,
+                      double nrm[3], double pos[3]) {
+  if (A->type == MRS_GEOM_CYLINDER || B->type == MRS_GEOM_CYLINDER) POL_FAIL(1);
+  const int curvedA = A->type == MRS_GEOM_SPHERE || A->type == MRS_GEOM_CAPSULE || A->type == MRS_GEOM_ELLIPSOID;
+  const int curvedB = B->type == MRS_GEOM_SPHERE || B->type == MRS_GEOM_CAPSULE || B->type == MRS_GEOM_ELLIPSOID;
+  if (!curvedA && !curvedB) POL_FAIL(2);
+  pol_part PA, PB;
+  if (!pol_part_of(A, 1, &PA) || !pol_part_of(B, -1, &PB)) POL_FAIL(3);
+  pol_state st;
+  st.P[0] = &PA; st.P[1] = &PB;
+  double n[3] = {n0[0], n0[1], n0[2]};
+  for (int q = 0; q < 2; ++q) {
+    double best = -1e300;
+    st.nf[q] = 1;
+    for (int k = 0; k < st.P[q]->nv; ++k) {
+      double v[3];
+      pol_vertex(st.P[q], k, v);
+      const double d = dot3(v, n);
+      if (d > best) { best = d; st.F[q][0] = k; }
+    }
+  }
+  double G[3], H[9], sS[2][3], w[2][POL_MAXV];
+  int done = 0;
+  for (int pass = 0; pass < POL_PASSES && !done; ++pass) {
+    double Q[3][3];
+    const int rank = pol_basis(&st, Q);
+    if (rank > 2) {
+      /* the step stopped where a third independent vertex tied: n is fixed by any two of the
+       * constraints; accept the first single-vertex drop whose feature is optimal at n */
+      pol_grad(&st, n, G, H, sS);
+      int found = 0;
+      for (int q = 0; q < 2 && !found; ++q)
+        for (int f = 0; f < st.nf[q] && !found; ++f) {
+          pol_state t = st;
+          pol_drop(&t, q, f);
+          double Qt[3][3];
+          if (pol_basis(&t, Qt) != 2) continue;
+          double Gt[3], Ht[9], sSt[2][3];
+          pol_grad(&t, n, Gt, Ht, sSt);
+          if (pol_kkt(&t, n, Gt, w) == 1) { st = t; found = 1; memcpy(G, Gt, sizeof Gt); memcpy(sS, sSt, sizeof sSt); }
+        }
+      if (!found) POL_FAIL(4);
+      done = 1;
+      break;
+    }
+    int moved = 0, conv = 0;
+    if (rank == 2) {
+      double t[3], dl[3];
+      cross3(t, Q[0], Q[1]);
+      normalize3(t);
+      if (dot3(t, n) < 0) for (int i = 0; i < 3; ++i) t[i] = -t[i];
+      for (int i = 0; i < 3; ++i) dl[i] = t[i] - n[i];
+      const int r = pol_move(&st, n, dl);
+      if (r < 0) POL_FAIL(5);
+      moved = r;
+      conv = !r;
+    } else {
+      for (int it = 0; it < POL_NEWTON; ++it) {
+        pol_grad(&st, n, G, H, sS);
+        const double lam = dot3(G, n);
+        double dl[3];
+        if (rank == 0) {
+          double t1[3], t2[3], Ht1[3], Ht2[3];
+          pol_tangent(n, t1, t2);
+          mat_vec(Ht1, H, t1);
+          mat_vec(Ht2, H, t2);
+          const double a11 = dot3(t1, Ht1) - lam, a22 = dot3(t2, Ht2) - lam, a12 = dot3(t1, Ht2);
+          const double det = a11 * a22 - a12 * a12;
+          if (!(a11 > 0 && det > 0)) POL_FAIL(6);
+          const double b1 = -dot3(G, t1), b2 = -dot3(G, t2);
+          const double x1 = (b1 * a22 - b2 * a12) / det, x2 = (b2 * a11 - b1 * a12) / det;
+          for (int i = 0; i < 3; ++i) dl[i] = x1 * t1[i] + x2 * t2[i];
+        } else {
+          /* great circle orthogonal to Q[0] through n */
+          double d = dot3(n, Q[0]);
+          for (int i = 0; i < 3; ++i) n[i] -= d * Q[0][i];
+          normalize3(n);
+          pol_grad(&st, n, G, H, sS);
+          const double lm = dot3(G, n);
+          double t[3], Ht[3];
+          cross3(t, Q[0], n);
+          mat_vec(Ht, H, t);
+          const double f2 = dot3(t, Ht) - lm;
+          if (!(f2 > 0)) POL_FAIL(7);
+          const double th = -dot3(G, t) / f2;
+          for (int i = 0; i < 3; ++i) dl[i] = th * t[i];
+        }
+        const double step = norm3(dl);
+        const int r = pol_move(&st, n, dl);
+        if (r < 0) POL_FAIL(8);
+        if (r > 0) { moved = 1; break; }
+        if (step < 1e-13) { conv = 1; break; }
+      }
+    }
+    if (moved) continue;
+    if (!conv) POL_FAIL(9);
+    pol_grad(&st, n, G, H, sS);
+    const int k = pol_kkt(&st, n, G, w);
+    if (k < 0) POL_FAIL(10);
+    done = k == 1;
+  }
+  if (!done) POL_FAIL(11);
+  /* sanity: next to MPR's answer */
+  double dp = dot3(G, n);
+  /* a local minimiser next to MPR's normal, never deeper than MPR's portal distance (MPR measures
+   * along the direction its portal search found, the polish minimises over directions) */
+  if (dot3(n, n0) < 0.8 || !(dp > 0) || dp > mpr_depth + MPR_TOL) POL_FAIL(12);
+  double pA[3], pB[3], v0[3], e[3];
+  for (int q = 0; q < 2; ++q) {
+    double* pt = q ? pB : pA;
+    pol_vertex(st.P[q], st.F[q][0], v0);
+    for (int i = 0; i < 3; ++i) pt[i] = v0[i] + sS[q][i];
+    for (int f = 1; f < st.nf[q]; ++f) {
+      pol_vertex(st.P[q], st.F[q][f], e);
+      for (int i = 0; i < 3; ++i) pt[i] += w[q][f] * (e[i] - v0[i]);
+    }
+  }
+  *depth = dp;
+  for (int i = 0; i < 3; ++i) { nrm[i] = n[i]; pos[i] = 0.5 * (pA[i] - pB[i]); }
+  return 1;
+}
+
 static int col_convex(const mrs_model_view* m, orc_ws* w, int g1, int g2, double margin, orc_contact* out, int n) {
   orc_shape A, B;
   shape_of(m, w, g1, margin, &A);
   shape_of(m, w, g2, margin, &B);
   double depth, nrm[3], pos[3];
   if (!mpr_penetration(&A, &B, &depth, nrm, pos)) return n;
+  static int no_polish = -1;  /* diagnostics: ORC_NO_POLISH=1 keeps MPR's contact (scripts/diag_mpr.py) */
+  if (no_polish < 0) no_polish = getenv("ORC_NO_POLISH") != NULL;
+  if (!no_polish) mpr_polish(&A, &B, nrm, depth, &depth, nrm, pos);
   return add_contact(out, n, margin - depth, pos, nrm);
 }
 /* plane (geom1) vs ellipsoid: the support point along -normal (mjc_PlaneEllipsoid) */
