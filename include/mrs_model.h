@@ -134,6 +134,15 @@ typedef struct mrs_model_view {
   const int *geom_dataid, *mesh_vertadr, *mesh_vertnum, *mesh_faceadr, *mesh_facenum, *mesh_hulladr,
       *mesh_hullnum, *mesh_face, *mesh_hull;
   const double *mesh_vert;
+
+  /* explicit <contact><pair> (mjModel npair / pair_*): collided before the candidate pairs above,
+   * whatever contype/conaffinity and the body filters say, with their own parameters (attributes the
+   * pair omits are mixed from its geoms as for candidate pairs); geom1 has the lower type.  And
+   * <contact><exclude> body pairs (mjModel exclude_signature), which -- like the bodies of an
+   * explicit pair -- the candidate list above already leaves out. */
+  int nexpair, nexclude;
+  const int *expair_geom1, *expair_geom2, *expair_dim, *exclude_body1, *exclude_body2;
+  const double *expair_friction /*5*/, *expair_solref /*2*/, *expair_solimp /*5*/, *expair_margin, *expair_gap;
 } mrs_model_view;
 
 #ifdef __cplusplus

@@ -1016,6 +1016,25 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   std::vector<int> pg1, pg2, pdim;
   std::vector<float> pmargin, pgap, pfric, psolref, psolimp;
   {
+    // explicit <contact><pair>s first, with their own parameters (mj_collision collides them before
+    // the dynamic pairs; mrs::Model::expair_*)
+    for (size_t q = 0; q < m.expair_geom1.size(); ++q) {
+      const int ga = m.expair_geom1[q], gb = m.expair_geom2[q];
+      const int ta = m.geom_type[ga], tb = m.geom_type[gb];
+      if ((ta == MRS_GEOM_PLANE && tb == MRS_GEOM_PLANE) || ta == MRS_GEOM_HFIELD || tb == MRS_GEOM_HFIELD)
+        throw UnsupportedError("explicit pair of geom types " + std::to_string(ta) + "/" + std::to_string(tb) +
+                               " is not implemented");
+      pg1.push_back(ga); pg2.push_back(gb);
+      pdim.push_back(m.expair_dim[q]);
+      pmargin.push_back(static_cast<float>(m.expair_margin[q]));
+      pgap.push_back(static_cast<float>(m.expair_gap[q]));
+      // (sliding, torsional, rolling) as the mixed pairs store them
+      pfric.push_back(static_cast<float>(m.expair_friction[5 * q]));
+      pfric.push_back(static_cast<float>(m.expair_friction[5 * q + 2]));
+      pfric.push_back(static_cast<float>(m.expair_friction[5 * q + 3]));
+      for (int i = 0; i < 2; ++i) psolref.push_back(static_cast<float>(m.expair_solref[2 * q + i]));
+      for (int i = 0; i < 5; ++i) psolimp.push_back(static_cast<float>(m.expair_solimp[5 * q + i]));
+    }
     // the compiler's statically admissible pairs (mrs::Model::pair_geom1/2, lower geom type first)
     for (size_t q = 0; q < m.pair_geom1.size(); ++q) {
         const int ga = m.pair_geom1[q], gb = m.pair_geom2[q];
@@ -1644,8 +1663,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // that is not plane-* and has an ellipsoid, cylinder or mesh (narrowphase's analytic routines cover
   // the rest) -- or rangefinders over more than 32 ray geoms
   b.ext = d.nrgeom > 32 && d.nrf > 0;
-  for (size_t p = 0; p < m.pair_geom1.size() && !b.ext; ++p) {
-    const int t1 = m.geom_type[m.pair_geom1[p]], t2 = m.geom_type[m.pair_geom2[p]];
+  for (size_t p = 0; p < b.pair_g1.size() && !b.ext; ++p) {
+    const int t1 = m.geom_type[b.pair_g1[p]], t2 = m.geom_type[b.pair_g2[p]];
     auto conv = [](int t) { return t == MRS_GEOM_ELLIPSOID || t == MRS_GEOM_CYLINDER || t == MRS_GEOM_MESH; };
     if (t1 != MRS_GEOM_PLANE && t2 != MRS_GEOM_PLANE && (conv(t1) || conv(t2))) b.ext = true;
   }

@@ -1711,12 +1711,72 @@ struct Compiler {
       else if (c->tag == "keyframe") parse_keyframes(c.get());
       else if (c->tag == "equality" || c->tag == "tendon")
         { if (!c->children.empty()) fail(c.get(), "equality constraints and tendons are not supported"); }
-      else if (c->tag == "contact") {
-        if (!c->children.empty()) fail(c.get(), "explicit <contact> pairs/excludes are not supported");
-      }
+      else if (c->tag == "contact") parse_contact(c.get());
     }
     candidate_pairs();
     return std::move(m);
+  }
+  // <contact>: explicit geom pairs and excluded body pairs [upstream mjCPair / mjCBodyPair].  A pair's
+  // omitted attributes take the values a candidate pair of its geoms would (max condim and friction,
+  // solmix-weighted solref / solimp, max margin and gap); friction has MuJoCo's 5 components, of which
+  // the pyramidal / elliptic rows use the sliding one (both sliding values must agree).
+  void parse_contact(const XmlElement* sec) {
+    for (auto& cp : sec->children) {
+      const XmlElement* e = cp.get();
+      const DefaultClass* cls = resolve_class(e, "");
+      if (e->tag == "exclude") {
+        std::string n1, n2;
+        if (!get_str(e, cls, "exclude", "body1", n1) || !get_str(e, cls, "exclude", "body2", n2))
+          fail(e, "exclude requires body1 and body2");
+        const int b1 = m.name2id(MRS_OBJ_BODY, n1), b2 = m.name2id(MRS_OBJ_BODY, n2);
+        if (b1 < 0 || b2 < 0) fail(e, "exclude references an unknown body");
+        m.exclude_body1.push_back(std::min(b1, b2));
+        m.exclude_body2.push_back(std::max(b1, b2));
+      } else if (e->tag == "pair") {
+        std::string n1, n2;
+        if (!get_str(e, cls, "pair", "geom1", n1) || !get_str(e, cls, "pair", "geom2", n2))
+          fail(e, "pair requires geom1 and geom2");
+        int g1 = m.name2id(MRS_OBJ_GEOM, n1), g2 = m.name2id(MRS_OBJ_GEOM, n2);
+        if (g1 < 0 || g2 < 0) fail(e, "pair references an unknown geom");
+        if (g1 == g2) fail(e, "pair of a geom with itself");
+        if (m.geom_type[g1] > m.geom_type[g2]) std::swap(g1, g2);
+        // the candidate-pair mixing of the two geoms, then the pair's own attributes on top
+        double s1 = m.geom_solmix[g1], s2 = m.geom_solmix[g2], mix;
+        if (s1 >= 1e-15 && s2 >= 1e-15) mix = s1 / (s1 + s2);
+        else if (s1 < 1e-15 && s2 < 1e-15) mix = 0.5;
+        else mix = s1 < 1e-15 ? 0 : 1;
+        int dim = std::max(m.geom_condim[g1], m.geom_condim[g2]);
+        double fr[5], sr[2], si[5], mg = std::max(m.geom_margin[g1], m.geom_margin[g2]);
+        double gp = std::max(m.geom_gap[g1], m.geom_gap[g2]);
+        const double f3[3] = {std::max(m.geom_friction[3 * g1], m.geom_friction[3 * g2]),
+                              std::max(m.geom_friction[3 * g1 + 1], m.geom_friction[3 * g2 + 1]),
+                              std::max(m.geom_friction[3 * g1 + 2], m.geom_friction[3 * g2 + 2])};
+        fr[0] = fr[1] = f3[0]; fr[2] = f3[1]; fr[3] = fr[4] = f3[2];
+        for (int i = 0; i < 2; ++i) sr[i] = mix * m.geom_solref[2 * g1 + i] + (1 - mix) * m.geom_solref[2 * g2 + i];
+        for (int i = 0; i < 5; ++i) si[i] = mix * m.geom_solimp[5 * g1 + i] + (1 - mix) * m.geom_solimp[5 * g2 + i];
+        get_int(e, cls, "pair", "condim", dim);
+        if (dim != 1 && dim != 3) fail(e, "only condim 1 and 3 are supported");
+        get_reals(e, cls, "pair", "friction", fr, 5);
+        if (fr[0] != fr[1]) fail(e, "anisotropic pair friction (sliding1 != sliding2) is not supported");
+        get_reals(e, cls, "pair", "solref", sr, 2, true);
+        get_reals(e, cls, "pair", "solimp", si, 5);
+        double srf[2] = {0, 0};
+        if (get_reals(e, cls, "pair", "solreffriction", srf, 2, true) && (srf[0] != 0 || srf[1] != 0))
+          fail(e, "pair solreffriction is not supported");
+        get_real(e, cls, "pair", "margin", mg);
+        get_real(e, cls, "pair", "gap", gp);
+        m.expair_geom1.push_back(g1);
+        m.expair_geom2.push_back(g2);
+        m.expair_dim.push_back(dim);
+        m.expair_friction.insert(m.expair_friction.end(), fr, fr + 5);
+        m.expair_solref.insert(m.expair_solref.end(), sr, sr + 2);
+        m.expair_solimp.insert(m.expair_solimp.end(), si, si + 5);
+        m.expair_margin.push_back(mg);
+        m.expair_gap.push_back(gp);
+      } else {
+        fail(e, "unsupported contact element");
+      }
+    }
   }
   // Static part of mj_collision's broad phase [upstream engine_collision_driver.c mj_collideGeoms /
   // filterBitmask]: geom pairs of different weld groups, not parent-child welds (unless the
@@ -1726,7 +1786,11 @@ struct Compiler {
   void candidate_pairs() {
     m.pair_geom1.clear();
     m.pair_geom2.clear();
-    if (m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) return;
+    if (m.disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) {
+      m.expair_geom1.clear(); m.expair_geom2.clear(); m.expair_dim.clear(); m.expair_friction.clear();
+      m.expair_solref.clear(); m.expair_solimp.clear(); m.expair_margin.clear(); m.expair_gap.clear();
+      return;
+    }
     for (int g1 = 0; g1 < m.ngeom; ++g1)
       for (int g2 = g1 + 1; g2 < m.ngeom; ++g2) {
         const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
@@ -1737,6 +1801,16 @@ struct Compiler {
           continue;
         if (!((m.geom_contype[g1] & m.geom_conaffinity[g2]) || (m.geom_contype[g2] & m.geom_conaffinity[g1])))
           continue;
+        // body pairs excluded, or covered by an explicit pair (mjModel exclude / pair signatures)
+        const int lo = std::min(b1, b2), hi = std::max(b1, b2);
+        bool skip = false;
+        for (size_t k = 0; k < m.exclude_body1.size() && !skip; ++k)
+          skip = m.exclude_body1[k] == lo && m.exclude_body2[k] == hi;
+        for (size_t k = 0; k < m.expair_geom1.size() && !skip; ++k) {
+          const int e1 = m.geom_bodyid[m.expair_geom1[k]], e2 = m.geom_bodyid[m.expair_geom2[k]];
+          skip = std::min(e1, e2) == lo && std::max(e1, e2) == hi;
+        }
+        if (skip) continue;
         const bool swap = m.geom_type[g1] > m.geom_type[g2];
         m.pair_geom1.push_back(swap ? g2 : g1);
         m.pair_geom2.push_back(swap ? g1 : g2);
@@ -1828,6 +1902,10 @@ mrs_model_view Model::view() const {
   v.nmeshhull = static_cast<int>(mesh_hull.size());
   MRS_V(geom_dataid); MRS_V(mesh_vertadr); MRS_V(mesh_vertnum); MRS_V(mesh_faceadr); MRS_V(mesh_facenum);
   MRS_V(mesh_hulladr); MRS_V(mesh_hullnum); MRS_V(mesh_face); MRS_V(mesh_hull); MRS_V(mesh_vert);
+  v.nexpair = static_cast<int>(expair_geom1.size());
+  v.nexclude = static_cast<int>(exclude_body1.size());
+  MRS_V(expair_geom1); MRS_V(expair_geom2); MRS_V(expair_dim); MRS_V(exclude_body1); MRS_V(exclude_body2);
+  MRS_V(expair_friction); MRS_V(expair_solref); MRS_V(expair_solimp); MRS_V(expair_margin); MRS_V(expair_gap);
 #undef MRS_V
   return v;
 }

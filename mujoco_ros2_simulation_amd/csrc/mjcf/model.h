@@ -64,6 +64,9 @@ struct Model {
   std::vector<double> mesh_vert;
   // statically admissible collision pairs (mj_collision's broad-phase filters), lower geom type first
   std::vector<int> pair_geom1, pair_geom2;
+  // explicit <contact><pair> (own parameters) and <contact><exclude> body pairs (mrs_model_view)
+  std::vector<int> expair_geom1, expair_geom2, expair_dim, exclude_body1, exclude_body2;
+  std::vector<double> expair_friction, expair_solref, expair_solimp, expair_margin, expair_gap;
 
   // names per object type (MRS_OBJ_*), index = object id
   std::map<int, std::vector<std::string>> names;

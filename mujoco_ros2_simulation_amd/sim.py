@@ -95,6 +95,14 @@ _MESH_ARRAYS = [
     ("mesh_hullnum", "i", "nmesh", 1), ("mesh_face", "i", "nmeshface", 3), ("mesh_hull", "i", "nmeshhull", 1),
     ("mesh_vert", "d", "nmeshvert", 3),
 ]
+# explicit contact pairs and excluded body pairs (after the mesh block)
+_CONTACT_SIZES = ["nexpair", "nexclude"]
+_CONTACT_ARRAYS = [
+    ("expair_geom1", "i", "nexpair", 1), ("expair_geom2", "i", "nexpair", 1), ("expair_dim", "i", "nexpair", 1),
+    ("exclude_body1", "i", "nexclude", 1), ("exclude_body2", "i", "nexclude", 1),
+    ("expair_friction", "d", "nexpair", 5), ("expair_solref", "d", "nexpair", 2), ("expair_solimp", "d", "nexpair", 5),
+    ("expair_margin", "d", "nexpair", 1), ("expair_gap", "d", "nexpair", 1),
+]
 
 
 class ModelView(C.Structure):
@@ -107,7 +115,9 @@ class ModelView(C.Structure):
                  ("vis_znear", C.c_double), ("vis_zfar", C.c_double)] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _ARRAYS] +
                 [(n, C.c_int) for n in _MESH_SIZES] +
-                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _MESH_ARRAYS])
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _MESH_ARRAYS] +
+                [(n, C.c_int) for n in _CONTACT_SIZES] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _CONTACT_ARRAYS])
 
 
 _lib = None
@@ -194,14 +204,14 @@ class Model:
         self.view = ModelView()
         _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
         v = self.view
-        for n in _SIZES + _MESH_SIZES:
+        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES:
             setattr(self, n, getattr(v, n))
         for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "restate", "integrator", "solver",
                   "iterations", "disableflags",
                   "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
             setattr(self, n, getattr(v, n))
         self.gravity = np.array(v.gravity[:])
-        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS:
+        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS:
             n = getattr(v, count)
             w = getattr(v, width) if isinstance(width, str) else width
             ptr = getattr(v, name)

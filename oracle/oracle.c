@@ -1724,7 +1724,18 @@ static int pair_admissible(const mrs_model_view* m, int g1, int g2) {
   if (!(m->disableflags & MRS_DSBL_FILTERPARENT) && w1 != 0 && w2 != 0 &&
       (w1 == m->body_weldid[m->body_parentid[w2]] || w2 == m->body_weldid[m->body_parentid[w1]]))
     return 0;
-  return (m->geom_contype[g1] & m->geom_conaffinity[g2]) || (m->geom_contype[g2] & m->geom_conaffinity[g1]);
+  if (!((m->geom_contype[g1] & m->geom_conaffinity[g2]) || (m->geom_contype[g2] & m->geom_conaffinity[g1])))
+    return 0;
+  /* body pairs excluded by <contact><exclude>, or covered by an explicit <pair> [upstream: the
+   * exclude / pair signatures filter dynamic body pairs; verify] */
+  const int lo = b1 < b2 ? b1 : b2, hi = b1 < b2 ? b2 : b1;
+  for (int k = 0; k < m->nexclude; ++k)
+    if (m->exclude_body1[k] == lo && m->exclude_body2[k] == hi) return 0;
+  for (int k = 0; k < m->nexpair; ++k) {
+    const int e1 = m->geom_bodyid[m->expair_geom1[k]], e2 = m->geom_bodyid[m->expair_geom2[k]];
+    if ((e1 < e2 ? e1 : e2) == lo && (e1 < e2 ? e2 : e1) == hi) return 0;
+  }
+  return 1;
 }
 
 int orc_candidate_pairs(const mrs_model_view* m, int max, int* geom1, int* geom2) {
@@ -1747,6 +1758,30 @@ static void collision(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   w->ncon = 0;
   if (m->disableflags & (MRS_DSBL_CONTACT | MRS_DSBL_CONSTRAINT)) return;
+  /* explicit <contact><pair>s first, with their own parameters (geom1 has the lower type) */
+  for (int k = 0; k < m->nexpair; ++k) {
+    const int ga = m->expair_geom1[k], gb = m->expair_geom2[k];
+    const double margin = m->expair_margin[k], gap = m->expair_gap[k];
+    if (m->geom_type[ga] != MRS_GEOM_PLANE && m->geom_type[gb] != MRS_GEOM_PLANE) {
+      double dv[3];
+      for (int i = 0; i < 3; ++i) dv[i] = w->geom_xpos[3 * ga + i] - w->geom_xpos[3 * gb + i];
+      if (norm3(dv) > m->geom_rbound[ga] + m->geom_rbound[gb] + margin) continue;
+    }
+    orc_contact tmp[8];
+    const int nc = narrowphase(m, w, ga, gb, margin, tmp);
+    for (int c = 0; c < nc && w->ncon < MAXCON; ++c) {
+      orc_contact* o = &w->con[w->ncon++];
+      *o = tmp[c];
+      o->geom[0] = ga; o->geom[1] = gb;
+      o->dim = m->expair_dim[k];
+      o->friction[0] = m->expair_friction[5 * k];
+      o->friction[1] = m->expair_friction[5 * k + 2];
+      o->friction[2] = m->expair_friction[5 * k + 3];
+      for (int i = 0; i < 2; ++i) o->solref[i] = m->expair_solref[2 * k + i];
+      for (int i = 0; i < 5; ++i) o->solimp[i] = m->expair_solimp[5 * k + i];
+      o->includemargin = margin - gap;
+    }
+  }
   for (int g1 = 0; g1 < m->ngeom; ++g1)
     for (int g2 = g1 + 1; g2 < m->ngeom; ++g2) {
       if (!pair_admissible(m, g1, g2)) continue;

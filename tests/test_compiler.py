@@ -216,3 +216,34 @@ def test_bench_solver_override():
     assert 'solver="Newton"' in out and 'solver="PGS"' not in out and 'iterations="50"' in out
     bare = "<mujoco><worldbody/></mujoco>"
     assert '<option solver="CG"/>' in bench.with_solver(bare, "CG")
+
+
+def test_contact_pairs_and_excludes():
+    """<contact><pair>: geom order (lower type first), omitted attributes mixed from the geoms,
+    <default><pair> classes, 5-component friction; <exclude> and the bodies of explicit pairs leave
+    the candidate list; the oracle's own broad-phase filter lists the same candidates"""
+    import binding
+    from mujoco_ros2_simulation_amd import sim
+    xml = """<mujoco><default><pair solref="0.01 1"/></default><worldbody>
+      <geom name="floor" type="plane" size="0 0 1" friction="0.8 0.01 0.001"/>
+      <body name="a"><freejoint/><geom name="ga" type="box" size="0.1 0.1 0.1" friction="0.6 0.02 0.002"/>
+        <geom name="ga2" type="sphere" size="0.05" pos="0 0 0.2"/></body>
+      <body name="b" pos="1 0 0"><freejoint/><geom name="gb" type="sphere" size="0.1"/></body>
+      <body name="c" pos="2 0 0"><freejoint/><geom name="gc" type="capsule" size="0.1 0.2"/></body>
+    </worldbody><contact><pair geom1="ga" geom2="floor"/><pair geom1="gc" geom2="gb" condim="1" margin="0.01"
+      friction="0.3 0.3 0.1 0.01 0.01" solref="0.05 2"/><exclude body1="c" body2="a"/></contact></mujoco>"""
+    m = sim.Model.from_string(xml)
+    assert m.nexpair == 2 and m.nexclude == 1
+    assert list(m.expair_geom1) == [0, 3] and list(m.expair_geom2) == [1, 4]  # plane < box; sphere < capsule
+    np.testing.assert_allclose(m.expair_friction[0], [0.8, 0.8, 0.02, 0.002, 0.002])
+    np.testing.assert_allclose(m.expair_solref, [[0.01, 1], [0.05, 2]])
+    assert list(m.expair_dim) == [3, 1] and m.expair_margin[1] == 0.01
+    cands = {(int(a), int(b)) for a, b in zip(m.pair_geom1, m.pair_geom2)}
+    # body pairs world-a (explicit floor-box pair: floor-ga2 goes too), a-c (excluded) and b-c
+    # (explicit) are gone; sphere-box stored sphere first
+    assert cands == {(0, 3), (0, 4), (3, 1), (2, 3)}
+    assert {tuple(sorted(p)) for p in binding.candidate_pairs(m).tolist()} == {tuple(sorted(p)) for p in cands}
+    for bad in ['<pair geom1="ga" geom2="nope"/>', '<pair geom1="ga" geom2="gb" friction="0.5 0.4"/>',
+                '<exclude body1="a"/>', '<pair geom1="ga" geom2="gb" condim="6"/>']:
+        with pytest.raises(sim.MrsError):
+            sim.Model.from_string(xml.replace('<exclude body1="c" body2="a"/>', bad))
