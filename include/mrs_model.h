@@ -32,6 +32,8 @@ enum { MRS_JNT_FREE = 0, MRS_JNT_BALL = 1, MRS_JNT_SLIDE = 2, MRS_JNT_HINGE = 3 
 enum { MRS_INT_EULER = 0, MRS_INT_RK4 = 1, MRS_INT_IMPLICIT = 2, MRS_INT_IMPLICITFAST = 3 };
 enum { MRS_SOL_PGS = 0, MRS_SOL_CG = 1, MRS_SOL_NEWTON = 2 };
 enum { MRS_CONE_PYRAMIDAL = 0, MRS_CONE_ELLIPTIC = 1 };  /* mjtCone */
+enum { MRS_EQ_CONNECT = 0, MRS_EQ_WELD = 1, MRS_EQ_JOINT = 2 };  /* mjtEq subset */
+#define MRS_NEQDATA 11
 enum { MRS_TRN_JOINT = 0 };
 enum { MRS_DYN_NONE = 0 };
 enum { MRS_GAIN_FIXED = 0, MRS_GAIN_AFFINE = 1 };
@@ -143,6 +145,16 @@ typedef struct mrs_model_view {
   int nexpair, nexclude;
   const int *expair_geom1, *expair_geom2, *expair_dim, *exclude_body1, *exclude_body2;
   const double *expair_friction /*5*/, *expair_solref /*2*/, *expair_solimp /*5*/, *expair_margin, *expair_gap;
+
+  /* equality constraints (mjModel neq / eq_*; MRS_EQ_*): obj1 / obj2 are bodies (connect, weld; obj2
+   * 0 = world) or joints (joint; obj2 -1 = none).  eq_data [neq][11]:
+   *   connect: anchor in body1's frame (0:3), the same point in body2's frame at qpos0 (3:6);
+   *   weld:    anchor in body2's frame (0:3), body2's pose in body1's frame: pos (3:6), quat (6:10),
+   *            torquescale (10);
+   *   joint:   polycoef (0:5), then qpos0 of joint1 (5) and joint2 (6). */
+  int neq;
+  const int *eq_type, *eq_obj1id, *eq_obj2id, *eq_active0;
+  const double *eq_solref /*2*/, *eq_solimp /*5*/, *eq_data /*11*/;
 } mrs_model_view;
 
 #ifdef __cplusplus

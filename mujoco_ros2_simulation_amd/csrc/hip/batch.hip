@@ -1067,6 +1067,20 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   d.npair = static_cast<int>(pg1.size());
   b.pair_g1 = pg1;
+  // active equality constraints (rows first in the solver order, as mj_makeConstraint)
+  std::vector<int> eq_t, eq_o1, eq_o2;
+  std::vector<double> eq_sr, eq_si, eq_dat;
+  d.neq = d.neq_rows = 0;
+  if (!(m.disableflags & (MRS_DSBL_EQUALITY | MRS_DSBL_CONSTRAINT)))
+    for (size_t q = 0; q < m.eq_type.size(); ++q) {
+      if (!m.eq_active0[q]) continue;
+      eq_t.push_back(m.eq_type[q]); eq_o1.push_back(m.eq_obj1id[q]); eq_o2.push_back(m.eq_obj2id[q]);
+      eq_sr.insert(eq_sr.end(), &m.eq_solref[2 * q], &m.eq_solref[2 * q] + 2);
+      eq_si.insert(eq_si.end(), &m.eq_solimp[5 * q], &m.eq_solimp[5 * q] + 5);
+      eq_dat.insert(eq_dat.end(), &m.eq_data[MRS_NEQDATA * q], &m.eq_data[MRS_NEQDATA * q] + MRS_NEQDATA);
+      d.neq_rows += m.eq_type[q] == MRS_EQ_CONNECT ? 3 : (m.eq_type[q] == MRS_EQ_WELD ? 6 : 1);
+    }
+  d.neq = static_cast<int>(eq_t.size());
   b.pair_g2 = pg2;
   // kinematic trees (bodies sharing a root child of the world) that own dofs: their dofs are one
   // contiguous range, M is block diagonal over them, and constraint rows touch at most two of them
@@ -1135,7 +1149,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   const int cap = max_con_req > 0 ? max_con_req : std::min(128, std::max(32, pair_max));
   d.max_con = d.npair == 0 ? 0 : std::min(pair_max, cap);
-  d.max_efc = d.nfric + 2 * d.nlim + 4 * d.max_con;
+  d.max_efc = d.neq_rows + d.nfric + 2 * d.nlim + 4 * d.max_con;
   // actuators
   std::vector<int> act_dof, act_qadr;
   std::vector<float> act_gear, act_gain, act_bias;
@@ -1225,6 +1239,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
   P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
   P.addi(&d.pair_g1, pg1); P.addi(&d.pair_g2, pg2); P.addi(&d.pair_dim, pdim);
+  P.addi(&d.eq_type, eq_t); P.addi(&d.eq_obj1id, eq_o1); P.addi(&d.eq_obj2id, eq_o2);
+  P.addf(&d.eq_solref, eq_sr); P.addf(&d.eq_solimp, eq_si); P.addf(&d.eq_data, eq_dat);
   P.addf(&d.pair_margin, pmargin); P.addf(&d.pair_gap, pgap); P.addf(&d.pair_friction, pfric);
   P.addf(&d.pair_solref, psolref); P.addf(&d.pair_solimp, psolimp);
   P.addi(&d.site_bodyid, m.site_bodyid); P.addf(&d.site_pos, m.site_pos); P.addf(&d.site_quat, m.site_quat);
@@ -1679,7 +1695,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   off = 0;
   const int ne = std::max(1, d.max_efc);
   // dense rows: dense mode, and blocked mode with a primal solver (the sparse records are PGS's)
-  const int dn = d.blocked && m.solver == MRS_SOL_PGS && m.cone != MRS_CONE_ELLIPTIC ? 0 : ne;
+  const int dn = d.blocked && m.solver == MRS_SOL_PGS && m.cone != MRS_CONE_ELLIPTIC && d.neq == 0 ? 0 : ne;
   S.efc_J = take(dn * nv); S.efc_MJ = take(dn * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(dn); S.efc_aref = take(dn);
   S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));
@@ -2077,7 +2093,7 @@ void batch_render_wait(BatchImpl* b) {
 int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force) {
   if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
   if (max < 0) throw std::invalid_argument("negative capacity");
-  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS && b->model->cone != MRS_CONE_ELLIPTIC)
+  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS && b->model->cone != MRS_CONE_ELLIPTIC && b->dm.neq == 0)
     throw UnsupportedError("blocked-mode PGS keeps its constraint rows in sparse records");
   HIP_CHECK(hipSetDevice(b->device));
   const ScratchLayout& S = b->S;

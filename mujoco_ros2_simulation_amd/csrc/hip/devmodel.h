@@ -147,6 +147,11 @@ struct DevModel {
   // b - a, c - a in fp32, 9 floats each -- one load per triangle instead of face -> vertex chains
   CPtr<float> mesh_tri;
   // candidate collision pairs (static filters applied; g1 has the smaller geom type)
+  // active equality constraints (mrs_model_view eq_*, inactive ones dropped on the host): neq of
+  // them giving neq_rows rows (connect 3, weld 6, joint 1), first in the row order
+  int neq, neq_rows;
+  CPtr<int> eq_type, eq_obj1id, eq_obj2id;
+  CPtr<float> eq_solref /*2*/, eq_solimp /*5*/, eq_data /*11*/;
   CPtr<int> pair_g1, pair_g2, pair_dim;
   CPtr<float> pair_margin, pair_gap, pair_friction /*3*/, pair_solref /*2*/, pair_solimp /*5*/;
   // sites

@@ -1499,7 +1499,11 @@ __device__ __forceinline__ float impedance(const PS si, float pos, float margin)
   return dmin + y * (dmax - dmin);
 }
 
-enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
+enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3, EFC_EQUALITY = 4 };
+// equality rows are unbounded: the solvers treat them as friction-loss rows with this bound (oracle.c
+// EQ_BOUND), quadratic in every primal state and unclamped in PGS
+constexpr float kEqBound = 1e15f;
+__device__ __forceinline__ bool fric_like(int t) { return t == EFC_FRICTION || t == EFC_EQUALITY; }
 
 // Per-phase cycle accounting, built only with -DMRS_PHASE_TIMING (profiling variant): s_memtime
 // around each phase, summed per wave and added to a device table at the end of the kernel.
@@ -4514,7 +4518,7 @@ __device__ float solve_primal(ENV_PARAMS, int nefc, bool newton) {
   const float scale = m.pgs_scale;
   const float qs = dof ? s[L.qacc_smooth + lane] : 0.0f;
   const float fs = dof ? s[L.qfrc_smooth + lane] : 0.0f;
-  auto is_fric = [&](int r) { return (__float_as_int(type[r]) >> 16) == EFC_FRICTION; };
+  auto is_fric = [&](int r) { return fric_like(__float_as_int(type[r]) >> 16); };
   auto is_con = [&](int r) { return (__float_as_int(type[r]) >> 16) == EFC_CONTACT; };
   const bool ell = m.cone == MRS_CONE_ELLIPTIC;  // 3-row contact blocks (floss slot: k + 1)
   // an elliptic block's zone cost at jar0 + a dj (dj null: at jar0) and its 1-D slope / curvature
@@ -5073,9 +5077,9 @@ template <int G, bool kPrimal = false>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) {
-    if (m.solver != MRS_SOL_PGS || m.cone == MRS_CONE_ELLIPTIC) {
-      // Newton / CG in blocked mode, and elliptic cones under every solver: dense rows (solve_primal,
-      // or the row-serial PGS with its 3-row contact blocks)
+    if (m.solver != MRS_SOL_PGS || m.cone == MRS_CONE_ELLIPTIC || m.neq > 0) {
+      // Newton / CG in blocked mode, elliptic cones and equality constraints under every solver:
+      // dense rows (solve_primal, or the row-serial PGS with its 3-row contact blocks)
       float qa;
       [[clang::noinline]] qa = constraints_dense<G>(ENV_ARGS, ncon, qacc_s);
       return qa;
@@ -5117,7 +5121,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     // (kPrimal: the G = 16 kernel instantiated for models whose solver is Newton or CG, so the
     // primal form is inlined only there and the PGS kernels keep their code and registers)
     if ((kPrimal ? m.solver != MRS_SOL_PGS : m.solver == MRS_SOL_PGS) && ncon == 0 && nf > 0 && nf <= 16 &&
-        !gany<G>(lim)) {
+        m.neq == 0 && !gany<G>(lim)) {
       if (lane == 0) scr[S.efc_n] = __int_as_float(-1);  // rows stay in registers
       int mydof = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
@@ -5182,21 +5186,116 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   unsigned long long t_sub = SUB_T();
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
   // keep ids in a small per-row int array inside the type slot (type*65536 + id)
+  // --- equality rows, first as mj_makeConstraint orders them (oracle.c equality_rows: connect and
+  // weld anchor points, weld's rotation error imag(conj(q1 relquat) q2) * torquescale with its exact
+  // derivative per dof, joint polynomial couplings); each row's diagApprox goes to the b slot until
+  // the impedance pass reads it
+  #pragma unroll 1
+  for (int q = 0; q < m.neq; ++q) {
+    const int t = m.eq_type[q], o1 = m.eq_obj1id[q], o2 = m.eq_obj2id[q];
+    const CPtr<float> dd = m.eq_data + MRS_NEQDATA * q;
+    const int code = EFC_EQUALITY * 65536 + q;
+    if (t == MRS_EQ_JOINT) {
+      const int d1 = m.jnt_dofadr[o1];
+      const float x1 = s[L.qpos + m.jnt_qposadr[o1]] - dd[5];
+      float poly = dd[0], dpoly = 0, diag = m.dof_invweight0[d1];
+      int d2 = -1;
+      if (o2 >= 0) {
+        d2 = m.jnt_dofadr[o2];
+        const float x = s[L.qpos + m.jnt_qposadr[o2]] - dd[6];
+        poly = dd[0] + x * (dd[1] + x * (dd[2] + x * (dd[3] + x * dd[4])));
+        dpoly = dd[1] + x * (2 * dd[2] + x * (3 * dd[3] + x * 4 * dd[4]));
+        diag += m.dof_invweight0[d2];
+      }
+      if (lane < nv) J[nefc * nv + lane] = (lane == d1 ? 1.0f : 0.0f) - (lane == d2 ? dpoly : 0.0f);
+      if (lane == 0) {
+        type[nefc] = __int_as_float(code);
+        pos[nefc] = x1 - poly; marg[nefc] = 0; floss[nefc] = kEqBound; bb[nefc] = diag;
+      }
+      ++nefc;
+      continue;
+    }
+    float x1[3] = {0, 0, 0}, x2[3] = {0, 0, 0}, q1[4] = {1, 0, 0, 0}, q2[4] = {1, 0, 0, 0};
+    if (o1 > 0) {
+      for (int i = 0; i < 3; ++i) x1[i] = s[L.xpos + 3 * o1 + i];
+      for (int i = 0; i < 4; ++i) q1[i] = s[L.xquat + 4 * o1 + i];
+    }
+    if (o2 > 0) {
+      for (int i = 0; i < 3; ++i) x2[i] = s[L.xpos + 3 * o2 + i];
+      for (int i = 0; i < 4; ++i) q2[i] = s[L.xquat + 4 * o2 + i];
+    }
+    float l1[3], l2[3];
+    if (t == MRS_EQ_CONNECT) {
+      for (int i = 0; i < 3; ++i) { l1[i] = dd[i]; l2[i] = dd[3 + i]; }
+    } else {
+      const float an[3] = {dd[0], dd[1], dd[2]}, rq[4] = {dd[6], dd[7], dd[8], dd[9]};
+      float ra[3];
+      rot_quat(ra, an, rq);
+      for (int i = 0; i < 3; ++i) { l2[i] = an[i]; l1[i] = dd[3 + i] + ra[i]; }
+    }
+    float p1[3], p2[3], rr[3];
+    rot_quat(rr, l1, q1);
+    for (int i = 0; i < 3; ++i) p1[i] = x1[i] + rr[i];
+    rot_quat(rr, l2, q2);
+    for (int i = 0; i < 3; ++i) p2[i] = x2[i] + rr[i];
+    float c1[3] = {0, 0, 0}, c2[3] = {0, 0, 0};
+    if (lane < nv) {
+      jac_col(m, s, o1, p1, lane, c1);
+      jac_col(m, s, o2, p2, lane, c2);
+    }
+    const float tdiag = m.body_invweight0[2 * o1] + m.body_invweight0[2 * o2];
+    for (int k = 0; k < 3; ++k) {
+      if (lane < nv) J[nefc * nv + lane] = c1[k] - c2[k];
+      if (lane == 0) {
+        type[nefc] = __int_as_float(code);
+        pos[nefc] = p1[k] - p2[k]; marg[nefc] = 0; floss[nefc] = kEqBound; bb[nefc] = tdiag;
+      }
+      ++nefc;
+    }
+    if (t != MRS_EQ_WELD) continue;
+    const float ts = dd[10], rq[4] = {dd[6], dd[7], dd[8], dd[9]};
+    float q1r[4], cq[4], e[4];
+    quat_mul(q1r, q1, rq);
+    cq[0] = q1r[0]; cq[1] = -q1r[1]; cq[2] = -q1r[2]; cq[3] = -q1r[3];
+    quat_mul(e, cq, q2);
+    // the lane's dof: angular motion (cdof's rotational part) of body2 minus body1
+    float wv[4] = {0, 0, 0, 0}, de[4] = {0, 0, 0, 0};
+    if (lane < nv) {
+      const int bj = m.dof_bodyid[lane], be = m.body_subtree_end[bj];
+      const bool a1 = o1 >= bj && o1 < be, a2 = o2 >= bj && o2 < be;
+      for (int i = 0; i < 3; ++i) wv[1 + i] = (a2 ? s[L.cdof + 6 * lane + i] : 0.0f) - (a1 ? s[L.cdof + 6 * lane + i] : 0.0f);
+      float tq[4];
+      quat_mul(tq, cq, wv);
+      quat_mul(de, tq, q2);
+    }
+    const float rdiag = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
+    for (int k = 0; k < 3; ++k) {
+      if (lane < nv) J[nefc * nv + lane] = 0.5f * de[1 + k] * ts;
+      if (lane == 0) {
+        type[nefc] = __int_as_float(code);
+        pos[nefc] = e[1 + k] * ts; marg[nefc] = 0; floss[nefc] = kEqBound; bb[nefc] = rdiag;
+      }
+      ++nefc;
+    }
+  }
+  if (m.neq > 0) wsync();
   // --- friction loss rows
   if (!(m.disableflags & MRS_DSBL_FRICTIONLOSS)) {
+    const int r0 = nefc;
     #pragma unroll 1
-    for (int r = 0; r < m.nfric; ++r) {
-      const int j = m.fric_dof[r];
+    for (int k = 0; k < m.nfric; ++k) {
+      const int j = m.fric_dof[k], r = r0 + k;
       if (lane < nv) J[r * nv + lane] = (lane == j) ? 1.0f : 0.0f;
       if (lane == 0) {
         type[r] = __int_as_float(EFC_FRICTION * 65536 + j);
         pos[r] = 0; marg[r] = 0; floss[r] = m.dof_frictionloss[j];
       }
     }
-    nefc = m.nfric;
+    nefc = r0 + m.nfric;
   }
   // --- joint limit rows (lane per limited joint, compacted)
   if (!(m.disableflags & MRS_DSBL_LIMIT)) {
+    const int lim0 = nefc;
     #pragma unroll 1
     for (int base = 0; base < m.nlim; base += G) {
       const int k = base + lane;
@@ -5229,7 +5328,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     wsync();
     // dense J of limit rows
     #pragma unroll 1
-    for (int r = m.nfric; r < nefc; ++r) {
+    for (int r = lim0; r < nefc; ++r) {
       const int code = __float_as_int(type[r]);
       const int jid = code & 0xffff;
       const int dof = m.jnt_dofadr[jid];
@@ -5239,7 +5338,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     wsync();
     if (lane == 0)
       #pragma unroll 1
-      for (int r = m.nfric; r < nefc; ++r) floss[r] = 0;
+      for (int r = lim0; r < nefc; ++r) floss[r] = 0;
   }
   // --- contact rows: lane per dof, loop over contacts
   if constexpr (G == 64) {
@@ -5376,6 +5475,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     CPtr<float> sr, si;
     float diag;
     if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
+    else if (t == EFC_EQUALITY) { sr = m.eq_solref + 2 * id; si = m.eq_solimp + 5 * id; diag = bb[r]; }
     else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
     else {
       const gfloat* rec = scr + S.con + kConRec * id;
@@ -5419,8 +5519,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       my_R = R;
       my_aref = -B * vel - pterm;
       my_b = jqs - my_aref;
-      my_fl = t == EFC_FRICTION ? floss[r] : 0.0f;
-      my_fric = t == EFC_FRICTION;
+      my_fl = fric_like(t) ? floss[r] : 0.0f;
+      my_fric = fric_like(t);
       aref[r] = my_aref;
       continue;
     }
@@ -5534,7 +5634,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
         for (int j = 0; j < nv; ++j) jar += Jr[j] * s[L.qacc_ws + j];
         const int t = __float_as_int(type[r]) >> 16;
         const float D = 1.0f / Rr[r];
-        if (t == EFC_FRICTION) {
+        if (fric_like(t)) {
           const float fl = floss[r];
           f = jar <= -Rr[r] * fl ? fl : (jar >= Rr[r] * fl ? -fl : -D * jar);
         } else {
@@ -5605,7 +5705,7 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       const float a = ARii[r];
       float nf = f0 - res / a;
       const int t = __float_as_int(type[r]) >> 16;
-      if (t == EFC_FRICTION) nf = clampf(nf, -floss[r], floss[r]);
+      if (fric_like(t)) nf = clampf(nf, -floss[r], floss[r]);
       else if (nf < 0) nf = 0;
       const float delta = nf - f0;
       if (delta != 0) {

@@ -1470,6 +1470,8 @@ struct Compiler {
       quat_mul(iq, q, &m.body_iquat[4 * b]);
       quat2mat(&ximat[9 * b], iq);
     }
+    x0pos = xpos;
+    x0quat = xquat;
     // subtree com
     std::vector<double> scom(3 * nb, 0);
     for (int b = 0; b < nb; ++b)
@@ -1709,12 +1711,112 @@ struct Compiler {
     for (auto& c : root->children) {
       if (c->tag == "sensor") parse_sensors(c.get());
       else if (c->tag == "keyframe") parse_keyframes(c.get());
-      else if (c->tag == "equality" || c->tag == "tendon")
-        { if (!c->children.empty()) fail(c.get(), "equality constraints and tendons are not supported"); }
+      else if (c->tag == "equality") parse_equality(c.get());
+      else if (c->tag == "tendon")
+        { if (!c->children.empty()) fail(c.get(), "tendons are not supported"); }
       else if (c->tag == "contact") parse_contact(c.get());
     }
     candidate_pairs();
     return std::move(m);
+  }
+  std::vector<double> x0pos, x0quat;  // body poses at qpos0 (set0)
+  // <equality> [upstream mjCEquality]: connect, weld and joint constraints with solref / solimp /
+  // active (defaults 0.02 1 / 0.9 0.95 0.001 0.5 2 / true); what MuJoCo's compiler completes at qpos0
+  // is completed here: connect's anchor in body2's frame, weld's relpose when not given (its quaternion
+  // all zeros), the joints' reference positions (eq_data layout: include/mrs_model.h)
+  void parse_equality(const XmlElement* sec) {
+    for (auto& cp : sec->children) {
+      const XmlElement* e = cp.get();
+      const std::string& tag = e->tag;
+      const DefaultClass* cls = resolve_class(e, "");
+      double sr[2] = {0.02, 1}, si[5] = {0.9, 0.95, 0.001, 0.5, 2}, data[MRS_NEQDATA] = {};
+      get_reals(e, cls, "equality", "solref", sr, 2, true);
+      get_reals(e, cls, "equality", "solimp", si, 5);
+      get_reals(e, cls, tag, "solref", sr, 2, true);
+      get_reals(e, cls, tag, "solimp", si, 5);
+      int active = 1;
+      std::string a;
+      if (get_str(e, cls, tag, "active", a) || get_str(e, cls, "equality", "active", a)) active = a == "true";
+      int type, o1, o2;
+      auto body = [&](const char* key, bool required) {
+        std::string n;
+        if (!get_str(e, cls, tag, key, n)) {
+          if (required) fail(e, std::string(tag) + " requires " + key);
+          return 0;  // world
+        }
+        const int b = m.name2id(MRS_OBJ_BODY, n);
+        if (b < 0) fail(e, "unknown body '" + n + "'");
+        return b;
+      };
+      auto pose_of = [&](int b, double p[3], double q[4]) {
+        for (int i = 0; i < 3; ++i) p[i] = x0pos[3 * b + i];
+        for (int i = 0; i < 4; ++i) q[i] = x0quat[4 * b + i];
+      };
+      if (tag == "connect") {
+        type = MRS_EQ_CONNECT;
+        o1 = body("body1", true);
+        o2 = body("body2", false);
+        if (!get_reals(e, cls, tag, "anchor", data, 3, true)) fail(e, "connect requires anchor");
+        // the same world point in body2's frame at qpos0
+        double p1[3], q1[4], p2[3], q2[4], w[3], r[3], qc[4];
+        pose_of(o1, p1, q1);
+        pose_of(o2, p2, q2);
+        rot_vec_quat(r, data, q1);
+        for (int i = 0; i < 3; ++i) w[i] = p1[i] + r[i] - p2[i];
+        qc[0] = q2[0]; qc[1] = -q2[1]; qc[2] = -q2[2]; qc[3] = -q2[3];
+        rot_vec_quat(data + 3, w, qc);
+      } else if (tag == "weld") {
+        type = MRS_EQ_WELD;
+        o1 = body("body1", true);
+        o2 = body("body2", false);
+        get_reals(e, cls, tag, "anchor", data, 3, true);
+        double rp[7] = {0, 1, 0, 0, 0, 0, 0};  // MuJoCo's default: quaternion zero = from qpos0
+        get_reals(e, cls, tag, "relpose", rp, 7, true);
+        data[10] = 1;
+        get_real(e, cls, tag, "torquescale", data[10]);
+        if (rp[3] == 0 && rp[4] == 0 && rp[5] == 0 && rp[6] == 0) {
+          // body2's pose in body1's frame at qpos0
+          double p1[3], q1[4], p2[3], q2[4], d[3], qc[4];
+          pose_of(o1, p1, q1);
+          pose_of(o2, p2, q2);
+          for (int i = 0; i < 3; ++i) d[i] = p2[i] - p1[i];
+          qc[0] = q1[0]; qc[1] = -q1[1]; qc[2] = -q1[2]; qc[3] = -q1[3];
+          rot_vec_quat(rp, d, qc);
+          quat_mul(rp + 3, qc, q2);
+        }
+        for (int i = 0; i < 7; ++i) data[3 + i] = rp[i];
+        quat_normalize(data + 6);
+      } else if (tag == "joint") {
+        type = MRS_EQ_JOINT;
+        std::string n1, n2;
+        if (!get_str(e, cls, tag, "joint1", n1)) fail(e, "joint equality requires joint1");
+        o1 = m.name2id(MRS_OBJ_JOINT, n1);
+        o2 = -1;
+        if (get_str(e, cls, tag, "joint2", n2)) o2 = m.name2id(MRS_OBJ_JOINT, n2);
+        if (o1 < 0 || (!n2.empty() && o2 < 0)) fail(e, "joint equality references an unknown joint");
+        double pc[5] = {0, 1, 0, 0, 0};
+        get_reals(e, cls, tag, "polycoef", pc, 5);
+        for (int k : {o1, o2}) {
+          if (k < 0) continue;
+          if (m.jnt_type[k] != MRS_JNT_HINGE && m.jnt_type[k] != MRS_JNT_SLIDE)
+            fail(e, "joint equality needs hinge or slide joints");
+        }
+        for (int i = 0; i < 5; ++i) data[i] = pc[i];
+        data[5] = m.qpos0[m.jnt_qposadr[o1]];
+        data[6] = o2 >= 0 ? m.qpos0[m.jnt_qposadr[o2]] : 0;
+      } else {
+        fail(e, "unsupported equality type '" + tag + "'");
+        return;
+      }
+      if ((type == MRS_EQ_CONNECT || type == MRS_EQ_WELD) && o1 == o2) fail(e, "equality of a body with itself");
+      m.eq_type.push_back(type);
+      m.eq_obj1id.push_back(o1);
+      m.eq_obj2id.push_back(o2);
+      m.eq_active0.push_back(active);
+      m.eq_solref.insert(m.eq_solref.end(), sr, sr + 2);
+      m.eq_solimp.insert(m.eq_solimp.end(), si, si + 5);
+      m.eq_data.insert(m.eq_data.end(), data, data + MRS_NEQDATA);
+    }
   }
   // <contact>: explicit geom pairs and excluded body pairs [upstream mjCPair / mjCBodyPair].  A pair's
   // omitted attributes take the values a candidate pair of its geoms would (max condim and friction,
@@ -1902,6 +2004,9 @@ mrs_model_view Model::view() const {
   v.nmeshhull = static_cast<int>(mesh_hull.size());
   MRS_V(geom_dataid); MRS_V(mesh_vertadr); MRS_V(mesh_vertnum); MRS_V(mesh_faceadr); MRS_V(mesh_facenum);
   MRS_V(mesh_hulladr); MRS_V(mesh_hullnum); MRS_V(mesh_face); MRS_V(mesh_hull); MRS_V(mesh_vert);
+  v.neq = static_cast<int>(eq_type.size());
+  MRS_V(eq_type); MRS_V(eq_obj1id); MRS_V(eq_obj2id); MRS_V(eq_active0); MRS_V(eq_solref); MRS_V(eq_solimp);
+  MRS_V(eq_data);
   v.nexpair = static_cast<int>(expair_geom1.size());
   v.nexclude = static_cast<int>(exclude_body1.size());
   MRS_V(expair_geom1); MRS_V(expair_geom2); MRS_V(expair_dim); MRS_V(exclude_body1); MRS_V(exclude_body2);

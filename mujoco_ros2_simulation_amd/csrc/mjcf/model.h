@@ -67,6 +67,9 @@ struct Model {
   // explicit <contact><pair> (own parameters) and <contact><exclude> body pairs (mrs_model_view)
   std::vector<int> expair_geom1, expair_geom2, expair_dim, exclude_body1, exclude_body2;
   std::vector<double> expair_friction, expair_solref, expair_solimp, expair_margin, expair_gap;
+  // equality constraints (mrs_model_view eq_*)
+  std::vector<int> eq_type, eq_obj1id, eq_obj2id, eq_active0;
+  std::vector<double> eq_solref, eq_solimp, eq_data;
 
   // names per object type (MRS_OBJ_*), index = object id
   std::map<int, std::vector<std::string>> names;

@@ -103,6 +103,13 @@ _CONTACT_ARRAYS = [
     ("expair_friction", "d", "nexpair", 5), ("expair_solref", "d", "nexpair", 2), ("expair_solimp", "d", "nexpair", 5),
     ("expair_margin", "d", "nexpair", 1), ("expair_gap", "d", "nexpair", 1),
 ]
+# equality constraints (after the contact block)
+_EQ_SIZES = ["neq"]
+_EQ_ARRAYS = [
+    ("eq_type", "i", "neq", 1), ("eq_obj1id", "i", "neq", 1), ("eq_obj2id", "i", "neq", 1), ("eq_active0", "i", "neq", 1),
+    ("eq_solref", "d", "neq", 2), ("eq_solimp", "d", "neq", 5), ("eq_data", "d", "neq", 11),
+]
+EQ_CONNECT, EQ_WELD, EQ_JOINT = 0, 1, 2
 
 
 class ModelView(C.Structure):
@@ -117,7 +124,9 @@ class ModelView(C.Structure):
                 [(n, C.c_int) for n in _MESH_SIZES] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _MESH_ARRAYS] +
                 [(n, C.c_int) for n in _CONTACT_SIZES] +
-                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _CONTACT_ARRAYS])
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _CONTACT_ARRAYS] +
+                [(n, C.c_int) for n in _EQ_SIZES] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _EQ_ARRAYS])
 
 
 _lib = None
@@ -204,14 +213,14 @@ class Model:
         self.view = ModelView()
         _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
         v = self.view
-        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES:
+        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES:
             setattr(self, n, getattr(v, n))
         for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "restate", "integrator", "solver",
                   "iterations", "disableflags",
                   "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
             setattr(self, n, getattr(v, n))
         self.gravity = np.array(v.gravity[:])
-        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS:
+        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS + _EQ_ARRAYS:
             n = getattr(v, count)
             w = getattr(v, width) if isinstance(width, str) else width
             ptr = getattr(v, name)

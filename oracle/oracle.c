@@ -56,7 +56,11 @@ typedef struct {
   orc_contact con[MAXCON];
 } orc_ws;
 
-enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3 };
+enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3, EFC_EQUALITY = 4 };
+/* equality rows are unbounded; the solvers treat them as friction-loss rows with this bound (never
+ * reached: a force of 1e15), so they are quadratic in every primal state and unclamped in PGS */
+#define EQ_BOUND 1e15
+#define FRIC_LIKE(t) ((t) == EFC_FRICTION || (t) == EFC_EQUALITY)
 /* an elliptic contact block starts at row r (its normal) */
 #define ELL_BLOCK(w, r) ((w)->efc_sub[r] == 0)
 
@@ -1849,12 +1853,99 @@ static void add_row(orc_ws* w, int nv, int type, int id, const double* J, double
   memcpy(w->efc_solimp[r], solimp, 5 * sizeof(double));
 }
 
+/* equality rows [upstream mj_instantiateEquality; restated, verify], first as mj_makeConstraint
+ * orders them (eq_data layout: include/mrs_model.h):
+ *   connect: p1 - p2 of the anchor on body1 and its qpos0 image on body2, 3 rows, J = J_p1 - J_p2,
+ *            diagApprox the bodies' translational invweight0;
+ *   weld:    the same for body2's anchor and where body1's relpose puts it (3 rows), then the rotation
+ *            error imag(e) * torquescale, e = conj(q1 relquat) q2 (3 rows; J column = the exact
+ *            derivative 1/2 imag(conj(q1 relquat) (w2 - w1) q2) of that error for the dof's angular
+ *            motion), diagApprox rotational invweight0;
+ *   joint:   (q1 - q1_0) - poly(q2 - q2_0), J = e_dof1 - poly'(q2 - q2_0) e_dof2, diagApprox the
+ *            dofs' invweight0.
+ * Unbounded (EQ_BOUND), position term as limits. */
+static void equality_rows(const mrs_model_view* m, orc_data* d, orc_ws* w, double* J) {
+  const int nv = m->nv;
+  for (int q = 0; q < m->neq; ++q) {
+    if (!m->eq_active0[q]) continue;
+    const double* dd = m->eq_data + MRS_NEQDATA * q;
+    const double* sr = m->eq_solref + 2 * q;
+    const double* si = m->eq_solimp + 5 * q;
+    const int t = m->eq_type[q], o1 = m->eq_obj1id[q], o2 = m->eq_obj2id[q];
+    if (t == MRS_EQ_JOINT) {
+      const int d1 = m->jnt_dofadr[o1];
+      const double x1 = d->qpos[m->jnt_qposadr[o1]] - dd[5];
+      double poly = dd[0], dpoly = 0, diag = m->dof_invweight0[d1];
+      memset(J, 0, nv * sizeof(double));
+      J[d1] = 1;
+      if (o2 >= 0) {
+        const int d2 = m->jnt_dofadr[o2];
+        const double x = d->qpos[m->jnt_qposadr[o2]] - dd[6];
+        poly = dd[0] + x * (dd[1] + x * (dd[2] + x * (dd[3] + x * dd[4])));
+        dpoly = dd[1] + x * (2 * dd[2] + x * (3 * dd[3] + x * 4 * dd[4]));
+        J[d2] -= dpoly;
+        diag += m->dof_invweight0[d2];
+      }
+      add_row(w, nv, EFC_EQUALITY, q, J, x1 - poly, 0, EQ_BOUND, diag, sr, si);
+      continue;
+    }
+    /* anchor points on body1 (p1) and body2 (p2) */
+    const double *q1 = w->xquat + 4 * o1, *q2 = w->xquat + 4 * o2;
+    double l1[3], l2[3], p1[3], p2[3], r[3], q1r[4];
+    if (t == MRS_EQ_CONNECT) {
+      for (int i = 0; i < 3; ++i) { l1[i] = dd[i]; l2[i] = dd[3 + i]; }
+    } else {
+      double ra[3];
+      double m6[9];
+      quat2mat(m6, dd + 6);
+      mat_vec(ra, m6, dd);
+      for (int i = 0; i < 3; ++i) { l2[i] = dd[i]; l1[i] = dd[3 + i] + ra[i]; }
+    }
+    mat_vec(r, w->xmat + 9 * o1, l1);
+    for (int i = 0; i < 3; ++i) p1[i] = w->xpos[3 * o1 + i] + r[i];
+    mat_vec(r, w->xmat + 9 * o2, l2);
+    for (int i = 0; i < 3; ++i) p2[i] = w->xpos[3 * o2 + i] + r[i];
+    const double tdiag = m->body_invweight0[2 * o1] + m->body_invweight0[2 * o2];
+    for (int k = 0; k < 3; ++k) {
+      for (int j = 0; j < nv; ++j) {
+        double c1[3] = {0, 0, 0}, c2[3] = {0, 0, 0};
+        if (dof_affects(m, j, o1)) jac_point_col(m, w, o1, p1, j, c1);
+        if (dof_affects(m, j, o2)) jac_point_col(m, w, o2, p2, j, c2);
+        J[j] = c1[k] - c2[k];
+      }
+      add_row(w, nv, EFC_EQUALITY, q, J, p1[k] - p2[k], 0, EQ_BOUND, tdiag, sr, si);
+    }
+    if (t != MRS_EQ_WELD) continue;
+    const double ts = dd[10];
+    double cq[4], e[4], tmp[4];
+    quat_mul(q1r, q1, dd + 6);
+    cq[0] = q1r[0]; cq[1] = -q1r[1]; cq[2] = -q1r[2]; cq[3] = -q1r[3];
+    quat_mul(e, cq, q2);
+    const double rdiag = m->body_invweight0[2 * o1 + 1] + m->body_invweight0[2 * o2 + 1];
+    for (int k = 0; k < 3; ++k) {
+      for (int j = 0; j < nv; ++j) {
+        double wv[4] = {0, 0, 0, 0};
+        for (int i = 0; i < 3; ++i) {
+          if (dof_affects(m, j, o2)) wv[1 + i] += w->cdof[6 * j + i];
+          if (dof_affects(m, j, o1)) wv[1 + i] -= w->cdof[6 * j + i];
+        }
+        quat_mul(tmp, cq, wv);
+        double de[4];
+        quat_mul(de, tmp, q2);
+        J[j] = 0.5 * de[1 + k] * ts;
+      }
+      add_row(w, nv, EFC_EQUALITY, q, J, e[1 + k] * ts, 0, EQ_BOUND, rdiag, sr, si);
+    }
+  }
+}
+
 static void make_constraint(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   int nv = m->nv;
   w->nefc = 0;
   if (m->disableflags & MRS_DSBL_CONSTRAINT) return;
   double* J = (double*)malloc(nv * sizeof(double) + 8);
+  if (!(m->disableflags & MRS_DSBL_EQUALITY)) equality_rows(m, d, w, J);
   if (!(m->disableflags & MRS_DSBL_FRICTIONLOSS))
     for (int j = 0; j < nv; ++j) {
       if (m->dof_frictionloss[j] <= 0) continue;
@@ -2127,7 +2218,7 @@ static void ell_pgs_split(const double A[9], const double res[3], const double o
 /* force of one row for a given jar = J qacc - aref (mj_constraintUpdate primal states) */
 static double row_force(orc_ws* w, int r, double jar) {
   double D = w->efc_D[r];
-  if (w->efc_type[r] == EFC_FRICTION) {
+  if (FRIC_LIKE(w->efc_type[r])) {
     double fl = w->efc_frictionloss[r], Rr = w->efc_R[r];
     if (jar <= -Rr * fl) return fl;
     if (jar >= Rr * fl) return -fl;
@@ -2155,7 +2246,7 @@ static double row_force(orc_ws* w, int r, double jar) {
 enum { ST_SAT = 0, ST_QUAD = 1, ST_LINNEG = 2, ST_LINPOS = 3 };
 
 static int row_state(const orc_ws* w, int r, double jar) {
-  if (w->efc_type[r] == EFC_FRICTION) {
+  if (FRIC_LIKE(w->efc_type[r])) {
     double rf = w->efc_R[r] * w->efc_frictionloss[r];
     return jar <= -rf ? ST_LINNEG : (jar >= rf ? ST_LINPOS : ST_QUAD);
   }
@@ -2535,6 +2626,13 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
         for (int k = 0; k < 3; ++k) cb[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
         if (m->restate & MRS_RESTATE_PGS_ELLIPTIC_BLOCK) ell_block_min(A, cb, w->efc_fr[r], nw);
         else ell_pgs_split(A, res, old, w->efc_fr[r], nw);
+        {
+          /* diagnostics (scripts only): ORC_ROUND_PGS=1 rounds the block's new forces to fp32, the
+           * device's storage precision, to measure how far that alone moves the iterates */
+          static int rnd = -1;
+          if (rnd < 0) rnd = getenv("ORC_ROUND_PGS") != NULL;
+          if (rnd) for (int k = 0; k < 3; ++k) nw[k] = (float)nw[k];
+        }
         double delta[3], quad = 0;
         for (int k = 0; k < 3; ++k) delta[k] = nw[k] - old[k];
         for (int k = 0; k < 3; ++k)
@@ -2549,7 +2647,7 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
       for (int s = 0; s < nefc; ++s) res += ar[s] * f[s];
       double old = f[r];
       double nf = old - res / ar[r];
-      if (w->efc_type[r] == EFC_FRICTION) {
+      if (FRIC_LIKE(w->efc_type[r])) {
         double fl = w->efc_frictionloss[r];
         nf = nf < -fl ? -fl : nf > fl ? fl : nf;
       } else if (nf < 0) {

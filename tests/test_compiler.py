@@ -247,3 +247,31 @@ def test_contact_pairs_and_excludes():
                 '<exclude body1="a"/>', '<pair geom1="ga" geom2="gb" condim="6"/>']:
         with pytest.raises(sim.MrsError):
             sim.Model.from_string(xml.replace('<exclude body1="c" body2="a"/>', bad))
+
+
+def test_equality_parse():
+    """<equality>: connect's second anchor is the first one's image in body2's frame at qpos0, weld's
+    relpose (when not given) is body2's pose in body1's frame at qpos0, joint couplings keep both
+    joints' reference positions; solref / solimp / active and default classes"""
+    from mujoco_ros2_simulation_amd import sim
+    xml = """<mujoco><default><equality solref="0.01 0.5"/></default><worldbody>
+      <body name="a" pos="1 0 0" euler="0 0 90"><joint name="ja" axis="0 0 1" ref="0.2"/><geom size="0.1"/>
+        <body name="b" pos="0 1 0"><joint name="jb" type="slide" axis="1 0 0"/><geom size="0.1"/></body></body>
+      <body name="c" pos="0 0 2"><freejoint/><geom size="0.1"/></body></worldbody>
+      <equality><connect body1="b" body2="c" anchor="0.1 0 0"/><weld body1="a" body2="c" torquescale="3" active="false"/>
+        <joint joint1="jb" joint2="ja" polycoef="0.1 2"/></equality></mujoco>"""
+    m = sim.Model.from_string(xml)
+    assert m.neq == 3 and list(m.eq_active0) == [1, 0, 1]
+    np.testing.assert_allclose(m.eq_solref, [[0.01, 0.5]] * 3)
+    # b at (1, 0, 0) + Rz(90) (0, 1, 0) = (0, 0, 0), rotated 90 deg: anchor (0.1, 0, 0) -> world (0, 0.1, 0);
+    # in c's frame (at (0, 0, 2), identity): (0, 0.1, -2)
+    np.testing.assert_allclose(m.eq_data[0, :6], [0.1, 0, 0, 0, 0.1, -2], atol=1e-12)
+    # c in a's frame: a at (1, 0, 0) rotated 90 deg about z, c at (0, 0, 2): (-1, 0, 2) -> (0, 1, 2)
+    np.testing.assert_allclose(m.eq_data[1, 3:6], [0, 1, 2], atol=1e-12)
+    np.testing.assert_allclose(np.abs(m.eq_data[1, 6:10]), [np.sqrt(0.5), 0, 0, np.sqrt(0.5)], atol=1e-12)
+    assert m.eq_data[1, 10] == 3
+    np.testing.assert_allclose(m.eq_data[2, :7], [0.1, 2, 0, 0, 0, 0, np.radians(0.2)])  # ref in degrees
+    for bad in ['<connect body1="nope" anchor="0 0 0"/>', '<connect body1="b"/>', '<joint joint1="ja" joint2="zz"/>',
+                '<flex/>']:
+        with pytest.raises(sim.MrsError):
+            sim.Model.from_string(xml.replace('<joint joint1="jb" joint2="ja" polycoef="0.1 2"/>', bad))

@@ -32,27 +32,37 @@ def elliptic_scene(name: str, solver: str, impratio: float = 1.0, tol: str = "")
     return m
 
 
-@pytest.mark.parametrize("scene, solver, imp, n, tol", [("arm_boxes", "PGS", 1.0, 16, ""), ("arm_boxes", "Newton", 3.0, 8, ""),
-                                                        ("arm_boxes", "CG", 1.0, 8, ""), ("mobile_base", "PGS", 1.0, 32, "0"),
-                                                        ("mobile_base", "Newton", 10.0, 32, "")])
-def test_reseeded_elliptic(scene, solver, imp, n, tol):
+@pytest.mark.parametrize("scene, solver, imp, n, tol, restate",
+                         [("arm_boxes", "PGS", 1.0, 16, "", 0), ("arm_boxes", "PGS", 1.0, 16, "", sim.RESTATE_PGS_ELLIPTIC_BLOCK),
+                          ("arm_boxes", "Newton", 3.0, 8, "", 0), ("arm_boxes", "Newton", 3.0, 8, "", sim.RESTATE_NEWTON_REFINE),
+                          ("arm_boxes", "CG", 1.0, 8, "", 0), ("mobile_base", "PGS", 1.0, 32, "0", 0),
+                          ("mobile_base", "PGS", 1.0, 32, "0", sim.RESTATE_PGS_ELLIPTIC_BLOCK),
+                          ("mobile_base", "Newton", 10.0, 32, "", 0)])
+def test_reseeded_elliptic(scene, solver, imp, n, tol, restate):
     """contact scenes under cone="elliptic" (blocked mode for the arm + boxes, 16-lane groups for the
-    mobile base), every step from the oracle's state, qpos / qvel within 1e-5 of scale.  The mobile
-    base's PGS converges within its 50 sweeps, so MuJoCo's improvement test (1e-8) ends it, and fp32 /
-    fp64 can cross that threshold one sweep apart (measured 1.5e-5 in qvel at the default tolerance):
+    mobile base), every step from the oracle's state, qpos / qvel within 1e-5 of scale -- PGS with
+    mj_solPGS's split block update (the default) and with the opt-in exact block step, Newton with
+    and without the opt-in refinement step.  The mobile base's PGS converges within its 50 sweeps, so
+    MuJoCo's improvement test (1e-8) ends it, and fp32 / fp64 can cross that threshold one sweep apart:
     tolerance 0 runs all 50 sweeps on both sides, separating the arithmetic from the stop rule (as
-    test_gpu_solvers.test_reseeded_step_parity does for C5).  That case is held to 2e-5: its worst
-    env-step over 32 envs x 40 steps measured 1.4e-5 with all 50 sweeps (the fp32 exact block minimiser
-    resolves each block's normal force to ~4e-7 relative, and 50 unconverged Gauss-Seidel sweeps carry
-    that), every other case to 1e-5"""
+    test_gpu_solvers.test_reseeded_step_parity does for C5).  Those two cases carry measured bounds:
+    the 50 unconverged sweeps carry the fp32 resolution of every block step --
+      * split update: rounding the oracle's own block forces to fp32 after every update (ORC_ROUND_PGS,
+        scripts/diag_elliptic_round.py) moves qvel by 1.2e-4 over the same 32 envs x 40 steps, so the
+        device's fp32 iterates cannot be held closer than that: bound 2e-4 (measured 8.7e-5);
+      * exact block step: the fp32 block minimiser resolves each normal force to ~4e-7 relative:
+        bound 2e-5 (measured 1.4e-5)."""
     model = elliptic_scene(scene, solver, imp, tol)
+    model.set_restate(restate)
     wq, wv, ncon, flips, unexplained = _reseeded(model, n, 40)
-    print(f"{scene} elliptic {solver} impratio {imp}: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; "
-          f"contacts per env {ncon.mean():.1f}; flips {flips}")
+    print(f"{scene} elliptic {solver} impratio {imp} restate {restate}: worst per-step rel err qpos {wq:.2e} "
+          f"qvel {wv:.2e}; contacts per env {ncon.mean():.1f}; flips {flips}")
     assert ncon.max() > 0
     assert flips <= max(1, 0.01 * n * 40)
     assert not unexplained, unexplained[:5]
-    tol_v = 2 * RTOL if (scene, solver) == ("mobile_base", "PGS") else RTOL
+    tol_v = RTOL
+    if (scene, solver) == ("mobile_base", "PGS"):
+        tol_v = 2 * RTOL if restate else 2e-4
     assert wq <= RTOL and wv <= tol_v
 
 

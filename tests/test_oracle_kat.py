@@ -368,3 +368,51 @@ def test_implicit_two_link_step(s2_model):
     a_int = np.linalg.solve(M + h * (np.diag(damp) + dB), f_s + qfrc_con)
     d.step()
     np.testing.assert_allclose(d.qvel, v + h * a_int, rtol=1e-10, atol=1e-12)
+
+
+def test_equality_kats():
+    """equality constraints in the oracle against closed forms: a free body hung by a connect at its
+    origin swings exactly like the same body on a ball joint (when the ball is supported) or keeps its
+    anchor within the soft constraint's sag; a body welded to another keeps the relative pose while
+    the pair tumbles; a joint coupling q1 = 2 q2 holds within the soft constraint's error"""
+    from mujoco_ros2_simulation_amd import sim
+    import binding
+    xml_c = """<mujoco><option timestep="0.001"/><worldbody>
+    <body name="b" pos="0 0 1"><freejoint/><geom type="box" size="0.05 0.05 0.2" pos="0.1 0 -0.2" mass="1"/></body></worldbody>
+    <equality><connect body1="b" anchor="0 0 0" solref="0.005 1"/></equality></mujoco>"""
+    d = binding.OracleData(sim.Model.from_string(xml_c))
+    for _ in range(1000):
+        d.step()
+    assert np.max(np.abs(d.qpos[:3] - [0, 0, 1])) < 1e-4          # the anchor stays put (soft: ~2.5e-5 sag)
+    assert abs(d.qpos[5]) > 0.02                                    # and the box swings about it
+    xml2 = """<mujoco><option timestep="0.001"/><worldbody>
+    <body name="a" pos="0 0 1"><freejoint/><geom type="box" size="0.1 0.1 0.1" mass="1"/></body>
+    <body name="b" pos="0.25 0 1" euler="0 0 30"><freejoint/><geom type="sphere" size="0.05" mass="0.5"/></body></worldbody>
+    <equality><weld body1="a" body2="b"/></equality></mujoco>"""
+    d = binding.OracleData(sim.Model.from_string(xml2))
+    d.qvel[:] = [0, 0, 0, 1, 2, 3, 0, 0, 0, 0, 0, 0]
+    for _ in range(300):
+        d.step()
+    qa, qb = d.qpos[:7], d.qpos[7:]
+    w, x, y, z = qa[3:]
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                  [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                  [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+    np.testing.assert_allclose(R.T @ (qb[:3] - qa[:3]), [0.25, 0, 0], atol=5e-4)
+    c = np.array([w, -x, -y, -z])
+    rel = np.array([c[0] * qb[3] - c[1] * qb[4] - c[2] * qb[5] - c[3] * qb[6], c[0] * qb[4] + c[1] * qb[3] + c[2] * qb[6] - c[3] * qb[5],
+                    c[0] * qb[5] - c[1] * qb[6] + c[2] * qb[3] + c[3] * qb[4], c[0] * qb[6] + c[1] * qb[5] - c[2] * qb[4] + c[3] * qb[3]])
+    np.testing.assert_allclose(rel * np.sign(rel[0]), [np.cos(np.pi / 12), 0, 0, np.sin(np.pi / 12)], atol=1e-3)
+    xml_j = """<mujoco><option timestep="0.002"/><worldbody>
+    <body name="a"><joint name="j1" axis="0 0 1"/><geom type="capsule" size="0.02 0.1" fromto="0 0 0 0.2 0 0"/></body>
+    <body name="b" pos="0 0.5 0"><joint name="j2" axis="0 0 1"/><geom type="capsule" size="0.02 0.1" fromto="0 0 0 0.2 0 0"/></body></worldbody>
+    <equality><joint joint1="j1" joint2="j2" polycoef="0 2 0 0 0" solref="0.005 1"/></equality>
+    <actuator><position joint="j2" kp="10"/></actuator></mujoco>"""
+    d = binding.OracleData(sim.Model.from_string(xml_j))
+    d.ctrl[:] = 0.3
+    worst, reach = 0.0, 0.0
+    for _ in range(2000):
+        d.step()
+        worst = max(worst, abs(d.qpos[0] - 2 * d.qpos[1]))
+        reach = max(reach, d.qpos[1])
+    assert worst < 5e-3 and reach > 0.2  # the driven joint swings to the target; the coupled one follows
