@@ -33,6 +33,9 @@ enum { MRS_INT_EULER = 0, MRS_INT_RK4 = 1, MRS_INT_IMPLICIT = 2, MRS_INT_IMPLICI
 enum { MRS_SOL_PGS = 0, MRS_SOL_CG = 1, MRS_SOL_NEWTON = 2 };
 enum { MRS_CONE_PYRAMIDAL = 0, MRS_CONE_ELLIPTIC = 1 };  /* mjtCone */
 enum { MRS_EQ_CONNECT = 0, MRS_EQ_WELD = 1, MRS_EQ_JOINT = 2 };  /* mjtEq subset */
+enum { MRS_TEX_2D = 0, MRS_TEX_CUBE = 1, MRS_TEX_SKYBOX = 2 };  /* mjtTexture */
+enum { MRS_BUILTIN_NONE = 0, MRS_BUILTIN_GRADIENT = 1, MRS_BUILTIN_CHECKER = 2, MRS_BUILTIN_FLAT = 3 };
+enum { MRS_MARK_NONE = 0, MRS_MARK_EDGE = 1, MRS_MARK_CROSS = 2 };
 #define MRS_NEQDATA 11
 enum { MRS_TRN_JOINT = 0 };
 enum { MRS_DYN_NONE = 0 };
@@ -155,6 +158,20 @@ typedef struct mrs_model_view {
   int neq;
   const int *eq_type, *eq_obj1id, *eq_obj2id, *eq_active0;
   const double *eq_solref /*2*/, *eq_solimp /*5*/, *eq_data /*11*/;
+
+  /* rendering (mjModel light_* / tex_* / mat_*, mjVisual headlight): the camera colour image's
+   * restatement of MuJoCo's OpenGL lighting.  Lights are fixed in the world (on the
+   * world body or a body welded to it; pos / dir world frame); textures are MuJoCo's procedural
+   * builtins (MRS_TEX_*: checker / gradient / flat, marks none / edge / cross), 2-D or skybox;
+   * geom_matid -1 = no material (rgba only). */
+  double vis_headlight[10];  /* ambient[3], diffuse[3], specular[3], active */
+  int nlight, ntex, nmat;
+  const int *light_directional, *light_castshadow, *light_active, *tex_type, *tex_builtin, *tex_mark,
+      *tex_width, *tex_height, *mat_texid, *mat_texuniform, *geom_matid;
+  const double *light_pos /*3*/, *light_dir /*3*/, *light_ambient /*3*/, *light_diffuse /*3*/,
+      *light_specular /*3*/, *light_attenuation /*3*/, *light_cutoff, *light_exponent, *tex_rgb1 /*3*/,
+      *tex_rgb2 /*3*/, *tex_markrgb /*3*/, *mat_rgba /*4*/, *mat_texrepeat /*2*/, *mat_specular,
+      *mat_shininess, *mat_emission;
 } mrs_model_view;
 
 #ifdef __cplusplus

@@ -18,6 +18,7 @@
 #include "batch.h"
 #include "devmodel.h"
 #include "raymesh.h"
+#include "lit.h"
 
 namespace mrs {
 
@@ -128,11 +129,8 @@ __device__ float ray_prim(int type, const float* s, const float lp[3], const flo
 }
 
 
-// ---- colour: flat headlight shading of the nearest geom (oracle.c orc_render_rgb restates it).
-// The reference renders RGB with OpenGL (mjr_render, src/mujoco_cameras.cpp:211-240); this is not a
-// rasteriser match: colour = rgba * (kAmbient + kDiffuse * max(0, -n.d)) with n the surface normal
-// at the hit and d the unit pixel ray, background black.
-constexpr float kAmbient = 0.3f, kDiffuse = 0.7f;
+// ---- colour: the lit model of lit.h (oracle.c lit_color restates it in fp64); local_normal gives
+// the geom-frame surface normal (unnormalised) at a hit point p
 __device__ __forceinline__ void local_normal(int type, const float* s, const float p[3], float n[3]) {
   n[0] = 0; n[1] = 0; n[2] = 1;
   switch (type) {
@@ -157,31 +155,22 @@ __device__ __forceinline__ void local_normal(int type, const float* s, const flo
     default: break;
   }
 }
-// Lambert term max(0, -cos) between the (unnormalised) normal nv and ray v, both in one frame
-__device__ __forceinline__ float lambert(const float nv[3], const float v[3]) {
-  const float nn = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
-  const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-  const float c = -(nv[0] * v[0] + nv[1] * v[1] + nv[2] * v[2]) * rsqrtf(fmaxf(nn * vv, 1e-30f));
-  return fmaxf(c, 0.0f);
-}
-__device__ __forceinline__ void shade(const float* rgba, float lam, unsigned char* px) {
-  const float k = kAmbient + kDiffuse * lam;
-  for (int c = 0; c < 3; ++c) px[c] = static_cast<unsigned char>(fminf(fmaxf(rgba[c] * k, 0.0f), 1.0f) * 255.0f + 0.5f);
-}
 
 // One workgroup renders a 16x16-pixel tile of one env.  The tile's pixel rays lie inside a cone
 // (apex at the camera, axis through the tile centre, half-angle to the widest corner ray); a geom
 // whose bounding sphere misses that cone, or a plane no ray of the cone can reach, is skipped by the
 // whole tile, and the pixels test only the remaining candidates.  Culling only removes geoms no pixel
 // ray can hit, so every pixel keeps the nearest hit over all geoms.
+template <bool kRGB>
 __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const int* geom_group,
                                                     const float* geom_size, const float* geom_rbound,
                                                     const float* geom_rgba, int ngeom, const float* geom_xpos,
                                                     const float* geom_xmat, const float* cam_xpos,
                                                     const float* cam_xmat, int ncam, int cam, int env0, int W,
                                                     int H, float f, float znear, float zfar, float* out,
-                                                    unsigned char* rgb, MeshRef mesh) {
+                                                    unsigned char* rgb, MeshRef mesh, LitRef lr) {
   __shared__ float gp[kMaxRenderGeoms * 3];
+  __shared__ LitFrame LF;
   __shared__ float gm[kMaxRenderGeoms * 9];
   __shared__ float cpos[3], cmat[9];
   __shared__ int cand[kMaxRenderGeoms];
@@ -193,6 +182,8 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
   if (threadIdx.x < 3) cpos[threadIdx.x] = cam_xpos[(eo * ncam + cam) * 3 + threadIdx.x];
   if (threadIdx.x < 9) cmat[threadIdx.x] = cam_xmat[(eo * ncam + cam) * 9 + threadIdx.x];
   if (threadIdx.x == 0) ncand = 0;
+  if (kRGB && threadIdx.x == 255)
+    lit_stage(LF, lr, cam_xpos + (eo * ncam + cam) * 3, cam_xmat + (eo * ncam + cam) * 9);
   const int tiles_x = (W + 15) / 16;
   const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
   __syncthreads();
@@ -284,13 +275,13 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
   }
   const bool hit = !(best < 0 || best > zfar);
   out[(size_t)blockIdx.y * W * H + pix] = hit ? best : zfar;
-  if (rgb) {
+  if constexpr (kRGB) {
     unsigned char* px = rgb + ((size_t)blockIdx.y * W * H + pix) * 3;
-    if (!hit) { px[0] = px[1] = px[2] = 0; return; }
+    if (!hit) { lit_sky(LF, dc[0], dc[1], px); return; }
     const float* p = gp + 3 * bestg;
     const float* mm = gm + 9 * bestg;
     const float dv[3] = {cpos[0] - p[0], cpos[1] - p[1], cpos[2] - p[2]};
-    float q[3], nl[3], nw[3];
+    float q[3], nl[3], nw[3], nc[3];
     for (int i = 0; i < 3; ++i)
       q[i] = mm[i] * dv[0] + mm[3 + i] * dv[1] + mm[6 + i] * dv[2] +
              best * (mm[i] * vec[0] + mm[3 + i] * vec[1] + mm[6 + i] * vec[2]);
@@ -311,7 +302,47 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
       local_normal(geom_type[bestg], geom_size + 3 * bestg, q, nl);
     }
     for (int i = 0; i < 3; ++i) nw[i] = mm[3 * i] * nl[0] + mm[3 * i + 1] * nl[1] + mm[3 * i + 2] * nl[2];
-    shade(geom_rgba + 4 * bestg, lambert(nw, vec), px);
+    for (int j = 0; j < 3; ++j) nc[j] = cmat[j] * nw[0] + cmat[3 + j] * nw[1] + cmat[6 + j] * nw[2];
+    float rgba3[3] = {geom_rgba[4 * bestg], geom_rgba[4 * bestg + 1], geom_rgba[4 * bestg + 2]};
+    // shadow rays in the world frame: every geom of groups 0-2 with alpha > 0, bounding-sphere reject
+    auto occ = [&](const float* o, const float* L, float dist) {
+      float ow[3], lw[3];
+      for (int i = 0; i < 3; ++i) {
+        ow[i] = cpos[i] + cmat[3 * i] * o[0] + cmat[3 * i + 1] * o[1] + cmat[3 * i + 2] * o[2];
+        lw[i] = cmat[3 * i] * L[0] + cmat[3 * i + 1] * L[1] + cmat[3 * i + 2] * L[2];
+      }
+      for (int g = 0; g < ngeom; ++g) {
+        const int grp = geom_group[g];
+        if (grp < 0 || grp > 2 || geom_rgba[4 * g + 3] == 0) continue;
+        const float* gpp = gp + 3 * g;
+        const float* gmm = gm + 9 * g;
+        const float d[3] = {ow[0] - gpp[0], ow[1] - gpp[1], ow[2] - gpp[2]};
+        const int t = geom_type[g];
+        if (t != MRS_GEOM_PLANE) {
+          const float rb = geom_rbound[g] * 1.001f + 1e-4f;
+          const float pr = -(d[0] * lw[0] + d[1] * lw[1] + d[2] * lw[2]);
+          const float dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+          if (dd > rb * rb && (pr < 0 || dd - pr * pr > rb * rb)) continue;
+        }
+        float lp[3], lv[3];
+        for (int i = 0; i < 3; ++i) {
+          lp[i] = gmm[i] * d[0] + gmm[3 + i] * d[1] + gmm[6 + i] * d[2];
+          lv[i] = gmm[i] * lw[0] + gmm[3 + i] * lw[1] + gmm[6 + i] * lw[2];
+        }
+        float th;
+        if (t == MRS_GEOM_MESH) {
+          const int id = mesh.dataid[g];
+          int tri;
+          th = ray_mesh(mesh.tri + 9 * mesh.faceadr[id], mesh.facenum[id], geom_size + 3 * g, lp, lv,
+                        mesh.bvh + 8 * mesh.bvhadr[id], mesh.bvhnum[id], &tri);
+        } else {
+          th = ray_prim(t, geom_size + 3 * g, lp, lv);
+        }
+        if (th >= 0 && th < dist) return true;
+      }
+      return false;
+    };
+    lit_pixel(LF, lr, bestg, rgba3, geom_type[bestg], geom_size + 3 * bestg, q, dc[0], dc[1], best, nc, occ, px);
   }
 }
 
@@ -330,11 +361,12 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
 #define MRS_DEPTH_TILE_H 16  // measured C4 (2048 frames): 4 rows 2.08 ms, 8 rows 1.70, 16 rows 1.68, 32 rows 2.13
 #endif
 constexpr int kDepthTileW = 64, kDepthTileH = MRS_DEPTH_TILE_H, kDepthGeoms = 64;
-struct DepthGeom {  // 28 floats in LDS
+struct DepthGeom {  // 30 words in LDS
   float lp[3], A[9], size[3];  // row i of A = R'C is also the geom's axis i in the camera frame
   float cc[3], ext[3];         // cull: centre in the camera frame, oriented-box half extents
   float rgba[3];               // colour (RGB output)
   int type, vis, dataid;
+  int cast;                    // casts shadows (groups 0-2, alpha > 0; no frustum cull)
 };
 __device__ __forceinline__ float ray_box_slab(const float* s, const float lp[3], const float lv[3]) {
   float tmin = -3.0e38f, tmax = 3.0e38f;
@@ -367,6 +399,7 @@ __device__ __forceinline__ void stage_depth_geom(DepthGeom* G, const int* geom_t
     DepthGeom& o = G[g];
     const int grp = geom_group[g];
     o.vis = !(grp < 0 || grp > 2 || geom_rgba[4 * g + 3] == 0);
+    o.cast = o.vis;
     const float* p = geom_xpos + eo * 3 * ngeom + 3 * g;
     const float* R = geom_xmat + eo * 9 * ngeom + 9 * g;
     const float d[3] = {cpos[0] - p[0], cpos[1] - p[1], cpos[2] - p[2]};
@@ -401,19 +434,53 @@ __device__ __forceinline__ void stage_depth_geom(DepthGeom* G, const int* geom_t
     }
   }
 }
+// shadow ray of the camera-frame kernels (lit_pixel's occluded): does a shadow-casting geom cross
+// o + s L, 0 <= s < dist?  Geom-frame ray through the staged lp and A (a camera-frame point o maps to
+// lp + A o); a bounding-sphere reject on the culling box first.  Oracle: ray_scene over groups 0-2.
+__device__ inline bool occluded_staged(const DepthGeom* G, int ngeom, const MeshRef& mesh, const float o[3],
+                                       const float L[3], float dist) {
+  for (int k = 0; k < ngeom; ++k) {
+    const DepthGeom& h = G[k];
+    if (!h.cast) continue;
+    if (h.type != MRS_GEOM_PLANE) {
+      const float v[3] = {h.cc[0] - o[0], h.cc[1] - o[1], h.cc[2] - o[2]};
+      const float r2 = h.ext[0] * h.ext[0] + h.ext[1] * h.ext[1] + h.ext[2] * h.ext[2];
+      const float pr = v[0] * L[0] + v[1] * L[1] + v[2] * L[2];
+      const float vv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+      if (vv > r2 && (pr < 0 || vv - pr * pr > r2)) continue;  // origin outside, sphere behind or beside
+    }
+    float lp[3], lv[3];
+    for (int i = 0; i < 3; ++i) {
+      lp[i] = h.lp[i] + h.A[3 * i] * o[0] + h.A[3 * i + 1] * o[1] + h.A[3 * i + 2] * o[2];
+      lv[i] = h.A[3 * i] * L[0] + h.A[3 * i + 1] * L[1] + h.A[3 * i + 2] * L[2];
+    }
+    float t;
+    if (h.type == MRS_GEOM_BOX) t = ray_box_slab(h.size, lp, lv);
+    else if (h.type == MRS_GEOM_MESH) {
+      int tri;
+      t = ray_mesh(mesh.tri + 9 * mesh.faceadr[h.dataid], mesh.facenum[h.dataid], h.size, lp, lv,
+                   mesh.bvh + 8 * mesh.bvhadr[h.dataid], mesh.bvhnum[h.dataid], &tri);
+    } else t = ray_prim(h.type, h.size, lp, lv);
+    if (t >= 0 && t < dist) return true;
+  }
+  return false;
+}
+template <bool kRGB>
 __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, const int* geom_group,
                                                        const float* geom_size, const float* geom_rgba, int ngeom,
                                                        const float* geom_xpos, const float* geom_xmat,
                                                        const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
                                                        int env0, int W, int H, float f, float znear, float zfar,
-                                                       float* out, unsigned char* rgb, MeshRef mesh) {
+                                                       float* out, unsigned char* rgb, MeshRef mesh, LitRef lr) {
   __shared__ DepthGeom G[kDepthGeoms];
+  __shared__ LitFrame LF;
   const int env = env0 + blockIdx.x;
   const size_t eo = static_cast<size_t>(env);
   const float* cp = cam_xpos + (eo * ncam + cam) * 3;
   const float* cm = cam_xmat + (eo * ncam + cam) * 9;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   stage_depth_geom(G, geom_type, geom_group, geom_size, geom_rgba, ngeom, geom_xpos, geom_xmat, cp, cm, eo, znear, zfar, mesh);
+  if (kRGB && threadIdx.x == 64) lit_stage(LF, lr, cp, cm);
   __syncthreads();
   const int tiles_x = (W + kDepthTileW - 1) / kDepthTileW, tiles_y = (H + kDepthTileH - 1) / kDepthTileH;
   float* img = out + static_cast<size_t>(blockIdx.x) * W * H;
@@ -486,23 +553,22 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         const int row = ty * kDepthTileH + k;
         if (row < H) img[static_cast<size_t>(row) * W + col] = (best[k] < 0 || best[k] > zfar) ? zfar : best[k];
       }
-      if (rgb) {
+      if constexpr (kRGB) {
         unsigned char* frame = rgb + static_cast<size_t>(blockIdx.x) * W * H * 3;
         for (int k = 0; k < kDepthTileH; ++k) {
           const int row = ty * kDepthTileH + k;
           if (row >= H) break;
           unsigned char* px = frame + (static_cast<size_t>(row) * W + col) * 3;
-          if (best[k] < 0 || best[k] > zfar) { px[0] = px[1] = px[2] = 0; continue; }
-          const DepthGeom& o = G[bestg[k]];
+          if (best[k] < 0 || best[k] > zfar) { lit_sky(LF, dx, dy[k], px); continue; }
+          const int g = bestg[k];
+          const DepthGeom& o = G[g];
           // hit point in the geom frame lp + t lv; normal back to the camera frame through A's rows
-          const float v[3] = {dx, dy[k], -1.0f};
-          float q[3], nl[3], nc[3];
-          for (int i = 0; i < 3; ++i) q[i] = o.lp[i] + best[k] * (o.A[3 * i] * dx + o.A[3 * i + 1] * dy[k] - o.A[3 * i + 2]);
+          float q[3], nl[3], nc[3], lv[3];
+          pixel_ray(o.A, dx, dy[k], lv);
+          for (int i = 0; i < 3; ++i) q[i] = o.lp[i] + best[k] * lv[i];
           if (o.type == MRS_GEOM_MESH) {  // the hit triangle's normal, facing the ray
             const float* mv = mesh.vert + 3 * mesh.vertadr[o.dataid];
             const int* mf = mesh.face + 3 * mesh.faceadr[o.dataid];
-            float lv[3];
-        pixel_ray(o.A, dx, dy[k], lv);
             int tri = 0;
             ray_mesh(mesh.tri + 9 * mesh.faceadr[o.dataid], mesh.facenum[o.dataid], o.size, o.lp, lv,
                      mesh.bvh + 8 * mesh.bvhadr[o.dataid], mesh.bvhnum[o.dataid], &tri);
@@ -511,7 +577,9 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
             local_normal(o.type, o.size, q, nl);
           }
           for (int j = 0; j < 3; ++j) nc[j] = nl[0] * o.A[j] + nl[1] * o.A[3 + j] + nl[2] * o.A[6 + j];
-          shade(o.rgba, lambert(nc, v), px);
+          lit_pixel(LF, lr, g, o.rgba, o.type, o.size, q, dx, dy[k], best[k], nc,
+                    [&](const float* so, const float* sl, float sd) { return occluded_staged(G, ngeom, mesh, so, sl, sd); },
+                    px);
         }
       }
     }
@@ -585,6 +653,7 @@ __device__ __forceinline__ int tri_box(const DepthGeom& o, const float* mv, cons
   return (r1 / kBandH - r0 / kBandH) > kMaxSpan ? 2 : 1;
 }
 
+template <bool kRGB>
 __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, const int* geom_group,
                                                          const float* geom_size, const float* geom_rgba, int ngeom,
                                                          const float* geom_xpos, const float* geom_xmat,
@@ -592,8 +661,9 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
                                                          int env0, int W, int H, float f, float znear, float zfar,
                                                          float* out, unsigned char* rgb, MeshRef mesh, const int* mgeom,
                                                          const int* mbase, int nmg, int npair,
-                                                         unsigned long long* lists) {
+                                                         unsigned long long* lists, LitRef lr) {
   __shared__ DepthGeom G[kDepthGeoms];
+  __shared__ LitFrame LF;
   __shared__ int cnt[kMaxBands + 1], cur[kMaxBands], mg[kDepthGeoms], mb[kDepthGeoms + 1];
   __shared__ int nside, maxspan;
   extern __shared__ unsigned long long band[];  // W x kBandH (t bits << 32 | geom << 24 | triangle)
@@ -608,6 +678,7 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
   for (int i = tid; i < nb; i += 256) cur[i] = 0;
   for (int i = tid; i < nmg; i += 256) { mg[i] = mgeom[i]; mb[i] = mbase[i]; }
   if (tid == 0) { mb[nmg] = npair; nside = 0; maxspan = 0; }
+  if (kRGB && tid == 64) lit_stage(LF, lr, cp, cm);
   __syncthreads();
   unsigned long long* list = lists + static_cast<size_t>(blockIdx.x) * npair;
   // 1-2: count, then fill the band-sorted list (the side list fills the frame's list from its end)
@@ -737,23 +808,23 @@ __global__ __launch_bounds__(256) void depth_kernel_mesh(const int* geom_type, c
         }
       }
       img[static_cast<size_t>(r) * W + c] = (best < 0 || best > zfar) ? zfar : best;
-      if (frame) {
+      if constexpr (kRGB) {
         unsigned char* px = frame + (static_cast<size_t>(r) * W + c) * 3;
-        if (best < 0 || best > zfar) { px[0] = px[1] = px[2] = 0; continue; }
+        if (best < 0 || best > zfar) { lit_sky(LF, dx, dy, px); continue; }
         const DepthGeom& o = G[bestg];
-        const float v[3] = {dx, dy, -1.0f};
-        float lv[3];
+        float lv[3], q[3];
         pixel_ray(o.A, dx, dy, lv);
+        for (int k = 0; k < 3; ++k) q[k] = o.lp[k] + best * lv[k];
         float nl[3], nc[3];
         if (tri >= 0) {
           mesh_tri_normal(mesh.vert + 3 * mesh.vertadr[o.dataid], mesh.face + 3 * mesh.faceadr[o.dataid], tri, lv, nl);
         } else {
-          float q[3];
-          for (int k = 0; k < 3; ++k) q[k] = o.lp[k] + best * lv[k];
           local_normal(o.type, o.size, q, nl);
         }
         for (int j = 0; j < 3; ++j) nc[j] = nl[0] * o.A[j] + nl[1] * o.A[3 + j] + nl[2] * o.A[6 + j];
-        shade(o.rgba, lambert(nc, v), px);
+        lit_pixel(LF, lr, bestg, o.rgba, o.type, o.size, q, dx, dy, best, nc,
+                  [&](const float* so, const float* sl, float sd) { return occluded_staged(G, ngeom, mesh, so, sl, sd); },
+                  px);
       }
     }
     __syncthreads();
@@ -1238,6 +1309,49 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   P.addf(&d.geom_size, m.geom_size); P.addf(&d.geom_pos, m.geom_pos); P.addf(&d.geom_quat, m.geom_quat);
   P.addf(&d.geom_rbound, m.geom_rbound); P.addf(&d.geom_rgba, m.geom_rgba);
+  {
+    // lit.h's rlit block (layout in its header comment); more than kLitMaxLights lights are refused
+    if (static_cast<int>(m.light_active.size()) > kLitMaxLights)
+      throw std::runtime_error("at most " + std::to_string(kLitMaxLights) + " lights are supported");
+    const int nl = static_cast<int>(m.light_active.size()), nm = static_cast<int>(m.mat_texid.size()),
+              nt = static_cast<int>(m.tex_type.size());
+    std::vector<double> r(kLitHead + kLitLight * nl + kLitMat * nm + kLitTex * nt, 0.0);
+    for (int i = 0; i < 10; ++i) r[i] = m.vis_headlight[i];
+    r[10] = nl;
+    d.lit_sky = -1;
+    for (int t = 0; t < nt && d.lit_sky < 0; ++t)
+      if (m.tex_type[t] == MRS_TEX_SKYBOX) d.lit_sky = t;
+    r[11] = d.lit_sky;
+    for (int l = 0; l < nl; ++l) {
+      double* o = r.data() + kLitHead + kLitLight * l;
+      for (int i = 0; i < 3; ++i) {
+        o[i] = m.light_pos[3 * l + i]; o[3 + i] = m.light_dir[3 * l + i];
+        o[6 + i] = m.light_ambient[3 * l + i]; o[9 + i] = m.light_diffuse[3 * l + i];
+        o[12 + i] = m.light_specular[3 * l + i]; o[15 + i] = m.light_attenuation[3 * l + i];
+      }
+      o[18] = std::cos(m.light_cutoff[l] * M_PI / 180); o[19] = m.light_exponent[l];
+      o[20] = m.light_directional[l]; o[21] = m.light_castshadow[l]; o[22] = m.light_active[l];
+    }
+    d.lit_nlight = nl;
+    d.lit_mat0 = kLitHead + kLitLight * nl;
+    d.lit_tex0 = d.lit_mat0 + kLitMat * nm;
+    for (int k = 0; k < nm; ++k) {
+      double* o = r.data() + d.lit_mat0 + kLitMat * k;
+      o[0] = m.mat_texid[k]; o[1] = m.mat_texuniform[k];
+      o[2] = m.mat_texrepeat[2 * k]; o[3] = m.mat_texrepeat[2 * k + 1];
+      o[4] = m.mat_specular[k]; o[5] = m.mat_shininess[k]; o[6] = m.mat_emission[k];
+    }
+    for (int t = 0; t < nt; ++t) {
+      double* o = r.data() + d.lit_tex0 + kLitTex * t;
+      o[0] = m.tex_type[t]; o[1] = m.tex_builtin[t]; o[2] = m.tex_mark[t];
+      o[3] = m.tex_width[t]; o[4] = m.tex_height[t];
+      for (int i = 0; i < 3; ++i) { o[5 + i] = m.tex_rgb1[3 * t + i]; o[8 + i] = m.tex_rgb2[3 * t + i]; o[11 + i] = m.tex_markrgb[3 * t + i]; }
+    }
+    P.addf(&d.rlit, r);
+    std::vector<int> mid(m.ngeom, -1);
+    for (int g = 0; g < m.ngeom && g < static_cast<int>(m.geom_matid.size()); ++g) mid[g] = m.geom_matid[g];
+    P.addi(&d.geom_matid, mid);
+  }
   P.addi(&d.pair_g1, pg1); P.addi(&d.pair_g2, pg2); P.addi(&d.pair_dim, pdim);
   P.addi(&d.eq_type, eq_t); P.addi(&d.eq_obj1id, eq_o1); P.addi(&d.eq_obj2id, eq_o2);
   P.addf(&d.eq_solref, eq_sr); P.addf(&d.eq_solimp, eq_si); P.addf(&d.eq_data, eq_dat);
@@ -1974,6 +2088,7 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
   const DevModel& d = b->dm;
   const MeshRef mesh{d.mesh_vert.p, d.mesh_face.p, d.geom_dataid.p, d.mesh_vertadr.p, d.mesh_faceadr.p,
                      d.mesh_facenum.p, d.mesh_bvh.p, d.mesh_bvhadr.p, d.mesh_bvhnum.p, d.mesh_tri.p};
+  const LitRef lr{d.rlit.p, d.geom_matid.p, d.lit_nlight, d.lit_mat0, d.lit_tex0, d.lit_sky};
   // the binned kernel needs its band of W x kBandH 64-bit keys in LDS (within the device's per-block
   // limit) and a per-frame triangle list in global memory: frames go in chunks whose lists fit a
   // budget (MRS_RAST_BUDGET_MB, default 2048 MB), so a large mesh over many envs renders in several
@@ -2005,20 +2120,23 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
     for (int c0 = 0; c0 < n; c0 += chunk) {
       const int nc = std::min(chunk, n - c0);
       const size_t px = static_cast<size_t>(c0) * W * H;
-      hipLaunchKernelGGL(depth_kernel_mesh, dim3(nc), dim3(256), band_lds, stream, d.geom_type.p, d.geom_group.p,
+      hipLaunchKernelGGL(drgb ? depth_kernel_mesh<true> : depth_kernel_mesh<false>, dim3(nc), dim3(256), band_lds,
+                         stream, d.geom_type.p, d.geom_group.p,
                          d.geom_size.p, d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam, cam,
                          env0 + c0, W, H, f, znear, zfar, dout + px, drgb ? drgb + 3 * px : nullptr, mesh,
-                         d.rast_geom.p, d.rast_base.p, d.nrast, d.nrast_pair, b->rast_list);
+                         d.rast_geom.p, d.rast_base.p, d.nrast, d.nrast_pair, b->rast_list, lr);
     }
   } else if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
-    hipLaunchKernelGGL(depth_kernel_v2, dim3(n), dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p,
+    hipLaunchKernelGGL(drgb ? depth_kernel_v2<true> : depth_kernel_v2<false>, dim3(n), dim3(256), 0, stream,
+                       d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr);
   } else {
     dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
-    hipLaunchKernelGGL(depth_kernel, grid, dim3(256), 0, stream, d.geom_type.p, d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
+    hipLaunchKernelGGL(drgb ? depth_kernel<true> : depth_kernel<false>, grid, dim3(256), 0, stream, d.geom_type.p,
+                       d.geom_group.p, d.geom_size.p, d.geom_rbound.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr);
   }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(b->ev1[1], stream));

@@ -146,6 +146,10 @@ struct DevModel {
   // the triangles pre-gathered in device face order (same index as mesh_face): vertex a and the edges
   // b - a, c - a in fp32, 9 floats each -- one load per triangle instead of face -> vertex chains
   CPtr<float> mesh_tri;
+  // colour render: lit.h's packed light / material / texture block and each geom's material id
+  CPtr<float> rlit;
+  CPtr<int> geom_matid;
+  int lit_nlight, lit_mat0, lit_tex0, lit_sky;
   // candidate collision pairs (static filters applied; g1 has the smaller geom type)
   // active equality constraints (mrs_model_view eq_*, inactive ones dropped on the host): neq of
   // them giving neq_rows rows (connect 3, weld 6, joint 1), first in the row order

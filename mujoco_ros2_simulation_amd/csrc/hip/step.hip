@@ -1286,7 +1286,8 @@ __device__ bool mpr_polish(const MeshTab mt, const Shape& A, const Shape& B, con
         const int r = pol_move(mt, P, st, n, dl);
         if (r < 0) return false;
         if (r > 0) { moved = true; break; }
-        if (step < 2e-7f) { conv = true; break; }
+        // (fp32: a step below 2e-6 leaves an error of order its square, under the rounding floor)
+        if (step < 2e-6f) { conv = true; break; }
       }
     }
     if (moved) continue;

@@ -221,6 +221,13 @@ struct GeomRec {
   double rgba[4] = {0.5, 0.5, 0.5, 1};
   double mass = -1, density = 1000;
   int mesh = -1;  // mesh id (type mesh)
+  int matid = -1;  // material id
+};
+// a <light> (MuJoCo's defaults), pose in its body's frame
+struct LightRec {
+  double pos[3] = {0, 0, 0}, dir[3] = {0, 0, -1}, ambient[3] = {0, 0, 0}, diffuse[3] = {0.7, 0.7, 0.7},
+         specular[3] = {0.3, 0.3, 0.3}, attenuation[3] = {1, 0, 0}, cutoff = 45, exponent = 10;
+  int directional = 0, castshadow = 1, active = 1;
 };
 // a processed mesh asset: vertices in its inertial frame; pos/quat place that frame in the mesh file's
 // frame; volume and unit-density principal moments for the geom's mass
@@ -263,6 +270,7 @@ struct BodyRec {
   std::vector<GeomRec> geoms;
   std::vector<SiteRec> sites;
   std::vector<CamRec> cams;
+  std::vector<LightRec> lights;
 };
 
 struct Compiler {
@@ -277,6 +285,7 @@ struct Compiler {
   std::vector<MeshRec> meshes;
   std::map<std::string, int> mesh_ids;
   std::map<std::string, std::vector<double>> materials;  // name -> rgba
+  std::map<std::string, int> material_ids, texture_ids;
 
   Compiler() {
     auto main = std::make_unique<DefaultClass>();
@@ -471,15 +480,73 @@ struct Compiler {
   // the inertial frame (centre of mass, principal axes, right-handed) and the geoms using the mesh
   // are offset by that frame.
   void parse_asset(const XmlElement* sec) {
+    // textures first (materials refer to them), then everything else in document order
+    for (int pass = 0; pass < 2; ++pass)
     for (auto& c : sec->children) {
       const XmlElement* e = c.get();
+      if ((pass == 0) != (e->tag == "texture")) continue;
       if (e->tag == "material") {
-        double rgba[4] = {1, 1, 1, 1};
-        get_reals(e, nullptr, "material", "rgba", rgba, 4, true);
-        if (auto* n = e->attr("name")) materials[*n] = std::vector<double>(rgba, rgba + 4);
+        // [upstream mjCMaterial] rgba, texture, texrepeat, texuniform, specular, shininess, emission
+        const DefaultClass* cls = resolve_class(e, "");
+        double rgba[4] = {1, 1, 1, 1}, rep[2] = {1, 1}, spec = 0.5, shin = 0.5, emis = 0;
+        get_reals(e, cls, "material", "rgba", rgba, 4, true);
+        get_reals(e, cls, "material", "texrepeat", rep, 2, true);
+        get_real(e, cls, "material", "specular", spec);
+        get_real(e, cls, "material", "shininess", shin);
+        get_real(e, cls, "material", "emission", emis);
+        std::string tex, uni;
+        int texid = -1;
+        if (get_str(e, cls, "material", "texture", tex)) {
+          auto it = texture_ids.find(tex);
+          if (it == texture_ids.end()) fail(e, "material references unknown texture '" + tex + "'");
+          texid = it->second;
+        }
+        get_str(e, cls, "material", "texuniform", uni);
+        if (auto* n = e->attr("name")) {
+          materials[*n] = std::vector<double>(rgba, rgba + 4);
+          material_ids[*n] = static_cast<int>(m.mat_texid.size());
+        }
+        m.mat_texid.push_back(texid);
+        m.mat_texuniform.push_back(uni == "true");
+        m.mat_rgba.insert(m.mat_rgba.end(), rgba, rgba + 4);
+        m.mat_texrepeat.insert(m.mat_texrepeat.end(), rep, rep + 2);
+        m.mat_specular.push_back(spec);
+        m.mat_shininess.push_back(shin);
+        m.mat_emission.push_back(emis);
         continue;
       }
-      if (e->tag == "texture" || e->tag == "hfield" || e->tag == "skin" || e->tag == "model") {
+      if (e->tag == "texture") {
+        // [upstream mjCTexture] procedural builtins only (no image files): checker, gradient, flat
+        std::string type = "cube", builtin = "none", mark = "none", file;
+        get_str(e, nullptr, "texture", "type", type);
+        get_str(e, nullptr, "texture", "builtin", builtin);
+        get_str(e, nullptr, "texture", "mark", mark);
+        if (get_str(e, nullptr, "texture", "file", file) || e->attr("fileright") || e->attr("gridsize"))
+          fail(e, "texture files are not supported (builtin checker / gradient / flat only)");
+        double rgb1[3] = {0.8, 0.8, 0.8}, rgb2[3] = {0.5, 0.5, 0.5}, markrgb[3] = {0, 0, 0}, w = 0, h = 0;
+        get_reals(e, nullptr, "texture", "rgb1", rgb1, 3, true);
+        get_reals(e, nullptr, "texture", "rgb2", rgb2, 3, true);
+        get_reals(e, nullptr, "texture", "markrgb", markrgb, 3, true);
+        get_real(e, nullptr, "texture", "width", w);
+        get_real(e, nullptr, "texture", "height", h);
+        const int t = type == "2d" ? MRS_TEX_2D : type == "cube" ? MRS_TEX_CUBE : type == "skybox" ? MRS_TEX_SKYBOX : -1;
+        const int b = builtin == "none" ? MRS_BUILTIN_NONE : builtin == "gradient" ? MRS_BUILTIN_GRADIENT
+                      : builtin == "checker" ? MRS_BUILTIN_CHECKER : builtin == "flat" ? MRS_BUILTIN_FLAT : -1;
+        const int mk = mark == "none" ? MRS_MARK_NONE : mark == "edge" ? MRS_MARK_EDGE : mark == "cross" ? MRS_MARK_CROSS : -1;
+        if (t < 0 || b < 0 || mk < 0) fail(e, "unsupported texture type / builtin / mark");
+        if (b == MRS_BUILTIN_NONE) fail(e, "a texture needs a builtin (texture files are not supported)");
+        if (auto* n = e->attr("name")) texture_ids[*n] = static_cast<int>(m.tex_type.size());
+        m.tex_type.push_back(t);
+        m.tex_builtin.push_back(b);
+        m.tex_mark.push_back(mk);
+        m.tex_width.push_back(std::max(1, static_cast<int>(w > 0 ? w : 2)));
+        m.tex_height.push_back(std::max(1, static_cast<int>(h > 0 ? h : (w > 0 ? w : 2))));
+        m.tex_rgb1.insert(m.tex_rgb1.end(), rgb1, rgb1 + 3);
+        m.tex_rgb2.insert(m.tex_rgb2.end(), rgb2, rgb2 + 3);
+        m.tex_markrgb.insert(m.tex_markrgb.end(), markrgb, markrgb + 3);
+        continue;
+      }
+      if (e->tag == "hfield" || e->tag == "skin" || e->tag == "model") {
         if (e->tag == "hfield") fail(e, "height fields are not supported");
         continue;
       }
@@ -675,8 +742,10 @@ struct Compiler {
         parse_body_children(c, body_id, cc, frame.compose(local), suffix);
       } else if (c->tag == "replicate") {
         parse_replicate(c, body_id, childclass, frame, suffix);
-      } else if (c->tag == "light" || c->tag == "composite" || c->tag == "plugin") {
-        if (c->tag != "light") fail(c, "unsupported element");
+      } else if (c->tag == "light") {
+        bodies[body_id].lights.push_back(parse_light(c, childclass, frame));
+      } else if (c->tag == "composite" || c->tag == "plugin") {
+        fail(c, "unsupported element");
       } else {
         fail(c, "unsupported element in body");
       }
@@ -844,8 +913,12 @@ struct Compiler {
     get_reals(e, cls, tag, "solimp", g.solimp, 5);
     const bool rgba_given = get_reals(e, cls, tag, "rgba", g.rgba, 4, true);
     std::string material;
-    if (!rgba_given && get_str(e, cls, tag, "material", material) && materials.count(material))
-      for (int k = 0; k < 4; ++k) g.rgba[k] = materials[material][k];
+    if (get_str(e, cls, tag, "material", material)) {
+      if (!materials.count(material)) fail(e, "geom references unknown material '" + material + "'");
+      g.matid = material_ids[material];
+      if (!rgba_given)
+        for (int k = 0; k < 4; ++k) g.rgba[k] = materials[material][k];
+    }
     get_real(e, cls, tag, "mass", g.mass);
     get_real(e, cls, tag, "density", g.density);
     if (g.condim != 1 && g.condim != 3) fail(e, "only condim 1 and 3 are supported");
@@ -885,6 +958,64 @@ struct Compiler {
     }
     frame.apply(g.pos, g.quat);
     return g;
+  }
+  // <light> [upstream mjCLight]: fixed mode only; pose in the body's frame (the enclosing frames applied)
+  LightRec parse_light(const XmlElement* e, const std::string& childclass, const Frame& frame) {
+    const DefaultClass* cls = resolve_class(e, childclass);
+    const std::string tag = "light";
+    LightRec l;
+    get_reals(e, cls, tag, "pos", l.pos, 3, true);
+    get_reals(e, cls, tag, "dir", l.dir, 3, true);
+    get_reals(e, cls, tag, "ambient", l.ambient, 3, true);
+    get_reals(e, cls, tag, "diffuse", l.diffuse, 3, true);
+    get_reals(e, cls, tag, "specular", l.specular, 3, true);
+    get_reals(e, cls, tag, "attenuation", l.attenuation, 3, true);
+    get_real(e, cls, tag, "cutoff", l.cutoff);
+    get_real(e, cls, tag, "exponent", l.exponent);
+    std::string s;
+    if (get_str(e, cls, tag, "directional", s)) l.directional = s == "true";
+    if (get_str(e, cls, tag, "type", s)) {
+      if (s != "directional" && s != "spot") fail(e, "light type '" + s + "' is not supported");
+      l.directional = s == "directional";
+    }
+    if (get_str(e, cls, tag, "castshadow", s)) l.castshadow = s == "true";
+    if (get_str(e, cls, tag, "active", s)) l.active = s == "true";
+    if (get_str(e, cls, tag, "mode", s) && s != "fixed") fail(e, "light mode '" + s + "' is not supported (fixed only)");
+    double n = std::sqrt(l.dir[0] * l.dir[0] + l.dir[1] * l.dir[1] + l.dir[2] * l.dir[2]);
+    if (n < 1e-12) fail(e, "light dir is zero");
+    for (int i = 0; i < 3; ++i) l.dir[i] /= n;
+    double q[4] = {1, 0, 0, 0}, d[3];
+    frame.apply(l.pos, q);
+    rot_vec_quat(d, l.dir, frame.quat);
+    for (int i = 0; i < 3; ++i) l.dir[i] = d[i];
+    return l;
+  }
+  // lights into the model in the world frame (after set0: the bodies' qpos0 poses); a light must be
+  // fixed in the world (on the world body or a body welded to it)
+  void flatten_lights() {
+    size_t nl = 0;
+    for (const auto& bd : bodies) nl += bd.lights.size();
+    // the fixed-function pipeline the colour image restates has 8 light slots (the headlight aside)
+    if (nl > 8) throw std::runtime_error("MJCF error: at most 8 lights are supported");
+    for (int b = 0; b < static_cast<int>(bodies.size()); ++b)
+      for (const LightRec& l : bodies[b].lights) {
+        if (m.body_weldid[b] != 0) throw std::runtime_error("MJCF error: lights on moving bodies are not supported");
+        double p[3], d[3];
+        rot_vec_quat(p, l.pos, &x0quat[4 * b]);
+        for (int i = 0; i < 3; ++i) p[i] += x0pos[3 * b + i];
+        rot_vec_quat(d, l.dir, &x0quat[4 * b]);
+        m.light_pos.insert(m.light_pos.end(), p, p + 3);
+        m.light_dir.insert(m.light_dir.end(), d, d + 3);
+        m.light_ambient.insert(m.light_ambient.end(), l.ambient, l.ambient + 3);
+        m.light_diffuse.insert(m.light_diffuse.end(), l.diffuse, l.diffuse + 3);
+        m.light_specular.insert(m.light_specular.end(), l.specular, l.specular + 3);
+        m.light_attenuation.insert(m.light_attenuation.end(), l.attenuation, l.attenuation + 3);
+        m.light_cutoff.push_back(l.cutoff);
+        m.light_exponent.push_back(l.exponent);
+        m.light_directional.push_back(l.directional);
+        m.light_castshadow.push_back(l.castshadow);
+        m.light_active.push_back(l.active);
+      }
   }
   SiteRec parse_site(const XmlElement* e, const std::string& childclass, const Frame& frame,
                      const std::string& suffix) {
@@ -1228,6 +1359,7 @@ struct Compiler {
         m.geom_solref.insert(m.geom_solref.end(), G.solref, G.solref + 2);
         m.geom_solimp.insert(m.geom_solimp.end(), G.solimp, G.solimp + 5);
         m.geom_rgba.insert(m.geom_rgba.end(), G.rgba, G.rgba + 4);
+        m.geom_matid.push_back(G.matid);
         ++m.ngeom;
       }
       for (SiteRec& S : B.sites) {
@@ -1689,6 +1821,12 @@ struct Compiler {
           if (v->tag == "map") {
             if (auto* s = v->attr("znear")) m.vis_znear = parse_reals(*s, v.get(), "znear").at(0);
             if (auto* s = v->attr("zfar")) m.vis_zfar = parse_reals(*s, v.get(), "zfar").at(0);
+          } else if (v->tag == "headlight") {
+            get_reals(v.get(), nullptr, "headlight", "ambient", m.vis_headlight, 3, true);
+            get_reals(v.get(), nullptr, "headlight", "diffuse", m.vis_headlight + 3, 3, true);
+            get_reals(v.get(), nullptr, "headlight", "specular", m.vis_headlight + 6, 3, true);
+            std::string a;
+            if (get_str(v.get(), nullptr, "headlight", "active", a)) m.vis_headlight[9] = a == "0" || a == "false" ? 0 : 1;
           }
       }
     }
@@ -1703,6 +1841,7 @@ struct Compiler {
     flatten();
     flatten_meshes();
     set0();
+    flatten_lights();
     // pass 3: elements that reference the tree
     for (auto& c : root->children) {
       if (c->tag == "actuator") parse_actuators(c.get());
@@ -2004,6 +2143,16 @@ mrs_model_view Model::view() const {
   v.nmeshhull = static_cast<int>(mesh_hull.size());
   MRS_V(geom_dataid); MRS_V(mesh_vertadr); MRS_V(mesh_vertnum); MRS_V(mesh_faceadr); MRS_V(mesh_facenum);
   MRS_V(mesh_hulladr); MRS_V(mesh_hullnum); MRS_V(mesh_face); MRS_V(mesh_hull); MRS_V(mesh_vert);
+  for (int i = 0; i < 10; ++i) v.vis_headlight[i] = vis_headlight[i];
+  v.nlight = static_cast<int>(light_active.size());
+  v.ntex = static_cast<int>(tex_type.size());
+  v.nmat = static_cast<int>(mat_texid.size());
+  MRS_V(light_directional); MRS_V(light_castshadow); MRS_V(light_active); MRS_V(tex_type); MRS_V(tex_builtin);
+  MRS_V(tex_mark); MRS_V(tex_width); MRS_V(tex_height); MRS_V(mat_texid); MRS_V(mat_texuniform); MRS_V(geom_matid);
+  MRS_V(light_pos); MRS_V(light_dir); MRS_V(light_ambient); MRS_V(light_diffuse); MRS_V(light_specular);
+  MRS_V(light_attenuation); MRS_V(light_cutoff); MRS_V(light_exponent); MRS_V(tex_rgb1); MRS_V(tex_rgb2);
+  MRS_V(tex_markrgb); MRS_V(mat_rgba); MRS_V(mat_texrepeat); MRS_V(mat_specular); MRS_V(mat_shininess);
+  MRS_V(mat_emission);
   v.neq = static_cast<int>(eq_type.size());
   MRS_V(eq_type); MRS_V(eq_obj1id); MRS_V(eq_obj2id); MRS_V(eq_active0); MRS_V(eq_solref); MRS_V(eq_solimp);
   MRS_V(eq_data);

@@ -70,6 +70,13 @@ struct Model {
   // equality constraints (mrs_model_view eq_*)
   std::vector<int> eq_type, eq_obj1id, eq_obj2id, eq_active0;
   std::vector<double> eq_solref, eq_solimp, eq_data;
+  // rendering (mrs_model_view light_* / tex_* / mat_*); MuJoCo's headlight defaults
+  double vis_headlight[10] = {0.1, 0.1, 0.1, 0.4, 0.4, 0.4, 0.5, 0.5, 0.5, 1};
+  std::vector<int> light_directional, light_castshadow, light_active, tex_type, tex_builtin, tex_mark, tex_width,
+      tex_height, mat_texid, mat_texuniform, geom_matid;
+  std::vector<double> light_pos, light_dir, light_ambient, light_diffuse, light_specular, light_attenuation,
+      light_cutoff, light_exponent, tex_rgb1, tex_rgb2, tex_markrgb, mat_rgba, mat_texrepeat, mat_specular,
+      mat_shininess, mat_emission;
 
   // names per object type (MRS_OBJ_*), index = object id
   std::map<int, std::vector<std::string>> names;

@@ -110,6 +110,21 @@ _EQ_ARRAYS = [
     ("eq_solref", "d", "neq", 2), ("eq_solimp", "d", "neq", 5), ("eq_data", "d", "neq", 11),
 ]
 EQ_CONNECT, EQ_WELD, EQ_JOINT = 0, 1, 2
+# rendering (after the equality block; vis_headlight is a fixed double[10] before the sizes)
+_REND_SIZES = ["nlight", "ntex", "nmat"]
+_REND_ARRAYS = [
+    ("light_directional", "i", "nlight", 1), ("light_castshadow", "i", "nlight", 1), ("light_active", "i", "nlight", 1),
+    ("tex_type", "i", "ntex", 1), ("tex_builtin", "i", "ntex", 1), ("tex_mark", "i", "ntex", 1),
+    ("tex_width", "i", "ntex", 1), ("tex_height", "i", "ntex", 1), ("mat_texid", "i", "nmat", 1),
+    ("mat_texuniform", "i", "nmat", 1), ("geom_matid", "i", "ngeom", 1),
+    ("light_pos", "d", "nlight", 3), ("light_dir", "d", "nlight", 3), ("light_ambient", "d", "nlight", 3),
+    ("light_diffuse", "d", "nlight", 3), ("light_specular", "d", "nlight", 3), ("light_attenuation", "d", "nlight", 3),
+    ("light_cutoff", "d", "nlight", 1), ("light_exponent", "d", "nlight", 1), ("tex_rgb1", "d", "ntex", 3),
+    ("tex_rgb2", "d", "ntex", 3), ("tex_markrgb", "d", "ntex", 3), ("mat_rgba", "d", "nmat", 4),
+    ("mat_texrepeat", "d", "nmat", 2), ("mat_specular", "d", "nmat", 1), ("mat_shininess", "d", "nmat", 1),
+    ("mat_emission", "d", "nmat", 1),
+]
+TEX_2D, TEX_CUBE, TEX_SKYBOX = 0, 1, 2
 
 
 class ModelView(C.Structure):
@@ -126,7 +141,9 @@ class ModelView(C.Structure):
                 [(n, C.c_int) for n in _CONTACT_SIZES] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _CONTACT_ARRAYS] +
                 [(n, C.c_int) for n in _EQ_SIZES] +
-                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _EQ_ARRAYS])
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _EQ_ARRAYS] +
+                [("vis_headlight", C.c_double * 10)] + [(n, C.c_int) for n in _REND_SIZES] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _REND_ARRAYS])
 
 
 _lib = None
@@ -213,14 +230,15 @@ class Model:
         self.view = ModelView()
         _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
         v = self.view
-        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES:
+        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES + _REND_SIZES:
             setattr(self, n, getattr(v, n))
         for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "restate", "integrator", "solver",
                   "iterations", "disableflags",
                   "stat_extent", "stat_meaninertia", "vis_znear", "vis_zfar"]:
             setattr(self, n, getattr(v, n))
         self.gravity = np.array(v.gravity[:])
-        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS + _EQ_ARRAYS:
+        self.vis_headlight = np.array(v.vis_headlight[:])
+        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS + _EQ_ARRAYS + _REND_ARRAYS:
             n = getattr(v, count)
             w = getattr(v, width) if isinstance(width, str) else width
             ptr = getattr(v, name)

@@ -3337,6 +3337,127 @@ static void local_normal(int type, const double* s, const double p[3], double n[
   }
 }
 
+/* ---- colour [restated from MuJoCo's OpenGL renderer (mjr_render: fixed-function lighting, materials,
+ * builtin textures, shadows, skybox); verify]: per pixel (not per vertex), per light l (the headlight
+ * first -- a directional light along the view axis with vis.headlight's colours, no shadow -- then the
+ * model's active lights, fixed in the world):
+ *   c = emission base + sum_l att_l spot_l (amb_l base + sh_l (max(0, N.L) diff_l base
+ *                                                               + [N.L > 0] max(0, N.H)^(128 shininess) spec_l specular))
+ * N the surface normal facing the viewer, L towards the light, H = normalize(L + E) with E the view
+ * axis (OpenGL's infinite viewer), att = 1 / (a0 + a1 d + a2 d^2) and spot = cos^exponent inside the
+ * cutoff cone for spot lights (1 for directional ones), sh_l = 0 when the ray from the surface (offset
+ * 1e-4 along N) towards the light hits a geom of groups 0-2 first (castshadow lights).  base = rgba,
+ * times the 2-D texture for planes (texcoords = the plane-frame hit x, y times texrepeat, per unit
+ * length when texuniform, else per plane size; nearest texel of the builtin image: 2 x 2 checker
+ * rgb1 / rgb2, vertical gradient rgb1 -> rgb2 or flat rgb1, marks edge / cross in markrgb).  Material
+ * defaults without one: specular 0.5, shininess 0.5, emission 0.  A miss shows the first skybox
+ * texture (gradient: rgb2 + (rgb1 - rgb2) (1 + d_z) / 2 of the world view direction; flat / checker:
+ * rgb1 above the horizon, rgb2 below), else black.  Channels clamped to [0, 1], rounded to 8 bits. */
+static void tex_sample(const mrs_model_view* m, int t, double u, double v, double out[3]) {
+  const int W = m->tex_width[t], H = m->tex_height[t];
+  u -= floor(u);
+  v -= floor(v);
+  int iu = (int)(u * W), iv = (int)(v * H);
+  iu = iu < 0 ? 0 : (iu >= W ? W - 1 : iu);
+  iv = iv < 0 ? 0 : (iv >= H ? H - 1 : iv);
+  const double *c1 = m->tex_rgb1 + 3 * t, *c2 = m->tex_rgb2 + 3 * t;
+  switch (m->tex_builtin[t]) {
+    case MRS_BUILTIN_CHECKER: {
+      const double* c = ((iu < W / 2) == (iv < H / 2)) ? c1 : c2;
+      for (int i = 0; i < 3; ++i) out[i] = c[i];
+      break;
+    }
+    case MRS_BUILTIN_GRADIENT: {
+      const double s = H > 1 ? (double)iv / (H - 1) : 0;
+      for (int i = 0; i < 3; ++i) out[i] = c1[i] + s * (c2[i] - c1[i]);
+      break;
+    }
+    default:
+      for (int i = 0; i < 3; ++i) out[i] = c1[i];
+  }
+  const int mk = m->tex_mark[t];
+  if ((mk == MRS_MARK_EDGE && (iu == 0 || iv == 0 || iu == W - 1 || iv == H - 1)) ||
+      (mk == MRS_MARK_CROSS && (iu == W / 2 || iv == H / 2)))
+    for (int i = 0; i < 3; ++i) out[i] = m->tex_markrgb[3 * t + i];
+}
+static void sky_color(const mrs_model_view* m, const double dir[3], double out[3]) {
+  out[0] = out[1] = out[2] = 0;
+  for (int t = 0; t < m->ntex; ++t) {
+    if (m->tex_type[t] != MRS_TEX_SKYBOX) continue;
+    const double dz = dir[2] / sqrt(dot3(dir, dir));
+    const double *c1 = m->tex_rgb1 + 3 * t, *c2 = m->tex_rgb2 + 3 * t;
+    if (m->tex_builtin[t] == MRS_BUILTIN_GRADIENT)
+      for (int i = 0; i < 3; ++i) out[i] = c2[i] + (c1[i] - c2[i]) * 0.5 * (1 + dz);
+    else
+      for (int i = 0; i < 3; ++i) out[i] = dz >= 0 ? c1[i] : c2[i];
+    return;
+  }
+}
+static void lit_color(const mrs_model_view* m, orc_ws* w, int g, const double P[3], const double nw[3],
+                      const double vec[3], const double q[3], const double E[3], double out[3]) {
+  double N[3] = {nw[0], nw[1], nw[2]}, base[3], spec_m = 0.5, shin = 0.5, emis = 0;
+  normalize3(N);
+  if (dot3(N, vec) > 0) for (int i = 0; i < 3; ++i) N[i] = -N[i];
+  for (int i = 0; i < 3; ++i) base[i] = m->geom_rgba[4 * g + i];
+  const int mat = m->nmat ? m->geom_matid[g] : -1;
+  if (mat >= 0) {
+    spec_m = m->mat_specular[mat]; shin = m->mat_shininess[mat]; emis = m->mat_emission[mat];
+    const int t = m->mat_texid[mat];
+    if (t >= 0 && m->tex_type[t] == MRS_TEX_2D && m->geom_type[g] == MRS_GEOM_PLANE) {
+      double sc[2];
+      for (int k = 0; k < 2; ++k) {
+        const double sz = m->geom_size[3 * g + k];
+        sc[k] = m->mat_texrepeat[2 * mat + k] * (m->mat_texuniform[mat] || sz <= 0 ? 1.0 : 1.0 / (2 * sz));
+      }
+      double tc[3];
+      tex_sample(m, t, q[0] * sc[0], q[1] * sc[1], tc);
+      for (int i = 0; i < 3; ++i) base[i] *= tc[i];
+    }
+  }
+  for (int i = 0; i < 3; ++i) out[i] = emis * base[i];
+  for (int l = -1; l < m->nlight; ++l) {
+    double L[3], amb[3], dif[3], spc[3], att = 1, spot = 1, dist = 1e300;
+    int shadow = 0;
+    if (l < 0) {
+      if (!m->vis_headlight[9]) continue;
+      for (int i = 0; i < 3; ++i) {
+        L[i] = E[i]; amb[i] = m->vis_headlight[i]; dif[i] = m->vis_headlight[3 + i]; spc[i] = m->vis_headlight[6 + i];
+      }
+    } else {
+      if (!m->light_active[l]) continue;
+      const double* dir = m->light_dir + 3 * l;
+      for (int i = 0; i < 3; ++i) {
+        amb[i] = m->light_ambient[3 * l + i]; dif[i] = m->light_diffuse[3 * l + i]; spc[i] = m->light_specular[3 * l + i];
+      }
+      shadow = m->light_castshadow[l];
+      if (m->light_directional[l]) {
+        for (int i = 0; i < 3; ++i) L[i] = -dir[i];
+      } else {
+        for (int i = 0; i < 3; ++i) L[i] = m->light_pos[3 * l + i] - P[i];
+        dist = normalize3(L);
+        const double* a = m->light_attenuation + 3 * l;
+        att = 1 / (a[0] + a[1] * dist + a[2] * dist * dist);
+        const double ca = -dot3(L, dir);
+        spot = ca < cos(m->light_cutoff[l] * M_PI / 180) ? 0 : pow(ca, m->light_exponent[l]);
+      }
+      normalize3(L);
+    }
+    const double nl = fmax(0, dot3(N, L));
+    double sh = 1;
+    if (shadow && nl > 0) {
+      double o[3];
+      for (int i = 0; i < 3; ++i) o[i] = P[i] + 1e-4 * N[i];
+      const double th = ray_scene(m, w, o, L, -1, 0x7, 0, NULL);
+      if (th >= 0 && th < dist) sh = 0;
+    }
+    double H[3] = {L[0] + E[0], L[1] + E[1], L[2] + E[2]};
+    normalize3(H);
+    const double sp = nl > 0 ? pow(fmax(0, dot3(N, H)), 128 * shin) : 0;
+    for (int i = 0; i < 3; ++i)
+      out[i] += att * spot * (amb[i] * base[i] + sh * (nl * dif[i] * base[i] + sp * spc[i] * spec_m));
+  }
+}
+
 void orc_render_rgbd(const mrs_model_view* m, orc_data* d, int cam, float* depth, unsigned char* rgb) {
   orc_ws* w = (orc_ws*)d->ws;
   kinematics(m, d);
@@ -3359,7 +3480,12 @@ void orc_render_rgbd(const mrs_model_view* m, orc_data* d, int cam, float* depth
       if (depth) depth[(size_t)row * W + col] = (float)(hit ? t : zfar);
       if (!rgb) continue;
       unsigned char* px = rgb + ((size_t)row * W + col) * 3;
-      if (!hit) { px[0] = px[1] = px[2] = 0; continue; }
+      double cl[3];
+      if (!hit) {
+        sky_color(m, vec, cl);
+        for (int ch = 0; ch < 3; ++ch) px[ch] = (unsigned char)(fmin(fmax(cl[ch], 0), 1) * 255.0 + 0.5);
+        continue;
+      }
       const double* gm = w->geom_xmat + 9 * g;
       double dv[3], q[3], lv[3], nl[3], nw[3];
       for (int i = 0; i < 3; ++i) dv[i] = cpos[i] + t * vec[i] - w->geom_xpos[3 * g + i];
@@ -3382,13 +3508,10 @@ void orc_render_rgbd(const mrs_model_view* m, orc_data* d, int cam, float* depth
         local_normal(m->geom_type[g], m->geom_size + 3 * g, q, nl);
       }
       mat_vec(nw, gm, nl);
-      double c = -dot3(nw, vec) / sqrt(fmax(dot3(nw, nw) * dot3(vec, vec), 1e-300));
-      double k = 0.3 + 0.7 * (c > 0 ? c : 0);
-      for (int ch = 0; ch < 3; ++ch) {
-        double v = m->geom_rgba[4 * g + ch] * k;
-        v = v < 0 ? 0 : (v > 1 ? 1 : v);
-        px[ch] = (unsigned char)(v * 255.0 + 0.5);
-      }
+      double P[3], E[3] = {cmat[2], cmat[5], cmat[8]};
+      for (int i = 0; i < 3; ++i) P[i] = cpos[i] + t * vec[i];
+      lit_color(m, w, g, P, nw, vec, q, E, cl);
+      for (int ch = 0; ch < 3; ++ch) px[ch] = (unsigned char)(fmin(fmax(cl[ch], 0), 1) * 255.0 + 0.5);
     }
 }
 

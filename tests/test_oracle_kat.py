@@ -97,37 +97,119 @@ def test_depth_plane_constant():
     np.testing.assert_allclose(img, z0, rtol=1e-6)  # eye-space z, not Euclidean range
 
 
-def test_rgb_plane_headlight_shading():
-    """colour KAT: a plane (rgba 0.8 0.5 0.2) seen straight down; pixel (x, y) in camera-frame slopes
-    gets rgba * (0.3 + 0.7 / sqrt(1 + x^2 + y^2)) (normal (0, 0, 1), ray (x, y, -1)); the depth is
+def _slopes(H, W, fovy=60):
+    f = 0.5 * H / np.tan(np.radians(fovy / 2))
+    x = (np.arange(W) + 0.5 - 0.5 * W) / f
+    y = (0.5 * H - np.arange(H) - 0.5) / f
+    return x[None, :] + 0 * y[:, None], y[:, None] + 0 * x[None, :]
+
+
+def _u8(c):
+    return np.floor(np.clip(c, 0, 1) * 255 + 0.5).astype(np.uint8)
+
+
+def test_rgb_plane_point_light():
+    """colour KAT (lit model, oracle.c lit_color): a plane (rgba 0.8 0.5 0.2, material specular 0.5
+    shininess 0.25) seen straight down from height z0, lit only by a point light at the camera
+    (headlight off, no attenuation, 90-degree cone, exponent 0).  Pixel slope (x, y): the light
+    direction has N.L = cos = 1/sqrt(1 + x^2 + y^2); the half vector with the view axis gives
+    N.H = sqrt((1 + cos) / 2), so colour = base (0.1 + 0.6 cos) + 0.3 * 0.5 (N.H)^32; the depth is
     unchanged by the colour pass"""
     z0 = 1.7
-    m = sim.Model.from_string(PLANE_CAM.format(z0=z0, tilt='rgba="0.8 0.5 0.2 1"'))
+    xml = PLANE_CAM.format(z0=z0, tilt='material="m" rgba="0.8 0.5 0.2 1"').replace(
+        "<worldbody>", '<asset><material name="m" specular="0.5" shininess="0.25"/></asset><worldbody>'
+        f'<light pos="0 0 {z0}" dir="0 0 -1" directional="false" cutoff="90" exponent="0" attenuation="1 0 0" '
+        'ambient="0.1 0.1 0.1" diffuse="0.6 0.6 0.6" specular="0.3 0.3 0.3" castshadow="false"/>').replace(
+        "<visual>", '<visual><headlight active="0"/>')
+    m = sim.Model.from_string(xml)
     d = binding.OracleData(m)
     d.forward()
     depth, rgb = d.render_rgbd(0)
     np.testing.assert_array_equal(depth, d.render_depth(0))
-    H, W = depth.shape
-    f = 0.5 * H / np.tan(np.radians(30))
-    x = (np.arange(W) + 0.5 - 0.5 * W) / f
-    y = (0.5 * H - np.arange(H) - 0.5) / f
-    cos = 1 / np.sqrt(1 + x[None, :] ** 2 + y[:, None] ** 2)
-    want = np.clip(np.array([0.8, 0.5, 0.2])[None, None, :] * (0.3 + 0.7 * cos)[..., None], 0, 1) * 255 + 0.5
-    np.testing.assert_array_equal(rgb, np.floor(want).astype(np.uint8))
+    x, y = _slopes(*depth.shape)
+    cos = 1 / np.sqrt(1 + x ** 2 + y ** 2)
+    spec = 0.15 * np.sqrt((1 + cos) / 2) ** 32
+    want = np.array([0.8, 0.5, 0.2]) * (0.1 + 0.6 * cos)[..., None] + spec[..., None]
+    assert np.abs(rgb.astype(int) - _u8(want).astype(int)).max() <= 1
+    assert (rgb == _u8(want)).mean() > 0.99
 
 
-def test_rgb_sphere_centre_and_background():
-    """a sphere in front of the camera: the centre pixel faces the ray (full rgba), rays that miss are
-    black"""
-    m = sim.Model.from_string("""<mujoco><worldbody>
+def test_rgb_sphere_centre_and_sky():
+    """a sphere in front of the camera under the default headlight (ambient 0.1, diffuse 0.4,
+    specular 0.5; default material specular 0.5): the centre pixel faces the ray, N.L = N.H = 1, so
+    colour = 0.5 rgba + 0.25; rays that miss are black without a skybox, and show the gradient skybox
+    rgb2 + (rgb1 - rgb2) (1 + d_z) / 2 of the world ray direction with one"""
+    xml = """<mujoco>{asset}<worldbody>
       <geom type="sphere" size="0.2" pos="0 0 -1" rgba="0.2 0.4 1 1"/>
-      <camera name="c" pos="0 0 0" fovy="60" resolution="65 49"/></worldbody></mujoco>""")
-    d = binding.OracleData(m)
+      <camera name="c" pos="0 0 0" fovy="60" resolution="65 49"/></worldbody></mujoco>"""
+    d = binding.OracleData(sim.Model.from_string(xml.format(asset="")))
     d.forward()
     depth, rgb = d.render_rgbd(0)
-    np.testing.assert_array_equal(rgb[24, 32], [51, 102, 255])
+    np.testing.assert_array_equal(rgb[24, 32], _u8(0.5 * np.array([0.2, 0.4, 1]) + 0.25))
     assert depth[24, 32] == pytest.approx(0.8, rel=1e-6)
     np.testing.assert_array_equal(rgb[0, 0], [0, 0, 0])
+    sky = '<asset><texture type="skybox" builtin="gradient" rgb1="0.4 0.6 0.8" rgb2="0 0.2 0" width="8" height="8"/></asset>'
+    d = binding.OracleData(sim.Model.from_string(xml.format(asset=sky)))
+    d.forward()
+    depth, rgb = d.render_rgbd(0)
+    x, y = _slopes(*depth.shape)
+    dz = -1 / np.sqrt(1 + x ** 2 + y ** 2)
+    c1, c2 = np.array([0.4, 0.6, 0.8]), np.array([0, 0.2, 0])
+    want = _u8(c2 + (c1 - c2) * (0.5 * (1 + dz))[..., None])
+    miss = depth >= depth.max()
+    assert miss.mean() > 0.9
+    assert np.abs(rgb[miss].astype(int) - want[miss].astype(int)).max() <= 1
+
+
+def test_rgb_directional_shadow():
+    """shadow KAT: plane z = 0 seen from (0, 0, 3), a sphere (r 0.2, centre (0, 0, 0.5)) and a
+    directional castshadow light along (1, 0, -1)/sqrt(2) (headlight off): a plane point P is in shadow
+    iff its ray towards the light, -(1, 0, -1)/sqrt(2), passes within 0.2 of the centre; there the
+    colour is the ambient base * 0.2, elsewhere base * (0.2 + 0.5 / sqrt(2)) (N.L = 1/sqrt(2), no
+    specular).  Pixels within 2 mm of the shadow edge and pixels that see the sphere are skipped."""
+    xml = """<mujoco><visual><headlight active="0"/></visual><worldbody>
+      <light directional="true" dir="1 0 -1" castshadow="true" ambient="0.2 0.2 0.2" diffuse="0.5 0.5 0.5" specular="0 0 0"/>
+      <geom type="plane" size="0 0 1" rgba="1 0.5 0.25 1"/>
+      <geom type="sphere" size="0.2" pos="0 0 0.5" rgba="0 1 0 1"/>
+      <camera name="c" pos="0 0 3" fovy="60" resolution="96 72"/></worldbody></mujoco>"""
+    d = binding.OracleData(sim.Model.from_string(xml))
+    d.forward()
+    depth, rgb = d.render_rgbd(0)
+    x, y = _slopes(*depth.shape)
+    on_plane = np.abs(depth - 3) < 1e-6
+    P = np.stack([3 * x, 3 * y, np.zeros_like(x)], -1)
+    L = np.array([-1, 0, 1]) / np.sqrt(2)
+    v = np.array([0, 0, 0.5]) - P
+    s = v @ L
+    dist = np.sqrt(np.maximum((v ** 2).sum(-1) - s ** 2, 0))
+    shadow = (dist < 0.2) & (s > 0)
+    clear = on_plane & (np.abs(dist - 0.2) > 2e-3)
+    base = np.array([1, 0.5, 0.25])
+    want = np.where(shadow[..., None], base * 0.2, base * (0.2 + 0.5 / np.sqrt(2)))
+    assert shadow[clear].sum() > 50 and (~shadow[clear]).sum() > 1000
+    assert np.abs(rgb[clear].astype(int) - _u8(want)[clear].astype(int)).max() <= 1
+
+
+def test_rgb_checker_texture():
+    """builtin checker texture on a plane (texuniform, texrepeat 1 1, 2 x 2 blocks of rgb1 / rgb2 per
+    unit length): plane point (u, v) shows rgb1 when frac(u) < 0.5 and frac(v) < 0.5 or both >= 0.5,
+    else rgb2; material specular 0 under the default headlight: colour = 0.5 * texel"""
+    xml = """<mujoco><asset>
+      <texture name="t" type="2d" builtin="checker" rgb1="0.9 0.9 0.9" rgb2="0.2 0.3 0.4" width="64" height="64"/>
+      <material name="m" texture="t" texrepeat="1 1" texuniform="true" specular="0"/></asset><worldbody>
+      <geom type="plane" size="0 0 1" material="m"/>
+      <camera name="c" pos="0.1 0.2 2" fovy="60" resolution="80 60"/></worldbody></mujoco>"""
+    d = binding.OracleData(sim.Model.from_string(xml))
+    d.forward()
+    depth, rgb = d.render_rgbd(0)
+    x, y = _slopes(*depth.shape)
+    u, v = 0.1 + 2 * x, 0.2 + 2 * y
+    fu, fv = u - np.floor(u), v - np.floor(v)
+    first = (fu < 0.5) == (fv < 0.5)
+    clear = (np.abs(fu - 0.5) > 0.02) & (np.abs(fv - 0.5) > 0.02) & (fu > 0.02) & (fu < 0.98) & (fv > 0.02) & (fv < 0.98)
+    want = _u8(0.5 * np.where(first[..., None], [0.9, 0.9, 0.9], [0.2, 0.3, 0.4]))
+    assert first[clear].sum() > 100 and (~first[clear]).sum() > 100
+    np.testing.assert_array_equal(rgb[clear], want[clear])
 
 
 def test_depth_tilted_plane_rows():

@@ -365,11 +365,15 @@ def test_camera_topics(pkg_dir):
     assert np.all(np.isfinite(depth)) and np.all(depth > 0)
     img = s.last_image("/camera/color/image_raw")
     assert img["encoding"] == "rgb8" and img["step"] == 1280 * 3 and img["bytes"] == 1280 * 720 * 3
-    # colour from the same ray pass: lit where the depth hits a geom, black where it reads zfar
+    # colour from the same ray pass: lit where the depth hits a geom (ambient light keeps every hit
+    # above black); where it reads zfar the scene's gradient skybox, s * (0.3, 0.5, 0.7) with s in
+    # [0, 1], so blue >= green >= red there
     rgb = s.last_image_data("/camera/color/image_raw")
     assert rgb.shape == (720, 1280, 3) and rgb.max() > 0
     zfar = depth.max()
-    assert np.all(rgb[depth < zfar].max(axis=-1) > 0) and np.all(rgb[depth >= zfar] == 0)
+    assert np.all(rgb[depth < zfar].max(axis=-1) > 0)
+    sky = rgb[depth >= zfar].astype(int)
+    assert np.all(sky[:, 2] >= sky[:, 1]) and np.all(sky[:, 1] >= sky[:, 0])
 
 
 @pytest.mark.gpu
