@@ -37,12 +37,12 @@ enum { MRS_TEX_2D = 0, MRS_TEX_CUBE = 1, MRS_TEX_SKYBOX = 2 };  /* mjtTexture */
 enum { MRS_BUILTIN_NONE = 0, MRS_BUILTIN_GRADIENT = 1, MRS_BUILTIN_CHECKER = 2, MRS_BUILTIN_FLAT = 3 };
 enum { MRS_MARK_NONE = 0, MRS_MARK_EDGE = 1, MRS_MARK_CROSS = 2 };
 #define MRS_NEQDATA 11
-enum { MRS_TRN_JOINT = 0 };
+enum { MRS_TRN_JOINT = 0, MRS_TRN_TENDON = 3 };
 enum { MRS_DYN_NONE = 0 };
 enum { MRS_GAIN_FIXED = 0, MRS_GAIN_AFFINE = 1 };
 enum { MRS_BIAS_NONE = 0, MRS_BIAS_AFFINE = 1 };
 enum { MRS_OBJ_UNKNOWN = 0, MRS_OBJ_BODY = 1, MRS_OBJ_JOINT = 3, MRS_OBJ_GEOM = 5, MRS_OBJ_SITE = 6,
-       MRS_OBJ_CAMERA = 7, MRS_OBJ_MESH = 10, MRS_OBJ_ACTUATOR = 19, MRS_OBJ_SENSOR = 20 };
+       MRS_OBJ_CAMERA = 7, MRS_OBJ_MESH = 10, MRS_OBJ_TENDON = 18, MRS_OBJ_ACTUATOR = 19, MRS_OBJ_SENSOR = 20 };
 enum { MRS_SENS_ACCELEROMETER = 1, MRS_SENS_GYRO = 3, MRS_SENS_FORCE = 4, MRS_SENS_TORQUE = 5,
        MRS_SENS_RANGEFINDER = 7, MRS_SENS_JOINTPOS = 9, MRS_SENS_JOINTVEL = 10,
        MRS_SENS_ACTUATORFRC = 15, MRS_SENS_FRAMEPOS = 25, MRS_SENS_FRAMEQUAT = 26 };
@@ -52,7 +52,8 @@ enum { MRS_SENS_ACCELEROMETER = 1, MRS_SENS_GYRO = 3, MRS_SENS_FORCE = 4, MRS_SE
  * iterating until its improvement / gradient tests stop it).  PGS_ELLIPTIC_BLOCK: PGS solves each
  * elliptic contact block exactly over its cone (mj_solPGS takes a normal / ray step, then the friction
  * by mju_QCQP2 with the normal fixed). */
-enum { MRS_RESTATE_NEWTON_REFINE = 1 << 0, MRS_RESTATE_PGS_ELLIPTIC_BLOCK = 1 << 1 };
+enum { MRS_RESTATE_NEWTON_REFINE = 1 << 0, MRS_RESTATE_PGS_ELLIPTIC_BLOCK = 1 << 1,
+       MRS_RESTATE_NO_MPR_POLISH = 1 << 2 /* diagnostics: keep MPR's own contact (no normal polish) */ };
 /* disable flags (mjtDisableBit subset) */
 enum { MRS_DSBL_CONSTRAINT = 1 << 0, MRS_DSBL_EQUALITY = 1 << 1, MRS_DSBL_FRICTIONLOSS = 1 << 2,
        MRS_DSBL_LIMIT = 1 << 3, MRS_DSBL_CONTACT = 1 << 4, MRS_DSBL_PASSIVE = 1 << 5,
@@ -172,6 +173,18 @@ typedef struct mrs_model_view {
       *light_specular /*3*/, *light_attenuation /*3*/, *light_cutoff, *light_exponent, *tex_rgb1 /*3*/,
       *tex_rgb2 /*3*/, *tex_markrgb /*3*/, *mat_rgba /*4*/, *mat_texrepeat /*2*/, *mat_specular,
       *mat_shininess, *mat_emission;
+
+  /* fixed tendons (mjModel ntendon / tendon_* / wrap_*, mjTRN_TENDON actuators): tendon t is the linear
+   * combination length = sum_k wrap_prm[k] qpos[jnt_qposadr[wrap_objid[k]]] over its wraps
+   * k in [tendon_adr[t], tendon_adr[t] + tendon_num[t]) of hinge / slide joints; ten_J is constant.
+   * Spring force -stiffness (length - lengthspring) outside the dead band [lengthspring[0],
+   * lengthspring[1]], damping -damping * velocity, limit rows on [range[0], range[1]] within margin,
+   * a friction-loss row when frictionloss > 0; diagApprox tendon_invweight0 = J M(qpos0)^-1 J'. */
+  int ntendon, nwrap;
+  const int *tendon_adr, *tendon_num, *tendon_limited, *wrap_objid;
+  const double *wrap_prm, *tendon_range /*2*/, *tendon_margin, *tendon_solref_lim /*2*/,
+      *tendon_solimp_lim /*5*/, *tendon_frictionloss, *tendon_solref_fri /*2*/, *tendon_solimp_fri /*5*/,
+      *tendon_stiffness, *tendon_damping, *tendon_lengthspring /*2*/, *tendon_invweight0, *tendon_length0;
 } mrs_model_view;
 
 #ifdef __cplusplus

@@ -1178,6 +1178,33 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       d.neq_rows += m.eq_type[q] == MRS_EQ_CONNECT ? 3 : (m.eq_type[q] == MRS_EQ_WELD ? 6 : 1);
     }
   d.neq = static_cast<int>(eq_t.size());
+  // fixed tendons: wraps (qpos / dof address, coefficient), the constant Jacobian rows (dense
+  // ntendon x nv), per tendon 12 constants (stiffness, damping, lengthspring[2], range[2], margin,
+  // frictionloss, invweight0), and the tendons that give friction-loss / limit rows
+  const int ntendon = static_cast<int>(m.tendon_adr.size());
+  std::vector<int> ten_adr(m.tendon_adr), ten_num(m.tendon_num), wrap_qadr, wrap_dof, ten_fric, ten_lim;
+  std::vector<double> wrap_coef(m.wrap_prm), tenJ(static_cast<size_t>(ntendon) * m.nv, 0.0), tenprm;
+  for (size_t k = 0; k < m.wrap_objid.size(); ++k) {
+    wrap_qadr.push_back(m.jnt_qposadr[m.wrap_objid[k]]);
+    wrap_dof.push_back(m.jnt_dofadr[m.wrap_objid[k]]);
+  }
+  for (int t = 0; t < ntendon; ++t) {
+    for (int k = m.tendon_adr[t]; k < m.tendon_adr[t] + m.tendon_num[t]; ++k)
+      tenJ[static_cast<size_t>(t) * m.nv + wrap_dof[k]] += m.wrap_prm[k];
+    const double pr[12] = {m.tendon_stiffness[t], m.tendon_damping[t], m.tendon_lengthspring[2 * t],
+                           m.tendon_lengthspring[2 * t + 1], m.tendon_range[2 * t], m.tendon_range[2 * t + 1],
+                           m.tendon_margin[t], m.tendon_frictionloss[t], m.tendon_invweight0[t], 0, 0, 0};
+    tenprm.insert(tenprm.end(), pr, pr + 12);
+    if (!(m.disableflags & (MRS_DSBL_FRICTIONLOSS | MRS_DSBL_CONSTRAINT)) && m.tendon_frictionloss[t] > 0)
+      ten_fric.push_back(t);
+    if (!(m.disableflags & (MRS_DSBL_LIMIT | MRS_DSBL_CONSTRAINT)) && m.tendon_limited[t]) ten_lim.push_back(t);
+  }
+  d.ntendon = ntendon;
+  d.nten_fric = static_cast<int>(ten_fric.size());
+  d.nten_lim = static_cast<int>(ten_lim.size());
+  // rows outside the blocked-mode sparse solver's kinds (equality, tendon friction / limits): the
+  // dense row path runs instead
+  d.xrows = d.neq + d.nten_fric + d.nten_lim;
   b.pair_g2 = pg2;
   // kinematic trees (bodies sharing a root child of the world) that own dofs: their dofs are one
   // contiguous range, M is block diagonal over them, and constraint rows touch at most two of them
@@ -1246,16 +1273,26 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   const int cap = max_con_req > 0 ? max_con_req : std::min(128, std::max(32, pair_max));
   d.max_con = d.npair == 0 ? 0 : std::min(pair_max, cap);
-  d.max_efc = d.neq_rows + d.nfric + 2 * d.nlim + 4 * d.max_con;
+  d.max_efc = d.neq_rows + d.nfric + d.nten_fric + 2 * (d.nlim + d.nten_lim) + 4 * d.max_con;
   // actuators
   std::vector<int> act_dof, act_qadr;
   std::vector<float> act_gear, act_gain, act_bias;
+  std::vector<int> act_ten;
   for (int a = 0; a < m.nu; ++a) {
     int j = m.actuator_trnid[2 * a];
-    if (m.jnt_type[j] != MRS_JNT_HINGE && m.jnt_type[j] != MRS_JNT_SLIDE)
-      throw UnsupportedError("actuators on free/ball joints are not supported");
-    act_dof.push_back(m.jnt_dofadr[j]);
-    act_qadr.push_back(m.jnt_qposadr[j]);
+    if (m.actuator_trntype[a] == MRS_TRN_TENDON) {
+      // a tendon transmission: the record's qpos / dof addresses hold -1 - tendon (length and
+      // velocity from the step's tendon slot in LDS), its moment is gear * ten_J
+      act_dof.push_back(-1 - j);
+      act_qadr.push_back(-1 - j);
+      act_ten.push_back(j);
+    } else {
+      if (m.jnt_type[j] != MRS_JNT_HINGE && m.jnt_type[j] != MRS_JNT_SLIDE)
+        throw UnsupportedError("actuators on free/ball joints are not supported");
+      act_dof.push_back(m.jnt_dofadr[j]);
+      act_qadr.push_back(m.jnt_qposadr[j]);
+      act_ten.push_back(-1);
+    }
     act_gear.push_back(static_cast<float>(m.actuator_gear[6 * a]));
     for (int i = 0; i < 3; ++i) {
       act_gain.push_back(static_cast<float>(m.actuator_gainprm[MRS_NGAIN * a + i]));
@@ -1379,6 +1416,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     P.addi(&d.geom_matid, mid);
   }
   P.addi(&d.pair_g1, pg1); P.addi(&d.pair_g2, pg2); P.addi(&d.pair_dim, pdim);
+  P.addi(&d.ten_adr, ten_adr); P.addi(&d.ten_num, ten_num); P.addi(&d.wrap_qadr, wrap_qadr);
+  P.addi(&d.wrap_dof, wrap_dof); P.addf(&d.wrap_coef, wrap_coef); P.addf(&d.ten_J, tenJ);
+  P.addf(&d.ten_prm, tenprm); P.addi(&d.ten_fric, ten_fric); P.addi(&d.ten_lim, ten_lim);
+  P.addf(&d.ten_solref_lim, m.tendon_solref_lim); P.addf(&d.ten_solimp_lim, m.tendon_solimp_lim);
+  P.addf(&d.ten_solref_fri, m.tendon_solref_fri); P.addf(&d.ten_solimp_fri, m.tendon_solimp_fri);
+  P.addi(&d.act_ten, act_ten);
   P.addi(&d.eq_type, eq_t); P.addi(&d.eq_obj1id, eq_o1); P.addi(&d.eq_obj2id, eq_o2);
   P.addf(&d.eq_solref, eq_sr); P.addf(&d.eq_solimp, eq_si); P.addf(&d.eq_data, eq_dat);
   P.addf(&d.pair_margin, pmargin); P.addf(&d.pair_gap, pgap); P.addf(&d.pair_friction, pfric);
@@ -1448,8 +1491,10 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     for (int j = 0; j < m.nv; ++j) {
       int act = -1;
       float gear = 0;
-      for (int a = 0; a < m.nu; ++a)
+      for (int a = 0; a < m.nu; ++a) {
         if (act_dof[a] == j) { act = act == -1 ? a : -2; gear = act_gear[a]; }
+        if (act_ten[a] >= 0 && tenJ[static_cast<size_t>(act_ten[a]) * m.nv + j] != 0) act = -2;  // the loop
+      }
       const int jid = m.dof_jntid[j], b = m.dof_bodyid[j];
       int gc = 0;
       for (int x = b; x < subtree_end[b]; ++x) gc |= m.body_gravcomp[x] != 0;
@@ -1727,6 +1772,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.qfrc_passive = take(nv); L.qfrc_act = take(nv); L.qfrc_smooth = take(nv); L.qacc_smooth = take(nv);
     L.qacc = take(nv + 1); L.qfrc_con = take(nv + 1);  // + a dummy word (blocked-mode solver)
     L.act_force = take(std::max(1, m.nu));
+    L.ten = d.ntendon > 0 ? take(2 * d.ntendon) : 0;  // tendon lengths and velocities of the step
     L.niter = take(1);
     L.rfmask = take(std::max(1, d.nrfblk));
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
@@ -1835,7 +1881,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   off = 0;
   const int ne = std::max(1, d.max_efc);
   // dense rows: dense mode, and blocked mode with a primal solver (the sparse records are PGS's)
-  const int dn = d.blocked && m.solver == MRS_SOL_PGS && m.cone != MRS_CONE_ELLIPTIC && d.neq == 0 ? 0 : ne;
+  const int dn = d.blocked && m.solver == MRS_SOL_PGS && m.cone != MRS_CONE_ELLIPTIC && d.xrows == 0 ? 0 : ne;
   S.efc_J = take(dn * nv); S.efc_MJ = take(dn * nv); S.efc_type = take(ne); S.efc_pos = take(ne);
   S.efc_margin = take(ne); S.efc_floss = take(ne); S.efc_R = take(dn); S.efc_aref = take(dn);
   S.efc_b = take(dn); S.efc_f = take(ne); S.efc_ARii = take(dn); S.con = take(kConRec * std::max(1, d.max_con));
@@ -2237,7 +2283,7 @@ void batch_render_wait(BatchImpl* b) {
 int batch_get_efc(BatchImpl* b, int env, int max, int* type, double* J, double* R, double* aref, double* force) {
   if (env < 0 || env >= b->n) throw std::invalid_argument("env out of bounds");
   if (max < 0) throw std::invalid_argument("negative capacity");
-  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS && b->model->cone != MRS_CONE_ELLIPTIC && b->dm.neq == 0)
+  if (b->dm.blocked && b->model->solver == MRS_SOL_PGS && b->model->cone != MRS_CONE_ELLIPTIC && b->dm.xrows == 0)
     throw UnsupportedError("blocked-mode PGS keeps its constraint rows in sparse records");
   HIP_CHECK(hipSetDevice(b->device));
   const ScratchLayout& S = b->S;

@@ -44,6 +44,7 @@ struct LdsLayout {
       dofb,    // blocked mode: per dof its body and that body's subtree end (int bits; jac_col)
       H,       // blocked mode with a primal solver (Newton/CG): dense nv x nv Hessian and its factor
       Li,      // blocked mode with PGS: L^-1 per tree block (same offsets as L): the records' Y = L^-1 J'
+      ten,     // fixed tendons: length and velocity per tendon of the step (smooth_forces)
       rk,      // RK4 models: the step's initial qpos [nq], then qvel [nv], stage velocity, B-weighted sums of
                // the stage velocities and accelerations [nv each]
       niter;   // constraint solver iterations of the last forward (int bits)
@@ -154,6 +155,13 @@ struct DevModel {
   // active equality constraints (mrs_model_view eq_*, inactive ones dropped on the host): neq of
   // them giving neq_rows rows (connect 3, weld 6, joint 1), first in the row order
   int neq, neq_rows;
+  // fixed tendons (batch.hip): wraps, dense Jacobian rows ten_J [ntendon][nv], 12 constants per tendon
+  // (stiffness, damping, lengthspring[2], range[2], margin, frictionloss, invweight0), the tendons
+  // with friction-loss rows / limits, each actuator's tendon (-1: joint transmission); xrows: row
+  // sources the blocked-mode sparse solver does not take (neq + nten_fric + nten_lim)
+  int ntendon, nten_fric, nten_lim, xrows;
+  CPtr<int> ten_adr, ten_num, wrap_qadr, wrap_dof, ten_fric, ten_lim, act_ten;
+  CPtr<float> wrap_coef, ten_J, ten_prm, ten_solref_lim, ten_solimp_lim, ten_solref_fri, ten_solimp_fri;
   CPtr<int> eq_type, eq_obj1id, eq_obj2id;
   CPtr<float> eq_solref /*2*/, eq_solimp /*5*/, eq_data /*11*/;
   CPtr<int> pair_g1, pair_g2, pair_dim;

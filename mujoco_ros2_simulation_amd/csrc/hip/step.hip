@@ -1338,7 +1338,7 @@ __device__ __forceinline__ int convex_convex(const DevModel& m, int g1, int g2, 
   float depth, nrm[3], pos[3];
   if (!mpr_penetration(MeshTab{m.mesh_vert, m.mesh_hull}, A, B, depth, nrm, pos)) return 0;
 #if MRS_EXT
-  {
+  if (!(m.restate & MRS_RESTATE_NO_MPR_POLISH)) {
     const float n0[3] = {nrm[0], nrm[1], nrm[2]};
     [[clang::noinline]] mpr_polish(MeshTab{m.mesh_vert, m.mesh_hull}, A, B, n0, depth, depth, nrm, pos);
   }
@@ -1500,11 +1500,11 @@ __device__ __forceinline__ float impedance(const PS si, float pos, float margin)
   return dmin + y * (dmax - dmin);
 }
 
-enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3, EFC_EQUALITY = 4 };
+enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3, EFC_EQUALITY = 4, EFC_TFRICTION = 5, EFC_TLIMIT = 6 };
 // equality rows are unbounded: the solvers treat them as friction-loss rows with this bound (oracle.c
 // EQ_BOUND), quadratic in every primal state and unclamped in PGS
 constexpr float kEqBound = 1e15f;
-__device__ __forceinline__ bool fric_like(int t) { return t == EFC_FRICTION || t == EFC_EQUALITY; }
+__device__ __forceinline__ bool fric_like(int t) { return t == EFC_FRICTION || t == EFC_EQUALITY || t == EFC_TFRICTION; }
 
 // Per-phase cycle accounting, built only with -DMRS_PHASE_TIMING (profiling variant): s_memtime
 // around each phase, summed per wave and added to a device table at the end of the kernel.
@@ -2319,6 +2319,21 @@ template <int G>
 __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
   ENV_UNPACK;
   const int nv = m.nv;
+  // fixed tendons (mj_tendon): length and velocity of each into the step's tendon slot (lane per tendon)
+  if (m.ntendon > 0) {
+    #pragma unroll 1
+    for (int t = lane; t < m.ntendon; t += G) {
+      float len = 0, vel = 0;
+      #pragma unroll 1
+      for (int k = m.ten_adr[t]; k < m.ten_adr[t] + m.ten_num[t]; ++k) {
+        len += m.wrap_coef[k] * s[L.qpos + m.wrap_qadr[k]];
+        vel += m.wrap_coef[k] * s[L.qvel + m.wrap_dof[k]];
+      }
+      s[L.ten + 2 * t] = len;
+      s[L.ten + 2 * t + 1] = vel;
+    }
+    wsync();
+  }
   // actuator forces (lane per actuator)
   #pragma unroll 1
   for (int a = lane; a < m.nu; a += G) {
@@ -2326,7 +2341,10 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
     if (!(m.disableflags & MRS_DSBL_ACTUATION)) {
       const auto ar = act_tab<G>(m, a);
       const float gear = ar[2];
-      const float len = gear * s[L.qpos + __float_as_int(ar[0])], vel = gear * s[L.qvel + __float_as_int(ar[1])];
+      // (a tendon transmission's addresses are -1 - tendon: its length and velocity from the slot)
+      const int qad = __float_as_int(ar[0]), dad = __float_as_int(ar[1]);
+      const float len = gear * (qad >= 0 ? s[L.qpos + qad] : s[L.ten + 2 * (-1 - qad)]);
+      const float vel = gear * (dad >= 0 ? s[L.qvel + dad] : s[L.ten + 2 * (-1 - dad) + 1]);
       float ctrl = s[L.ctrl + a];
       if (__float_as_int(ar[3]) && !(m.disableflags & MRS_DSBL_CLAMPCTRL)) ctrl = clampf(ctrl, ar[4], ar[5]);
       float gain = __float_as_int(ar[6]) == MRS_GAIN_AFFINE ? ar[7] + ar[8] * len + ar[9] * vel : ar[7];
@@ -2347,8 +2365,11 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
       qa = dr[1] * s[L.act_force + da];
     } else if (da == -2) {
       #pragma unroll 1
-      for (int a = 0; a < m.nu; ++a)
+      for (int a = 0; a < m.nu; ++a) {
         if (m.act_dof[a] == j) qa += m.act_gear[a] * s[L.act_force + a];
+        else if (m.ntendon > 0 && m.act_ten[a] >= 0)
+          qa += m.act_gear[a] * s[L.act_force + a] * m.ten_J[m.act_ten[a] * nv + j];  // moment gear * J
+      }
     }
     if (__float_as_int(dr[2])) qa = clampf(qa, dr[3], dr[4]);
     s[L.qfrc_act + j] = qa;
@@ -2360,6 +2381,17 @@ __device__ MRS_PHASE float smooth_forces(ENV_PARAMS) {
         pas -= dr[6] * (s[L.qpos + qadr] - dr[8]);
       }
       pas -= dr[9] * s[L.qvel + j];
+      // tendon springs (dead band [lengthspring0, lengthspring1]) and dampers through J'
+      #pragma unroll 1
+      for (int t = 0; t < m.ntendon; ++t) {
+        const float jt = m.ten_J[t * nv + j];
+        if (jt == 0) continue;
+        const CPtr<float> tp = m.ten_prm + 12 * t;
+        const float len = s[L.ten + 2 * t], k = tp[0];
+        float f = k == 0 ? 0.0f : (len > tp[3] ? k * (tp[3] - len) : (len < tp[2] ? k * (tp[2] - len) : 0.0f));
+        f -= tp[1] * s[L.ten + 2 * t + 1];
+        pas += jt * f;
+      }
       if (!(m.disableflags & MRS_DSBL_GRAVITY) && __float_as_int(dr[12])) {
         const int bj = __float_as_int(dr[10]), e = __float_as_int(dr[11]);
         #pragma unroll 1
@@ -5078,8 +5110,8 @@ template <int G, bool kPrimal = false>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   ENV_UNPACK;
   if constexpr (G == 64) {
-    if (m.solver != MRS_SOL_PGS || m.cone == MRS_CONE_ELLIPTIC || m.neq > 0) {
-      // Newton / CG in blocked mode, elliptic cones and equality constraints under every solver:
+    if (m.solver != MRS_SOL_PGS || m.cone == MRS_CONE_ELLIPTIC || m.xrows > 0) {
+      // Newton / CG in blocked mode, elliptic cones, equality and tendon rows under every solver:
       // dense rows (solve_primal, or the row-serial PGS with its 3-row contact blocks)
       float qa;
       [[clang::noinline]] qa = constraints_dense<G>(ENV_ARGS, ncon, qacc_s);
@@ -5122,7 +5154,7 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     // (kPrimal: the G = 16 kernel instantiated for models whose solver is Newton or CG, so the
     // primal form is inlined only there and the PGS kernels keep their code and registers)
     if ((kPrimal ? m.solver != MRS_SOL_PGS : m.solver == MRS_SOL_PGS) && ncon == 0 && nf > 0 && nf <= 16 &&
-        m.neq == 0 && !gany<G>(lim)) {
+        m.xrows == 0 && !gany<G>(lim)) {
       if (lane == 0) scr[S.efc_n] = __int_as_float(-1);  // rows stay in registers
       int mydof = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
@@ -5293,6 +5325,17 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
       }
     }
     nefc = r0 + m.nfric;
+    // tendon friction loss rows, J = ten_J (mj_instantiateFriction: after the dofs')
+    #pragma unroll 1
+    for (int k = 0; k < m.nten_fric; ++k) {
+      const int t = m.ten_fric[k], r = nefc + k;
+      if (lane < nv) J[r * nv + lane] = m.ten_J[t * nv + lane];
+      if (lane == 0) {
+        type[r] = __int_as_float(EFC_TFRICTION * 65536 + t);
+        pos[r] = 0; marg[r] = 0; floss[r] = m.ten_prm[12 * t + 7];
+      }
+    }
+    nefc += m.nten_fric;
   }
   // --- joint limit rows (lane per limited joint, compacted)
   if (!(m.disableflags & MRS_DSBL_LIMIT)) {
@@ -5340,6 +5383,24 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     if (lane == 0)
       #pragma unroll 1
       for (int r = lim0; r < nefc; ++r) floss[r] = 0;
+    // tendon limit rows, lower then upper, J = +-ten_J (mj_instantiateLimit: after the joints')
+    #pragma unroll 1
+    for (int k = 0; k < m.nten_lim; ++k) {
+      const int t = m.ten_lim[k];
+      const CPtr<float> tp = m.ten_prm + 12 * t;
+      const float len = s[L.ten + 2 * t], mg = tp[6];
+      const float dist[2] = {len - tp[4], tp[5] - len};
+      for (int sd = 0; sd < 2; ++sd) {
+        if (!(dist[sd] < mg)) continue;
+        if (lane < nv) J[nefc * nv + lane] = sd == 0 ? m.ten_J[t * nv + lane] : -m.ten_J[t * nv + lane];
+        if (lane == 0) {
+          type[nefc] = __int_as_float(EFC_TLIMIT * 65536 + t);
+          pos[nefc] = dist[sd]; marg[nefc] = mg; floss[nefc] = 0;
+        }
+        ++nefc;
+      }
+    }
+    if (m.nten_lim > 0) wsync();
   }
   // --- contact rows: lane per dof, loop over contacts
   if constexpr (G == 64) {
@@ -5478,6 +5539,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
     else if (t == EFC_EQUALITY) { sr = m.eq_solref + 2 * id; si = m.eq_solimp + 5 * id; diag = bb[r]; }
     else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
+    else if (t == EFC_TFRICTION) { sr = m.ten_solref_fri + 2 * id; si = m.ten_solimp_fri + 5 * id; diag = m.ten_prm[12 * id + 8]; }
+    else if (t == EFC_TLIMIT) { sr = m.ten_solref_lim + 2 * id; si = m.ten_solimp_lim + 5 * id; diag = m.ten_prm[12 * id + 8]; }
     else {
       const gfloat* rec = scr + S.con + kConRec * id;
       const int p = __float_as_int(rec[0]);
@@ -5515,7 +5578,8 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
     #pragma unroll 4
     for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
     // (friction-loss rows and the tangent rows of an elliptic block carry no position term)
-    const float pterm = (t == EFC_FRICTION || (t == EFC_CONTACT && floss[r] > 1.5f)) ? 0.0f : K * imp * (pos[r] - marg[r]);
+    const float pterm = (t == EFC_FRICTION || t == EFC_TFRICTION || (t == EFC_CONTACT && floss[r] > 1.5f))
+                            ? 0.0f : K * imp * (pos[r] - marg[r]);
     if (small) {
       my_R = R;
       my_aref = -B * vel - pterm;

@@ -1055,10 +1055,19 @@ struct Compiler {
       if (tag != "motor" && tag != "position" && tag != "velocity" && tag != "general")
         fail(e, "unsupported actuator type");
       const DefaultClass* cls = resolve_class(e, "");
-      std::string joint;
-      if (!get_str(e, cls, tag, "joint", joint)) fail(e, "only joint transmissions are supported");
-      int jid = m.name2id(MRS_OBJ_JOINT, joint);
-      if (jid < 0) fail(e, "unknown joint '" + joint + "'");
+      std::string joint, tendon;
+      int jid, trn = MRS_TRN_JOINT;
+      if (get_str(e, cls, tag, "joint", joint)) {
+        jid = m.name2id(MRS_OBJ_JOINT, joint);
+        if (jid < 0) fail(e, "unknown joint '" + joint + "'");
+      } else if (get_str(e, cls, tag, "tendon", tendon)) {
+        jid = m.name2id(MRS_OBJ_TENDON, tendon);
+        if (jid < 0) fail(e, "unknown tendon '" + tendon + "'");
+        trn = MRS_TRN_TENDON;
+      } else {
+        fail(e, "only joint and tendon transmissions are supported");
+        return;
+      }
       double gear[6] = {1, 0, 0, 0, 0, 0}, gain[MRS_NGAIN] = {0}, bias[MRS_NBIAS] = {0};
       get_reals(e, cls, tag, "gear", gear, 6);
       double ctrlrange[2] = {0, 0}, forcerange[2] = {0, 0};
@@ -1108,7 +1117,10 @@ struct Compiler {
         if (v && !(r[0] < r[1])) fail(e, "invalid range on a limited actuator");
         return v;
       };
-      m.actuator_trntype.push_back(MRS_TRN_JOINT);
+      if (trn == MRS_TRN_TENDON && m.integrator != MRS_INT_EULER && m.integrator != MRS_INT_RK4 &&
+          (biastype == MRS_BIAS_AFFINE || gaintype == MRS_GAIN_AFFINE))
+        fail(e, "velocity-dependent actuators on tendons are supported with the Euler and RK4 integrators only");
+      m.actuator_trntype.push_back(trn);
       m.actuator_dyntype.push_back(MRS_DYN_NONE);
       m.actuator_gaintype.push_back(gaintype);
       m.actuator_biastype.push_back(biastype);
@@ -1668,7 +1680,8 @@ struct Compiler {
     for (int i = 0; i < nv; ++i) { m.dof_M0[i] = M[i * nv + i]; trace += M[i * nv + i]; }
     m.stat_meaninertia = nv > 0 ? trace / nv : 1;
     // inverse of M (dense Cholesky) for invweight0
-    std::vector<double> Minv(nv * nv, 0);
+    std::vector<double>& Minv = Minv0;
+    Minv.assign(nv * nv, 0);
     if (nv > 0) dense_inverse_spd(M, Minv, nv);
     m.dof_invweight0.assign(nv, 0);
     for (int j = 0; j < m.njnt; ++j) {
@@ -1843,6 +1856,8 @@ struct Compiler {
     set0();
     flatten_lights();
     // pass 3: elements that reference the tree
+    for (auto& c : root->children)
+      if (c->tag == "tendon") parse_tendons(c.get());
     for (auto& c : root->children) {
       if (c->tag == "actuator") parse_actuators(c.get());
     }
@@ -1851,14 +1866,100 @@ struct Compiler {
       if (c->tag == "sensor") parse_sensors(c.get());
       else if (c->tag == "keyframe") parse_keyframes(c.get());
       else if (c->tag == "equality") parse_equality(c.get());
-      else if (c->tag == "tendon")
-        { if (!c->children.empty()) fail(c.get(), "tendons are not supported"); }
       else if (c->tag == "contact") parse_contact(c.get());
     }
     candidate_pairs();
     return std::move(m);
   }
   std::vector<double> x0pos, x0quat;  // body poses at qpos0 (set0)
+  std::vector<double> Minv0;          // M(qpos0)^-1, dense (set0)
+  // <tendon><fixed> [upstream mjCTendon, fixed only]: wraps of hinge / slide joints with coefficients;
+  // limited (autolimits: a range given), range, margin, solreflimit / solimplimit, frictionloss,
+  // solreffriction / solimpfriction, stiffness, damping, springlength (one value, two for a dead band;
+  // -1: the length at qpos_spring), tendon_invweight0 = J M(qpos0)^-1 J' [upstream mj_setConst]
+  void parse_tendons(const XmlElement* sec) {
+    const int nv = m.nv;
+    for (auto& cp : sec->children) {
+      const XmlElement* e = cp.get();
+      const std::string& tag = e->tag;
+      if (tag == "spatial") fail(e, "spatial tendons are not supported");
+      if (tag != "fixed") fail(e, "unsupported tendon type '" + tag + "'");
+      const DefaultClass* cls = resolve_class(e, "");
+      double range[2] = {0, 0}, margin = 0, srl[2] = {0.02, 1}, sil[5] = {0.9, 0.95, 0.001, 0.5, 2};
+      double fl = 0, srf[2] = {0.02, 1}, sif[5] = {0.9, 0.95, 0.001, 0.5, 2}, k = 0, b = 0, ls[2] = {-1, -1};
+      const bool has_range = get_reals(e, cls, "tendon", "range", range, 2, true);
+      get_real(e, cls, "tendon", "margin", margin);
+      get_reals(e, cls, "tendon", "solreflimit", srl, 2, true);
+      get_reals(e, cls, "tendon", "solimplimit", sil, 5);
+      get_real(e, cls, "tendon", "frictionloss", fl);
+      get_reals(e, cls, "tendon", "solreffriction", srf, 2, true);
+      get_reals(e, cls, "tendon", "solimpfriction", sif, 5);
+      get_real(e, cls, "tendon", "stiffness", k);
+      get_real(e, cls, "tendon", "damping", b);
+      double arm = 0;
+      if (get_real(e, cls, "tendon", "armature", arm) && arm != 0) fail(e, "tendon armature is not supported");
+      int nls = 0;
+      {
+        std::string sl;
+        if (get_str(e, cls, "tendon", "springlength", sl)) {
+          const auto v = parse_reals(sl, e, "springlength");
+          if (v.empty() || v.size() > 2) fail(e, "springlength takes one or two numbers");
+          nls = static_cast<int>(v.size());
+          for (int i = 0; i < nls; ++i) ls[i] = v[i];
+          if (nls == 2 && ls[1] == -1 && ls[0] != -1) nls = 1;
+        }
+      }
+      int lim = get_tristate(e, cls, "tendon", "limited");
+      lim = lim == 2 ? (opt.autolimits && has_range ? 1 : 0) : lim;
+      if (lim && !(range[0] < range[1])) fail(e, "invalid range on a limited tendon");
+      if (b != 0 && m.integrator != MRS_INT_EULER && m.integrator != MRS_INT_RK4)
+        fail(e, "tendon damping is supported with the Euler and RK4 integrators only");
+      const int adr = static_cast<int>(m.wrap_objid.size());
+      double len_spring = 0, len0 = 0;
+      std::vector<double> J(nv, 0.0);
+      for (auto& wp : e->children) {
+        const XmlElement* w = wp.get();
+        if (w->tag != "joint") fail(w, "fixed tendons wrap joints only");
+        std::string jn;
+        if (!get_str(w, nullptr, "joint", "joint", jn)) fail(w, "tendon joint requires 'joint'");
+        const int j = m.name2id(MRS_OBJ_JOINT, jn);
+        if (j < 0) fail(w, "unknown joint '" + jn + "'");
+        if (m.jnt_type[j] != MRS_JNT_HINGE && m.jnt_type[j] != MRS_JNT_SLIDE)
+          fail(w, "fixed tendons need hinge or slide joints");
+        double coef = 0;
+        if (!get_real(w, nullptr, "joint", "coef", coef)) fail(w, "tendon joint requires 'coef'");
+        m.wrap_objid.push_back(j);
+        m.wrap_prm.push_back(coef);
+        len_spring += coef * m.qpos_spring[m.jnt_qposadr[j]];
+        len0 += coef * m.qpos0[m.jnt_qposadr[j]];
+        J[m.jnt_dofadr[j]] += coef;
+      }
+      const int num = static_cast<int>(m.wrap_objid.size()) - adr;
+      if (num == 0) fail(e, "a fixed tendon needs at least one joint");
+      if (nls == 0 || ls[0] == -1) ls[0] = ls[1] = len_spring;
+      else if (nls == 1) ls[1] = ls[0];
+      if (ls[0] > ls[1]) fail(e, "springlength dead band must be non-decreasing");
+      double iw = 0;
+      for (int i = 0; i < nv; ++i)
+        for (int jj = 0; jj < nv; ++jj) iw += J[i] * Minv0[i * nv + jj] * J[jj];
+      m.tendon_adr.push_back(adr);
+      m.tendon_num.push_back(num);
+      m.tendon_limited.push_back(lim);
+      m.tendon_range.insert(m.tendon_range.end(), range, range + 2);
+      m.tendon_margin.push_back(margin);
+      m.tendon_solref_lim.insert(m.tendon_solref_lim.end(), srl, srl + 2);
+      m.tendon_solimp_lim.insert(m.tendon_solimp_lim.end(), sil, sil + 5);
+      m.tendon_frictionloss.push_back(fl);
+      m.tendon_solref_fri.insert(m.tendon_solref_fri.end(), srf, srf + 2);
+      m.tendon_solimp_fri.insert(m.tendon_solimp_fri.end(), sif, sif + 5);
+      m.tendon_stiffness.push_back(k);
+      m.tendon_damping.push_back(b);
+      m.tendon_lengthspring.insert(m.tendon_lengthspring.end(), ls, ls + 2);
+      m.tendon_invweight0.push_back(iw);
+      m.tendon_length0.push_back(len0);
+      m.names[MRS_OBJ_TENDON].push_back(elem_name(e, ""));
+    }
+  }
   // <equality> [upstream mjCEquality]: connect, weld and joint constraints with solref / solimp /
   // active (defaults 0.02 1 / 0.9 0.95 0.001 0.5 2 / true); what MuJoCo's compiler completes at qpos0
   // is completed here: connect's anchor in body2's frame, weld's relpose when not given (its quaternion
@@ -2068,10 +2169,18 @@ struct Compiler {
       if (gain[0] != -bias[1] || bias[2] <= 0) continue;
       int j = m.actuator_trnid[2 * a];
       double gear = m.actuator_gear[6 * a];
-      int d = m.jnt_dofadr[j];
       double mass = 0;
-      if ((m.jnt_type[j] == MRS_JNT_HINGE || m.jnt_type[j] == MRS_JNT_SLIDE) && gear != 0)
-        mass = m.dof_M0[d] / (gear * gear);
+      if (m.actuator_trntype[a] == MRS_TRN_TENDON) {
+        // moment gear * coef on each wrapped dof
+        for (int k = m.tendon_adr[j]; k < m.tendon_adr[j] + m.tendon_num[j]; ++k) {
+          const double mo = gear * m.wrap_prm[k];
+          if (mo != 0) mass += m.dof_M0[m.jnt_dofadr[m.wrap_objid[k]]] / (mo * mo);
+        }
+      } else {
+        int d = m.jnt_dofadr[j];
+        if ((m.jnt_type[j] == MRS_JNT_HINGE || m.jnt_type[j] == MRS_JNT_SLIDE) && gear != 0)
+          mass = m.dof_M0[d] / (gear * gear);
+      }
       bias[2] = -bias[2] * 2 * std::sqrt(gain[0] * mass);
     }
   }
@@ -2156,6 +2265,12 @@ mrs_model_view Model::view() const {
   v.neq = static_cast<int>(eq_type.size());
   MRS_V(eq_type); MRS_V(eq_obj1id); MRS_V(eq_obj2id); MRS_V(eq_active0); MRS_V(eq_solref); MRS_V(eq_solimp);
   MRS_V(eq_data);
+  v.ntendon = static_cast<int>(tendon_adr.size());
+  v.nwrap = static_cast<int>(wrap_objid.size());
+  MRS_V(tendon_adr); MRS_V(tendon_num); MRS_V(tendon_limited); MRS_V(wrap_objid); MRS_V(wrap_prm);
+  MRS_V(tendon_range); MRS_V(tendon_margin); MRS_V(tendon_solref_lim); MRS_V(tendon_solimp_lim);
+  MRS_V(tendon_frictionloss); MRS_V(tendon_solref_fri); MRS_V(tendon_solimp_fri); MRS_V(tendon_stiffness);
+  MRS_V(tendon_damping); MRS_V(tendon_lengthspring); MRS_V(tendon_invweight0); MRS_V(tendon_length0);
   v.nexpair = static_cast<int>(expair_geom1.size());
   v.nexclude = static_cast<int>(exclude_body1.size());
   MRS_V(expair_geom1); MRS_V(expair_geom2); MRS_V(expair_dim); MRS_V(exclude_body1); MRS_V(exclude_body2);

@@ -70,6 +70,11 @@ struct Model {
   // equality constraints (mrs_model_view eq_*)
   std::vector<int> eq_type, eq_obj1id, eq_obj2id, eq_active0;
   std::vector<double> eq_solref, eq_solimp, eq_data;
+  // fixed tendons (mrs_model_view tendon_* / wrap_*)
+  std::vector<int> tendon_adr, tendon_num, tendon_limited, wrap_objid;
+  std::vector<double> wrap_prm, tendon_range, tendon_margin, tendon_solref_lim, tendon_solimp_lim,
+      tendon_frictionloss, tendon_solref_fri, tendon_solimp_fri, tendon_stiffness, tendon_damping,
+      tendon_lengthspring, tendon_invweight0, tendon_length0;
   // rendering (mrs_model_view light_* / tex_* / mat_*); MuJoCo's headlight defaults
   double vis_headlight[10] = {0.1, 0.1, 0.1, 0.4, 0.4, 0.4, 0.5, 0.5, 0.5, 1};
   std::vector<int> light_directional, light_castshadow, light_active, tex_type, tex_builtin, tex_mark, tex_width,

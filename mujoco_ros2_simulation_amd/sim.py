@@ -26,10 +26,11 @@ LIB_PATH = Path(os.environ["MRS_LIB"]) if os.environ.get("MRS_LIB") else _PKG / 
 GEOM_PLANE, GEOM_HFIELD, GEOM_SPHERE, GEOM_CAPSULE, GEOM_ELLIPSOID, GEOM_CYLINDER, GEOM_BOX, GEOM_MESH = range(8)
 JNT_FREE, JNT_BALL, JNT_SLIDE, JNT_HINGE = range(4)
 OBJ_BODY, OBJ_JOINT, OBJ_GEOM, OBJ_SITE, OBJ_CAMERA, OBJ_ACTUATOR, OBJ_SENSOR = 1, 3, 5, 6, 7, 19, 20
+OBJ_TENDON = 18
 SENS_ACCELEROMETER, SENS_GYRO, SENS_FORCE, SENS_TORQUE, SENS_RANGEFINDER = 1, 3, 4, 5, 7
 SENS_JOINTPOS, SENS_JOINTVEL, SENS_ACTUATORFRC, SENS_FRAMEPOS, SENS_FRAMEQUAT = 9, 10, 15, 25, 26
 BIAS_NONE, BIAS_AFFINE = 0, 1
-RESTATE_NEWTON_REFINE, RESTATE_PGS_ELLIPTIC_BLOCK = 1, 2
+RESTATE_NEWTON_REFINE, RESTATE_PGS_ELLIPTIC_BLOCK, RESTATE_NO_MPR_POLISH = 1, 2, 4
 (FIELD_QPOS, FIELD_QVEL, FIELD_CTRL, FIELD_QFRC_APPLIED, FIELD_QACC_WARMSTART, FIELD_QACC,
  FIELD_QFRC_ACTUATOR, FIELD_SENSORDATA, FIELD_TIME, FIELD_WARNING, FIELD_NCON, FIELD_SOLVER_NITER) = range(12)
 # ActuatorType (include/mujoco_ros2_control/data.hpp:43-51 numbering)
@@ -125,6 +126,19 @@ _REND_ARRAYS = [
     ("mat_emission", "d", "nmat", 1),
 ]
 TEX_2D, TEX_CUBE, TEX_SKYBOX = 0, 1, 2
+# fixed tendons (after the rendering block)
+_TEN_SIZES = ["ntendon", "nwrap"]
+_TEN_ARRAYS = [
+    ("tendon_adr", "i", "ntendon", 1), ("tendon_num", "i", "ntendon", 1), ("tendon_limited", "i", "ntendon", 1),
+    ("wrap_objid", "i", "nwrap", 1), ("wrap_prm", "d", "nwrap", 1), ("tendon_range", "d", "ntendon", 2),
+    ("tendon_margin", "d", "ntendon", 1), ("tendon_solref_lim", "d", "ntendon", 2),
+    ("tendon_solimp_lim", "d", "ntendon", 5), ("tendon_frictionloss", "d", "ntendon", 1),
+    ("tendon_solref_fri", "d", "ntendon", 2), ("tendon_solimp_fri", "d", "ntendon", 5),
+    ("tendon_stiffness", "d", "ntendon", 1), ("tendon_damping", "d", "ntendon", 1),
+    ("tendon_lengthspring", "d", "ntendon", 2), ("tendon_invweight0", "d", "ntendon", 1),
+    ("tendon_length0", "d", "ntendon", 1),
+]
+TRN_JOINT, TRN_TENDON = 0, 3
 
 
 class ModelView(C.Structure):
@@ -143,7 +157,9 @@ class ModelView(C.Structure):
                 [(n, C.c_int) for n in _EQ_SIZES] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _EQ_ARRAYS] +
                 [("vis_headlight", C.c_double * 10)] + [(n, C.c_int) for n in _REND_SIZES] +
-                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _REND_ARRAYS])
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _REND_ARRAYS] +
+                [(n, C.c_int) for n in _TEN_SIZES] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _TEN_ARRAYS])
 
 
 _lib = None
@@ -230,7 +246,7 @@ class Model:
         self.view = ModelView()
         _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
         v = self.view
-        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES + _REND_SIZES:
+        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES + _REND_SIZES + _TEN_SIZES:
             setattr(self, n, getattr(v, n))
         for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "restate", "integrator", "solver",
                   "iterations", "disableflags",
@@ -238,7 +254,8 @@ class Model:
             setattr(self, n, getattr(v, n))
         self.gravity = np.array(v.gravity[:])
         self.vis_headlight = np.array(v.vis_headlight[:])
-        for name, kind, count, width in _ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS + _EQ_ARRAYS + _REND_ARRAYS:
+        for name, kind, count, width in (_ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS + _EQ_ARRAYS + _REND_ARRAYS +
+                                         _TEN_ARRAYS):
             n = getattr(v, count)
             w = getattr(v, width) if isinstance(width, str) else width
             ptr = getattr(v, name)

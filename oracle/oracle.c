@@ -56,11 +56,11 @@ typedef struct {
   orc_contact con[MAXCON];
 } orc_ws;
 
-enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3, EFC_EQUALITY = 4 };
+enum { EFC_FRICTION = 1, EFC_LIMIT = 2, EFC_CONTACT = 3, EFC_EQUALITY = 4, EFC_TFRICTION = 5, EFC_TLIMIT = 6 };
 /* equality rows are unbounded; the solvers treat them as friction-loss rows with this bound (never
  * reached: a force of 1e15), so they are quadratic in every primal state and unclamped in PGS */
 #define EQ_BOUND 1e15
-#define FRIC_LIKE(t) ((t) == EFC_FRICTION || (t) == EFC_EQUALITY)
+#define FRIC_LIKE(t) ((t) == EFC_FRICTION || (t) == EFC_EQUALITY || (t) == EFC_TFRICTION)
 /* an elliptic contact block starts at row r (its normal) */
 #define ELL_BLOCK(w, r) ((w)->efc_sub[r] == 0)
 
@@ -494,7 +494,24 @@ static void jac_point_col(const mrs_model_view* m, orc_ws* w, int b, const doubl
   for (int i = 0; i < 3; ++i) col[i] = w->cdof[6 * j + 3 + i] + cr[i];
 }
 
-/* mj_passive [upstream engine_passive.c]: joint springs, dampers, gravity compensation */
+/* fixed tendon t [upstream mj_tendon, fixed tendons]: length sum_k coef_k qpos_k; velocity and the
+ * constant Jacobian row J (nv, may be NULL) from the wrapped joints' dofs */
+static double tendon_length(const mrs_model_view* m, const orc_data* d, int t, double* J, double* vel) {
+  double L = 0, v = 0;
+  if (J) memset(J, 0, m->nv * sizeof(double));
+  for (int k = m->tendon_adr[t]; k < m->tendon_adr[t] + m->tendon_num[t]; ++k) {
+    const int j = m->wrap_objid[k];
+    const double c = m->wrap_prm[k];
+    L += c * d->qpos[m->jnt_qposadr[j]];
+    v += c * d->qvel[m->jnt_dofadr[j]];
+    if (J) J[m->jnt_dofadr[j]] += c;
+  }
+  if (vel) *vel = v;
+  return L;
+}
+
+/* mj_passive [upstream engine_passive.c]: joint springs, dampers, tendon springs (dead band
+ * [lengthspring0, lengthspring1]) and dampers through J', gravity compensation */
 static void passive(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   memset(w->qfrc_passive, 0, m->nv * sizeof(double));
@@ -507,6 +524,21 @@ static void passive(const mrs_model_view* m, orc_data* d) {
     }
   }
   for (int i = 0; i < m->nv; ++i) w->qfrc_passive[i] -= m->dof_damping[i] * d->qvel[i];
+  if (m->ntendon > 0) {
+    double* J = (double*)malloc(m->nv * sizeof(double) + 8);
+    for (int t = 0; t < m->ntendon; ++t) {
+      const double k = m->tendon_stiffness[t], b = m->tendon_damping[t];
+      if (k == 0 && b == 0) continue;
+      double v;
+      const double L = tendon_length(m, d, t, J, &v);
+      const double* ls = m->tendon_lengthspring + 2 * t;
+      double f = 0;
+      if (k != 0) f = L > ls[1] ? k * (ls[1] - L) : (L < ls[0] ? k * (ls[0] - L) : 0);
+      f -= b * v;
+      for (int i = 0; i < m->nv; ++i) w->qfrc_passive[i] += J[i] * f;
+    }
+    free(J);
+  }
   if (!(m->disableflags & MRS_DSBL_GRAVITY)) {
     for (int b = 1; b < m->nbody; ++b) {
       if (m->body_gravcomp[b] == 0) continue;
@@ -527,11 +559,21 @@ static void actuation(const mrs_model_view* m, orc_data* d) {
   orc_ws* w = (orc_ws*)d->ws;
   memset(d->qfrc_actuator, 0, m->nv * sizeof(double));
   if (m->disableflags & MRS_DSBL_ACTUATION) { memset(w->actuator_force, 0, m->nu * sizeof(double)); return; }
+  double* Jt = m->ntendon > 0 ? (double*)malloc(m->nv * sizeof(double) + 8) : NULL;
   for (int a = 0; a < m->nu; ++a) {
     int j = m->actuator_trnid[2 * a];
-    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    const int tendon = m->actuator_trntype[a] == MRS_TRN_TENDON;
+    int qa = tendon ? 0 : m->jnt_qposadr[j], da = tendon ? 0 : m->jnt_dofadr[j];
     double gear = m->actuator_gear[6 * a];
-    double len = gear * d->qpos[qa], vel = gear * d->qvel[da];
+    double len, vel;
+    if (tendon) {
+      double tv;
+      len = gear * tendon_length(m, d, j, Jt, &tv);
+      vel = gear * tv;
+    } else {
+      len = gear * d->qpos[qa];
+      vel = gear * d->qvel[da];
+    }
     double ctrl = d->ctrl[a];
     if (m->actuator_ctrllimited[a] && !(m->disableflags & MRS_DSBL_CLAMPCTRL)) {
       const double* r = m->actuator_ctrlrange + 2 * a;
@@ -549,8 +591,12 @@ static void actuation(const mrs_model_view* m, orc_data* d) {
       force = force < r[0] ? r[0] : force > r[1] ? r[1] : force;
     }
     w->actuator_force[a] = force;
-    d->qfrc_actuator[da] += gear * force;
+    if (tendon)
+      for (int i = 0; i < m->nv; ++i) d->qfrc_actuator[i] += gear * force * Jt[i];
+    else
+      d->qfrc_actuator[da] += gear * force;
   }
+  free(Jt);
   for (int j = 0; j < m->njnt; ++j) {
     if (!m->jnt_actfrclimited[j]) continue;
     const double* r = m->jnt_actfrcrange + 2 * j;
@@ -1603,7 +1649,7 @@ static int col_convex(const mrs_model_view* m, orc_ws* w, int g1, int g2, double
   if (!mpr_penetration(&A, &B, &depth, nrm, pos)) return n;
   static int no_polish = -1;  /* diagnostics: ORC_NO_POLISH=1 keeps MPR's contact (scripts/diag_mpr.py) */
   if (no_polish < 0) no_polish = getenv("ORC_NO_POLISH") != NULL;
-  if (!no_polish) mpr_polish(&A, &B, nrm, depth, &depth, nrm, pos);
+  if (!no_polish && !(m->restate & MRS_RESTATE_NO_MPR_POLISH)) mpr_polish(&A, &B, nrm, depth, &depth, nrm, pos);
   return add_contact(out, n, margin - depth, pos, nrm);
 }
 /* plane (geom1) vs ellipsoid: the support point along -normal (mjc_PlaneEllipsoid) */
@@ -1954,6 +2000,14 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
       add_row(w, nv, EFC_FRICTION, j, J, 0, 0, m->dof_frictionloss[j], m->dof_invweight0[j],
               m->dof_solref + 2 * j, m->dof_solimp + 5 * j);
     }
+  /* tendon friction loss rows [upstream mj_instantiateFriction: after the dofs'], J = ten_J */
+  if (!(m->disableflags & MRS_DSBL_FRICTIONLOSS))
+    for (int t = 0; t < m->ntendon; ++t) {
+      if (m->tendon_frictionloss[t] <= 0) continue;
+      tendon_length(m, d, t, J, NULL);
+      add_row(w, nv, EFC_TFRICTION, t, J, 0, 0, m->tendon_frictionloss[t], m->tendon_invweight0[t],
+              m->tendon_solref_fri + 2 * t, m->tendon_solimp_fri + 5 * t);
+    }
   if (!(m->disableflags & MRS_DSBL_LIMIT))
     for (int j = 0; j < m->njnt; ++j) {
       if (!m->jnt_limited[j]) continue;
@@ -1968,6 +2022,22 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
           J[da] = -side;
           add_row(w, nv, EFC_LIMIT, j, J, dist, margin, 0, m->dof_invweight0[da],
                   m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j);
+        }
+      }
+    }
+  /* tendon limit rows [upstream mj_instantiateLimit: after the joints'], lower then upper, J = +-ten_J */
+  if (!(m->disableflags & MRS_DSBL_LIMIT))
+    for (int t = 0; t < m->ntendon; ++t) {
+      if (!m->tendon_limited[t]) continue;
+      const double L = tendon_length(m, d, t, J, NULL), margin = m->tendon_margin[t];
+      for (int side = -1; side <= 1; side += 2) {
+        const double dist = side * (m->tendon_range[2 * t + (side + 1) / 2] - L);
+        if (dist < margin) {
+          double* Js = (double*)malloc(nv * sizeof(double) + 8);
+          for (int i = 0; i < nv; ++i) Js[i] = -side * J[i];
+          add_row(w, nv, EFC_TLIMIT, t, Js, dist, margin, 0, m->tendon_invweight0[t],
+                  m->tendon_solref_lim + 2 * t, m->tendon_solimp_lim + 5 * t);
+          free(Js);
         }
       }
     }
@@ -2044,7 +2114,8 @@ static void make_constraint(const mrs_model_view* m, orc_data* d) {
     for (int j = 0; j < nv; ++j) vel += w->efc_J[(size_t)r * nv + j] * d->qvel[j];
     w->efc_vel[r] = vel;
     /* (friction loss rows and the tangent rows of an elliptic cone carry no position term) */
-    double pterm = (w->efc_type[r] == EFC_FRICTION || w->efc_sub[r] > 0) ? 0 : K * imp * (w->efc_pos[r] - w->efc_margin[r]);
+    double pterm = (w->efc_type[r] == EFC_FRICTION || w->efc_type[r] == EFC_TFRICTION || w->efc_sub[r] > 0)
+                       ? 0 : K * imp * (w->efc_pos[r] - w->efc_margin[r]);
     w->efc_aref[r] = -B * vel - pterm;
     w->efc_KBIP[r][0] = K; w->efc_KBIP[r][1] = B; w->efc_KBIP[r][2] = imp; w->efc_KBIP[r][3] = 0;
   }
@@ -3134,6 +3205,8 @@ static void integrate(const mrs_model_view* m, orc_data* d) {
       for (int j = 0; j < nv; ++j) Dg[j] = m->dof_damping[j];
     if (!(m->disableflags & MRS_DSBL_ACTUATION))
       for (int a = 0; a < m->nu; ++a) {
+        /* (tendon actuators on these integrators have no velocity term: the compiler requires it) */
+        if (m->actuator_trntype[a] == MRS_TRN_TENDON) continue;
         if (m->actuator_forcelimited[a]) {
           double f = w->actuator_force[a];
           const double* r = m->actuator_forcerange + 2 * a;

@@ -13,8 +13,9 @@ import binding  # noqa: E402
 from test_gpu_mesh import MPR_SCENE  # noqa: E402
 
 
-def main(n_states=100):
+def main(n_states=100, restate=0):
     model = sim.Model.from_string(MPR_SCENE)
+    print(f"--- restate {restate}")
     d = binding.OracleData(model)
     d.qpos[:] = synth.initial_qpos(model, np.arange(1))[0]
     Q, V = [], []
@@ -23,6 +24,7 @@ def main(n_states=100):
         if t >= 75:
             Q.append(d.qpos.astype(np.float32).astype(np.float64))
             V.append(d.qvel.astype(np.float32).astype(np.float64))
+    model.set_restate(restate)
     b = sim.Batch(model, len(Q))
     b.set(sim.FIELD_QPOS, np.array(Q))
     b.set(sim.FIELD_QVEL, np.array(V))
@@ -43,6 +45,9 @@ def main(n_states=100):
             dn = float(np.max(np.abs(frame[k, :3] - fr[k, :3])))
             dd = abs(float(dist[k] - dr[k]))
             dp = float(np.max(np.abs(pos[k] - pr[k])))
+            if dn > 1e-3:
+                print(f"  state {e} contact {k} {kind}: gpu n {np.round(frame[k, :3], 5).tolist()} dist {dist[k]:.4e}; "
+                      f"oracle n {np.round(fr[k, :3], 5).tolist()} dist {dr[k]:.4e}")
             w = worst.setdefault(kind, [0, 0, 0, None])
             if dn > w[0]:
                 w[0] = dn
@@ -54,4 +59,6 @@ def main(n_states=100):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 100)
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    main(n, 0)
+    main(n, sim.RESTATE_NO_MPR_POLISH)
