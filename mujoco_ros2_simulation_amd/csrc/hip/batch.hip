@@ -471,8 +471,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                                                        const float* geom_xpos, const float* geom_xmat,
                                                        const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
                                                        int env0, int W, int H, float f, float znear, float zfar,
-                                                       float* out, unsigned char* rgb, MeshRef mesh, LitRef lr,
-                                                       int order) {
+                                                       float* out, unsigned char* rgb, MeshRef mesh, LitRef lr) {
   __shared__ DepthGeom G[kDepthGeoms];
   __shared__ LitFrame LF;
   const int env = env0 + blockIdx.x;
@@ -493,7 +492,6 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
     const float y1 = (0.5f * H - ty * kDepthTileH - 0.5f) / f;
     const float y0 = (0.5f * H - fminf(ty * kDepthTileH + kDepthTileH - 1.0f, H - 1.0f) - 0.5f) / f;
     bool keep = false;
-    int zlo = 0;  // lower bound of the geom's eye depth (float bits, >= 0): hits have t >= zlo
     if (lane < ngeom && G[lane].vis) {
       const DepthGeom& o = G[lane];
       if (o.type == MRS_GEOM_PLANE) {
@@ -502,9 +500,6 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         const float bx = fminf(x0 * n[0], x1 * n[0]), by = fminf(y0 * n[1], y1 * n[1]);
         keep = bx + by - n[2] < 1e-6f;
       } else {
-        float rz = 0;
-        for (int i = 0; i < 3; ++i) rz += o.ext[i] * fabsf(o.A[3 * i + 2]);
-        zlo = __float_as_int(fmaxf(0.0f, (-o.cc[2] - rz) * (1 - 1e-5f)));
         // oriented box vs the four side planes n.p >= 0 of the tile pyramid (unnormalised normals:
         // left (1, 0, x0), right (-1, 0, -x1), bottom (0, 1, y0), top (0, -1, -y1))
         auto outside = [&](float nx, float ny, float nz) {
@@ -528,28 +523,9 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       bestg[k] = 0;
       dy[k] = (0.5f * H - (ty * kDepthTileH + k) - 0.5f) / f;
     }
-    // Candidates nearest-first by their eye-depth bound zlo (planes first, at 0): once every pixel of
-    // the tile holds a hit nearer than the next candidate's bound, no remaining candidate can take a
-    // pixel, and the tile is done.  Ties of t keep the lower geom index, as the index-order loop.
-    int key = keep ? zlo : 0x7f800000;
     while (cand) {
-      int g;
-      if (order) {
-        int mn = key;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) mn = min(mn, __shfl_xor(mn, o));
-        g = __builtin_ctzll(__ballot(key == mn) & cand);
-        int far = 0;
-#pragma unroll
-        for (int k = 0; k < kDepthTileH; ++k) far = max(far, best[k] < 0 ? 0x7f800000 : __float_as_int(best[k]));
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) far = max(far, __shfl_xor(far, o));
-        if (far < mn) break;
-        if (lane == g) key = 0x7f800000;
-      } else {
-        g = __builtin_ctzll(cand);
-      }
-      cand &= ~(1ull << g);
+      const int g = __builtin_ctzll(cand);
+      cand &= cand - 1;
       const DepthGeom& o = G[g];
       const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]}, sz[3] = {o.size[0], o.size[1], o.size[2]};
       float A[9];
@@ -568,7 +544,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                        mesh.bvh + 8 * mesh.bvhadr[o.dataid], mesh.bvhnum[o.dataid], &tri);
         }
         else t = ray_prim(type, sz, lp, lv);
-        if (t >= znear && (best[k] < 0 || t < best[k] || (t == best[k] && g < bestg[k]))) { best[k] = t; bestg[k] = g; }
+        if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
     }
     if (col < W) {
@@ -909,8 +885,6 @@ struct BatchImpl {
   unsigned long long* rast_list = nullptr;
   int rast_frames = 0;
   int max_lds = 0;  // hipDeviceAttributeMaxSharedMemoryPerBlock of the batch's device
-  // depth_kernel_v2 visits a tile's candidates nearest-first and stops early (MRS_DEPTH_ORDER=0: index order)
-  int depth_order = std::getenv("MRS_DEPTH_ORDER") ? std::atoi(std::getenv("MRS_DEPTH_ORDER")) : 1;
   // the model needs the extended step kernels (step.hip MRS_EXT): general convex (MPR) collision
   // pairs, or rangefinders with more than 32 ray geoms
   bool ext = false;
@@ -1966,15 +1940,11 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     // padded to whole workgroups of the chosen group width: idle groups use it
     const size_t epb = static_cast<size_t>(envs_per_block(b->group));
     const size_t n_pad = (static_cast<size_t>(n) + epb - 1) / epb * epb;
-    // env spread: lane groups per env so that a small batch still fills two waves per SIMD (the
-    // resident limit of the 256-VGPR step kernels); MRS_SPREAD=<shift> overrides (0: off)
+    // env spread (opt-in, MRS_SPREAD=<shift>): 2^shift lane groups per env, the extra ones mirroring
+    // the first, so a small batch occupies more waves.  Measured slower (round 5, same box: C4 18.2
+    // vs 22.9 M env-steps/s at shift 2, C2 147 vs 156 M at shift 1): the mirrors' issue slots cost
+    // more than the latency they hide, so it is off by default
     int shift = 0;
-    if (b->group < 64) {
-      int cus = 0;
-      HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device));
-      const long waves = (static_cast<long>(n) * b->group + 63) / 64, target = 2L * 4 * std::max(cus, 1);
-      while (shift < 2 && (waves << (shift + 1)) <= target) ++shift;
-    }
     if (const char* e = std::getenv("MRS_SPREAD")) shift = std::max(0, std::min(3, std::atoi(e)));
     const size_t n_virt = ((static_cast<size_t>(n) << shift) + epb - 1) / epb * epb;
     b->st.spread_shift = shift;
@@ -2202,7 +2172,7 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
     hipLaunchKernelGGL(drgb ? depth_kernel_v2<true> : depth_kernel_v2<false>, dim3(n), dim3(256), 0, stream,
                        d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr, b->depth_order);
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr);
   } else {
     dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
     hipLaunchKernelGGL(drgb ? depth_kernel<true> : depth_kernel<false>, grid, dim3(256), 0, stream, d.geom_type.p,

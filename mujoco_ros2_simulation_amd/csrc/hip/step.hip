@@ -849,6 +849,30 @@ __device__ __forceinline__ void closest_on_triangle(const float a[3], const floa
   const float den = 1.0f / (va + vb + vc), v = vb * den, w = vc * den;
   for (int i = 0; i < 3; ++i) out[i] = a[i] + ab[i] * v + ac[i] * w;
 }
+// MPR's penetration vector: the point of the final portal nearest the origin.  When the origin's
+// projection onto the portal plane falls inside the portal (the usual end: the origin ray crosses it)
+// that point is depth * n with n the portal normal and depth = n.p1 -- well conditioned even for a
+// long thin portal, whose barycentric closest-point formula cancels catastrophically in fp32 (a 0.3 m
+// portal 0.07 mm from the origin: fp32 put the point on the wrong edge, 1.1 rad off).  Otherwise the
+// nearest edge / vertex point (closest_on_triangle).  oracle.c mpr_nearest takes the same branches.
+__device__ __forceinline__ void mpr_nearest(const float a[3], const float b[3], const float c[3], float out[3]) {
+  float n[3];
+  tri_normal(n, a, b, c);
+  const float d = dot3(n, a);
+  const float q[3] = {d * n[0], d * n[1], d * n[2]};
+  // inside: q on the inner side of each edge (sign of (e x (q - v)).n, edges in winding order)
+  auto side = [&](const float* u, const float* v) {
+    const float e[3] = {v[0] - u[0], v[1] - u[1], v[2] - u[2]}, w[3] = {q[0] - u[0], q[1] - u[1], q[2] - u[2]};
+    float x[3];
+    cross3(x, e, w);
+    return dot3(x, n);
+  };
+  if (side(a, b) >= 0 && side(b, c) >= 0 && side(c, a) >= 0) {
+    for (int i = 0; i < 3; ++i) out[i] = q[i];
+    return;
+  }
+  closest_on_triangle(a, b, c, out);
+}
 __device__ __forceinline__ void mpr_expand(MprPoint p[4], const MprPoint& v4) {
   float x[3];
   cross3(x, v4.v, p[0].v);
@@ -952,7 +976,7 @@ __device__ __forceinline__ bool mpr_penetration(const MeshTab m, const Shape A, 
     tri_normal(n, p[1].v, p[2].v, p[3].v);
     mpr_support(m, A, B, n, v4);
     if (mpr_reach_tolerance(p, v4, n) || it > kMprIter) {
-      closest_on_triangle(p[1].v, p[2].v, p[3].v, nrm);
+      mpr_nearest(p[1].v, p[2].v, p[3].v, nrm);
       depth = sqrtf(dot3(nrm, nrm));
       if (depth < kMinVal) return false;
       for (int i = 0; i < 3; ++i) nrm[i] /= depth;

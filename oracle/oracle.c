@@ -1129,6 +1129,26 @@ static void closest_on_triangle(const double a[3], const double b[3], const doub
   double den = 1 / (va + vb + vc), v = vb * den, ww = vc * den;
   for (int i = 0; i < 3; ++i) out[i] = a[i] + ab[i] * v + ac[i] * ww;
 }
+/* MPR's penetration vector, the point of the final portal nearest the origin: depth * n (n the portal
+ * normal, depth = n.p1) when the origin projects inside the portal, else the nearest edge / vertex
+ * point.  Equal to closest_on_triangle; written this way because that formula cancels in fp32 for a
+ * long thin portal near the origin, and the device (step.hip mpr_nearest) takes the same branches. */
+static void mpr_nearest(const double a[3], const double b[3], const double c[3], double out[3]) {
+  double n[3];
+  tri_normal(n, a, b, c);
+  const double d = dot3(n, a);
+  const double q[3] = {d * n[0], d * n[1], d * n[2]};
+  const double* V[4] = {a, b, c, a};
+  int inside = 1;
+  for (int k = 0; k < 3; ++k) {
+    double e[3], w[3], x[3];
+    for (int i = 0; i < 3; ++i) { e[i] = V[k + 1][i] - V[k][i]; w[i] = q[i] - V[k][i]; }
+    cross3(x, e, w);
+    if (dot3(x, n) < 0) inside = 0;
+  }
+  if (inside) { memcpy(out, q, sizeof q); return; }
+  closest_on_triangle(a, b, c, out);
+}
 static void mpr_expand(mpr_point p[4], const mpr_point* v4) {
   double x[3];
   cross3(x, v4->v, p[0].v);
@@ -1231,7 +1251,7 @@ static int mpr_penetration(const orc_shape* A, const orc_shape* B, double* depth
     tri_normal(n, p[1].v, p[2].v, p[3].v);
     mpr_support(A, B, n, &v4);
     if (mpr_reach_tolerance(p, &v4, n) || it > MPR_ITER) {
-      closest_on_triangle(p[1].v, p[2].v, p[3].v, nrm);
+      mpr_nearest(p[1].v, p[2].v, p[3].v, nrm);
       *depth = normalize3(nrm);
       if (*depth < MINVAL) return 0;
       mpr_position(p, pos);

@@ -31,7 +31,9 @@ OUT = Path(sys.argv[1])
 KEY = sys.argv[2]
 CFG = KEY.split("_")[0]
 EXTRA = os.environ.get("BENCH_ARGS", "")
-KERNEL = "step_kernel"
+# SQ_KERNEL=depth_kernel summarizes the frame kernel of a render config instead (its time: the bench
+# line's roofline.kernel_ms, which for C4 / C3m is the frame kernel)
+KERNEL = os.environ.get("SQ_KERNEL", "step_kernel")
 rows = [r for r in csv.DictReader(open(ROOT / f"gpurun_out/pmc_sq_{KEY}/run_counter_collection.csv"))
         if KERNEL in r["Kernel_Name"] and not re.search(r"step_kernel<\d+, true", r["Kernel_Name"])]
 per = defaultdict(lambda: defaultdict(float))
@@ -41,7 +43,8 @@ disp = sorted(per, key=int)
 steady = disp[1:] if len(disp) > 2 else disp
 avg = {k: sum(per[d][k] for d in steady) / len(steady) for k in per[steady[0]]}
 bench = json.loads((ROOT / f"gpurun_out/bench_{KEY}.json").read_text().strip().splitlines()[-1])
-kms = bench["roofline"].get("step_kernel_ms") or bench["roofline"]["kernel_ms"]
+kms = (bench["roofline"]["kernel_ms"] if KERNEL != "step_kernel"
+       else bench["roofline"].get("step_kernel_ms") or bench["roofline"]["kernel_ms"])
 wc = avg["SQ_WAVE_CYCLES"]
 valu_tf = avg["SQ_INSTS_VALU"] * 64 * 2 / (kms * 1e-3) / 1e12
 rec = {

@@ -54,7 +54,11 @@ def test_closed_chain_rollout():
     """the four-bar (two links on hinges closed by a connect) under the motor for 1000 steps: the
     connect's anchor points stay together on the device (within the soft constraint's own sag, as
     the oracle's), and qpos follows the oracle within the scene's fp32 sensitivity"""
-    model = scene("PGS")
+    # the chain's capsules do not collide here: a link grazing the floor is a contact threshold event
+    # (present on one side only for a step), after which the chaotic swing separates the two rollouts
+    # far beyond the rounding sensitivity measured below
+    model = sim.Model.from_string(EQ_SCENE.format(solver="PGS", it="50").replace(
+        '<geom type="capsule"', '<geom type="capsule" contype="0" conaffinity="0"'))
     n, steps = 4, 1000
     q0 = synth.initial_qpos(model, np.arange(n))
     tab = synth.ctrl_table(model, np.arange(n), steps // 10 + 1, 10)
