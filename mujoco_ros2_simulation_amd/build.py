@@ -97,11 +97,15 @@ def build_variant(name: str, flags: list[str]) -> Path:
     vdir.mkdir(parents=True, exist_ok=True)
     src = CSRC / "hip" / "step.hip"
     objs, procs = [], []
-    for part in STEP_PARTS:
+    # the profiling build keeps one translation unit: its device-side phase counters
+    # (g_phase_cycles) must be the one copy every kernel instantiation adds into
+    parts = [None] if "-DMRS_PHASE_TIMING" in flags else STEP_PARTS
+    for part in parts:
         obj = vdir / f"step.part{part}.o"
         objs.append(obj)
-        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *HIP_FLAGS, f"-DMRS_STEP_PART={part}",
-               f"-DMRS_EXT={0 if part in STEP_NO_EXT else 1}", *flags, "-c", str(src), "-o", str(obj)]
+        pflags = [] if part is None else [f"-DMRS_STEP_PART={part}", f"-DMRS_EXT={0 if part in STEP_NO_EXT else 1}"]
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *HIP_FLAGS, *pflags,
+               *flags, "-c", str(src), "-o", str(obj)]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
     for cmd, p in procs:
         out, _ = p.communicate()

@@ -3116,7 +3116,10 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 // acc + a * (v of lane K of the row): one v_fmac_f32 with the row broadcast as its DPP source
 // operand (the compiler keeps a separate v_mov_dpp).  The s_nop covers the two wait states a DPP read
 // of a VGPR needs after the VALU write that produced it (the hazard recognizer does not see inside
-// inline asm).
+// inline asm).  The recognizer does not see the asm's own writes either, so a compiler-placed DPP
+// read of the result within two instructions after it would miss its wait states: no such read occurs
+// (tests/test_kernel_code.py checks the built kernels' disassembly; a trailing s_nop in the asm cost
+// C5 2.8 % in the sweep).
 template <int K>
 __device__ __forceinline__ float fmac_rowb(float acc, float a, float v) {
   asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
@@ -6198,7 +6201,11 @@ __device__ __forceinline__ void rangefinders(const DevModel& m, const lfloat* se
     if (m.rf_mode == 1) {
       if (act[j]) m.rf_static[k0 + j * stride] = dist[j];  // producer pass: the static hits
     } else if (act[j] && MRS_SD_OK(sd)) {
+#ifdef MRS_DIAG_SD_SINK
+      asm volatile("" ::"v"(dist[j]));  // diagnostic build: the ray result is kept live, not stored
+#else
       sd[adr[j]] = dist[j];
+#endif
     }
   }
   SUB_ADD(PH_SENS_GEOMS, t_geoms);
