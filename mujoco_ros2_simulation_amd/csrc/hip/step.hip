@@ -2524,6 +2524,38 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
   return ncon;
 }
 
+// acc + a * (v of lane K of the row): one v_fmac_f32 with the row broadcast as its DPP source
+// operand (the compiler keeps a separate v_mov_dpp).  The s_nop covers the two wait states a DPP read
+// of a VGPR needs after the VALU write that produced it (the hazard recognizer does not see inside
+// inline asm).  The recognizer does not see the asm's own writes either, so a compiler-placed DPP
+// read of the result within two instructions after it would miss its wait states: no such read occurs
+// (tests/test_kernel_code.py checks the built kernels' disassembly; a trailing s_nop in the asm cost
+// C5 2.8 % in the sweep).
+template <int K>
+__device__ __forceinline__ float fmac_rowb(float acc, float a, float v) {
+  asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "+v"(acc) : "v"(v), "v"(a), "n"(K));
+  return acc;
+}
+// three held rows at once, the chain's own first: a += x * b, c += x * d, e += x * f with x lane K's
+// v (every update a v_fmac_f32 with the broadcast as its DPP operand, one wait for all three)
+template <int K>
+__device__ __forceinline__ void fmac3_rowb(float& g0, float& g1, float& g2, float v, float a0, float a1, float a2) {
+  asm("s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %3, %4 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %1, %3, %5 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %2, %3, %6 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(g0), "+v"(g1), "+v"(g2) : "v"(v), "v"(a0), "v"(a1), "v"(a2), "n"(K));
+}
+// v = own on lanes O, O + 16, O + 32, O + 48 (slot O of every 16-lane pipe), other elsewhere: one
+// v_cndmask with a constant lane mask (no per-use compare)
+template <int O>
+__device__ __forceinline__ float sel_slot16(float own, float other) {
+  constexpr unsigned long long mask = 0x0001000100010001ull << O;
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(own), "s"(mask));
+  return r;
+}
 // mj_makeConstraint + mj_makeImpedance + PGS (matrix-free rows) -> qacc, qfrc_constraint
 // Small constraint systems on G = 16 groups (nv <= 16, nefc <= 16): lane j holds column j of J and
 // of M^-1 J' for every row (registers, rows unrolled), row scalars are replicated in every lane of
@@ -2637,14 +2669,13 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   // a row costs one broadcast of its residual and one FMA per lane instead of a group reduction of
   // J_r qacc.  Lane r also keeps row r's residual and step of the sweep; the sweep's cost improvement
   // sum_r -(delta_r res_r + 0.5 A_rr delta_r^2) (every term >= 0) is one group sum at its end.
-  float f[KR], iA[KR], flo[KR], fhi[KR];
-  unroll<KR>([&](auto rc) {
-    constexpr int r = decltype(rc)::value;
-    f[r] = rowb<r>(myf); iA[r] = 1.0f / rowb<r>(myA);
-    const float fl = rowb<r>(myfl);
-    flo[r] = fl > 0 ? -fl : 0.0f;
-    fhi[r] = fl > 0 ? fl : __builtin_inff();
-  });
+  // The sweeps carry, in lane t, the normalised residual gn_t = -g_t / A_tt of its own row and the
+  // normalised column ARn[r] = -AR_tr / A_tt (as the island-dual solver, constraints_sparse): row r's
+  // step is the owner's med3 of its own gn (no broadcast on the chain), and every lane moves by
+  // ARn[r] times that step with the DPP row broadcast folded into the FMA (fmac_rowb) -- a row is
+  // med3 -> fmac_dpp on the chain instead of broadcast-multiply -> med3 -> FMA.  The owner's bounds
+  // (lo - f, hi - f) move only at its own level, so they are updated after the sweep from the
+  // residual it kept there (gb), with the sweep's improvement.
   float g;
   {
     float ga = lane < rmax ? myb : 0.0f, gb = 0, gc = 0, gd = 0;
@@ -2652,17 +2683,15 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       constexpr int r = decltype(rc)::value;
       if (r < rmax) {
         float& acc = (r & 3) == 0 ? ga : (r & 3) == 1 ? gb : (r & 3) == 2 ? gc : gd;
-        acc += AR[r] * f[r];
+        acc += AR[r] * rowb<r>(myf);
       }
     });
     g = (ga + gb) + (gc + gd);
   }
-  const float halfA = 0.5f * myA;
-  float niA[KR], lof[KR], hif[KR];
-  unroll<KR>([&](auto rc) {
-    constexpr int r = decltype(rc)::value;
-    niA[r] = -iA[r]; lof[r] = flo[r] - f[r]; hif[r] = fhi[r] - f[r];
-  });
+  const float nia = -1.0f / myA;
+  float gn = nia * g, ARn[KR];
+  unroll<KR>([&](auto rc) { ARn[decltype(rc)::value] = nia * AR[decltype(rc)::value]; });
+  float mylo = (myfl > 0 ? -myfl : 0.0f) - myf, myhi = (myfl > 0 ? myfl : __builtin_inff()) - myf;
   int nit = 0;  // sweeps done (mjData.solver_niter)
   // the sweep is unrolled to the wave's row count rounded up to 4 (rows past rmax are the zero rows,
   // which never move): no per-row bound tests inside the sweep
@@ -2670,18 +2699,17 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
     constexpr int N = decltype(nc)::value;
     #pragma unroll 1
     for (int it = 0; it < m.iterations; ++it) {
-      float myres = 0, mydelta = 0;
+      float gb = gn;
       unroll<N>([&](auto rc) {
         constexpr int r = decltype(rc)::value;
-        // the step itself is clamped: delta = med3(-res / A, lo - f, hi - f), with lo - f and hi - f
-        // carried instead of f (one op fewer per row than clamping f and differencing)
-        const float delta = __builtin_amdgcn_fmed3f(rowb<r>(g) * niA[r], lof[r], hif[r]);
-        if (lane == r) { myres = g; mydelta = delta; }
-        g += AR[r] * delta;
-        lof[r] -= delta;
-        hif[r] -= delta;
+        const float cand = __builtin_amdgcn_fmed3f(gn, mylo, myhi);  // row r's clamped step, in lane r
+        gb = sel_slot16<r>(gn, gb);
+        gn = fmac_rowb<r>(gn, ARn[r], cand);
       });
-      const float improvement = gsum<16>(-mydelta * (myres + halfA * mydelta));
+      const float dm = __builtin_amdgcn_fmed3f(gb, mylo, myhi);
+      mylo -= dm;
+      myhi -= dm;
+      const float improvement = gsum<16>(lane < rmax ? myA * dm * (gb - 0.5f * dm) : 0.0f);
       nit = it + 1;
       if (improvement * m.pgs_scale < m.tolerance) break;
     }
@@ -2690,10 +2718,9 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   else if (KR <= 8 || rmax <= 8) sweeps(std::integral_constant<int, (KR < 8 ? KR : 8)>{});
   else if (KR <= 12 || rmax <= 12) sweeps(std::integral_constant<int, (KR < 12 ? KR : 12)>{});
   else sweeps(std::integral_constant<int, KR>{});
-  unroll<KR>([&](auto rc) {
-    constexpr int r = decltype(rc)::value;
-    f[r] = flo[r] - lof[r];
-  });
+  myf = (myfl > 0 ? -myfl : 0.0f) - mylo;
+  float f[KR];
+  unroll<KR>([&](auto rc) { f[decltype(rc)::value] = rowb<decltype(rc)::value>(myf); });
   float qa = lane < nv ? qacc_s : 0.0f;  // qacc = qacc_smooth + M^-1 J' f
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
@@ -2704,7 +2731,6 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
     if (r < rmax) qc += Jt[r] * f[r];
-    if (lane == r) myf = f[r];
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
   // row forces (mj_rnePostConstraint's contact forces, mrs_batch_get_efc)
@@ -2841,7 +2867,6 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
     if (r < rmax) qc += Jt[r] * f[r];
-    if (lane == r) myf = f[r];
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
   // row forces (mj_rnePostConstraint's contact forces, mrs_batch_get_efc)
@@ -3112,38 +3137,6 @@ __device__ __forceinline__ int wave_max(int v) {
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mask), 0));
-}
-// acc + a * (v of lane K of the row): one v_fmac_f32 with the row broadcast as its DPP source
-// operand (the compiler keeps a separate v_mov_dpp).  The s_nop covers the two wait states a DPP read
-// of a VGPR needs after the VALU write that produced it (the hazard recognizer does not see inside
-// inline asm).  The recognizer does not see the asm's own writes either, so a compiler-placed DPP
-// read of the result within two instructions after it would miss its wait states: no such read occurs
-// (tests/test_kernel_code.py checks the built kernels' disassembly; a trailing s_nop in the asm cost
-// C5 2.8 % in the sweep).
-template <int K>
-__device__ __forceinline__ float fmac_rowb(float acc, float a, float v) {
-  asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-               : "+v"(acc) : "v"(v), "v"(a), "n"(K));
-  return acc;
-}
-// three held rows at once, the chain's own first: a += x * b, c += x * d, e += x * f with x lane K's
-// v (every update a v_fmac_f32 with the broadcast as its DPP operand, one wait for all three)
-template <int K>
-__device__ __forceinline__ void fmac3_rowb(float& g0, float& g1, float& g2, float v, float a0, float a1, float a2) {
-  asm("s_nop 1\n\t"
-      "v_fmac_f32_dpp %0, %3, %4 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_fmac_f32_dpp %1, %3, %5 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_fmac_f32_dpp %2, %3, %6 row_newbcast:%7 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "+v"(g0), "+v"(g1), "+v"(g2) : "v"(v), "v"(a0), "v"(a1), "v"(a2), "n"(K));
-}
-// v = own on lanes O, O + 16, O + 32, O + 48 (slot O of every 16-lane pipe), other elsewhere: one
-// v_cndmask with a constant lane mask (no per-use compare)
-template <int O>
-__device__ __forceinline__ float sel_slot16(float own, float other) {
-  constexpr unsigned long long mask = 0x0001000100010001ull << O;
-  float r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(other), "v"(own), "s"(mask));
-  return r;
 }
 // one record as the sweeps read it
 template <int P>

@@ -28,9 +28,10 @@ for v in $VARIANTS; do
   key=${v%%:*}; rest=${v#*:}; cfg=${rest%%:*}; extra=$(echo ${rest#*:} | tr ',' ' ')
   [ "${SKIP_STATS:-0}" = 1 ] || timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rocprof_$key -o run -- python3 bench.py --config $cfg $extra --no-cpu-baseline > gpurun_out/rocprof_$key.log 2>&1 || exit $?
   [ "${SKIP_PMC:-0}" = 1 ] && continue
-  ps=5; [ $cfg = c4 ] && ps=200; [ $cfg = c3m ] && ps=20
+  # (render configs: enough bench steps for several frame batches -- C4 renders every 10 bench steps)
+  ps=5; [ $cfg = c4 ] && ps=40; [ $cfg = c3m ] && ps=20
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$key -o run -- python3 bench.py --config $cfg $extra --steps $ps --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch_$key.log 2>&1 || exit $?
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_$key -o run -- python3 bench.py --config $cfg $extra --steps $ps --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write_$key.log 2>&1 || exit $?
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_flops_$key -o run -- python3 bench.py --config $cfg $extra --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_flops_$key.log 2>&1 || exit $?
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq_$key -o run -- python3 bench.py --config $cfg $extra --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_sq_$key.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq_$key -o run -- python3 bench.py --config $cfg $extra --steps $ps --warmup 1 --no-cpu-baseline > gpurun_out/pmc_sq_$key.log 2>&1 || exit $?
 done

@@ -13,7 +13,8 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def _disasm():
-    objs = sorted((ROOT / "build" / "obj").glob("hip_step.hip.part64.o"))  # blocked mode: the sparse PGS
+    # blocked mode (the sparse PGS) and the 16-lane kernels (the dense register PGS)
+    objs = sorted(o for o in (ROOT / "build" / "obj").glob("hip_step.hip.part*.o") if o.name != "hip_step.hip.part0.o")
     if not objs:
         pytest.skip("no step.hip objects in build/obj (library built elsewhere)")
     r = subprocess.run(["bash", str(ROOT / "scripts" / "disasm.sh"), *map(str, objs)], capture_output=True, text=True,
