@@ -1448,8 +1448,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // qpos / dof address, gear, ctrl limit flag and range, gain type and prm[3], bias type and prm[3],
   // force limit flag and range; per dof (16 floats) its single actuator (-1 none, -2 several: the
   // actuator loop runs), that actuator's gear, the joint's actuator-force limit flag and range,
-  // joint type, stiffness, qpos address, qpos_spring, the dof's damping, body, subtree end and
-  // whether any body of the subtree has gravcomp
+  // joint type, stiffness, qpos address, qpos_spring, the dof's damping, body, subtree end,
+  // whether any body of the subtree has gravcomp and the dof's friction-loss row (-1 none)
   std::vector<float> actrec, dofrec;
   {
     auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
@@ -1462,6 +1462,10 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
                               static_cast<float>(m.actuator_forcerange[2 * a + 1]), 0.0f, 0.0f, 0.0f};
       actrec.insert(actrec.end(), r.begin(), r.end());
     }
+    // each dof's friction-loss row (its index in the friction rows, -1 none): the 16-lane register
+    // solvers index the friction rows by dof (step.hip constraints)
+    std::vector<int> fric_row(m.nv, -1);
+    for (size_t k = 0; k < fric.size(); ++k) fric_row[fric[k]] = static_cast<int>(k);
     for (int j = 0; j < m.nv; ++j) {
       int act = -1;
       float gear = 0;
@@ -1476,7 +1480,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
                               static_cast<float>(m.jnt_actfrcrange[2 * jid + 1]), fbits(m.jnt_type[jid]),
                               static_cast<float>(m.jnt_stiffness[jid]), fbits(m.jnt_qposadr[jid]),
                               static_cast<float>(m.qpos_spring[m.jnt_qposadr[jid]]), static_cast<float>(m.dof_damping[j]),
-                              fbits(b), fbits(subtree_end[b]), fbits(gc), 0.0f, 0.0f, 0.0f};
+                              fbits(b), fbits(subtree_end[b]), fbits(gc), fbits(fric_row[j]), 0.0f, 0.0f};
       dofrec.insert(dofrec.end(), r.begin(), r.end());
     }
   }

@@ -2745,17 +2745,22 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
 template <bool kUnit = false, int KR = 16>
 __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
                                              float myR, float myaref, float myb, float myfl, float qacc_s,
-                                             int lane, int mydof = -1) {
+                                             int lane, int mydof = -1, unsigned fmask = 0) {
   const LdsLayout& L = m.L;
   const int nv = m.nv;
+  // kUnit (dof friction-loss rows): row r is the unit vector of dof r, held in lane r (rows indexed by
+  // dof, the bit of fmask says whether dof r has a row; mydof is then the lane's row index in the
+  // efc order, for the row forces).  J_r x is then lane r's x -- a DPP broadcast or nothing, not a
+  // group reduction -- and the rows keep mj_makeConstraint's order (dof order).
+  const bool myrow = kUnit ? ((fmask >> lane) & 1u) != 0 : lane < nefc;
   // J and M^-1 J' columns per row in registers; row scalars (R, aref, b, bound, diagonal of A, force)
   // stay in the row's own lane and reach the other lanes by DPP row broadcasts when used
   float Jt[KR], MJt[KR];
-  if (lane >= nefc) { myR = 1; myaref = 0; myb = 0; myfl = 0; }
+  if (!myrow) { myR = 1; myaref = 0; myb = 0; myfl = 0; }
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
     if constexpr (kUnit)
-      Jt[r] = (r < nefc && lane == __float_as_int(rowb<r>(__int_as_float(mydof)))) ? 1.0f : 0.0f;
+      Jt[r] = (lane == r && ((fmask >> r) & 1u)) ? 1.0f : 0.0f;
     else
       Jt[r] = (r < nefc && lane < nv) ? J[r * nv + lane] : 0.0f;
     MJt[r] = Jt[r];
@@ -2792,7 +2797,9 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
   float myA = 1, myf = 0;  // lane r: A_rr = J_r M^-1 J_r' + R_r and the force of row r
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if (r < rmax) {
+    if constexpr (kUnit) {
+      if (lane == r) myA = MJt[r] + myR;  // (M^-1)_rr + R_r, in lane r itself
+    } else if (r < rmax) {
       const float a = gsum<16>(Jt[r] * MJt[r]) + rowb<r>(myR);
       if (lane == r) myA = a;
     }
@@ -2804,16 +2811,20 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
   if (!(m.disableflags & MRS_DSBL_WARMSTART)) {
     const float qw = lane < nv ? s[L.qacc_ws + lane] : 0.0f;
     float myjar = 0;
-    unroll<KR>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if (r < rmax) {
-        const float jr = gsum<16>(Jt[r] * qw);
-        if (lane == r) myjar = jr - myaref;
-      }
-    });
+    if constexpr (kUnit) {
+      myjar = qw - myaref;
+    } else {
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (r < rmax) {
+          const float jr = gsum<16>(Jt[r] * qw);
+          if (lane == r) myjar = jr - myaref;
+        }
+      });
+    }
     {
       const float D = 1.0f / myR;
-      myf = lane >= nefc ? 0.0f
+      myf = !myrow ? 0.0f
                          : (myfl > 0 ? (myjar <= -myR * myfl ? myfl : (myjar >= myR * myfl ? -myfl : -D * myjar))
                                      : (myjar < 0 ? -D * myjar : 0.0f));
     }
@@ -2823,13 +2834,17 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
       if (r < rmax) v += MJt[r] * rowb<r>(myf);
     });
     float cost = 0;
-    unroll<KR>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if (r < rmax) {
-        const float f = rowb<r>(myf);
-        cost += f * (0.5f * (gsum<16>(Jt[r] * v) + rowb<r>(myR) * f) + rowb<r>(myb));
-      }
-    });
+    if constexpr (kUnit) {
+      cost = gsum<16>(myrow ? myf * (0.5f * (v + myR * myf) + myb) : 0.0f);
+    } else {
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if (r < rmax) {
+          const float f = rowb<r>(myf);
+          cost += f * (0.5f * (gsum<16>(Jt[r] * v) + rowb<r>(myR) * f) + rowb<r>(myb));
+        }
+      });
+    }
     if (cost > 0) {
       myf = 0;
     } else {
@@ -2849,8 +2864,8 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
     float improvement = 0;
     unroll<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
-      if (r < rmax) {
-        const float res = gsum<16>(Jt[r] * qa) - bref[r] + bR[r] * f[r];
+      if (kUnit ? ((fmask >> r) & 1u) != 0 : r < rmax) {
+        const float res = (kUnit ? rowb<r>(qa) : gsum<16>(Jt[r] * qa)) - bref[r] + bR[r] * f[r];
         float nf = f[r] - res * iA[r];
         nf = bfl[r] > 0 ? clampf(nf, -bfl[r], bfl[r]) : (nf < 0 ? 0.0f : nf);
         const float delta = nf - f[r];
@@ -2866,12 +2881,17 @@ __device__ __forceinline__ float pgs_small16_qacc(const DevModel& m, lfloat* s, 
   float qc = 0;
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if (r < rmax) qc += Jt[r] * f[r];
+    if constexpr (kUnit) {
+      if (lane == r) qc = Jt[r] * f[r];
+    } else if (r < rmax) {
+      qc += Jt[r] * f[r];
+    }
+    if (lane == r) myf = f[r];
   });
   if (lane < nv) s[L.qfrc_con + lane] = qc;
-  // row forces (mj_rnePostConstraint's contact forces, mrs_batch_get_efc)
-  // (the friction-loss fast path stores them only when force/torque sensors read them)
-  if (ff && (!kUnit || (m.acc_sens & 2)) && lane < nefc) ff[lane] = myf;
+  // row forces (mj_rnePostConstraint's contact forces, mrs_batch_get_efc; kUnit: at the row's efc
+  // index, only when force/torque sensors read them)
+  if (ff && (!kUnit || (m.acc_sens & 2)) && myrow) ff[kUnit ? mydof : lane] = myf;
   return qa;
 }
 
@@ -4938,14 +4958,14 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
   ENV_UNPACK;
   const int nv = m.nv;
   const bool dof = lane < nv;
-  const bool row = lane < nefc;
+  const bool row = kUnit ? myfric : lane < nefc;
   if (!row) { myR = 1; myaref = 0; myfl = 0; myfric = false; }
   qs = dof ? qs : 0.0f;
   float Jt[KR];
   unroll<KR>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
     if constexpr (kUnit)
-      Jt[r] = (r < nefc && lane == __float_as_int(rowb<r>(__int_as_float(mydof)))) ? 1.0f : 0.0f;
+      Jt[r] = 0.0f;  // (unused: the unit rows' products are lane-local)
     else
       Jt[r] = (r < nefc && dof) ? J[r * nv + lane] : 0.0f;
   });
@@ -4955,11 +4975,15 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
   // lane r: J_r x (KR independent row reductions)
   auto rows_dot = [&](float x) {
     float out = 0;
-    unroll<KR>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      const float t = gsum<16>(Jt[r] * x);
-      if (lane == r) out = t;
-    });
+    if constexpr (kUnit) {
+      out = row ? x : 0.0f;
+    } else {
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        const float t = gsum<16>(Jt[r] * x);
+        if (lane == r) out = t;
+      });
+    }
     return out;
   };
   // lane j: (M x)_j, (J' f)_j
@@ -4973,10 +4997,14 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
   };
   auto jtmul = [&](float f) {
     float q = 0;
-    unroll<KR>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      q += Jt[r] * rowb<r>(f);
-    });
+    if constexpr (kUnit) {
+      q = row ? f : 0.0f;
+    } else {
+      unroll<KR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        q += Jt[r] * rowb<r>(f);
+      });
+    }
     return q;
   };
   float jar = 0, myf = 0;  // row lanes
@@ -5019,15 +5047,19 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
       float dj[KR];
       unroll<KR>([&](auto rc) {
         constexpr int r = decltype(rc)::value;
-        dj[r] = Jt[r] * rowb<r>(Dr);
+        dj[r] = kUnit ? 0.0f : Jt[r] * rowb<r>(Dr);
       });
       unroll<KV>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         float h = mrow(k);
-        unroll<KR>([&](auto rc) {
-          constexpr int r = decltype(rc)::value;
-          h += dj[r] * rowb<k>(Jt[r]);
-        });
+        if constexpr (kUnit) {
+          if (lane == k) h += Dr;  // J' D J of unit rows: diagonal
+        } else {
+          unroll<KR>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            h += dj[r] * rowb<k>(Jt[r]);
+          });
+        }
         if (dof && k < nv) H[lane * nv + k] = h;
       });
       wsync();
@@ -5117,7 +5149,7 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
     }
   }
   if (dof) s[L.qfrc_con + lane] = qfrc;
-  if (row && (!kUnit || (m.acc_sens & 2))) ff[lane] = myf;  // row forces (mj_rnePostConstraint, mrs_batch_get_efc)
+  if (row && (!kUnit || (m.acc_sens & 2))) ff[kUnit ? mydof : lane] = myf;  // row forces (mj_rnePostConstraint, mrs_batch_get_efc)
   if (lane == 0) s[L.niter] = __int_as_float(nit);
   wsync();
   return dof ? qa : 0.0f;
@@ -5176,36 +5208,38 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
     if ((kPrimal ? m.solver != MRS_SOL_PGS : m.solver == MRS_SOL_PGS) && ncon == 0 && nf > 0 && nf <= 16 &&
         m.xrows == 0 && !gany<G>(lim)) {
       if (lane == 0) scr[S.efc_n] = __int_as_float(-1);  // rows stay in registers
-      int mydof = -1;
+      // rows indexed by dof: lane j holds the friction-loss row of dof j, if it has one (its index in
+      // the efc order from the dof table, batch.hip dofrec[13]); the rows' order is the dof order,
+      // mj_makeConstraint's, and every group of the wave has the same rows (one model)
+      int myk = -1;
       float myR = 1, myaref = 0, myb = 0, myfl = 0;
-      if (lane < nf) {
-        // the row's model constants from workgroup LDS (batch.hip fricrec: dof, R, B, frictionloss)
-        const lfloat* fr = shared_lds(m) + m.shr_fric + 4 * lane;
-        const int j = __float_as_int(fr[0]);
-        mydof = j;
-        myR = fr[1];
-        myaref = -fr[2] * s[L.qvel + j];  // friction rows have no position term
-        myb = s[L.qacc_smooth + j] - myaref;
-        myfl = fr[3];
+      if (lane < nv) {
+        myk = __float_as_int(dof_tab<G>(m, lane)[13]);
+        if (myk >= 0) {
+          // the row's model constants from workgroup LDS (batch.hip fricrec: dof, R, B, frictionloss)
+          const lfloat* fr = shared_lds(m) + m.shr_fric + 4 * myk;
+          myR = fr[1];
+          myaref = -fr[2] * s[L.qvel + lane];  // friction rows have no position term
+          myb = s[L.qacc_smooth + lane] - myaref;
+          myfl = fr[3];
+        }
       }
+      const unsigned fmask = static_cast<unsigned>(__ballot(myk >= 0)) & 0xffffu;
       float qa;
       if constexpr (kPrimal) {
         // Newton / CG (MuJoCo's default solver): the register-resident primal form on the same rows
         const bool newton = m.solver == MRS_SOL_NEWTON;
-        if (nf <= 4 && m.nv <= 8)
-          qa = primal_small16<true, 4, 8>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, lane < nf, qacc_s, newton, mydof);
-        else if (nf <= 8 && m.nv <= 8)
-          qa = primal_small16<true, 8, 8>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, lane < nf, qacc_s, newton, mydof);
+        if (m.nv <= 8)
+          qa = primal_small16<true, 8, 8>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, myk >= 0, qacc_s, newton, myk);
         else
-          qa = primal_small16<true, 16, 16>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, lane < nf, qacc_s, newton, mydof);
+          qa = primal_small16<true, 16, 16>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, myk >= 0, qacc_s, newton, myk);
         return qa;
       }
-      // rows (and the dofs they touch) unrolled to 8 when the model has at most 8 friction dofs:
-      // a quarter of the substitution code
-      if (nf <= 8 && m.nv <= 8)
-        qa = pgs_small16_qacc<true, 8>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+      // dofs unrolled to 8 when the model has at most 8: a quarter of the substitution code
+      if (m.nv <= 8)
+        qa = pgs_small16_qacc<true, 8>(m, s, nullptr, scr + S.efc_f, nf, 8, myR, myaref, myb, myfl, qacc_s, lane, myk, fmask);
       else
-        qa = pgs_small16_qacc<true, 16>(m, s, nullptr, scr + S.efc_f, nf, nf, myR, myaref, myb, myfl, qacc_s, lane, mydof);
+        qa = pgs_small16_qacc<true, 16>(m, s, nullptr, scr + S.efc_f, nf, 16, myR, myaref, myb, myfl, qacc_s, lane, myk, fmask);
       wsync();
       return qa;
     }
