@@ -5229,7 +5229,10 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
       if constexpr (kPrimal) {
         // Newton / CG (MuJoCo's default solver): the register-resident primal form on the same rows
         const bool newton = m.solver == MRS_SOL_NEWTON;
-        if (m.nv <= 8)
+        // (dofs unrolled to the model's size class: the reference's 2-DoF scene runs the 4-wide form)
+        if (m.nv <= 4)
+          qa = primal_small16<true, 4, 4>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, myk >= 0, qacc_s, newton, myk);
+        else if (m.nv <= 8)
           qa = primal_small16<true, 8, 8>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, myk >= 0, qacc_s, newton, myk);
         else
           qa = primal_small16<true, 16, 16>(ENV_ARGS, nullptr, scr + S.efc_f, nf, myR, myaref, myfl, myk >= 0, qacc_s, newton, myk);

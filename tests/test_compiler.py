@@ -275,3 +275,42 @@ def test_equality_parse():
                 '<flex/>']:
         with pytest.raises(sim.MrsError):
             sim.Model.from_string(xml.replace('<joint joint1="jb" joint2="ja" polycoef="0.1 2"/>', bad))
+
+
+def test_rendering_assets_compile():
+    """lights (world-fixed, flattened to world pos / dir), materials with builtin textures, the
+    headlight and each geom's material id (mjModel light_* / tex_* / mat_* / geom_matid)"""
+    xml = """<mujoco><visual><headlight ambient="0.2 0.2 0.2" active="1"/></visual><asset>
+      <texture name="sky" type="skybox" builtin="gradient" rgb1="1 1 1" rgb2="0 0 0" width="8" height="8"/>
+      <texture name="grid" type="2d" builtin="checker" mark="cross" rgb1="0.1 0.2 0.3" rgb2="0.4 0.5 0.6"
+               markrgb="1 0 0" width="10" height="10"/>
+      <material name="m" texture="grid" texrepeat="2 3" texuniform="true" specular="0.3" shininess="0.7" emission="0.1"/>
+      </asset><worldbody>
+      <body pos="1 0 0" euler="0 0 90"><light pos="0 0 2" dir="1 0 -1" directional="true" castshadow="false"/></body>
+      <geom type="plane" size="0 0 1" material="m"/><geom type="sphere" size="0.1" pos="0 0 1"/>
+      </worldbody></mujoco>"""
+    m = sim.Model.from_string(xml)
+    assert (m.nlight, m.ntex, m.nmat) == (1, 2, 1)
+    np.testing.assert_allclose(m.vis_headlight[:3], 0.2)
+    np.testing.assert_allclose(m.light_pos[0], [1, 0, 2], atol=1e-12)  # world-welded body frame applied
+    np.testing.assert_allclose(m.light_dir[0], np.array([0, 1, -1]) / np.sqrt(2), atol=1e-12)
+    assert m.light_directional[0] == 1 and m.light_castshadow[0] == 0
+    assert list(m.tex_type) == [sim.TEX_SKYBOX, sim.TEX_2D]
+    assert list(m.geom_matid) == [0, -1]
+    np.testing.assert_allclose(m.mat_texrepeat[0], [2, 3])
+    assert m.mat_texid[0] == 1 and m.mat_texuniform[0] == 1
+
+
+@pytest.mark.parametrize("body, msg", [
+    ('<body><freejoint/><light pos="0 0 1"/><geom size="0.1"/></body>', "lights on moving bodies"),
+    ("".join('<light pos="0 0 %d"/>' % k for k in range(9)), "at most 8 lights"),
+])
+def test_rendering_rejects(body, msg):
+    with pytest.raises(sim.MrsError, match=msg):
+        sim.Model.from_string(f"<mujoco><worldbody>{body}</worldbody></mujoco>")
+
+
+def test_file_texture_rejected():
+    xml = '<mujoco><asset><texture name="t" type="2d" file="wood.png"/></asset><worldbody/></mujoco>'
+    with pytest.raises(sim.MrsError):
+        sim.Model.from_string(xml)
