@@ -41,12 +41,6 @@ namespace {
 // (src/mujoco_cameras.cpp:222-235) produce; rows in ROS order (flip of :229-240 applied).
 constexpr int kMaxRenderGeoms = 256;
 // the model's meshes for the render kernels (mrs_model.h mesh arrays, device copies)
-// depth_kernel_v2's candidate order (MRS_DEPTH_ORDER=1: nearest-first with early exit; default index
-// order)
-inline int depth_order() {
-  const char* e = std::getenv("MRS_DEPTH_ORDER");
-  return e ? std::atoi(e) : 0;
-}
 struct MeshRef {
   const float* vert;
   const int *face, *dataid, *vertadr, *faceadr, *facenum;
@@ -477,8 +471,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                                                        const float* geom_xpos, const float* geom_xmat,
                                                        const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
                                                        int env0, int W, int H, float f, float znear, float zfar,
-                                                       float* out, unsigned char* rgb, MeshRef mesh, LitRef lr,
-                                                       int order) {
+                                                       float* out, unsigned char* rgb, MeshRef mesh, LitRef lr) {
   __shared__ DepthGeom G[kDepthGeoms];
   __shared__ LitFrame LF;
   const int env = env0 + blockIdx.x;
@@ -499,7 +492,6 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
     const float y1 = (0.5f * H - ty * kDepthTileH - 0.5f) / f;
     const float y0 = (0.5f * H - fminf(ty * kDepthTileH + kDepthTileH - 1.0f, H - 1.0f) - 0.5f) / f;
     bool keep = false;
-    int zlo = 0;  // (order) lower bound of the geom's eye depth, float bits >= 0: its hits have t >= zlo
     if (lane < ngeom && G[lane].vis) {
       const DepthGeom& o = G[lane];
       if (o.type == MRS_GEOM_PLANE) {
@@ -508,11 +500,6 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         const float bx = fminf(x0 * n[0], x1 * n[0]), by = fminf(y0 * n[1], y1 * n[1]);
         keep = bx + by - n[2] < 1e-6f;
       } else {
-        if (order) {
-          float rz = 0;
-          for (int i = 0; i < 3; ++i) rz += o.ext[i] * fabsf(o.A[3 * i + 2]);
-          zlo = __float_as_int(fmaxf(0.0f, (-o.cc[2] - rz) * (1 - 1e-5f)));
-        }
         // oriented box vs the four side planes n.p >= 0 of the tile pyramid (unnormalised normals:
         // left (1, 0, x0), right (-1, 0, -x1), bottom (0, 1, y0), top (0, -1, -y1))
         auto outside = [&](float nx, float ny, float nz) {
@@ -536,24 +523,9 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       bestg[k] = 0;
       dy[k] = (0.5f * H - (ty * kDepthTileH + k) - 0.5f) / f;
     }
-    // (order, MRS_DEPTH_ORDER=1) candidates nearest-first by their eye-depth bound (planes first, at
-    // 0), picked by a scalar scan of the bounds (readlane); once every pixel of the tile holds a hit
-    // nearer than the next bound (one ballot), no remaining candidate can take a pixel.  Ties of t
-    // keep the lower geom index, so frames are bit-identical to the index order.
     while (cand) {
-      int g = __builtin_ctzll(cand);
-      if (order) {
-        int kb = __builtin_amdgcn_readlane(zlo, g);
-        for (unsigned long long rem = cand & (cand - 1); rem; rem &= rem - 1) {
-          const int h = __builtin_ctzll(rem), kh = __builtin_amdgcn_readlane(zlo, h);
-          if (kh < kb) { kb = kh; g = h; }
-        }
-        float far = 0;
-#pragma unroll
-        for (int k = 0; k < kDepthTileH; ++k) far = fmaxf(far, best[k] < 0 ? 3.0e38f : best[k]);
-        if (__all(far < __int_as_float(kb))) break;
-      }
-      cand &= ~(1ull << g);
+      const int g = __builtin_ctzll(cand);
+      cand &= cand - 1;
       const DepthGeom& o = G[g];
       const float lp[3] = {o.lp[0], o.lp[1], o.lp[2]}, sz[3] = {o.size[0], o.size[1], o.size[2]};
       float A[9];
@@ -572,10 +544,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
                        mesh.bvh + 8 * mesh.bvhadr[o.dataid], mesh.bvhnum[o.dataid], &tri);
         }
         else t = ray_prim(type, sz, lp, lv);
-        if (t >= znear && (best[k] < 0 || t < best[k] || (order && t == best[k] && g < bestg[k]))) {
-          best[k] = t;
-          bestg[k] = g;
-        }
+        if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
     }
     if (col < W) {
@@ -2207,7 +2176,7 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
     hipLaunchKernelGGL(drgb ? depth_kernel_v2<true> : depth_kernel_v2<false>, dim3(n), dim3(256), 0, stream,
                        d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
-                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr, depth_order());
+                       cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr);
   } else {
     dim3 grid(((W + 15) / 16) * ((H + 15) / 16), n);
     hipLaunchKernelGGL(drgb ? depth_kernel<true> : depth_kernel<false>, grid, dim3(256), 0, stream, d.geom_type.p,

@@ -944,26 +944,3 @@ def test_c2_bench_variant():
             assert err <= RTOL, (e, err)
 
 
-
-def test_depth_order_bit_identical(monkeypatch):
-    """depth_kernel_v2's nearest-first candidate order with early exit (MRS_DEPTH_ORDER=1) gives the
-    same depth and colour frames, bit for bit, as the index order on the C4 room after the base has
-    driven around (ties of t keep the lower geom index in both)"""
-    from conftest import ROOT
-    model = sim.Model.load(ROOT / "scenes" / "mobile_base.xml")
-    n = 32
-    envs = np.arange(n)
-    b = sim.Batch(model, n)
-    b.set(sim.FIELD_QPOS, synth.initial_qpos(model, envs))
-    table = synth.ctrl_table(model, envs, 30, 10)
-    for p in range(30):
-        b.set(sim.FIELD_CTRL, table[p])
-        b.step(10)
-    out = []
-    for order in ("1", "0"):
-        monkeypatch.setenv("MRS_DEPTH_ORDER", order)
-        out.append(b.render_rgbd(0, 0, n))
-    b.close()
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    assert (out[0][0] < out[0][0].max()).mean() > 0.3
