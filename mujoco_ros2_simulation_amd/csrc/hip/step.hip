@@ -3671,21 +3671,13 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
           fr[j] = act ? sc.y : 0.0f;                           // R, folded into the diagonal below
           hisl[j] = act ? __float_as_int(o[P]) : -1;
         });
-        // AR[j][l] = Y_(16j+slot) . Y_l: each level's Y (lane = slot) read once and broadcast slot
-        // by slot into the FMAs of the three held rows.  The level loads run kPre levels ahead
-        // (a rotating register buffer): one at a time, each level waited a full L2 round trip
-        constexpr int kPre = 8;
-        float ypre[kPre];
-        unroll<kPre>([&](auto pc) {
-          constexpr int q = decltype(pc)::value;
-          ypre[q] = q < nlev && q < my_n ? rec[(my_start + q) * RF + slot] : 0.0f;
-        });
+        // AR[j][l] = Y_(16j+slot) . Y_l.  Level l's Y is already in registers: it is held row l / 16
+        // of lane l % 16 (Jt, zero past the pipe's rows), so slot q of it is one DPP row broadcast of
+        // Jt[l / 16][q] from that lane, folded into the FMAs of the three held rows -- the records are
+        // read once here, not again per level
         unroll<NL>([&](auto lc) {
           constexpr int l = decltype(lc)::value;
           unroll<NJ>([&](auto jc) { ARn[decltype(jc)::value][l] = 0.0f; });
-          const float mj = ypre[l % kPre];
-          if constexpr (l + kPre < NL)
-            ypre[l % kPre] = l + kPre < nlev && l + kPre < my_n ? rec[(my_start + l + kPre) * RF + slot] : 0.0f;
           if (l < nlev) {
             const int il = __float_as_int(rowb<l % 16>(__int_as_float(hisl[l / 16])));
             unroll<NJ>([&](auto jc) {
@@ -3693,8 +3685,8 @@ __device__ float constraints_sparse(ENV_PARAMS, int ncon, float qacc_s) {
               float a0 = 0, a1 = 0;
               unroll<16>([&](auto sc) {
                 constexpr int q = decltype(sc)::value;
-                if constexpr (q & 1) a1 += Jt[j][q] * rowb<q>(mj);
-                else a0 += Jt[j][q] * rowb<q>(mj);
+                if constexpr (q & 1) a1 += Jt[j][q] * rowb<l % 16>(Jt[l / 16][q]);
+                else a0 += Jt[j][q] * rowb<l % 16>(Jt[l / 16][q]);
               });
               float a = a0 + a1;
               const bool diag = l / 16 == j && slot == l % 16;
