@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for e in ${ENVS:--}; do
-  tag=$(echo "$e" | tr '=,' '__')
+  tag=$(echo "$e" | tr '=,/' '___')
   if [ "$e" = "-" ]; then envset=""; else envset=$(echo "$e" | tr ',' ' '); fi
   env $envset timeout -k 10 200 python bench.py --config $CFG --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_${CFG}_$tag.json 2> gpurun_out/ab_${CFG}_$tag.err || exit $?
   python -c "import json; d=json.load(open('gpurun_out/ab_${CFG}_$tag.json')); r=d['roofline']; print('$CFG', '$e', round(d['value']/1e6,3), 'M', round(r['kernel_ms'],4), r.get('step_kernel_ms'))"

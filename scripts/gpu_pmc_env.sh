@@ -6,7 +6,7 @@ set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for e in ${ENVS:--}; do
-  tag=$(echo "$e" | tr '=,' '__')
+  tag=$(echo "$e" | tr '=,/' '___')
   if [ "$e" = "-" ]; then envset=""; else envset=$(echo "$e" | tr ',' ' '); fi
   for c in fetch write; do
     C=$(echo $c | tr a-z A-Z)_SIZE
