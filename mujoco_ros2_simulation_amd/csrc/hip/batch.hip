@@ -862,6 +862,7 @@ struct BatchImpl {
   int n = 0, device = 0;
   int group = 64;  // lanes per environment in the step kernel (64/group envs per wavefront)
   int g16_one_wg = 0;  // G = 16 with one workgroup per CU (tables past the two-per-CU budget)
+  int wpb16 = WavesPerBlock<16>::value;  // waves per workgroup of the G = 16 kernels (DevState::wpb16)
   DevModel dm{};
   DevModel* d_dm = nullptr;  // device copy of dm
   LdsLayout& L = dm.L;
@@ -1837,6 +1838,22 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     const int g = std::atoi(e);
     if ((g == 8 || g == 16 || g == 32 || g == 64) && m.nv <= g) b.group = g;
   }
+  // G = 16 with fewer waves than the device has SIMDs (C4: 2048 envs = 512 waves on 1024 SIMDs):
+  // one-wave workgroups, so the waves spread over every CU instead of filling half of them four to
+  // a CU (measured C4: 0.802 vs 0.822 ms per launch; C3 and C2 have a wave per SIMD or more and keep
+  // four-wave workgroups -- C3's LDS tables per workgroup would cost it residency).  MRS_G16_WPB
+  // overrides (1, 2 or 4)
+  b.wpb16 = WavesPerBlock<16>::value;
+  if (b.group == 16 && !b.g16_one_wg) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b.device) != hipSuccess) cus = 0;
+    const long waves = (static_cast<long>(b.n) * 16 + 63) / 64;
+    if (cus > 0 && waves < 4L * cus) b.wpb16 = 1;
+    if (const char* e = std::getenv("MRS_G16_WPB")) {
+      const int w = std::atoi(e);
+      if (w == 1 || w == 2 || w == 4) b.wpb16 = std::min(w, static_cast<int>(WavesPerBlock<16>::value));
+    }
+  }
   d.blocked = b.group == 64 ? 1 : 0;
   if (b.group == 64) d.shr_total = shr_small;
   // extended step kernels (step.hip MRS_EXT) for models with general convex (MPR) pairs -- a pair
@@ -1850,7 +1867,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
 
   if (d.blocked) lds_layout(true);
-  d.shr_off = L.total * envs_per_block(b.group);
+  d.shr_off = L.total * envs_per_block(b.group, b.wpb16);
   if ((static_cast<size_t>(d.shr_off) + d.shr_total) * sizeof(float) > 160 * 1024)
     throw UnsupportedError("model too large for the per-environment LDS working set");
   // --- scratch layout (floats).  Dense mode: rows J and M^-1 J' as nefc x nv plus per-row scalars;
@@ -1942,7 +1959,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     b->st.ncon = static_cast<int*>(dalloc(*b, n * sizeof(int)));
     b->st.niter = static_cast<int*>(dalloc(*b, n * sizeof(int)));
     // padded to whole workgroups of the chosen group width: idle groups use it
-    const size_t epb = static_cast<size_t>(envs_per_block(b->group));
+    const size_t epb = static_cast<size_t>(envs_per_block(b->group, b->wpb16));
     const size_t n_pad = (static_cast<size_t>(n) + epb - 1) / epb * epb;
     // env spread (opt-in, MRS_SPREAD=<shift>): 2^shift lane groups per env, the extra ones mirroring
     // the first, so a small batch occupies more waves.  Measured slower (round 5, same box: C4 18.2
@@ -1952,6 +1969,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     if (const char* e = std::getenv("MRS_SPREAD")) shift = std::max(0, std::min(3, std::atoi(e)));
     const size_t n_virt = ((static_cast<size_t>(n) << shift) + epb - 1) / epb * epb;
     b->st.spread_shift = shift;
+    b->st.wpb16 = b->wpb16;
     b->st.scr_mirror = static_cast<int>(n_pad);
     b->st.scratch = static_cast<float*>(dalloc(*b, (n_pad + (shift ? n_virt : 0)) * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));

@@ -205,11 +205,12 @@ template <int G>
 #define MRS_G16_WAVES 4
 #endif
 struct WavesPerBlock { static constexpr int value = G == 64 ? 1 : (G == 16 ? MRS_G16_WAVES : 4); };
-// environments per workgroup of the step kernel at group width g (kEnvsPerBlock)
-inline int envs_per_block(int g) {
+// environments per workgroup of the step kernel at group width g (kEnvsPerBlock); G = 16 kernels
+// take their waves per workgroup at run time (DevState::wpb16, at most WavesPerBlock<16>)
+inline int envs_per_block(int g, int wpb16 = WavesPerBlock<16>::value) {
   switch (g) {
     case 8: return WavesPerBlock<8>::value * 8;
-    case 16: return WavesPerBlock<16>::value * 4;
+    case 16: return wpb16 * 4;
     case 32: return WavesPerBlock<32>::value * 2;
     default: return WavesPerBlock<64>::value;
   }
@@ -231,6 +232,9 @@ struct DevState {
   // (primary) writes the results, the others mirror it in their own scratch (slot scr_mirror + group);
   // a batch of few envs then spreads over more waves / SIMDs.  0 = one group per env.
   int spread_shift, scr_mirror;
+  // waves per workgroup of the G = 16 kernels (1 .. WavesPerBlock<16>): one-wave workgroups when the
+  // batch has fewer waves than the device has SIMDs, so they spread over every CU (batch_create)
+  int wpb16;
 };
 
 }  // namespace mrs

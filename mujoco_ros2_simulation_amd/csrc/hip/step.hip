@@ -6805,6 +6805,8 @@ __device__ void integrate_implicit(ENV_PARAMS) {
     if (lane == 0) s[L.qvel + j] = vj;
     if (lane < nv && j >= ta && j < ta + tn) s[L.M + midx<G>(m, lane, j)] += h * (0.5f * (bias[0] - bias[1]));
   }
+  // (the velocity-stage LDS fields -- cvel, cdofdot, cacc, cfrc / crb, qfrc_bias -- are left at the
+  // last perturbed velocity; nothing reads them before the next step's forward() recomputes them)
   wsync();
   auto from = [&](float v, int src) {  // the value of lane src of this env's group
     if constexpr (G == 64) return __shfl(v, src);
@@ -6917,7 +6919,7 @@ template <int G, bool kForwardOnly, bool kPrimal = false>
 __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
+  const int kEnvsPerBlock = G == 16 ? 4 * st.wpb16 : WavesPerBlock<G>::value * 64 / G;
   const DevModel& m = *mp;
   const LdsLayout& L = m.L;
   const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
@@ -7108,25 +7110,26 @@ constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelAll = 7;
 template <int G, int kSel = kSelAll>
 static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
                      int n_steps, bool forward_only, bool primal, hipStream_t stream) {
-  constexpr int kEnvsPerBlock = WavesPerBlock<G>::value * 64 / G;
+  const int wpb = G == 16 ? st.wpb16 : WavesPerBlock<G>::value;
+  const int kEnvsPerBlock = wpb * 64 / G;
   const int blocks = ((n_envs << st.spread_shift) + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
   if constexpr (G == 16 && (kSel & kSelPrimal)) {
     if (primal && !forward_only) {
-      hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st,
+      hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * wpb), lds, stream, d_model, st,
                          n_envs, n_steps);
       return;
     }
   }
   if constexpr ((kSel & kSelForward) != 0) {
     if (forward_only) {
-      hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs, 1);
+      hipLaunchKernelGGL((step_kernel<G, true>), dim3(blocks), dim3(64 * wpb), lds, stream, d_model, st, n_envs, 1);
       return;
     }
   }
   if constexpr ((kSel & kSelStep) != 0) {
     if (!forward_only)
-      hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * WavesPerBlock<G>::value), lds, stream, d_model, st, n_envs,
+      hipLaunchKernelGGL((step_kernel<G, false>), dim3(blocks), dim3(64 * wpb), lds, stream, d_model, st, n_envs,
                          n_steps);
   }
 }
