@@ -21,9 +21,9 @@ HIP_SOURCES = ["hip/step.hip", "hip/batch.hip"]
 # step.hip is compiled once per part (-DMRS_STEP_PART=n), in parallel: part 0 is the dispatcher, the
 # others each instantiate one group width's kernels (17: the G = 16 primal-solver kernel; 18 / 65: the
 # G = 16 / 64 kernels with the extended code, MRS_EXT -- MPR contact polish, > 32 ray geoms -- which
-# parts 16, 17 and 64 leave out)
-STEP_PARTS = [0, 8, 16, 17, 18, 32, 64, 65]
-STEP_NO_EXT = {16, 17, 64}
+# parts 16, 17, 19 and 64 leave out; 19: the G = 16 step kernels with ray helper waves)
+STEP_PARTS = [0, 8, 16, 17, 18, 19, 32, 64, 65]
+STEP_NO_EXT = {16, 17, 19, 64}
 # fp32 division/sqrt via v_rcp/v_sqrt (<= 2.5 ulp) instead of the correctly-rounded sequences:
 # the parity tolerance is 1e-5 relative, and the ray/contact math is division-heavy
 HIP_FLAGS = ["-fno-hip-fp32-correctly-rounded-divide-sqrt"]

@@ -1970,6 +1970,17 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     const size_t n_virt = ((static_cast<size_t>(n) << shift) + epb - 1) / epb * epb;
     b->st.spread_shift = shift;
     b->st.wpb16 = b->wpb16;
+    // ray helper waves: with one-wave workgroups (fewer waves than SIMDs, so the helpers take SIMDs
+    // that would idle) every physics wave gets a second wave that traces its envs' rangefinders each
+    // step while it runs the dynamics (step_kernel); the <= 32-ray-geom pass without RK4 and without
+    // the extended kernels only.
+    // MRS_RAY_HELPERS=0 turns them off
+    {
+      const char* e = std::getenv("MRS_RAY_HELPERS");
+      const bool want = e ? std::atoi(e) != 0 : true;
+      b->st.ray_helpers = want && b->group == 16 && b->wpb16 == 1 && !b->ext && b->dm.nrf > 0 && b->dm.nrgeom <= 32 &&
+                          m.integrator != MRS_INT_RK4 && !(m.disableflags & MRS_DSBL_SENSOR) ? 1 : 0;
+    }
     b->st.scr_mirror = static_cast<int>(n_pad);
     b->st.scratch = static_cast<float*>(dalloc(*b, (n_pad + (shift ? n_virt : 0)) * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));

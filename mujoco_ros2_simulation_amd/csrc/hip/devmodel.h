@@ -235,6 +235,8 @@ struct DevState {
   // waves per workgroup of the G = 16 kernels (1 .. WavesPerBlock<16>): one-wave workgroups when the
   // batch has fewer waves than the device has SIMDs, so they spread over every CU (batch_create)
   int wpb16;
+  // 1: G = 16 step launches add a ray helper wave per physics wave (step_kernel; batch_create)
+  int ray_helpers;
 };
 
 }  // namespace mrs

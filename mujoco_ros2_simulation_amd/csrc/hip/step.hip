@@ -75,6 +75,14 @@ typedef __attribute__((address_space(1))) float gfloat;
     }                                              \
   } while (0)
 
+// workgroup barrier between a step kernel's physics waves and their ray helper waves, which share
+// only LDS (the helpers read the poses) and write disjoint sensordata words: the caller's LDS writes
+// complete (lgkmcnt), and with `drain` its global stores too (vmcnt: a helper's ray results land
+// before a physics wave's re-run of the step may overwrite them), then s_barrier
+__device__ __forceinline__ void helper_barrier(bool drain) {
+  if (drain) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -6313,7 +6321,7 @@ __device__ void rays_chunked(ENV_PARAMS, gfloat* sensordata) {
 // mj_sensorPos/Vel for the implemented sensor types; rangefinders lane-parallel within the group,
 // RayBatch<G> rays per lane per pass
 template <int G>
-__device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
+__device__ __forceinline__ void rays_pass(ENV_PARAMS, gfloat* sensordata) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   if (m.disableflags & MRS_DSBL_SENSOR) return;
@@ -6464,6 +6472,16 @@ __device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata) {
   else if (G < 64 && RayBatch<G>::value > 2 && m.nrf <= 2 * G) passes(std::integral_constant<int, 2>{});
   else passes(std::integral_constant<int, RayBatch<G>::value>{});
 #endif
+}
+
+// the step's sensors: the rangefinder passes (rays: 0 when the workgroup's ray helper waves take them,
+// step_kernel) and the other sensor types
+template <int G>
+__device__ MRS_PHASE void sensors(ENV_PARAMS, gfloat* sensordata, bool rays = true) {
+  ENV_UNPACK;
+  if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
+  if (m.disableflags & MRS_DSBL_SENSOR) return;
+  if (rays) rays_pass<G>(ENV_ARGS, sensordata);
   if (!MRS_SD_OK(sensordata)) return;
 #ifdef MRS_DIAG_NO_OTHER
   return;  // diagnostic build: rangefinders only
@@ -6591,11 +6609,14 @@ __device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
 
 // full forward pass; returns qacc (lane per dof)
 template <int G, bool kPrimal = false>
-__device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
+__device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bool helper = false) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   PH_BEGIN();
   MRS_CALL(G, kinematics<G>(ENV_ARGS));
+  // ray helper waves (step_kernel): the poses are in LDS -- release the helpers (barrier A); they
+  // trace this step's rays while the wave goes on, and nothing below writes what they read
+  if (helper) helper_barrier(false);
   PH_END(ph_acc, PH_KIN);
   MRS_CALL(G, com_pos<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COMPOS);
@@ -6625,7 +6646,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM) {
   // sensordata == nullptr: mj_forwardSkip(skipsensor) (the RK4 stages)
   if (sensordata) {
     if (m.acc_sens && !(m.disableflags & MRS_DSBL_SENSOR)) { [[clang::noinline]] rne_post<G>(ENV_ARGS, ncon); }
-    if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata));
+    if (!(m.diag_skip & 1)) MRS_CALL(G, sensors<G>(ENV_ARGS, sensordata, !helper));
   }
   PH_END(ph_acc, PH_SENS);
   return ncon;
@@ -6915,14 +6936,21 @@ template <int G>
 #endif
 struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
 
-template <int G, bool kForwardOnly, bool kPrimal = false>
+// kHelpers: the G = 16 step kernel with ray helper waves (DevState::ray_helpers; its own instantiation,
+// so the kernels without helpers keep their code and registers -- the run-time switch alone cost C3 5%)
+template <int G, bool kForwardOnly, bool kPrimal = false, bool kHelpers = false>
 __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int kEnvsPerBlock = G == 16 ? 4 * st.wpb16 : WavesPerBlock<G>::value * 64 / G;
   const DevModel& m = *mp;
   const LdsLayout& L = m.L;
-  const int lane = threadIdx.x & (G - 1), slot = threadIdx.x / G;
+  // ray helper waves (DevState::ray_helpers, G = 16 step launches): the workgroup's second half, wave
+  // w + wpb16 tracing the rangefinders of physics wave w's envs each step between two barriers
+  constexpr bool helpers = G == 16 && !kForwardOnly && kHelpers;
+  const bool is_helper = helpers && threadIdx.x >= 64 * st.wpb16;
+  const int tid = is_helper ? threadIdx.x - 64 * st.wpb16 : threadIdx.x;
+  const int lane = tid & (G - 1), slot = tid / G;
   // group -> env: with spread 2^k (DevState::spread_shift), 2^k consecutive groups step one env and
   // only the first writes back (the others mirror it: same state, same arithmetic, own scratch), so
   // a small batch occupies 2^k times the waves (C4's 2048 envs: 512 waves on 1024 SIMDs otherwise)
@@ -6936,15 +6964,15 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
   gfloat* scr = (gfloat*)(st.scratch + (size_t)(valid || st.spread_shift == 0 ? env : st.scr_mirror + vgroup) * m.S.total);
   const size_t e = (size_t)(env < n_envs ? env : n_envs - 1);
   #pragma unroll 1
-  for (int i = lane; i < m.nq; i += G) s[L.qpos + i] = st.qpos[e * m.nq + i];
+  for (int i = lane; i < (is_helper ? 0 : m.nq); i += G) s[L.qpos + i] = st.qpos[e * m.nq + i];
   #pragma unroll 1
-  for (int i = lane; i < m.nv; i += G) {
+  for (int i = lane; i < (is_helper ? 0 : m.nv); i += G) {
     s[L.qvel + i] = st.qvel[e * m.nv + i];
     s[L.qfrc_applied + i] = st.qfrc_applied[e * m.nv + i];
     s[L.qacc_ws + i] = st.qacc_ws[e * m.nv + i];
   }
   #pragma unroll 1
-  for (int i = lane; i < m.nu; i += G) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
+  for (int i = lane; i < (is_helper ? 0 : m.nu); i += G) s[L.ctrl + i] = st.ctrl[e * m.nu + i];
   if constexpr (G == 64) {
     #pragma unroll 1
     for (int t = lane; t < m.ntree; t += G) {
@@ -6995,6 +7023,17 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
   }
   __syncthreads();
   wsync();
+  if (is_helper) {
+    // barrier A (the physics wave's poses are in LDS), the rays, barrier B (results stored); the
+    // physics waves pass A and B exactly once per step (forward() after kinematics, then below)
+    #pragma unroll 1
+    for (int step = 0; step < n_steps; ++step) {
+      helper_barrier(false);
+      MRS_CALL(G, rays_pass<G>(ENV_ARGS, sensordata));
+      helper_barrier(true);
+    }
+    return;
+  }
   int ncon = 0;
   int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
 #ifdef MRS_PHASE_TIMING
@@ -7017,7 +7056,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 #else
     gfloat* sd_step = sensordata;
 #endif
-    MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG)));
+    MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG, helpers)));
+    if (helpers) helper_barrier(false);  // barrier B: this step's rays are stored
 #if MRS_EXT
     // rangefinders of a model with more than 32 ray geoms (sensors() leaves them to this call)
     if (m.nrgeom > 32 && m.nrf > 0 && !(m.disableflags & MRS_DSBL_SENSOR))
@@ -7105,7 +7145,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 }  // namespace
 
 // kernel selection bits of launch_g (the split build compiles each part in its own translation unit)
-constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelAll = 7;
+constexpr int kSelForward = 1, kSelStep = 2, kSelPrimal = 4, kSelHelpers = 8, kSelAll = 15;
 
 template <int G, int kSel = kSelAll>
 static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats, const DevState& st, int n_envs,
@@ -7114,6 +7154,18 @@ static void launch_g(const DevModel* d_model, int lds_floats, int shared_floats,
   const int kEnvsPerBlock = wpb * 64 / G;
   const int blocks = ((n_envs << st.spread_shift) + kEnvsPerBlock - 1) / kEnvsPerBlock;
   const size_t lds = sizeof(float) * ((size_t)lds_floats * kEnvsPerBlock + shared_floats);
+  if constexpr (G == 16 && (kSel & kSelHelpers)) {
+    // step launches with ray helper waves: twice the waves per workgroup
+    if (st.ray_helpers && !forward_only) {
+      if (primal)
+        hipLaunchKernelGGL((step_kernel<G, false, true, true>), dim3(blocks), dim3(128 * wpb), lds, stream, d_model, st,
+                           n_envs, n_steps);
+      else
+        hipLaunchKernelGGL((step_kernel<G, false, false, true>), dim3(blocks), dim3(128 * wpb), lds, stream, d_model, st,
+                           n_envs, n_steps);
+      return;
+    }
+  }
   if constexpr (G == 16 && (kSel & kSelPrimal)) {
     if (primal && !forward_only) {
       hipLaunchKernelGGL((step_kernel<G, false, true>), dim3(blocks), dim3(64 * wpb), lds, stream, d_model, st,
@@ -7183,6 +7235,7 @@ void launch_part_8(MRS_LAUNCH_ARGS);
 void launch_part_16(MRS_LAUNCH_ARGS);
 void launch_part_17(MRS_LAUNCH_ARGS);
 void launch_part_18(MRS_LAUNCH_ARGS);
+void launch_part_19(MRS_LAUNCH_ARGS);
 void launch_part_32(MRS_LAUNCH_ARGS);
 void launch_part_64(MRS_LAUNCH_ARGS);
 void launch_part_65(MRS_LAUNCH_ARGS);
@@ -7193,6 +7246,7 @@ hipError_t launch_step(const DevModel* d_model, int lds_floats, int shared_float
     case 8: launch_part_8(MRS_LAUNCH_PASS); break;
     case 16:
       if (ext) launch_part_18(MRS_LAUNCH_PASS);
+      else if (st.ray_helpers && !forward_only) launch_part_19(MRS_LAUNCH_PASS);
       else if (primal && !forward_only) launch_part_17(MRS_LAUNCH_PASS);
       else launch_part_16(MRS_LAUNCH_PASS);
       break;
@@ -7210,7 +7264,10 @@ void launch_part_16(MRS_LAUNCH_ARGS) { launch_g<16, kSelForward | kSelStep>(MRS_
 #elif MRS_STEP_PART == 17
 void launch_part_17(MRS_LAUNCH_ARGS) { launch_g<16, kSelPrimal>(MRS_LAUNCH_PASS); }
 #elif MRS_STEP_PART == 18
-void launch_part_18(MRS_LAUNCH_ARGS) { launch_g<16>(MRS_LAUNCH_PASS); }
+void launch_part_18(MRS_LAUNCH_ARGS) { launch_g<16, kSelForward | kSelStep | kSelPrimal>(MRS_LAUNCH_PASS); }
+#elif MRS_STEP_PART == 19
+// G = 16 step kernels (PGS and primal) with ray helper waves, without the extended code
+void launch_part_19(MRS_LAUNCH_ARGS) { launch_g<16, kSelHelpers>(MRS_LAUNCH_PASS); }
 #elif MRS_STEP_PART == 65
 void launch_part_65(MRS_LAUNCH_ARGS) { launch_g<64>(MRS_LAUNCH_PASS); }
 #else
