@@ -1753,6 +1753,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.act_force = take(std::max(1, m.nu));
     L.ten = d.ntendon > 0 ? take(2 * d.ntendon) : 0;  // tendon lengths and velocities of the step
     L.niter = take(1);
+    L.hcon = take(1);
     L.rfmask = take(std::max(1, d.nrfblk));
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
     L.dofb = blocked ? take(2 * nv) : 0;
@@ -1970,10 +1971,10 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     const size_t n_virt = ((static_cast<size_t>(n) << shift) + epb - 1) / epb * epb;
     b->st.spread_shift = shift;
     b->st.wpb16 = b->wpb16;
-    // ray helper waves: with one-wave workgroups (fewer waves than SIMDs, so the helpers take SIMDs
-    // that would idle) every physics wave gets a second wave that traces its envs' rangefinders each
-    // step while it runs the dynamics (step_kernel); the <= 32-ray-geom pass without RK4 and without
-    // the extended kernels only.
+    // helper waves: with one-wave workgroups (fewer waves than SIMDs, so the helpers take SIMDs that
+    // would idle) every physics wave gets a second wave that runs its envs' collision pass and traces
+    // their rangefinders each step while it runs the dynamics (step_kernel); models with
+    // rangefinders (<= 32 ray geoms) without RK4 and without the extended kernels only.
     // MRS_RAY_HELPERS=0 turns them off
     {
       const char* e = std::getenv("MRS_RAY_HELPERS");

@@ -47,7 +47,8 @@ struct LdsLayout {
       ten,     // fixed tendons: length and velocity per tendon of the step (smooth_forces)
       rk,      // RK4 models: the step's initial qpos [nq], then qvel [nv], stage velocity, B-weighted sums of
                // the stage velocities and accelerations [nv each]
-      niter;   // constraint solver iterations of the last forward (int bits)
+      niter,   // constraint solver iterations of the last forward (int bits)
+      hcon;    // ray helper waves: the step's contact count from the helper's collision pass (int bits)
   int total;  // floats per env (multiple of 4)
 };
 

@@ -6614,8 +6614,9 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   PH_BEGIN();
   MRS_CALL(G, kinematics<G>(ENV_ARGS));
-  // ray helper waves (step_kernel): the poses are in LDS -- release the helpers (barrier A); they
-  // trace this step's rays while the wave goes on, and nothing below writes what they read
+  // helper waves (step_kernel): the poses are in LDS -- release the helpers (barrier A); they run this
+  // step's collision pass and trace its rays while the wave goes on, and nothing below writes what
+  // they read
   if (helper) helper_barrier(false);
   PH_END(ph_acc, PH_KIN);
   MRS_CALL(G, com_pos<G>(ENV_ARGS));
@@ -6632,7 +6633,14 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   MRS_CALL(G, qacc_s = smooth_forces<G>(ENV_ARGS));
   PH_END(ph_acc, PH_SMOOTH);
   int ncon = 0;
-  if (!(m.diag_skip & 2)) MRS_CALL(G, ncon = collision<G>(ENV_ARGS));
+  if (helper) {
+    // barrier C: the helper's contact records are stored (its collision pass ran beside the smooth
+    // dynamics above, which do not depend on it)
+    helper_barrier(false);
+    ncon = __float_as_int(s[L.hcon]);
+  } else if (!(m.diag_skip & 2)) {
+    MRS_CALL(G, ncon = collision<G>(ENV_ARGS));
+  }
   PH_END(ph_acc, PH_COLL);
   float qacc = qacc_s;
   if (lane == 0) {
@@ -7024,11 +7032,16 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
   __syncthreads();
   wsync();
   if (is_helper) {
-    // barrier A (the physics wave's poses are in LDS), the rays, barrier B (results stored); the
-    // physics waves pass A and B exactly once per step (forward() after kinematics, then below)
+    // barrier A (the physics wave's poses are in LDS), the collision pass, barrier C (contacts
+    // stored, their count in LDS), the rays, barrier B (results stored); the physics waves pass A, C
+    // and B exactly once per step (forward() after kinematics and before constraints, then below)
     #pragma unroll 1
     for (int step = 0; step < n_steps; ++step) {
       helper_barrier(false);
+      int nc = 0;
+      if (!(m.diag_skip & 2)) MRS_CALL(G, nc = collision<G>(ENV_ARGS));
+      if (lane == 0) s[L.hcon] = __int_as_float(nc);
+      helper_barrier(true);
       MRS_CALL(G, rays_pass<G>(ENV_ARGS, sensordata));
       helper_barrier(true);
     }
