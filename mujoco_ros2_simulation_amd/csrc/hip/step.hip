@@ -83,6 +83,9 @@ __device__ __forceinline__ void helper_barrier(bool drain) {
   if (drain) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+// the helper wave also builds the dense constraint rows when none of them reads what the smooth
+// dynamics compute (tendon rows read the step's tendon lengths from smooth_forces)
+__device__ __forceinline__ bool helper_rows(const DevModel& m) { return m.ntendon == 0; }
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -5216,10 +5219,12 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
 }
 
 template <int G, bool kPrimal = false>
-__device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s);
+__device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_nefc = -1);
+template <int G>
+__device__ int dense_rows(ENV_PARAMS, int ncon);
 
 template <int G, bool kPrimal = false>
-__device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
+__device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s, int pre_nefc = -1) {
   ENV_UNPACK;
   if constexpr (G == 64) {
     if (m.solver != MRS_SOL_PGS || m.cone == MRS_CONE_ELLIPTIC || m.xrows > 0) {
@@ -5308,30 +5313,28 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s) {
   // rows with contacts or active joint limits: the dense row path, out of line -- cold in C3's
   // steady state, and keeping it out of the inlined step loop keeps the hot code footprint small
   float qa;
-  [[clang::noinline]] qa = constraints_dense<G, kPrimal>(ENV_ARGS, ncon, qacc_s);
+  [[clang::noinline]] qa = constraints_dense<G, kPrimal>(ENV_ARGS, ncon, qacc_s, pre_nefc);
   return qa;
 }
 
 // dense constraint rows in the env's global scratch (J, M^-1 J', row scalars), then the
 // register-resident PGS (<= 16 rows on G = 16) or the row-serial PGS with wave reductions
-template <int G, bool kPrimal>
-__device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
+// mj_makeConstraint's rows into the env's scratch (dense J, type, pos, margin, friction-loss bound;
+// contact records' first-row index): equality, friction loss, limits, contacts; returns nefc (also
+// in scr[S.efc_n]).  Reads kinematics, com_pos (cdof, subtree coms) and, for tendon limits, the
+// step's tendon lengths (smooth_forces)
+template <int G>
+__device__ int dense_rows(ENV_PARAMS, int ncon) {
   ENV_UNPACK;
   if constexpr (G == 64) ncon = uniform_int(ncon);
   const int nv = m.nv;
   gfloat* J = scr + S.efc_J;
-  gfloat* MJ = scr + S.efc_MJ;
   gfloat* type = scr + S.efc_type;
   gfloat* pos = scr + S.efc_pos;
   gfloat* marg = scr + S.efc_margin;
   gfloat* floss = scr + S.efc_floss;
-  gfloat* Rr = scr + S.efc_R;
-  gfloat* aref = scr + S.efc_aref;
   gfloat* bb = scr + S.efc_b;
-  gfloat* ff = scr + S.efc_f;
-  gfloat* ARii = scr + S.efc_ARii;
   int nefc = 0;
-  unsigned long long t_sub = SUB_T();
   // solref/solimp/diagApprox per row are re-derived from (type, id) when computing impedance;
   // keep ids in a small per-row int array inside the type slot (type*65536 + id)
   // --- equality rows, first as mj_makeConstraint orders them (oracle.c equality_rows: connect and
@@ -5631,6 +5634,28 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s) {
   }
   if (lane == 0) scr[S.efc_n] = __int_as_float(nefc);
   wsync();
+  return nefc;
+}
+
+template <int G, bool kPrimal>
+__device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_nefc) {
+  ENV_UNPACK;
+  if constexpr (G == 64) ncon = uniform_int(ncon);
+  const int nv = m.nv;
+  gfloat* J = scr + S.efc_J;
+  gfloat* MJ = scr + S.efc_MJ;
+  gfloat* type = scr + S.efc_type;
+  gfloat* pos = scr + S.efc_pos;
+  gfloat* marg = scr + S.efc_margin;
+  gfloat* floss = scr + S.efc_floss;
+  gfloat* Rr = scr + S.efc_R;
+  gfloat* aref = scr + S.efc_aref;
+  gfloat* bb = scr + S.efc_b;
+  gfloat* ff = scr + S.efc_f;
+  gfloat* ARii = scr + S.efc_ARii;
+  unsigned long long t_sub = SUB_T();
+  // the rows (pre_nefc >= 0: already built by the workgroup's helper wave, step_kernel)
+  const int nefc = pre_nefc >= 0 ? pre_nefc : dense_rows<G>(ENV_ARGS, ncon);
   SUB_ADD(PH_CON_ROWS, t_sub);
   t_sub = SUB_T();
   if (nefc == 0) {
@@ -6624,6 +6649,10 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   MRS_CALL(G, make_M<G>(ENV_ARGS));
   PH_END(ph_acc, PH_MAKEM);
   MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
+  // helper waves: barrier D -- com_pos's cdof and subtree coms are in LDS, so the helper may build
+  // the constraint rows after its collision pass (placed after the factor so that the helper's
+  // collision pass has run by then)
+  if (helper && helper_rows(m)) helper_barrier(false);
   PH_END(ph_acc, PH_CHOL);
   MRS_CALL(G, com_vel<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COMVEL);
@@ -6632,12 +6661,14 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   float qacc_s;
   MRS_CALL(G, qacc_s = smooth_forces<G>(ENV_ARGS));
   PH_END(ph_acc, PH_SMOOTH);
-  int ncon = 0;
+  int ncon = 0, pre_nefc = -1;
   if (helper) {
-    // barrier C: the helper's contact records are stored (its collision pass ran beside the smooth
-    // dynamics above, which do not depend on it)
+    // barrier C: the helper's contact records (and with helper_rows its constraint rows) are stored
+    // -- its collision pass and rows ran beside the smooth dynamics above, which need neither
     helper_barrier(false);
-    ncon = __float_as_int(s[L.hcon]);
+    const int hc = __float_as_int(s[L.hcon]);
+    ncon = hc & 0xffff;
+    pre_nefc = (hc >> 16) - 1;
   } else if (!(m.diag_skip & 2)) {
     MRS_CALL(G, ncon = collision<G>(ENV_ARGS));
   }
@@ -6645,9 +6676,10 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   float qacc = qacc_s;
   if (lane == 0) {
     s[L.niter] = __int_as_float(0);
-    scr[S.efc_n] = __int_as_float(0);  // no rows unless constraints() builds some (mrs_batch_get_efc)
+    // no rows unless constraints() builds some (mrs_batch_get_efc), or the helper's
+    scr[S.efc_n] = __int_as_float(pre_nefc >= 0 ? pre_nefc : 0);
   }
-  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = (constraints<G, kPrimal>(ENV_ARGS, ncon, qacc_s)));
+  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = (constraints<G, kPrimal>(ENV_ARGS, ncon, qacc_s, pre_nefc)));
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   wsync();
@@ -7035,12 +7067,18 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     // barrier A (the physics wave's poses are in LDS), the collision pass, barrier C (contacts
     // stored, their count in LDS), the rays, barrier B (results stored); the physics waves pass A, C
     // and B exactly once per step (forward() after kinematics and before constraints, then below)
+    // with helper_rows also barrier D (the physics wave's com_pos outputs are in LDS) and the dense
+    // constraint rows between D and C; their count goes to LDS with the contact count
     #pragma unroll 1
     for (int step = 0; step < n_steps; ++step) {
       helper_barrier(false);
-      int nc = 0;
+      int nc = 0, nr = -1;
       if (!(m.diag_skip & 2)) MRS_CALL(G, nc = collision<G>(ENV_ARGS));
-      if (lane == 0) s[L.hcon] = __int_as_float(nc);
+      if (helper_rows(m)) {
+        helper_barrier(false);
+        [[clang::noinline]] nr = dense_rows<G>(ENV_ARGS, nc);
+      }
+      if (lane == 0) s[L.hcon] = __int_as_float(nc + 65536 * (nr + 1));
       helper_barrier(true);
       MRS_CALL(G, rays_pass<G>(ENV_ARGS, sensordata));
       helper_barrier(true);
