@@ -863,6 +863,7 @@ struct BatchImpl {
   int group = 64;  // lanes per environment in the step kernel (64/group envs per wavefront)
   int g16_one_wg = 0;  // G = 16 with one workgroup per CU (tables past the two-per-CU budget)
   int wpb16 = WavesPerBlock<16>::value;  // waves per workgroup of the G = 16 kernels (DevState::wpb16)
+  int helpers = 0;  // helper waves (DevState::ray_helpers), decided with the layout (build_devmodel)
   DevModel dm{};
   DevModel* d_dm = nullptr;  // device copy of dm
   LdsLayout& L = dm.L;
@@ -1735,6 +1736,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   int off = 0;
   auto take = [&](int n) { int o = off; off += n; off = (off + 3) & ~3; return o; };
   const int nb = m.nbody, nj = std::max(1, m.njnt), nv = std::max(1, m.nv), ng = std::max(1, m.ngeom);
+  bool want_lh = false;  // the helper waves' integrator factor (set once the helpers are decided)
   auto lds_layout = [&](bool blocked) {
     off = 0;
     L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
@@ -1754,6 +1756,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     L.ten = d.ntendon > 0 ? take(2 * d.ntendon) : 0;  // tendon lengths and velocities of the step
     L.niter = take(1);
     L.hcon = take(1);
+    L.Lh = want_lh ? take(nv * nv) : 0;
     L.rfmask = take(std::max(1, d.nrfblk));
     L.trees = blocked ? take(4 * std::max(1, d.ntree)) : 0;
     L.dofb = blocked ? take(2 * nv) : 0;
@@ -1855,8 +1858,6 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       if (w == 1 || w == 2 || w == 4) b.wpb16 = std::min(w, static_cast<int>(WavesPerBlock<16>::value));
     }
   }
-  d.blocked = b.group == 64 ? 1 : 0;
-  if (b.group == 64) d.shr_total = shr_small;
   // extended step kernels (step.hip MRS_EXT) for models with general convex (MPR) pairs -- a pair
   // that is not plane-* and has an ellipsoid, cylinder or mesh (narrowphase's analytic routines cover
   // the rest) -- or rangefinders over more than 32 ray geoms
@@ -1866,6 +1867,25 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     auto conv = [](int t) { return t == MRS_GEOM_ELLIPSOID || t == MRS_GEOM_CYLINDER || t == MRS_GEOM_MESH; };
     if (t1 != MRS_GEOM_PLANE && t2 != MRS_GEOM_PLANE && (conv(t1) || conv(t2))) b.ext = true;
   }
+  // helper waves: with one-wave workgroups (fewer waves than SIMDs, so the helpers take SIMDs that
+  // would idle) every physics wave gets a second wave that runs its envs' collision pass, builds their
+  // constraint rows, traces their rangefinders and factors the integrator's M + h D each step while it
+  // runs the dynamics (step_kernel); models with rangefinders (<= 32 ray geoms) without RK4 and
+  // without the extended kernels only.  MRS_RAY_HELPERS=0 turns them off
+  {
+    const char* e = std::getenv("MRS_RAY_HELPERS");
+    const bool want = e ? std::atoi(e) != 0 : true;
+    b.helpers = want && b.group == 16 && b.wpb16 == 1 && !b.ext && d.nrf > 0 && d.nrgeom <= 32 &&
+                m.integrator != MRS_INT_RK4 && !(m.disableflags & MRS_DSBL_SENSOR) ? 1 : 0;
+    // the integrator factor slot (implicit-damping Euler and implicitfast; the full implicit
+    // integrator factors its own LU)
+    if (b.helpers && m.integrator != MRS_INT_IMPLICIT) {
+      want_lh = true;
+      lds_layout(false);
+    }
+  }
+  d.blocked = b.group == 64 ? 1 : 0;
+  if (b.group == 64) d.shr_total = shr_small;
 
   if (d.blocked) lds_layout(true);
   d.shr_off = L.total * envs_per_block(b.group, b.wpb16);
@@ -1971,17 +1991,7 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
     const size_t n_virt = ((static_cast<size_t>(n) << shift) + epb - 1) / epb * epb;
     b->st.spread_shift = shift;
     b->st.wpb16 = b->wpb16;
-    // helper waves: with one-wave workgroups (fewer waves than SIMDs, so the helpers take SIMDs that
-    // would idle) every physics wave gets a second wave that runs its envs' collision pass and traces
-    // their rangefinders each step while it runs the dynamics (step_kernel); models with
-    // rangefinders (<= 32 ray geoms) without RK4 and without the extended kernels only.
-    // MRS_RAY_HELPERS=0 turns them off
-    {
-      const char* e = std::getenv("MRS_RAY_HELPERS");
-      const bool want = e ? std::atoi(e) != 0 : true;
-      b->st.ray_helpers = want && b->group == 16 && b->wpb16 == 1 && !b->ext && b->dm.nrf > 0 && b->dm.nrgeom <= 32 &&
-                          m.integrator != MRS_INT_RK4 && !(m.disableflags & MRS_DSBL_SENSOR) ? 1 : 0;
-    }
+    b->st.ray_helpers = b->helpers;  // (build_devmodel)
     b->st.scr_mirror = static_cast<int>(n_pad);
     b->st.scratch = static_cast<float*>(dalloc(*b, (n_pad + (shift ? n_virt : 0)) * b->S.total * sizeof(float)));
     b->st.geom_xpos = static_cast<float*>(dalloc(*b, n * std::max(1, m.ngeom) * 3 * sizeof(float)));

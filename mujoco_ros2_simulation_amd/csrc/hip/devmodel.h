@@ -48,7 +48,8 @@ struct LdsLayout {
       rk,      // RK4 models: the step's initial qpos [nq], then qvel [nv], stage velocity, B-weighted sums of
                // the stage velocities and accelerations [nv each]
       niter,   // constraint solver iterations of the last forward (int bits)
-      hcon;    // ray helper waves: the step's contact count from the helper's collision pass (int bits)
+      hcon,    // helper waves: the step's contact and row counts from the helper (int bits)
+      Lh;      // helper waves: the factor of M + h D for the integrator, built by the helper (0: none)
   int total;  // floats per env (multiple of 4)
 };
 

@@ -6723,18 +6723,12 @@ __device__ __forceinline__ void integrate_pos(const DevModel& m, lfloat* s, cons
 template <int G>
 __device__ void integrate_implicit(ENV_PARAMS);
 
-// mj_Euler / mj_implicit(implicitfast) + mj_advance
+// the integrator's implicit damping of lane's dof (mj_Euler: dof damping; implicitfast: damping and
+// the actuators' velocity derivatives), 0 past nv
 template <int G>
-__device__ MRS_PHASE void integrate(ENV_PARAMS) {
+__device__ __forceinline__ float integrate_dg(ENV_PARAMS) {
   ENV_UNPACK;
-  if (m.integrator == MRS_INT_IMPLICIT) {
-    [[clang::noinline]] integrate_implicit<G>(ENV_ARGS);
-    return;
-  }
   const int nv = m.nv;
-  const float h = m.timestep;
-  const float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
-  bool need_solve = false;
   float dg = 0;
   if (lane < nv) {
     const auto dr = dof_tab<G>(m, lane);
@@ -6770,15 +6764,55 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS) {
       }
     }
   }
-  need_solve = m.integrator != MRS_INT_EULER || gany<G>(dg != 0);
+  return dg;
+}
+
+// the helper waves' share of the integrator (step_kernel): M + h diag(dg) factored into L.Lh while
+// the physics wave runs the constraint solve (M, the dof damping, ctrl and the actuator forces of the
+// step are final by then); integrate() then only solves.  Returns nothing when no solve is needed.
+template <int G>
+__device__ __forceinline__ void integrate_prefactor(ENV_PARAMS) {
+  ENV_UNPACK;
+  const int nv = m.nv;
+  const float dg = integrate_dg<G>(ENV_ARGS);
+  if (!(m.integrator != MRS_INT_EULER || gany<G>(dg != 0))) return;
+  const float h = m.timestep;
+  #pragma unroll 1
+  for (int j = 0; j < nv; ++j)
+    if (lane < nv) s[L.Lh + midx<G>(m, lane, j)] = s[L.M + midx<G>(m, lane, j)];
+  // (the diagonal update in the same statement form as integrate()'s in-place M_ii += h dg, so it
+  // contracts the same way: one fma, bit-identical factors)
+  if (lane < nv) s[L.Lh + midx<G>(m, lane, lane)] += h * dg;
+  wsync();
+  MRS_CALL(G, cholesky<G>(mp, s + L.Lh, s + L.Lh, lane));
+}
+
+// mj_Euler / mj_implicit(implicitfast) + mj_advance (prefac: the factor of M + h D is in L.Lh,
+// built by the helper wave)
+template <int G>
+__device__ MRS_PHASE void integrate(ENV_PARAMS, bool prefac = false) {
+  ENV_UNPACK;
+  if (m.integrator == MRS_INT_IMPLICIT) {
+    [[clang::noinline]] integrate_implicit<G>(ENV_ARGS);
+    return;
+  }
+  const int nv = m.nv;
+  const float h = m.timestep;
+  const float qacc = lane < nv ? s[L.qacc + lane] : 0.0f;
+  const float dg = integrate_dg<G>(ENV_ARGS);
+  const bool need_solve = m.integrator != MRS_INT_EULER || gany<G>(dg != 0);
   float qacc_int = qacc;
   if (need_solve) {
-    // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
-    if (lane < nv) s[L.M + midx<G>(m, lane, lane)] += h * dg;
-    wsync();
-    MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
-    float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
-    MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + L.L, rhs, lane));
+    const float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
+    if (prefac) {
+      MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + L.Lh, rhs, lane));
+    } else {
+      // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
+      if (lane < nv) s[L.M + midx<G>(m, lane, lane)] += h * dg;
+      wsync();
+      MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
+      MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + L.L, rhs, lane));
+    }
   }
   if (lane < nv) {
     s[L.qacc_ws + lane] = qacc;
@@ -7081,6 +7115,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       if (lane == 0) s[L.hcon] = __int_as_float(nc + 65536 * (nr + 1));
       helper_barrier(true);
       MRS_CALL(G, rays_pass<G>(ENV_ARGS, sensordata));
+      // the integrator's factor of M + h D (the physics wave solves with it after B)
+      if (L.Lh != 0) MRS_CALL(G, integrate_prefactor<G>(ENV_ARGS));
       helper_barrier(true);
     }
     return;
@@ -7143,7 +7179,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       [[clang::noinline]] rk4_final<G>(ENV_ARGS);
     } else {
       PH_BEGIN();
-      MRS_CALL(G, integrate<G>(ENV_ARGS));
+      // (a re-run step's factor is its own: the helper's was of the first forward's state)
+      MRS_CALL(G, integrate<G>(ENV_ARGS, helpers && L.Lh != 0 && !__any(redo)));
       PH_END(ph_acc, PH_INTEG);
     }
     time += m.timestep_d;
