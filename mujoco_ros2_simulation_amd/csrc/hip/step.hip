@@ -5319,6 +5319,86 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s, int p
 
 // dense constraint rows in the env's global scratch (J, M^-1 J', row scalars), then the
 // register-resident PGS (<= 16 rows on G = 16) or the row-serial PGS with wave reductions
+// mj_makeImpedance of row r (mj_makeConstraint's rows in the env's scratch): its regulariser R and
+// reference acceleration aref = -B J qvel - K imp (pos - margin), from the row's type, distance and
+// model parameters.  The dense solve's set-up and the helper waves (dense_impedance) share it.
+template <int G>
+__device__ __forceinline__ void row_impedance(const DevModel& m, const lfloat* s, const gfloat* scr, int r, float& R_out,
+                                              float& aref_out) {
+  const LdsLayout& L = m.L;
+  const ScratchLayout& S = m.S;
+  const int nv = m.nv;
+  const gfloat* J = scr + S.efc_J;
+  const gfloat* type = scr + S.efc_type;
+  const gfloat* pos = scr + S.efc_pos;
+  const gfloat* marg = scr + S.efc_margin;
+  const gfloat* floss = scr + S.efc_floss;
+  const gfloat* bb = scr + S.efc_b;
+  const int code = __float_as_int(type[r]);
+  const int t = code >> 16, id = code & 0xffff;
+  CPtr<float> sr, si;
+  float diag;
+  if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
+  else if (t == EFC_EQUALITY) { sr = m.eq_solref + 2 * id; si = m.eq_solimp + 5 * id; diag = bb[r]; }
+  else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
+  else if (t == EFC_TFRICTION) { sr = m.ten_solref_fri + 2 * id; si = m.ten_solimp_fri + 5 * id; diag = m.ten_prm[12 * id + 8]; }
+  else if (t == EFC_TLIMIT) { sr = m.ten_solref_lim + 2 * id; si = m.ten_solimp_lim + 5 * id; diag = m.ten_prm[12 * id + 8]; }
+  else {
+    const gfloat* rec = scr + S.con + kConRec * id;
+    const int p = __float_as_int(rec[0]);
+    sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
+    const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
+    float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+    diag = tran;
+    if (m.pair_dim[p] == 3 && m.cone == MRS_CONE_ELLIPTIC) {
+      // elliptic: diagApprox tran for every row of the block, the tangents' regulariser / impratio
+      if (floss[r] > 1.5f) diag = tran / m.impratio;
+    } else if (m.pair_dim[p] == 3) {
+      // pyramid edge: diagApprox tran (1 + mu^2) (mu sliding, for both tangent directions);
+      // mj_makeImpedance scales the edges' regulariser by 2 mu^2 / impratio
+      const float mu = m.pair_friction[3 * p];
+      diag = tran * (1 + mu * mu) * (2 * mu * mu / m.impratio);
+    }
+  }
+  const float imp = impedance(si, pos[r], marg[r]);
+  float R = (1 - imp) * diag / imp;
+  R = R > kMinVal ? R : kMinVal;
+  const float dmax = clampf(si[1], 0.0001f, 0.9999f);
+  float K, B;
+  if (sr[0] > 0) {
+    float tc = sr[0], dr = sr[1];
+    if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
+    K = 1 / (dmax * dmax * tc * tc * dr * dr);
+    B = 2 / (dmax * tc);
+  } else {
+    K = -sr[0] / (dmax * dmax);
+    B = -sr[1] / dmax;
+  }
+  float vel = 0;
+  const gfloat* Jr = J + r * nv;
+  #pragma unroll 4
+  for (int j = 0; j < nv; ++j) vel += Jr[j] * s[L.qvel + j];
+  // (friction-loss rows and the tangent rows of an elliptic block carry no position term)
+  const float pterm = (t == EFC_FRICTION || t == EFC_TFRICTION || (t == EFC_CONTACT && floss[r] > 1.5f))
+                          ? 0.0f : K * imp * (pos[r] - marg[r]);
+  R_out = R;
+  aref_out = -B * vel - pterm;
+}
+
+// the helper waves' share of the dense set-up (step_kernel): R and aref of every row into the scratch
+template <int G>
+__device__ __forceinline__ void dense_impedance(ENV_PARAMS, int nefc) {
+  ENV_UNPACK;
+  #pragma unroll 1
+  for (int r = lane; r < nefc; r += G) {
+    float R, ar;
+    row_impedance<G>(m, s, scr, r, R, ar);
+    scr[S.efc_R + r] = R;
+    scr[S.efc_aref + r] = ar;
+  }
+  wsync();
+}
+
 // mj_makeConstraint's rows into the env's scratch (dense J, type, pos, margin, friction-loss bound;
 // contact records' first-row index): equality, friction loss, limits, contacts; returns nefc (also
 // in scr[S.efc_n]).  Reads kinematics, com_pos (cdof, subtree coms) and, for tendon limits, the
@@ -5673,63 +5753,30 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_n
   #pragma unroll 1
   for (int r = lane; r < nefc; r += G) {
     const int code = __float_as_int(type[r]);
-    const int t = code >> 16, id = code & 0xffff;
-    CPtr<float> sr, si;
-    float diag;
-    if (t == EFC_FRICTION) { sr = m.dof_solref + 2 * id; si = m.dof_solimp + 5 * id; diag = m.dof_invweight0[id]; }
-    else if (t == EFC_EQUALITY) { sr = m.eq_solref + 2 * id; si = m.eq_solimp + 5 * id; diag = bb[r]; }
-    else if (t == EFC_LIMIT) { sr = m.jnt_solref + 2 * id; si = m.jnt_solimp + 5 * id; diag = m.dof_invweight0[m.jnt_dofadr[id]]; }
-    else if (t == EFC_TFRICTION) { sr = m.ten_solref_fri + 2 * id; si = m.ten_solimp_fri + 5 * id; diag = m.ten_prm[12 * id + 8]; }
-    else if (t == EFC_TLIMIT) { sr = m.ten_solref_lim + 2 * id; si = m.ten_solimp_lim + 5 * id; diag = m.ten_prm[12 * id + 8]; }
-    else {
-      const gfloat* rec = scr + S.con + kConRec * id;
-      const int p = __float_as_int(rec[0]);
-      sr = m.pair_solref + 2 * p; si = m.pair_solimp + 5 * p;
-      const int b1 = m.geom_bodyid[m.pair_g1[p]], b2 = m.geom_bodyid[m.pair_g2[p]];
-      float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-      diag = tran;
-      if (m.pair_dim[p] == 3 && m.cone == MRS_CONE_ELLIPTIC) {
-        // elliptic: diagApprox tran for every row of the block, the tangents' regulariser / impratio
-        if (floss[r] > 1.5f) diag = tran / m.impratio;
-      } else if (m.pair_dim[p] == 3) {
-        // pyramid edge: diagApprox tran (1 + mu^2) (mu sliding, for both tangent directions);
-        // mj_makeImpedance scales the edges' regulariser by 2 mu^2 / impratio
-        const float mu = m.pair_friction[3 * p];
-        diag = tran * (1 + mu * mu) * (2 * mu * mu / m.impratio);
-      }
-    }
-    const float imp = impedance(si, pos[r], marg[r]);
-    float R = (1 - imp) * diag / imp;
-    R = R > kMinVal ? R : kMinVal;
-    Rr[r] = R;
-    const float dmax = clampf(si[1], 0.0001f, 0.9999f);
-    float K, B;
-    if (sr[0] > 0) {
-      float tc = sr[0], dr = sr[1];
-      if (!(m.disableflags & MRS_DSBL_REFSAFE) && tc < 2 * m.timestep) tc = 2 * m.timestep;
-      K = 1 / (dmax * dmax * tc * tc * dr * dr);
-      B = 2 / (dmax * tc);
+    const int t = code >> 16;
+    // R and aref (mj_makeImpedance), from the helper wave when it built the rows
+    float R, ar;
+    if (pre_nefc >= 0) {
+      R = Rr[r];
+      ar = aref[r];
     } else {
-      K = -sr[0] / (dmax * dmax);
-      B = -sr[1] / dmax;
+      row_impedance<G>(m, s, scr, r, R, ar);
+      Rr[r] = R;
     }
-    float vel = 0, jqs = 0;
+    float jqs = 0;
     const gfloat* Jr = J + r * nv;
     #pragma unroll 4
-    for (int j = 0; j < nv; ++j) { vel += Jr[j] * s[L.qvel + j]; jqs += Jr[j] * s[L.qacc_smooth + j]; }
-    // (friction-loss rows and the tangent rows of an elliptic block carry no position term)
-    const float pterm = (t == EFC_FRICTION || t == EFC_TFRICTION || (t == EFC_CONTACT && floss[r] > 1.5f))
-                            ? 0.0f : K * imp * (pos[r] - marg[r]);
+    for (int j = 0; j < nv; ++j) jqs += Jr[j] * s[L.qacc_smooth + j];
     if (small) {
       my_R = R;
-      my_aref = -B * vel - pterm;
+      my_aref = ar;
       my_b = jqs - my_aref;
       my_fl = fric_like(t) ? floss[r] : 0.0f;
       my_fric = fric_like(t);
       aref[r] = my_aref;
       continue;
     }
-    aref[r] = -B * vel - pterm;
+    aref[r] = ar;
     bb[r] = jqs - aref[r];
     if (primal || G == 64) continue;
     // M^-1 J_r'
@@ -7111,6 +7158,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       if (helper_rows(m)) {
         helper_barrier(false);
         [[clang::noinline]] nr = dense_rows<G>(ENV_ARGS, nc);
+        MRS_CALL(G, dense_impedance<G>(ENV_ARGS, nr));
       }
       if (lane == 0) s[L.hcon] = __int_as_float(nc + 65536 * (nr + 1));
       helper_barrier(true);
