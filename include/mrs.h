@@ -116,8 +116,9 @@ int mrs_batch_render_depth(mrs_batch* b, int cam, int env0, int n, float* host_o
 /* same, into a device buffer [n][H][W] (stays in HBM) */
 int mrs_batch_render_depth_device(mrs_batch* b, int cam, int env0, int n, float* d_out);
 /* depth and colour in one pass (the RGB8 image of src/mujoco_cameras.cpp:211-240): depth as above,
- * rgb [n][H][W][3] uint8, ROS row order, flat headlight shading of each pixel's nearest geom
- * (rgba x (0.3 + 0.7 max(0, -n.d))), black where nothing is hit -- not an OpenGL raster match */
+ * rgb [n][H][W][3] uint8, ROS row order, each pixel's nearest geom shaded by MuJoCo's fixed-function
+ * lighting model restated per pixel (headlight and model lights, shadows, materials, builtin
+ * textures; the skybox where nothing is hit) -- not an OpenGL raster match */
 int mrs_batch_render_rgbd(mrs_batch* b, int cam, int env0, int n, float* host_depth, unsigned char* host_rgb);
 /* same, into device buffers */
 int mrs_batch_render_rgbd_device(mrs_batch* b, int cam, int env0, int n, float* d_depth, unsigned char* d_rgb);
@@ -164,7 +165,9 @@ int mrs_debug_phase_cycles(double* out, int n, int reset);
  * [4] dof slots per constraint row (pipe width), [5] constraint-row capacity, [6] contact capacity,
  * [7] kinematic trees with dofs, [8] workgroup-shared LDS floats, [9] lidar rays read from the
  * workgroup's LDS table (1) or the model block (0), [10] one workgroup per CU (16-lane groups kept for
- * tables past the two-per-CU budget).  Returns the number of values written. */
+ * tables past the two-per-CU budget), [11] waves per workgroup of a 16-lane batch (0 otherwise),
+ * [12] helper waves (collision, rows, rays and the integrator factor beside the dynamics).  Returns
+ * the number of values written. */
 int mrs_debug_batch_layout(const mrs_batch* b, int* out, int n);
 
 #ifdef __cplusplus

@@ -2038,10 +2038,11 @@ void batch_free(BatchImpl* b) {
 int batch_num_envs(const BatchImpl* b) { return b->n; }
 
 int batch_layout(const BatchImpl* b, int* out, int n) {
-  const int v[11] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
-                     b->dm.max_con, b->dm.ntree, b->dm.shr_total, b->dm.rf_common, b->g16_one_wg};
+  const int v[13] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
+                     b->dm.max_con, b->dm.ntree, b->dm.shr_total, b->dm.rf_common, b->g16_one_wg,
+                     b->group == 16 ? b->wpb16 : 0, b->helpers};
   int k = 0;
-  for (; k < n && k < 11; ++k) out[k] = v[k];
+  for (; k < n && k < 13; ++k) out[k] = v[k];
   return k;
 }
 

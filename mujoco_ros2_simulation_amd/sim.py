@@ -352,10 +352,10 @@ class Batch:
     def layout(self) -> dict:
         """kernel configuration of this batch (diagnostics): group width, LDS and scratch floats per
         env, blocked mode, pipe width, row and contact capacity, kinematic trees"""
-        out = np.zeros(11, dtype=np.int32)
-        k = lib().mrs_debug_batch_layout(self._h, out.ctypes.data, 11)
+        out = np.zeros(13, dtype=np.int32)
+        k = lib().mrs_debug_batch_layout(self._h, out.ctypes.data, 13)
         keys = ["group", "lds_floats", "scratch_floats", "blocked", "pipe_w", "max_efc", "max_con", "ntree",
-                "shared_floats", "rf_common", "one_workgroup_per_cu"]
+                "shared_floats", "rf_common", "one_workgroup_per_cu", "waves_per_workgroup", "helper_waves"]
         return dict(zip(keys[:k], out[:k].tolist()))
 
     def step(self, n_steps: int = 1) -> None:

@@ -42,3 +42,17 @@ def test_ray_helpers_bit_identical(scene, n, monkeypatch):
             assert np.array_equal(u, v), (scene, k, name, np.abs(u - v).max())
     # the lidar saw something (the comparison is not of empty outputs)
     assert np.any(a[-1][2] > 0)
+
+
+def test_helper_configuration_per_batch_size(monkeypatch):
+    """the batch picks one-wave workgroups and helper waves below one wave per SIMD (C4's 2048 envs)
+    and keeps four-wave workgroups without helpers at C3's size"""
+    monkeypatch.delenv("MRS_RAY_HELPERS", raising=False)
+    c4 = sim.Batch(sim.Model.load(ROOT / "scenes" / "mobile_base.xml"), 2048)
+    lay = c4.layout()
+    c4.close()
+    assert lay["group"] == 16 and lay["waves_per_workgroup"] == 1 and lay["helper_waves"] == 1, lay
+    c3 = sim.Batch(sim.Model.load(ROOT / "scenes" / "arm7_lidar.xml"), 8192)
+    lay = c3.layout()
+    c3.close()
+    assert lay["group"] == 16 and lay["waves_per_workgroup"] == 4 and lay["helper_waves"] == 0, lay
