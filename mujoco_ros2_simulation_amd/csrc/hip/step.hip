@@ -1600,6 +1600,21 @@ __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_read
 // the workgroup-shared LDS tables (DevModel::shr_*), staged by step_kernel at launch
 extern __shared__ __attribute__((aligned(16))) float g_dyn_lds[];
 __device__ __forceinline__ const lfloat* shared_lds(const DevModel& m) { return (const lfloat*)(g_dyn_lds + m.shr_off); }
+// helper waves' one-way signal (step_kernel): the physics wave counts its com_pos passes in a
+// workgroup LDS word (release: com_pos's LDS writes land first); the helper waits for the count it
+// needs (acquire) before building the rows from them, so the physics wave never waits for the
+// helper there.  The wait gives up after ~2^26 polls (seconds), far past any real step, so that a
+// broken protocol cannot hang the device.
+__device__ __forceinline__ int* helper_flag(const DevModel& m) { return (int*)(g_dyn_lds + m.shr_off + m.shr_flag); }
+__device__ __forceinline__ void helper_signal(const DevModel& m) {
+  if (__lane_id() == 0) __hip_atomic_fetch_add(helper_flag(m), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void helper_wait(const DevModel& m, int count) {
+  for (unsigned k = 0; k < (1u << 26); ++k) {
+    if (__hip_atomic_load(helper_flag(m), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= count) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 // by-value copy of the model descriptor read through the constant address space: only the fields a
 // phase uses are loaded (scalar loads), and they stay in SGPRs for the whole phase
 __device__ __forceinline__ DevModel load_model(const DevModel* mp) {
@@ -6692,15 +6707,13 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   if (helper) helper_barrier(false);
   PH_END(ph_acc, PH_KIN);
   MRS_CALL(G, com_pos<G>(ENV_ARGS));
+  // helper waves: com_pos's cdof and subtree coms are in LDS -- signal the helper, which builds the
+  // constraint rows from them after its collision pass (no wait here)
+  if (helper && helper_rows(m)) helper_signal(m);
   PH_END(ph_acc, PH_COMPOS);
   MRS_CALL(G, make_M<G>(ENV_ARGS));
   PH_END(ph_acc, PH_MAKEM);
   MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
-  // helper waves: barrier D -- com_pos's cdof and subtree coms are in LDS, so the helper may build
-  // the constraint rows after its collision pass (placed after the factor so that the helper's
-  // collision pass has run by then; one phase later, after com_vel, the helper's rows reach barrier
-  // C late: C4 0.707 vs 0.683 ms per launch)
-  if (helper && helper_rows(m)) helper_barrier(false);
   PH_END(ph_acc, PH_CHOL);
   MRS_CALL(G, com_vel<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COMVEL);
@@ -7143,21 +7156,22 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       for (int i = threadIdx.x; i < m.njump * m.nbody; i += blockDim.x) shr[m.shr_jump + i] = __int_as_float(m.jump[i]);
     }
   }
+  if (helpers && threadIdx.x == 0) *helper_flag(m) = 0;
   __syncthreads();
   wsync();
   if (is_helper) {
     // barrier A (the physics wave's poses are in LDS), the collision pass, barrier C (contacts
     // stored, their count in LDS), the rays, barrier B (results stored); the physics waves pass A, C
     // and B exactly once per step (forward() after kinematics and before constraints, then below)
-    // with helper_rows also barrier D (the physics wave's com_pos outputs are in LDS) and the dense
-    // constraint rows between D and C; their count goes to LDS with the contact count
+    // with helper_rows also the dense constraint rows, after the physics wave's signal that its
+    // com_pos outputs are in LDS (helper_wait); their count goes to LDS with the contact count
     #pragma unroll 1
     for (int step = 0; step < n_steps; ++step) {
       helper_barrier(false);
       int nc = 0, nr = -1;
       if (!(m.diag_skip & 2)) MRS_CALL(G, nc = collision<G>(ENV_ARGS));
       if (helper_rows(m)) {
-        helper_barrier(false);
+        helper_wait(m, step + 1);  // the physics wave's com_pos of this step is done
         [[clang::noinline]] nr = dense_rows<G>(ENV_ARGS, nc);
         MRS_CALL(G, dense_impedance<G>(ENV_ARGS, nr));
       }
