@@ -42,7 +42,9 @@ enum {
   MRS_FIELD_QFRC_ACTUATOR = 6, /* nv,  fp32 (output) */
   MRS_FIELD_SENSORDATA = 7,    /* nsensordata, fp32 (output) */
   MRS_FIELD_TIME = 8,          /* 1,   fp64 */
-  MRS_FIELD_WARNING = 9,       /* 4,   int32: counts of bad qpos, bad qvel, bad qacc, last info */
+  MRS_FIELD_WARNING = 9,       /* 4,   int32: counts of bad qpos, bad qvel, bad qacc (auto-resets), and of
+                                  helper-wave signal timeouts (an internal protocol fault: the step then
+                                  built its rows inline; 0 in every correct run) */
   MRS_FIELD_NCON = 10,         /* 1,   int32: contacts found in the last step (output) */
   MRS_FIELD_SOLVER_NITER = 11, /* 1,   int32: constraint solver iterations of the last step (mjData.solver_niter) */
   MRS_FIELD_COUNT = 12
@@ -50,9 +52,14 @@ enum {
 
 /* last error message of the calling thread ("" if none) */
 const char* mrs_last_error(void);
+/* status code (MRS_OK or MRS_ERR_*) of the calling thread's last call, for the entry points that
+ * return a handle (NULL on failure) rather than a code */
+int mrs_last_status(void);
 
 /* ------------------------------------------------------------------ model
- * replaces mj_loadXML (src/mujoco_system_interface.cpp:318) and mj_loadModel (:310) */
+ * replaces mj_loadXML (src/mujoco_system_interface.cpp:318).  The reference's other branch, a path
+ * ending in ".mjb" loaded by mj_loadModel (:307-310), is not supported: such a path fails with
+ * MRS_ERR_UNSUPPORTED (mrs_last_status) and "could not load binary model ..." in `error` */
 mrs_model* mrs_model_load_xml(const char* path, char* error, int error_len);
 /* replaces mj_parseXMLString + mj_compile (src/mujoco_system_interface.cpp:398-399, model from the
  * /mujoco_robot_description topic); `basedir` resolves <include> (may be NULL) */

@@ -21,11 +21,12 @@ struct mrs_batch {
 namespace {
 
 thread_local std::string g_last_error;
+thread_local int g_last_code = MRS_OK;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 template <class F>
-int guarded(F&& f) {
+int guarded_impl(F&& f) {
   try {
     g_last_error.clear();
     f();
@@ -48,6 +49,17 @@ int guarded(F&& f) {
   }
 }
 
+template <class F>
+int guarded(F&& f) {
+  g_last_code = guarded_impl(f);
+  return g_last_code;
+}
+
+bool ends_with(const std::string& s, const char* suffix) {
+  const size_t n = std::strlen(suffix);
+  return s.size() > n && s.compare(s.size() - n, n, suffix) == 0;
+}
+
 void copy_error(char* error, int error_len) {
   if (error && error_len > 0) {
     std::strncpy(error, g_last_error.c_str(), static_cast<size_t>(error_len) - 1);
@@ -60,14 +72,26 @@ void copy_error(char* error, int error_len) {
 extern "C" {
 
 const char* mrs_last_error(void) { return g_last_error.c_str(); }
+int mrs_last_status(void) { return g_last_code; }
 
 mrs_model* mrs_model_load_xml(const char* path, char* error, int error_len) {
   std::unique_ptr<mrs_model> out;
   int rc = guarded([&] {
     if (!path || !*path) throw std::invalid_argument("empty model path");
+    // the reference loads a path ending in ".mjb" with mj_loadModel (src/mujoco_system_interface.cpp:
+    // 307-310): MuJoCo's binary format is a version-specific dump of mjModel that this compiler does
+    // not read -- fail with MRS_ERR_UNSUPPORTED instead of handing binary data to the XML parser
+    if (ends_with(path, ".mjb") || ends_with(path, ".MJB"))
+      throw mrs::UnsupportedError(std::string("could not load binary model ") + path +
+                                  ": MuJoCo .mjb files (mj_loadModel) are not supported, load the MJCF XML");
     out.reset(new mrs_model{mrs::compile_mjcf_file(path)});
   });
-  if (rc != MRS_OK) { copy_error(error, error_len); return nullptr; }
+  if (rc != MRS_OK) {
+    // parse / compile failures report MRS_ERR_LOAD; features outside the subset MRS_ERR_UNSUPPORTED
+    if (rc != MRS_ERR_UNSUPPORTED) g_last_code = MRS_ERR_LOAD;
+    copy_error(error, error_len);
+    return nullptr;
+  }
   if (error && error_len > 0) error[0] = '\0';
   return out.release();
 }
@@ -78,7 +102,12 @@ mrs_model* mrs_model_load_xml_string(const char* xml, const char* basedir, char*
     if (!xml) throw std::invalid_argument("null XML string");
     out.reset(new mrs_model{mrs::compile_mjcf_string(xml, basedir ? basedir : ".")});
   });
-  if (rc != MRS_OK) { copy_error(error, error_len); return nullptr; }
+  if (rc != MRS_OK) {
+    // parse / compile failures report MRS_ERR_LOAD; features outside the subset MRS_ERR_UNSUPPORTED
+    if (rc != MRS_ERR_UNSUPPORTED) g_last_code = MRS_ERR_LOAD;
+    copy_error(error, error_len);
+    return nullptr;
+  }
   if (error && error_len > 0) error[0] = '\0';
   return out.release();
 }

@@ -1803,7 +1803,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     // LDS per env
     shr_small = d.shr_act;
     d.shr_total = d.shr_jump + d.njump * m.nbody;
-    d.shr_flag = d.shr_total++;  // (helper waves' signal word)
+    d.shr_flag = d.shr_total;  // (helper waves' signal words, one per physics wave)
+    d.shr_total += 4;
   };
   layout_shared();
   // lanes per environment: the narrowest group that still gives every dof its own lane (the

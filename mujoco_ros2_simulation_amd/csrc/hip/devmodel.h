@@ -110,7 +110,7 @@ struct DevModel {
   // tree tables (bodytab, 8 floats per body; mpairtab, 4 floats per pair of M) at shr_body, shr_mpair
   int shr_body, shr_mpair;
   int shr_jump;  // the kinematics' pointer-jumping table (jump, int bits) with lane groups
-  int shr_flag;  // helper waves: the physics wave's count of com_pos passes this launch (int bits)
+  int shr_flag;  // helper waves: per physics wave (4 words) its count of com_pos passes this launch (int bits)
   unsigned rf_static_mask;
   float* rf_static;
   // options

@@ -1600,20 +1600,26 @@ __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_read
 // the workgroup-shared LDS tables (DevModel::shr_*), staged by step_kernel at launch
 extern __shared__ __attribute__((aligned(16))) float g_dyn_lds[];
 __device__ __forceinline__ const lfloat* shared_lds(const DevModel& m) { return (const lfloat*)(g_dyn_lds + m.shr_off); }
-// helper waves' one-way signal (step_kernel): the physics wave counts its com_pos passes in a
-// workgroup LDS word (release: com_pos's LDS writes land first); the helper waits for the count it
-// needs (acquire) before building the rows from them, so the physics wave never waits for the
-// helper there.  The wait gives up after ~2^26 polls (seconds), far past any real step, so that a
-// broken protocol cannot hang the device.
-__device__ __forceinline__ int* helper_flag(const DevModel& m) { return (int*)(g_dyn_lds + m.shr_off + m.shr_flag); }
-__device__ __forceinline__ void helper_signal(const DevModel& m) {
-  if (__lane_id() == 0) __hip_atomic_fetch_add(helper_flag(m), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+// helper waves' one-way signal (step_kernel): each physics wave counts its com_pos passes in a
+// workgroup LDS word of its own (release: com_pos's LDS writes land first); its helper wave waits for
+// the count it needs (acquire) before building the rows from them, so the physics wave never waits for
+// the helper there.  One word per physics wave (DevModel::shr_flag, 4 words), so the protocol holds
+// for any number of physics waves per workgroup.  The wait gives up after ~2^26 polls (seconds), far
+// past any real step, so that a broken protocol cannot hang the device; it then returns false, the
+// helper leaves the rows to the physics wave (which builds them inline from its own com_pos) and
+// counts the timeout in the env's warning[3] (MRS_FIELD_WARNING) -- never silently stale rows.
+__device__ __forceinline__ int* helper_flag(const DevModel& m, int wave) {
+  return (int*)(g_dyn_lds + m.shr_off + m.shr_flag) + wave;
 }
-__device__ __forceinline__ void helper_wait(const DevModel& m, int count) {
+__device__ __forceinline__ void helper_signal(const DevModel& m, int wave) {
+  if (__lane_id() == 0) __hip_atomic_fetch_add(helper_flag(m, wave), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool helper_wait(const DevModel& m, int wave, int count) {
   for (unsigned k = 0; k < (1u << 26); ++k) {
-    if (__hip_atomic_load(helper_flag(m), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= count) return;
+    if (__hip_atomic_load(helper_flag(m, wave), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= count) return true;
     __builtin_amdgcn_s_sleep(1);
   }
+  return false;
 }
 // by-value copy of the model descriptor read through the constant address space: only the fields a
 // phase uses are loaded (scalar loads), and they stay in SGPRs for the whole phase
@@ -6709,7 +6715,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   MRS_CALL(G, com_pos<G>(ENV_ARGS));
   // helper waves: com_pos's cdof and subtree coms are in LDS -- signal the helper, which builds the
   // constraint rows from them after its collision pass (no wait here)
-  if (helper && helper_rows(m)) helper_signal(m);
+  if (helper && helper_rows(m)) helper_signal(m, __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6);
   PH_END(ph_acc, PH_COMPOS);
   MRS_CALL(G, make_M<G>(ENV_ARGS));
   PH_END(ph_acc, PH_MAKEM);
@@ -7156,7 +7162,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       for (int i = threadIdx.x; i < m.njump * m.nbody; i += blockDim.x) shr[m.shr_jump + i] = __int_as_float(m.jump[i]);
     }
   }
-  if (helpers && threadIdx.x == 0) *helper_flag(m) = 0;
+  if (helpers && threadIdx.x < 4) *helper_flag(m, threadIdx.x) = 0;
   __syncthreads();
   wsync();
   if (is_helper) {
@@ -7165,15 +7171,22 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     // and B exactly once per step (forward() after kinematics and before constraints, then below)
     // with helper_rows also the dense constraint rows, after the physics wave's signal that its
     // com_pos outputs are in LDS (helper_wait); their count goes to LDS with the contact count
+    const int hwave = (__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) - st.wpb16;  // its physics wave
+    int timeouts = 0;
     #pragma unroll 1
     for (int step = 0; step < n_steps; ++step) {
       helper_barrier(false);
       int nc = 0, nr = -1;
       if (!(m.diag_skip & 2)) MRS_CALL(G, nc = collision<G>(ENV_ARGS));
       if (helper_rows(m)) {
-        helper_wait(m, step + 1);  // the physics wave's com_pos of this step is done
-        [[clang::noinline]] nr = dense_rows<G>(ENV_ARGS, nc);
-        MRS_CALL(G, dense_impedance<G>(ENV_ARGS, nr));
+        // the physics wave's com_pos of this step is done; on a timeout (a protocol fault) nr stays
+        // -1 and the physics wave builds the rows itself
+        if (helper_wait(m, hwave, step + 1)) {
+          [[clang::noinline]] nr = dense_rows<G>(ENV_ARGS, nc);
+          MRS_CALL(G, dense_impedance<G>(ENV_ARGS, nr));
+        } else {
+          ++timeouts;
+        }
       }
       if (lane == 0) s[L.hcon] = __int_as_float(nc + 65536 * (nr + 1));
       helper_barrier(true);
@@ -7182,10 +7195,11 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       if (L.Lh != 0) MRS_CALL(G, integrate_prefactor<G>(ENV_ARGS));
       helper_barrier(true);
     }
+    if (timeouts && valid && lane == 0) st.warning[4 * e + 3] += timeouts;
     return;
   }
   int ncon = 0;
-  int w_pos = 0, w_vel = 0, w_acc = 0, w_info = -1;
+  int w_pos = 0, w_vel = 0, w_acc = 0;
 #ifdef MRS_PHASE_TIMING
   unsigned long long ph_acc[PH_COUNT] = {};
 #endif
@@ -7284,11 +7298,10 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     st.time[e] = time;
     st.ncon[e] = ncon;
     st.niter[e] = __float_as_int(s[L.niter]);
-    if (w_pos | w_vel | w_acc) {
+    if (w_pos | w_vel | w_acc) {  // (warning[3] is the helper wave's: its signal timeouts)
       st.warning[4 * e + 0] += w_pos;
       st.warning[4 * e + 1] += w_vel;
       st.warning[4 * e + 2] += w_acc;
-      st.warning[4 * e + 3] = w_info;
     }
   }
 }

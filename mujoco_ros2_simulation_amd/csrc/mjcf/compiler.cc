@@ -2143,14 +2143,18 @@ struct Compiler {
           continue;
         if (!((m.geom_contype[g1] & m.geom_conaffinity[g2]) || (m.geom_contype[g2] & m.geom_conaffinity[g1])))
           continue;
-        // body pairs excluded, or covered by an explicit pair (mjModel exclude / pair signatures)
+        // body pairs excluded (mjModel exclude signatures), or this very geom pair given explicitly:
+        // mj_collision merges the dynamic pairs of a body pair with the explicit pairs of the same body
+        // signature by skipping only the geom pairs the explicit list holds (mj_collideGeoms' merge
+        // test over the signature's pair range) -- the bodies' other geoms still collide dynamically
+        // [upstream engine_collision_driver.c; verify]
         const int lo = std::min(b1, b2), hi = std::max(b1, b2);
         bool skip = false;
         for (size_t k = 0; k < m.exclude_body1.size() && !skip; ++k)
           skip = m.exclude_body1[k] == lo && m.exclude_body2[k] == hi;
         for (size_t k = 0; k < m.expair_geom1.size() && !skip; ++k) {
-          const int e1 = m.geom_bodyid[m.expair_geom1[k]], e2 = m.geom_bodyid[m.expair_geom2[k]];
-          skip = std::min(e1, e2) == lo && std::max(e1, e2) == hi;
+          const int e1 = m.expair_geom1[k], e2 = m.expair_geom2[k];
+          skip = (e1 == g1 && e2 == g2) || (e1 == g2 && e2 == g1);
         }
         if (skip) continue;
         const bool swap = m.geom_type[g1] > m.geom_type[g2];

@@ -173,6 +173,7 @@ def lib() -> C.CDLL:
             raise MrsError(-3, f"{LIB_PATH} not built; run `python -m mujoco_ros2_simulation_amd.build`")
         L = C.CDLL(str(LIB_PATH))
         L.mrs_last_error.restype = C.c_char_p
+        L.mrs_last_status.restype = C.c_int
         L.mrs_model_load_xml.restype = C.c_void_p
         L.mrs_model_load_xml.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
         L.mrs_model_load_xml_string.restype = C.c_void_p
@@ -274,7 +275,7 @@ class Model:
         err = C.create_string_buffer(1024)
         h = lib().mrs_model_load_xml(str(path).encode(), err, 1024)
         if not h:
-            raise MrsError(-2, err.value.decode())
+            raise MrsError(lib().mrs_last_status() or -2, err.value.decode())
         return cls(h)
 
     @classmethod
@@ -282,7 +283,7 @@ class Model:
         err = C.create_string_buffer(1024)
         h = lib().mrs_model_load_xml_string(xml.encode(), (basedir or ".").encode(), err, 1024)
         if not h:
-            raise MrsError(-2, err.value.decode())
+            raise MrsError(lib().mrs_last_status() or -2, err.value.decode())
         return cls(h)
 
     def set_restate(self, flags: int) -> None:
@@ -327,7 +328,7 @@ class Batch:
         self.n = n_envs
         h = lib().mrs_batch_create(model.handle, n_envs, device)
         if not h:
-            raise MrsError(-3, lib().mrs_last_error().decode())
+            raise MrsError(lib().mrs_last_status() or -3, lib().mrs_last_error().decode())
         self._h = h
 
     def _dim(self, field: int) -> int:

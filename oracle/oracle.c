@@ -1796,14 +1796,16 @@ static int pair_admissible(const mrs_model_view* m, int g1, int g2) {
     return 0;
   if (!((m->geom_contype[g1] & m->geom_conaffinity[g2]) || (m->geom_contype[g2] & m->geom_conaffinity[g1])))
     return 0;
-  /* body pairs excluded by <contact><exclude>, or covered by an explicit <pair> [upstream: the
-   * exclude / pair signatures filter dynamic body pairs; verify] */
+  /* body pairs excluded by <contact><exclude> (exclude signatures), or the very geom pair an explicit
+   * <pair> names: mj_collision's merge skips, among a body pair's dynamic geom pairs, only those in the
+   * explicit list of the same body signature; the bodies' other geoms still collide dynamically
+   * [upstream engine_collision_driver.c mj_collideGeoms merge test; verify] */
   const int lo = b1 < b2 ? b1 : b2, hi = b1 < b2 ? b2 : b1;
   for (int k = 0; k < m->nexclude; ++k)
     if (m->exclude_body1[k] == lo && m->exclude_body2[k] == hi) return 0;
   for (int k = 0; k < m->nexpair; ++k) {
-    const int e1 = m->geom_bodyid[m->expair_geom1[k]], e2 = m->geom_bodyid[m->expair_geom2[k]];
-    if ((e1 < e2 ? e1 : e2) == lo && (e1 < e2 ? e2 : e1) == hi) return 0;
+    const int e1 = m->expair_geom1[k], e2 = m->expair_geom2[k];
+    if ((e1 == g1 && e2 == g2) || (e1 == g2 && e2 == g1)) return 0;
   }
   return 1;
 }

@@ -31,3 +31,27 @@ def test_batch_create_without_gpu_fails_loudly(s2_model):
         assert e.code == -3
     else:
         raise AssertionError("batch creation must fail without a GPU (no CPU fallback)")
+
+
+def test_binary_model_path_is_unsupported(tmp_path, built):
+    """the reference loads a ".mjb" path with mj_loadModel (src/mujoco_system_interface.cpp:307-310);
+    this library does not read MuJoCo's binary format, so such a path fails with MRS_ERR_UNSUPPORTED
+    and the reference's message rather than reaching the XML parser"""
+    p = tmp_path / "robot.mjb"
+    p.write_bytes(b"\x00\x01binary model\x00")
+    try:
+        sim.Model.load(p)
+    except sim.MrsError as e:
+        assert e.code == -4, e
+        assert "could not load binary model" in str(e)
+    else:
+        raise AssertionError(".mjb must be rejected")
+    # a parse error of an XML path is MRS_ERR_LOAD
+    bad = tmp_path / "bad.xml"
+    bad.write_text("<mujoco><worldbody><body></mujoco>")
+    try:
+        sim.Model.load(bad)
+    except sim.MrsError as e:
+        assert e.code == -2, e
+    else:
+        raise AssertionError("malformed XML must fail")

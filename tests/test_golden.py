@@ -44,11 +44,22 @@ def gpu_rollout(scene, ids, steps, cps, period=10):
     return {k: np.stack(v, axis=1) for k, v in out.items()}, m
 
 
+# G = 16 workgroup layouts (batch.hip picks waves per workgroup and helper waves by batch size):
+# the C3 bench's four-wave layout without helpers, and C4's one-wave layout with and without them
+_LAYOUTS = {"auto": {}, "wpb4": {"MRS_G16_WPB": "4", "MRS_RAY_HELPERS": "0"},
+            "wpb1": {"MRS_G16_WPB": "1", "MRS_RAY_HELPERS": "0"},
+            "wpb1_help": {"MRS_G16_WPB": "1", "MRS_RAY_HELPERS": "1"}}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("group", [16, 64])
+@pytest.mark.parametrize("group, layout", [(16, k) for k in _LAYOUTS] + [(64, "auto")])
 @pytest.mark.parametrize("name", ["s2", "arm7"])
-def test_hip_matches_golden(name, group, built, monkeypatch):
+def test_hip_matches_golden(name, group, layout, built, monkeypatch):
     monkeypatch.setenv("MRS_GROUP", str(group))
+    for k in ("MRS_G16_WPB", "MRS_RAY_HELPERS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in _LAYOUTS[layout].items():
+        monkeypatch.setenv(k, v)
     import make_golden
     from mujoco_ros2_simulation_amd import sim
     scene, ids, steps, cps = make_golden.CASES[name]

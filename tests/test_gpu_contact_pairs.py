@@ -56,3 +56,35 @@ def test_reseeded_pairs():
     assert ncon.max() > 0
     assert not unexplained, unexplained[:5]
     assert wq <= 1e-5 and wv <= 1e-5
+
+
+# one body, two geoms: only the foot has an explicit pair with the floor.  The merge skips only that
+# geom pair, so the body's second geom (a knee sphere, lower than the foot) still gets its dynamic
+# floor contact (mj_collision merge [upstream; verify])
+TWO_GEOM_BODY = """<mujoco><option timestep="0.002" solver="PGS" iterations="50"/>
+<worldbody><geom name="floor" type="plane" size="0 0 1"/>
+<body name="leg" pos="0 0 0.12"><freejoint/>
+  <geom name="foot" type="box" size="0.1 0.05 0.03" pos="0.2 0 0"/>
+  <geom name="knee" type="sphere" size="0.06" pos="-0.2 0 -0.05"/></body>
+</worldbody>
+<contact><pair geom1="foot" geom2="floor" friction="0.5 0.5 0.01 0.001 0.001"/></contact>
+</mujoco>"""
+
+
+def test_explicit_pair_keeps_other_geoms_of_the_body():
+    model = sim.Model.from_string(TWO_GEOM_BODY)
+    cands = {tuple(sorted((int(a), int(b)))) for a, b in zip(model.pair_geom1, model.pair_geom2)}
+    assert cands == {(0, 2)}, cands              # floor-knee dynamic; floor-foot only explicit
+    b = sim.Batch(model, 4)
+    b.step(100)
+    q = b.get(sim.FIELD_QPOS)
+    b.forward()
+    g, _, _, _ = b.contacts(0)
+    d = binding.OracleData(model)
+    d.qpos[:] = q[0]
+    d.forward()
+    gr, _, _, _ = d.contacts()
+    assert np.array_equal(g, gr), (g.tolist(), gr.tolist())
+    pairs = {tuple(sorted(x)) for x in g.tolist()}
+    assert (0, 2) in pairs and (0, 1) in pairs, pairs  # the knee on the floor (dynamic) and the foot (explicit)
+    b.close()

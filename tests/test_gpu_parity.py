@@ -129,25 +129,69 @@ def _oracle_rollout_f32_state(model, qpos0, table, period, checkpoints):
 
 GROUPS = [16, 32, 64]   # lanes per env; the batch picks one from nv and the env count, tests force each
 
+# G = 16 workgroup layouts (batch.hip: waves per workgroup and helper waves are chosen per batch size).
+# "auto" is what the batch picks for the test's env count (one-wave + helpers below one wave per SIMD);
+# "wpb4" is the layout bench.py times on C3 (8192 envs: four-wave workgroups sharing the LDS ray
+# tables, no helper waves -- step_kernel<16,false,false,false>); "wpb1" / "wpb1_help" are C4's layout
+# without and with helper waves.  Other group widths have one layout.
+LAYOUTS = {"auto": {}, "wpb4": {"MRS_G16_WPB": "4", "MRS_RAY_HELPERS": "0"},
+           "wpb1": {"MRS_G16_WPB": "1", "MRS_RAY_HELPERS": "0"},
+           "wpb1_help": {"MRS_G16_WPB": "1", "MRS_RAY_HELPERS": "1"}}
+EXPECT = {"wpb4": (4, 0), "wpb1": (1, 0), "wpb1_help": (1, 1)}
 
-@pytest.mark.parametrize("group", GROUPS)
-@pytest.mark.parametrize("scene, n_envs, steps", [(REF_SCENE, 64, 1000), (ARM7, 16, 1000)])
-def test_rollout_parity(scene, n_envs, steps, group, monkeypatch):
+
+def _layout_cases():
+    out = []
+    for g in GROUPS:
+        for lay in (LAYOUTS if g == 16 else ["auto"]):
+            out.append(pytest.param(g, lay, id=f"{g}-{lay}"))
+    return out
+
+
+def _apply_layout(monkeypatch, group, layout):
     monkeypatch.setenv("MRS_GROUP", str(group))
+    for k in ("MRS_G16_WPB", "MRS_RAY_HELPERS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in LAYOUTS[layout].items():
+        monkeypatch.setenv(k, v)
+
+
+def _check_layout(model, n, group, layout, has_rays):
+    """the batch really runs the layout the case names (waves per workgroup, helper waves)"""
+    if layout not in EXPECT:
+        return
+    b = sim.Batch(model, n)
+    lay = b.layout()
+    b.close()
+    wpb, helpers = EXPECT[layout]
+    assert lay["group"] == group and lay["waves_per_workgroup"] == wpb, lay
+    assert lay["helper_waves"] == (helpers if has_rays else 0), lay
+
+
+@pytest.mark.parametrize("group, layout", _layout_cases())
+@pytest.mark.parametrize("scene, n_envs, steps", [(REF_SCENE, 64, 1000), (ARM7, 16, 1000)])
+def test_rollout_parity(scene, n_envs, steps, group, layout, monkeypatch):
+    _apply_layout(monkeypatch, group, layout)
     model = sim.Model.load(scene)
     envs = np.arange(n_envs)
     period = 10
     qpos0 = synth.initial_qpos(model, envs)
     table = synth.ctrl_table(model, envs, steps // period + 1, period)
     checkpoints = [1, 10, 100, steps]
+    has_rays = any(model.sensor_type[i] == sim.SENS_RANGEFINDER for i in range(model.nsensor))
+    _check_layout(model, n_envs, group, layout, has_rays)
     ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
     got = _gpu_rollout(model, qpos0, table, period, checkpoints)
+    _compare_rollout(model, scene.name, checkpoints, ref, got)
+
+
+def _compare_rollout(model, name, checkpoints, ref, got):
     for c in checkpoints:
         q_ref, v_ref, s_ref = ref[c]
         q, v, s = got[c]
         eq = np.max(np.abs(q - q_ref) / _scale(q_ref))
         ev = np.max(np.abs(v - v_ref) / _scale(v_ref))
-        print(f"{scene.name} step {c}: max rel err qpos {eq:.2e} qvel {ev:.2e}")
+        print(f"{name} step {c}: max rel err qpos {eq:.2e} qvel {ev:.2e}")
         assert eq <= RTOL, f"qpos rel err {eq} at step {c}"
         assert ev <= RTOL, f"qvel rel err {ev} at step {c}"
         rf = np.array([i for i in range(model.nsensor) if model.sensor_type[i] == sim.SENS_RANGEFINDER])
@@ -405,6 +449,39 @@ def test_full_size_c3_batch_properties():
     d.ctrl[:] = ctrl[0]
     d.step(100)
     np.testing.assert_allclose(q[0], d.qpos, rtol=RTOL, atol=RTOL)
+
+
+def test_full_size_c3_1000_steps_vs_oracle(monkeypatch):
+    """the exact kernel bench.py times on C3 (8192 envs: G = 16, four-wave workgroups with the shared
+    LDS ray tables, no helper waves) held to the 1000-step pin: 64 distinct envs (synthetic initial
+    states and Philox ctrl tables), tiled over the batch, against the oracle within 1e-5; every copy
+    of an env identical to the first wherever it sits"""
+    for k in ("MRS_GROUP", "MRS_G16_WPB", "MRS_RAY_HELPERS"):
+        monkeypatch.delenv(k, raising=False)
+    model = sim.Model.load(ARM7)
+    n, reps, steps, period = 8192, 64, 1000, 10
+    envs = np.arange(reps)
+    q0 = synth.initial_qpos(model, envs)
+    table = synth.ctrl_table(model, envs, steps // period + 1, period)
+    b = sim.Batch(model, n)
+    lay = b.layout()
+    assert lay["group"] == 16 and lay["waves_per_workgroup"] == 4 and lay["helper_waves"] == 0, lay
+    b.set(sim.FIELD_QPOS, np.tile(q0, (n // reps, 1)))
+    checkpoints = [1, 10, 100, steps]
+    got, t = {}, 0
+    for c in checkpoints:
+        while t < c:
+            b.set(sim.FIELD_CTRL, np.tile(table[t // period], (n // reps, 1)))
+            k = min(period - t % period, c - t)
+            b.step(k)
+            t += k
+        q, v, s = b.get(sim.FIELD_QPOS), b.get(sim.FIELD_QVEL), b.get(sim.FIELD_SENSORDATA)
+        for x in (q, v, s):
+            assert np.all(x.reshape(n // reps, reps, -1) == x[:reps][None]), c
+        got[c] = (q[:reps], v[:reps], s[:reps])
+    b.close()
+    ref = _oracle_rollout(model, q0, table, period, checkpoints)
+    _compare_rollout(model, "c3-8192", checkpoints, ref, got)
 
 
 def test_abi_errors_leave_batch_usable():
