@@ -1909,6 +1909,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   S.efc_fq = take(d.blocked ? ne : 0);
   S.efc_hdr = take(d.blocked ? 24 * ne : 0);  // step.hip kHdr
   S.efc_quad = take(d.blocked ? 64 : 0);
+  S.efc_fd = take(m.cone == MRS_CONE_ELLIPTIC && m.solver == MRS_SOL_PGS ? 2 * ne : 0);  // (16-byte aligned)
   S.stage = take(d.npair > 0 ? 64 * kMaxPairCon * 7 : 0);  // <= 64 lanes x 8 contacts x 7 floats
   S.efc_n = take(1);
   S.sens = take(std::max(1, m.nsensordata));

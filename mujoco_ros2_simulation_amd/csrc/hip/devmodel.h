@@ -64,6 +64,7 @@ struct ScratchLayout {
       efc_fq,                // blocked mode: row forces by record (global-record fallback path)
       efc_hdr,               // blocked mode: 8-float header of the item starting at a record
       efc_quad,              // blocked mode: per pipe, its first 16 items (record | rows << 16)
+      efc_fd,                // elliptic models: the PGS row forces in fp64 (2 floats per row)
       sens,                  // sensordata sink of idle lane groups (envs past n_envs)
       efc_n;                 // rows of the dense layout of the last forward (int bits; -1: none stored)
   int total;

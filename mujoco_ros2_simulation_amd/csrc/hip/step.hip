@@ -124,6 +124,16 @@ __device__ __forceinline__ float gsum(float v) {
   if constexpr (G == 64) v += __shfl_xor(v, 32);
   return v;
 }
+// fp64 group sum (the elliptic PGS sweep's residuals): a butterfly of lane swaps within the group, so
+// every lane adds the same two values and ends with the same bits (the asm keeps the caller's
+// product from being contracted into the first add, as in gsum)
+template <int G>
+__device__ __forceinline__ double gsum_d(double v) {
+  asm volatile("" : "+v"(v));
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, G);
+  return v;
+}
 template <int G>
 __device__ __forceinline__ int gscan_excl(int v, int glane, int& total) {
   int x = v;
@@ -4451,23 +4461,28 @@ __device__ __forceinline__ int ell_zone(float ft, float imp, const float D[3], c
   }
   return PST_CONE;
 }
-// mju_QCQP2 with its multiplier (oracle.c qcqp2_la)
-__device__ __forceinline__ float qcqp2_la(float res[2], const float A[4], const float b[2], float d, float r) {
-  const float b1 = b[0] * d, b2 = b[1] * d;
-  const float A11 = A[0] * d * d, A22 = A[3] * d * d, A12 = A[1] * d * d;
-  float la = 0, v1 = 0, v2 = 0;
+// mju_QCQP2 with its multiplier (oracle.c qcqp2_la).  The elliptic PGS block updates below run in
+// fp64 (the sweep keeps its iterate in fp64, constraints_dense): the split update converges slowly
+// enough that fp32 storage of the block forces alone leaves a noise floor of ~1e-4 in qvel
+// (scripts/diag_elliptic_round.py: rounding the oracle's iterate to fp32 moves qvel by 1.2e-4,
+// rounding its Delassus rows and b -- the solver's inputs -- by 2e-7), so the iterate, the residuals
+// and these updates take the oracle's precision and thresholds
+__device__ __forceinline__ double qcqp2_la(double res[2], const double A[4], const double b[2], double d, double r) {
+  const double b1 = b[0] * d, b2 = b[1] * d;
+  const double A11 = A[0] * d * d, A22 = A[3] * d * d, A12 = A[1] * d * d;
+  double la = 0, v1 = 0, v2 = 0;
   #pragma unroll 1
   for (int it = 0; it < 20; ++it) {
-    const float det = (A11 + la) * (A22 + la) - A12 * A12;
-    if (det < 1e-10f) { res[0] = res[1] = 0; return 0; }
-    const float di = 1 / det, P11 = (A22 + la) * di, P22 = (A11 + la) * di, P12 = -A12 * di;
+    const double det = (A11 + la) * (A22 + la) - A12 * A12;
+    if (det < 1e-10) { res[0] = res[1] = 0; return 0; }
+    const double di = 1 / det, P11 = (A22 + la) * di, P22 = (A11 + la) * di, P12 = -A12 * di;
     v1 = -P11 * b1 - P12 * b2;
     v2 = -P12 * b1 - P22 * b2;
-    const float val = v1 * v1 + v2 * v2 - r * r;
-    if (val < 1e-10f) break;
-    const float deriv = -2.0f * (P11 * v1 * v1 + 2.0f * P12 * v1 * v2 + P22 * v2 * v2);
-    const float delta = -val / deriv;
-    if (delta < 1e-10f) break;
+    const double val = v1 * v1 + v2 * v2 - r * r;
+    if (val < 1e-10) break;
+    const double deriv = -2.0 * (P11 * v1 * v1 + 2.0 * P12 * v1 * v2 + P22 * v2 * v2);
+    const double delta = -val / deriv;
+    if (delta < 1e-10) break;
     la += delta;
   }
   res[0] = v1 * d;
@@ -4475,18 +4490,18 @@ __device__ __forceinline__ float qcqp2_la(float res[2], const float A[4], const 
   return la;
 }
 // the exact minimiser of 1/2 y'Ay + y'c over |y_t| <= mu y_n (oracle.c ell_block_min): secant /
-// bisection on g'(s) = (A y + c)_n - la s with the QCQP inside; the bracket stops at fp32 resolution
-__device__ __forceinline__ void ell_block_min(const float A[9], const float c[3], float mu, float y[3]) {
-  const float At[4] = {A[4], A[5], A[7], A[8]};
-  float x[2];
-  float gp_lo = c[0] - mu * sqrtf(c[1] * c[1] + c[2] * c[2]), s_lo = 0, gp_hi = 0;
+// bisection on g'(s) = (A y + c)_n - la s with the QCQP inside
+__device__ __forceinline__ void ell_block_min(const double A[9], const double c[3], double mu, double y[3]) {
+  const double At[4] = {A[4], A[5], A[7], A[8]};
+  double x[2];
+  double gp_lo = c[0] - mu * sqrt(c[1] * c[1] + c[2] * c[2]), s_lo = 0, gp_hi = 0;
   if (gp_lo >= 0) { y[0] = y[1] = y[2] = 0; return; }
-  auto eval = [&](float s) {
-    const float bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
-    const float la = qcqp2_la(x, At, bc, mu, s);
+  auto eval = [&](double s) {
+    const double bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
+    const double la = qcqp2_la(x, At, bc, mu, s);
     return A[0] * s + A[1] * x[0] + A[2] * x[1] + c[0] - la * s;
   };
-  float s_hi = -c[0] / A[0];
+  double s_hi = -c[0] / A[0];
   if (!(s_hi > 0)) s_hi = 1;
   #pragma unroll 1
   for (int k = 0; k < 60; ++k) {
@@ -4496,17 +4511,15 @@ __device__ __forceinline__ void ell_block_min(const float A[9], const float c[3]
     s_hi *= 2;
   }
   #pragma unroll 1
-  for (int it = 0; it < 60 && s_hi - s_lo > 4e-7f * s_hi; ++it) {
-    float sn = s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo);
-    if (!(sn > s_lo + 0.01f * (s_hi - s_lo) && sn < s_hi - 0.01f * (s_hi - s_lo))) sn = 0.5f * (s_lo + s_hi);
-    const float gp = eval(sn);
-    if (gp == 0) { s_lo = s_hi = sn; gp_lo = gp_hi = 0; break; }
+  for (int it = 0; it < 100 && s_hi - s_lo > 1e-14 * (1 + s_hi); ++it) {
+    double sn = s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo);
+    if (!(sn > s_lo + 0.01 * (s_hi - s_lo) && sn < s_hi - 0.01 * (s_hi - s_lo))) sn = 0.5 * (s_lo + s_hi);
+    const double gp = eval(sn);
+    if (gp == 0) { s_lo = s_hi = sn; break; }
     if (gp < 0) { s_lo = sn; gp_lo = gp; } else { s_hi = sn; gp_hi = gp; }
   }
-  // the root of the final bracket's secant (the bracket itself stops at a few ulps of s)
-  float s = gp_hi > gp_lo ? s_lo - gp_lo * (s_hi - s_lo) / (gp_hi - gp_lo) : 0.5f * (s_lo + s_hi);
-  s = fminf(fmaxf(s, s_lo), s_hi);
-  const float bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
+  const double s = 0.5 * (s_lo + s_hi);
+  const double bc[2] = {c[1] + A[3] * s, c[2] + A[6] * s};
   qcqp2_la(x, At, bc, mu, s);
   y[0] = s; y[1] = x[0]; y[2] = x[1];
 }
@@ -4514,31 +4527,29 @@ __device__ __forceinline__ void ell_block_min(const float A[9], const float c[3]
 // mj_solPGS's split update of one elliptic block (oracle.c ell_pgs_split): a normal step (old normal
 // force 0) or the exact step along the ray of the old force (normal kept >= 0), then the friction by
 // mju_QCQP2 with the normal fixed
-__device__ __forceinline__ void ell_pgs_split(const float A[9], const float res[3], const float old[3], float mu,
-                                              float y[3]) {
+__device__ __forceinline__ void ell_pgs_split(const double A[9], const double res[3], const double old[3], double mu,
+                                              double y[3]) {
+  constexpr double kMin = 1e-15;
   y[0] = old[0]; y[1] = old[1]; y[2] = old[2];
-  if (A[0] < kMinVal) return;
-  if (old[0] < kMinVal) {
-    y[0] = fmaxf(old[0] - res[0] / A[0], 0.0f);
+  if (A[0] < kMin) return;
+  if (old[0] < kMin) {
+    y[0] = fmax(old[0] - res[0] / A[0], 0.0);
   } else {
-    float vAv = 0, vr = 0;
-    for (int k = 0; k < 3; ++k) {
-      const float Av = A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2];
-      vAv += old[k] * Av;
-      vr += old[k] * res[k];
-    }
-    if (vAv >= kMinVal) {
-      float x = -vr / vAv;
-      if (old[0] + x * old[0] < 0) x = -1.0f;
+    double Av[3], vAv = 0, vr = 0;
+    for (int k = 0; k < 3; ++k) Av[k] = A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2];
+    for (int k = 0; k < 3; ++k) { vAv += old[k] * Av[k]; vr += old[k] * res[k]; }
+    if (vAv >= kMin) {
+      double x = -vr / vAv;
+      if (old[0] + x * old[0] < 0) x = -1.0;
       for (int k = 0; k < 3; ++k) y[k] = old[k] + x * old[k];
     }
   }
-  if (y[0] < kMinVal) { y[0] = fmaxf(y[0], 0.0f); y[1] = y[2] = 0; return; }
-  const float At[4] = {A[4], A[5], A[7], A[8]};
-  const float dn = y[0] - old[0];
-  const float bt[2] = {res[1] + A[3] * dn - (A[4] * old[1] + A[5] * old[2]),
-                       res[2] + A[6] * dn - (A[7] * old[1] + A[8] * old[2])};
-  float x[2];
+  if (y[0] < kMin) { y[0] = fmax(y[0], 0.0); y[1] = y[2] = 0; return; }
+  const double At[4] = {A[4], A[5], A[7], A[8]};
+  const double dn = y[0] - old[0];
+  const double bt[2] = {res[1] + A[3] * dn - (A[4] * old[1] + A[5] * old[2]),
+                        res[2] + A[6] * dn - (A[7] * old[1] + A[8] * old[2])};
+  double x[2];
   qcqp2_la(x, At, bt, mu, y[0]);
   y[1] = x[0]; y[2] = x[1];
 }
@@ -5940,38 +5951,88 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_n
   }
   // --- PGS sweeps (rows serial, dot products across lanes)
   int nit = 0;  // sweeps done (mjData.solver_niter)
+  if (m.cone == MRS_CONE_ELLIPTIC) {
+    // elliptic models: the sweeps keep qacc, the residuals and the row forces in fp64 (the split block
+    // update's slow convergence carries fp32 rounding of its iterate into the result, qcqp2_la); the
+    // solver's inputs (J, M^-1 J', the Delassus entries, aref, R) stay the fp32 ones built above
+    typedef __attribute__((address_space(1))) double gdouble;
+    gdouble* fd = (gdouble*)(scr + S.efc_fd);
+    #pragma unroll 1
+    for (int r = lane; r < nefc; r += G) fd[r] = ff[r];
+    wsync();
+    double qd = lane < nv ? static_cast<double>(qa) : 0.0;
+    #pragma unroll 1
+    for (int it = 0; it < m.iterations; ++it) {
+      double improvement = 0;
+      #pragma unroll 1
+      for (int r = 0; r < nefc; ++r) {
+        if (ell_start(m, type, floss, r)) {
+          // elliptic block: mj_solPGS's split update (ell_pgs_split), or with the opt-in
+          // MRS_RESTATE_PGS_ELLIPTIC_BLOCK the exact minimiser of the block's local cost over the cone
+          // (ell_block_min; oracle.c fwd_constraint)
+          double res[3], A[9], old[3], c[3], y[3];
+          for (int k = 0; k < 3; ++k) {
+            old[k] = fd[r + k];
+            res[k] = gsum_d<G>(lane < nv ? static_cast<double>(J[(r + k) * nv + lane]) * qd : 0.0) - aref[r + k] +
+                     static_cast<double>(Rr[r + k]) * old[k];
+            A[4 * k] = ARii[r + k];
+          }
+          for (int a = 0; a < 3; ++a)
+            for (int b = a + 1; b < 3; ++b)
+              A[3 * a + b] = A[3 * b + a] = gsum<G>(lane < nv ? J[(r + a) * nv + lane] * MJ[(r + b) * nv + lane] : 0.0f);
+          for (int k = 0; k < 3; ++k) c[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
+          if (m.restate & MRS_RESTATE_PGS_ELLIPTIC_BLOCK) ell_block_min(A, c, ell_friction(m, scr, type, r), y);
+          else ell_pgs_split(A, res, old, ell_friction(m, scr, type, r), y);
+          double dl[3], quad = 0;
+          for (int k = 0; k < 3; ++k) dl[k] = y[k] - old[k];
+          for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) quad += dl[a] * A[3 * a + b] * dl[b];
+          if (lane < nv)
+            qd += static_cast<double>(MJ[r * nv + lane]) * dl[0] + static_cast<double>(MJ[(r + 1) * nv + lane]) * dl[1] +
+                  static_cast<double>(MJ[(r + 2) * nv + lane]) * dl[2];
+          if (lane == 0) { fd[r] = y[0]; fd[r + 1] = y[1]; fd[r + 2] = y[2]; }
+          improvement -= dl[0] * res[0] + dl[1] * res[1] + dl[2] * res[2] + 0.5 * quad;
+          wsync();
+          r += 2;
+          continue;
+        }
+        const double jq = gsum_d<G>(lane < nv ? static_cast<double>(J[r * nv + lane]) * qd : 0.0);
+        const double f0 = fd[r];
+        const double res = jq - aref[r] + static_cast<double>(Rr[r]) * f0;
+        const double a = ARii[r];
+        double nf = f0 - res / a;
+        const int t = __float_as_int(type[r]) >> 16;
+        if (fric_like(t)) nf = fmin(fmax(nf, -static_cast<double>(floss[r])), static_cast<double>(floss[r]));
+        else if (nf < 0) nf = 0;
+        const double delta = nf - f0;
+        if (delta != 0) {
+          if (lane < nv) qd += static_cast<double>(MJ[r * nv + lane]) * delta;
+          if (lane == 0) fd[r] = nf;
+        }
+        improvement -= delta * res + 0.5 * delta * delta * a;
+        wsync();
+      }
+      nit = it + 1;
+      if (improvement * m.pgs_scale < m.tolerance) break;
+    }
+    if (lane == 0) s[L.niter] = __int_as_float(nit);
+    // qfrc_constraint = J' f; the row forces exported in fp32 (mrs_batch_get_efc)
+    if (lane < nv) {
+      double v = 0;
+      #pragma unroll 1
+      for (int r = 0; r < nefc; ++r) v += static_cast<double>(J[r * nv + lane]) * fd[r];
+      s[L.qfrc_con + lane] = static_cast<float>(v);
+    }
+    #pragma unroll 1
+    for (int r = lane; r < nefc; r += G) ff[r] = static_cast<float>(fd[r]);
+    wsync();
+    return static_cast<float>(qd);
+  }
   #pragma unroll 1
   for (int it = 0; it < m.iterations; ++it) {
     float improvement = 0;
     #pragma unroll 1
     for (int r = 0; r < nefc; ++r) {
-      if (ell_start(m, type, floss, r)) {
-        // elliptic block: mj_solPGS's split update (ell_pgs_split), or with the opt-in
-        // MRS_RESTATE_PGS_ELLIPTIC_BLOCK the exact minimiser of the block's local cost over the cone
-        // (ell_block_min; oracle.c fwd_constraint)
-        float res[3], A[9], old[3], c[3], y[3];
-        for (int k = 0; k < 3; ++k) {
-          old[k] = ff[r + k];
-          res[k] = gsum<G>(lane < nv ? J[(r + k) * nv + lane] * qa : 0.0f) - aref[r + k] + Rr[r + k] * old[k];
-          A[4 * k] = ARii[r + k];
-        }
-        for (int a = 0; a < 3; ++a)
-          for (int b = a + 1; b < 3; ++b)
-            A[3 * a + b] = A[3 * b + a] = gsum<G>(lane < nv ? J[(r + a) * nv + lane] * MJ[(r + b) * nv + lane] : 0.0f);
-        for (int k = 0; k < 3; ++k) c[k] = res[k] - (A[3 * k] * old[0] + A[3 * k + 1] * old[1] + A[3 * k + 2] * old[2]);
-        if (m.restate & MRS_RESTATE_PGS_ELLIPTIC_BLOCK) ell_block_min(A, c, ell_friction(m, scr, type, r), y);
-        else ell_pgs_split(A, res, old, ell_friction(m, scr, type, r), y);
-        float dl[3], quad = 0;
-        for (int k = 0; k < 3; ++k) dl[k] = y[k] - old[k];
-        for (int a = 0; a < 3; ++a)
-          for (int b = 0; b < 3; ++b) quad += dl[a] * A[3 * a + b] * dl[b];
-        if (lane < nv) qa += MJ[r * nv + lane] * dl[0] + MJ[(r + 1) * nv + lane] * dl[1] + MJ[(r + 2) * nv + lane] * dl[2];
-        if (lane == 0) { ff[r] = y[0]; ff[r + 1] = y[1]; ff[r + 2] = y[2]; }
-        improvement -= dl[0] * res[0] + dl[1] * res[1] + dl[2] * res[2] + 0.5f * quad;
-        wsync();
-        r += 2;
-        continue;
-      }
       const float jq = gsum<G>(lane < nv ? J[r * nv + lane] * qa : 0.0f);
       const float f0 = ff[r];
       const float res = jq - aref[r] + Rr[r] * f0;

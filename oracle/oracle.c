@@ -2672,6 +2672,16 @@ static void fwd_constraint(const mrs_model_view* m, orc_data* d) {
     for (int j = 0; j < nv; ++j) v += w->efc_J[(size_t)r * nv + j] * w->qacc_smooth[j];
     w->efc_b[r] = v - w->efc_aref[r];
   }
+  {
+    /* diagnostics (scripts only): ORC_ROUND_AR=1 rounds the Delassus rows and b to fp32 (the device's
+     * precision of the solver's inputs) while the iterate stays fp64 */
+    static int rnd_ar = -1;
+    if (rnd_ar < 0) rnd_ar = getenv("ORC_ROUND_AR") != NULL;
+    if (rnd_ar) {
+      for (size_t i = 0; i < (size_t)nefc * nefc; ++i) w->AR[i] = (float)w->AR[i];
+      for (int r = 0; r < nefc; ++r) w->efc_b[r] = (float)w->efc_b[r];
+    }
+  }
   double* f = w->efc_force;
   memset(f, 0, nefc * sizeof(double));
   if (!(m->disableflags & MRS_DSBL_WARMSTART)) {

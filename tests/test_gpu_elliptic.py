@@ -36,6 +36,7 @@ def elliptic_scene(name: str, solver: str, impratio: float = 1.0, tol: str = "")
                          [("arm_boxes", "PGS", 1.0, 16, "", 0), ("arm_boxes", "PGS", 1.0, 16, "", sim.RESTATE_PGS_ELLIPTIC_BLOCK),
                           ("arm_boxes", "Newton", 3.0, 8, "", 0), ("arm_boxes", "Newton", 3.0, 8, "", sim.RESTATE_NEWTON_REFINE),
                           ("arm_boxes", "CG", 1.0, 8, "", 0), ("mobile_base", "PGS", 1.0, 32, "0", 0),
+                          ("mobile_base", "PGS", 1.0, 32, "", 0),
                           ("mobile_base", "PGS", 1.0, 32, "0", sim.RESTATE_PGS_ELLIPTIC_BLOCK),
                           ("mobile_base", "Newton", 10.0, 32, "", 0)])
 def test_reseeded_elliptic(scene, solver, imp, n, tol, restate):
@@ -45,13 +46,12 @@ def test_reseeded_elliptic(scene, solver, imp, n, tol, restate):
     and without the opt-in refinement step.  The mobile base's PGS converges within its 50 sweeps, so
     MuJoCo's improvement test (1e-8) ends it, and fp32 / fp64 can cross that threshold one sweep apart:
     tolerance 0 runs all 50 sweeps on both sides, separating the arithmetic from the stop rule (as
-    test_gpu_solvers.test_reseeded_step_parity does for C5).  Those two cases carry measured bounds:
-    the 50 unconverged sweeps carry the fp32 resolution of every block step --
-      * split update: rounding the oracle's own block forces to fp32 after every update (ORC_ROUND_PGS,
-        scripts/diag_elliptic_round.py) moves qvel by 1.2e-4 over the same 32 envs x 40 steps, so the
-        device's fp32 iterates cannot be held closer than that: bound 2e-4 (measured 8.7e-5);
-      * exact block step: the fp32 block minimiser resolves each normal force to ~4e-7 relative:
-        bound 2e-5 (measured 1.4e-5)."""
+    test_gpu_solvers.test_reseeded_step_parity does for C5); the default tolerance is run too.  The
+    elliptic sweeps keep their iterate, residuals and block updates in fp64 on the device
+    (step.hip constraints_dense): the split update converges so slowly on the mobile base that fp32
+    storage of the block forces alone moved qvel by 1.2e-4 (scripts/diag_elliptic_round.py rounds the
+    oracle's iterate to fp32: 1.2e-4; its Delassus rows and b, the solver's fp32 inputs: 2e-7) -- with
+    an fp32 iterate the device measured 8.7e-5 here (round 5)."""
     model = elliptic_scene(scene, solver, imp, tol)
     model.set_restate(restate)
     wq, wv, ncon, flips, unexplained = _reseeded(model, n, 40)
@@ -60,10 +60,7 @@ def test_reseeded_elliptic(scene, solver, imp, n, tol, restate):
     assert ncon.max() > 0
     assert flips <= max(1, 0.01 * n * 40)
     assert not unexplained, unexplained[:5]
-    tol_v = RTOL
-    if (scene, solver) == ("mobile_base", "PGS"):
-        tol_v = 2 * RTOL if restate else 2e-4
-    assert wq <= RTOL and wv <= tol_v
+    assert wq <= RTOL and wv <= RTOL
 
 
 def test_elliptic_forces_match_oracle():

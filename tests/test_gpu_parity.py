@@ -22,10 +22,15 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
 
-def _oracle_rollout(model, qpos0, table, period, checkpoints):
-    """Per-env oracle rollout returning qpos/qvel/sensordata at each checkpoint (steps)."""
+def _oracle_rollout(model, qpos0, table, period, checkpoints, pre=None):
+    """Per-env oracle rollout returning qpos/qvel/sensordata at each checkpoint (steps).  With `pre`
+    (a dict), pre[c] receives each env's qpos at the start of step c - 1: mj_step evaluates the
+    sensors in its forward() before integrating, so that is the pose the checkpoint's sensordata
+    (rangefinder scans) was computed at."""
     n = qpos0.shape[0]
     out = {c: (np.zeros((n, model.nq)), np.zeros((n, model.nv)), np.zeros((n, model.nsensordata))) for c in checkpoints}
+    if pre is not None:
+        pre.update({c: np.zeros((n, model.nq)) for c in checkpoints})
     for e in range(n):
         d = binding.OracleData(model)
         d.qpos[:] = qpos0[e]
@@ -34,6 +39,8 @@ def _oracle_rollout(model, qpos0, table, period, checkpoints):
             while t < c:
                 if t % period == 0:
                     d.ctrl[:] = table[t // period, e]
+                if pre is not None and t == c - 1:
+                    pre[c][e] = d.qpos
                 d.step()
                 t += 1
             out[c][0][e] = d.qpos
@@ -180,12 +187,13 @@ def test_rollout_parity(scene, n_envs, steps, group, layout, monkeypatch):
     checkpoints = [1, 10, 100, steps]
     has_rays = any(model.sensor_type[i] == sim.SENS_RANGEFINDER for i in range(model.nsensor))
     _check_layout(model, n_envs, group, layout, has_rays)
-    ref = _oracle_rollout(model, qpos0, table, period, checkpoints)
+    pre = {}
+    ref = _oracle_rollout(model, qpos0, table, period, checkpoints, pre)
     got = _gpu_rollout(model, qpos0, table, period, checkpoints)
-    _compare_rollout(model, scene.name, checkpoints, ref, got)
+    _compare_rollout(model, scene.name, checkpoints, ref, got, pre)
 
 
-def _compare_rollout(model, name, checkpoints, ref, got):
+def _compare_rollout(model, name, checkpoints, ref, got, pre):
     for c in checkpoints:
         q_ref, v_ref, s_ref = ref[c]
         q, v, s = got[c]
@@ -207,8 +215,8 @@ def _compare_rollout(model, name, checkpoints, ref, got):
         assert np.median(err[hit]) < 1e-6
         # every outlier and every hit/miss flip is a grazing ray: within 1e-4 rad of a silhouette
         bad = np.argwhere(flip | (err > 2e-5))
-        for e, k in bad:
-            assert _grazing(model, q_ref[e], rf[k]), (c, e, k, s[e, adr[k]], s_ref[e, adr[k]])
+        for e, k in bad:  # (at the pose the scan was taken at: the start of the checkpoint's last step)
+            assert _grazing(model, pre[c][e], rf[k]), (c, e, k, s[e, adr[k]], s_ref[e, adr[k]])
         print(f"  {len(bad)} rangefinder outliers / flips, all grazing a silhouette")
 
 
@@ -480,8 +488,9 @@ def test_full_size_c3_1000_steps_vs_oracle(monkeypatch):
             assert np.all(x.reshape(n // reps, reps, -1) == x[:reps][None]), c
         got[c] = (q[:reps], v[:reps], s[:reps])
     b.close()
-    ref = _oracle_rollout(model, q0, table, period, checkpoints)
-    _compare_rollout(model, "c3-8192", checkpoints, ref, got)
+    pre = {}
+    ref = _oracle_rollout(model, q0, table, period, checkpoints, pre)
+    _compare_rollout(model, "c3-8192", checkpoints, ref, got, pre)
 
 
 def test_abi_errors_leave_batch_usable():
