@@ -145,6 +145,25 @@ __device__ __forceinline__ int gscan_excl(int v, int glane, int& total) {
   total = __shfl(x, G - 1, G);
   return x - v;
 }
+// the same exclusive group scan for small non-negative values (< 2^kBits): one ballot per bit and a
+// masked lane count (v_mbcnt) -- no LDS round trips (the shuffles above are ds_bpermute chains), and
+// lanes outside the exec mask count as 0
+template <int G, int kBits>
+__device__ __forceinline__ int gscan_excl_small(int v, int& total) {
+  const int base = __lane_id() & ~(G - 1);
+  const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << (G & 63)) - 1) << base);
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < kBits; ++b) {
+    const unsigned long long bal = __ballot((v >> b) & 1) & gmask;
+    off += static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0u)))
+           << b;
+    tot += __popcll(bal) << b;
+  }
+  total = tot;
+  return off;
+}
 // value of lane `src` of the caller's group, in every lane of the group: one readlane per group and
 // a per-lane select (readlane reads a lane's register whatever the exec mask, and each group only
 // selects its own group's value)
@@ -2524,7 +2543,8 @@ __device__ MRS_PHASE int collision(ENV_PARAMS) {
     SUB_ADD(PH_COLL_NARROW, t_np);
     unsigned long long t_out = SUB_T();
     int total;
-    int off = gscan_excl<G>(n, lane, total);
+    static_assert(kMaxPairCon < 16, "contacts per pair must fit the 4-bit scan");
+    int off = gscan_excl_small<G, 4>(n, total);  // (n <= kMaxPairCon = 8)
     if constexpr (G == 64) {
       // the next staged contact is loaded before this one's record is stored: a staging load issued
       // after a store would wait for it (vmcnt counts stores too), one store round trip per contact
@@ -5587,7 +5607,7 @@ __device__ int dense_rows(ENV_PARAMS, int ncon) {
         cnt = (int)act[0] + (int)act[1];
       }
       int total;
-      int off = gscan_excl<G>(cnt, lane, total);
+      int off = gscan_excl_small<G, 2>(cnt, total);  // (cnt <= 2)
       int r = nefc + off;
       for (int sd = 0; sd < 2; ++sd) {
         if (!act[sd]) continue;
@@ -6761,9 +6781,21 @@ __device__ MRS_PHASE bool any_bad(ENV_PARAMS, int off, int n) {
   return gany<G>(bad);
 }
 
-// full forward pass; returns qacc (lane per dof)
+// mj_checkPos / mj_checkVel of the step loop: a vector of at most G entries is one LDS read per lane and
+// a group vote, inline; longer ones take any_bad.  (The step loop keeps these checks off out-of-line
+// calls: a call starts with the ABI's s_waitcnt vmcnt(0), which at the step boundary waited for the
+// step's sensordata stores to land -- inlining the loop of any_bad instead cost C3 3 % in spills.)
+template <int G>
+__device__ __forceinline__ bool any_bad_step(ENV_PARAMS, int off, int n) {
+  if (n <= G) return gany<G>(lane < n && is_bad(s[off + lane]));
+  return any_bad<G>(ENV_ARGS, off, n);
+}
+
+// full forward pass; returns the contact count.  With acc_bad, *acc_bad is the group's vote on qacc
+// (mj_checkAcc), taken from the solver's lane-per-dof result in registers
 template <int G, bool kPrimal = false>
-__device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bool helper = false) {
+__device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bool helper = false,
+                                 bool* acc_bad = nullptr) {
   ENV_UNPACK;
   if constexpr (G == 64) sensordata = uniform_ptr(sensordata);
   PH_BEGIN();
@@ -6810,6 +6842,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = (constraints<G, kPrimal>(ENV_ARGS, ncon, qacc_s, pre_nefc)));
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
+  if (acc_bad) *acc_bad = gany<G>(lane < m.nv && is_bad(qacc));
   wsync();
   // sensordata == nullptr: mj_forwardSkip(skipsensor) (the RK4 stages)
   if (sensordata) {
@@ -7136,7 +7169,10 @@ template <int G>
 #ifndef MRS_G64_WAVES
 #define MRS_G64_WAVES 2
 #endif
-struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? 2 : 1)); };
+#ifndef MRS_G16_OCC
+#define MRS_G16_OCC 2
+#endif
+struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 32 ? 4 : (G == 16 ? MRS_G16_OCC : 1)); };
 
 // kHelpers: the G = 16 step kernel with ray helper waves (DevState::ray_helpers; its own instantiation,
 // so the kernels without helpers keep their code and registers -- the run-time switch alone cost C3 5%)
@@ -7266,11 +7302,11 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 #endif
   for (int step = 0; step < n_steps; ++step) {
     if (!kForwardOnly) {
-      if (any_bad<G>(ENV_ARGS, L.qpos, m.nq)) {
+      if (any_bad_step<G>(ENV_ARGS, L.qpos, m.nq)) {
         ++w_pos;
         if (!(m.disableflags & MRS_DSBL_AUTORESET)) { [[clang::noinline]] reset_env<G>(ENV_ARGS); time = 0; }
       }
-      if (any_bad<G>(ENV_ARGS, L.qvel, m.nv)) {
+      if (any_bad_step<G>(ENV_ARGS, L.qvel, m.nv)) {
         ++w_vel;
         if (!(m.disableflags & MRS_DSBL_AUTORESET)) { [[clang::noinline]] reset_env<G>(ENV_ARGS); time = 0; }
       }
@@ -7281,7 +7317,8 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 #else
     gfloat* sd_step = sensordata;
 #endif
-    MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG, helpers)));
+    bool acc_bad = false;
+    MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG, helpers, &acc_bad)));
     if (helpers) helper_barrier(false);  // barrier B: this step's rays are stored
 #if MRS_EXT
     // rangefinders of a model with more than 32 ray geoms (sensors() leaves them to this call)
@@ -7290,7 +7327,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
 #endif
     if (kForwardOnly) break;
     bool redo = false;
-    if (any_bad<G>(ENV_ARGS, L.qacc, m.nv)) {
+    if (acc_bad) {
       ++w_acc;
       if (!(m.disableflags & MRS_DSBL_AUTORESET)) {
         [[clang::noinline]] reset_env<G>(ENV_ARGS);
