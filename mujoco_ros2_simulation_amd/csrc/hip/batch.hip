@@ -1506,6 +1506,45 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   P.addf(&d.bodytab, bodytab);
   P.addf(&d.mpairtab, mpairtab);
+  // kinematics tables (step.hip body_pose / body_frame_out / kinematics / com_pos), staged in workgroup
+  // LDS with lane groups: per body (25 floats) pos[3], quat[4], ipos[3], iquat[4], inertia[3], first
+  // joint, joint count (int bits), pad; per joint (13) pos[3], axis[3], qpos address, type, qpos0 of
+  // the address, body, dof address, the body's root (int bits), pad; per geom (9) body (int bits),
+  // pos[3], quat[4], pad
+  {
+    auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
+    std::vector<float> kb, kj, kg;
+    for (int b = 0; b < m.nbody; ++b) {
+      for (int i = 0; i < 3; ++i) kb.push_back(static_cast<float>(m.body_pos[3 * b + i]));
+      for (int i = 0; i < 4; ++i) kb.push_back(static_cast<float>(m.body_quat[4 * b + i]));
+      for (int i = 0; i < 3; ++i) kb.push_back(static_cast<float>(m.body_ipos[3 * b + i]));
+      for (int i = 0; i < 4; ++i) kb.push_back(static_cast<float>(m.body_iquat[4 * b + i]));
+      for (int i = 0; i < 3; ++i) kb.push_back(static_cast<float>(m.body_inertia[3 * b + i]));
+      kb.push_back(fbits(m.body_jntadr[b]));
+      kb.push_back(fbits(m.body_jntnum[b]));
+      while (kb.size() % 25) kb.push_back(0.0f);
+    }
+    for (int j = 0; j < m.njnt; ++j) {
+      for (int i = 0; i < 3; ++i) kj.push_back(static_cast<float>(m.jnt_pos[3 * j + i]));
+      for (int i = 0; i < 3; ++i) kj.push_back(static_cast<float>(m.jnt_axis[3 * j + i]));
+      kj.push_back(fbits(m.jnt_qposadr[j]));
+      kj.push_back(fbits(m.jnt_type[j]));
+      kj.push_back(static_cast<float>(m.qpos0[m.jnt_qposadr[j]]));
+      kj.push_back(fbits(m.jnt_bodyid[j]));
+      kj.push_back(fbits(m.jnt_dofadr[j]));
+      kj.push_back(fbits(m.body_rootid[m.jnt_bodyid[j]]));
+      while (kj.size() % 13) kj.push_back(0.0f);
+    }
+    for (int g = 0; g < m.ngeom; ++g) {
+      kg.push_back(fbits(m.geom_bodyid[g]));
+      for (int i = 0; i < 3; ++i) kg.push_back(static_cast<float>(m.geom_pos[3 * g + i]));
+      for (int i = 0; i < 4; ++i) kg.push_back(static_cast<float>(m.geom_quat[4 * g + i]));
+      kg.push_back(0.0f);
+    }
+    P.addf(&d.kinbody, kb);
+    P.addf(&d.kinjnt, kj);
+    P.addf(&d.kingeom, kg);
+  }
   // the non-ray sensors' descriptors, 16 floats each (staged in workgroup LDS at shr_sens): type,
   // objtype, sensordata address, dim (int bits), cutoff, the object's qpos / dof / actuator / body
   // index (int bits), the root body (int bits), then the site's or geom's local pos[3] and quat[4]
@@ -1798,11 +1837,14 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
     d.shr_body = d.shr_dof + 16 * m.nv;
     d.shr_mpair = d.shr_body + 8 * m.nbody;
     d.shr_jump = d.shr_mpair + 4 * d.nMpair;
+    d.shr_kbody = d.shr_jump + d.njump * m.nbody;
+    d.shr_kjnt = d.shr_kbody + 25 * m.nbody;
+    d.shr_kgeom = d.shr_kjnt + 13 * m.njnt;
     // the smooth-dynamics tables (from shr_act on) are staged only by lane-group kernels (G < 64);
     // blocked mode (one env per workgroup) reads them from the model block instead of paying their
     // LDS per env
     shr_small = d.shr_act;
-    d.shr_total = d.shr_jump + d.njump * m.nbody;
+    d.shr_total = d.shr_kgeom + 9 * m.ngeom;
     d.shr_flag = d.shr_total;  // (helper waves' signal words, one per physics wave)
     d.shr_total += 4;
   };

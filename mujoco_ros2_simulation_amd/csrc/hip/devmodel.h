@@ -111,6 +111,9 @@ struct DevModel {
   // tree tables (bodytab, 8 floats per body; mpairtab, 4 floats per pair of M) at shr_body, shr_mpair
   int shr_body, shr_mpair;
   int shr_jump;  // the kinematics' pointer-jumping table (jump, int bits) with lane groups
+  // kinematics tables (kinbody 25, kinjnt 13, kingeom 9 floats per entry; odd strides: lanes reading
+  // consecutive entries hit distinct LDS banks) at shr_kbody, shr_kjnt, shr_kgeom with lane groups
+  int shr_kbody, shr_kjnt, shr_kgeom;
   int shr_flag;  // helper waves: per physics wave (4 words) its count of com_pos passes this launch (int bits)
   unsigned rf_static_mask;
   float* rf_static;
@@ -187,6 +190,7 @@ struct DevModel {
   CPtr<float> fricrec, limrec;  // 4 floats per friction-loss dof / limited joint (batch.hip)
   CPtr<float> actrec, dofrec;   // smooth-force tables (batch.hip)
   CPtr<float> bodytab, mpairtab;  // tree tables of the smooth dynamics (batch.hip)
+  CPtr<float> kinbody, kinjnt, kingeom;  // kinematics tables (batch.hip; step.hip kin_body / kin_jnt / kin_geom)
   // ray-visible geoms (rgba alpha != 0, what mj_ray tests), packed 8 floats per geom so one wide
   // scalar load fetches a record: geom id, type, body (int bits), rbound, size[3], pad
   CPtr<float> rgeom;

@@ -1881,17 +1881,33 @@ template <int G>
 __device__ __forceinline__ auto mpair_tab(const DevModel& m, int p) {
   if constexpr (G == 64) return m.mpairtab + 4 * p; else return shared_lds(m) + m.shr_mpair + 4 * p;
 }
+// kinematics tables (batch.hip kinbody / kinjnt / kingeom): from workgroup LDS with lane groups -- the
+// per-lane model reads of the kinematics were global loads, which wait (vmcnt counts stores too) for
+// the previous step's sensordata stores -- from the model block in blocked mode
+template <int G>
+__device__ __forceinline__ auto kin_body(const DevModel& m, int b) {
+  if constexpr (G == 64) return m.kinbody + 25 * b; else return shared_lds(m) + m.shr_kbody + 25 * b;
+}
+template <int G>
+__device__ __forceinline__ auto kin_jnt(const DevModel& m, int j) {
+  if constexpr (G == 64) return m.kinjnt + 13 * j; else return shared_lds(m) + m.shr_kjnt + 13 * j;
+}
+template <int G>
+__device__ __forceinline__ auto kin_geom(const DevModel& m, int g) {
+  if constexpr (G == 64) return m.kingeom + 9 * g; else return shared_lds(m) + m.shr_kgeom + 9 * g;
+}
 
 // pose of body b from its parent's frame (P, Q): body offset, then its joints in order (mj_kinematics
 // per body).  With kJoints the world anchors/axes of the joints are written (P, Q must be the
 // parent's world frame then).  A free joint gives the world pose directly (its parent is the world).
-template <bool kJoints>
+template <int G, bool kJoints>
 __device__ __forceinline__ void body_pose(const DevModel& m, lfloat* s, int b, const float P[3], const float Q[4],
                                           float pos[3], float q[4]) {
   const LdsLayout& L = m.L;
-  const int ja = m.body_jntadr[b], nj = m.body_jntnum[b];
-  if (nj > 0 && m.jnt_type[ja] == MRS_JNT_FREE) {
-    const lfloat* qp = s + L.qpos + m.jnt_qposadr[ja];
+  const auto kb = kin_body<G>(m, b);
+  const int ja = __float_as_int(kb[17]), nj = __float_as_int(kb[18]);
+  if (nj > 0 && __float_as_int(kin_jnt<G>(m, ja)[7]) == MRS_JNT_FREE) {
+    const lfloat* qp = s + L.qpos + __float_as_int(kin_jnt<G>(m, ja)[6]);
     pos[0] = qp[0]; pos[1] = qp[1]; pos[2] = qp[2];
     q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
     quat_normalize(q);
@@ -1902,26 +1918,28 @@ __device__ __forceinline__ void body_pose(const DevModel& m, lfloat* s, int b, c
     }
     return;
   }
-  const float bpos[3] = {m.body_pos[3 * b], m.body_pos[3 * b + 1], m.body_pos[3 * b + 2]};
-  const float bq[4] = {m.body_quat[4 * b], m.body_quat[4 * b + 1], m.body_quat[4 * b + 2], m.body_quat[4 * b + 3]};
+  const float bpos[3] = {kb[0], kb[1], kb[2]};
+  const float bq[4] = {kb[3], kb[4], kb[5], kb[6]};
   float r[3];
   rot_quat(r, bpos, Q);
   for (int i = 0; i < 3; ++i) pos[i] = P[i] + r[i];
   quat_mul(q, Q, bq);
   #pragma unroll 1
   for (int k2 = 0; k2 < nj; ++k2) {
-    const int j = ja + k2, qa = m.jnt_qposadr[j];
-    const float jp[3] = {m.jnt_pos[3 * j], m.jnt_pos[3 * j + 1], m.jnt_pos[3 * j + 2]};
-    const float ja3[3] = {m.jnt_axis[3 * j], m.jnt_axis[3 * j + 1], m.jnt_axis[3 * j + 2]};
+    const int j = ja + k2;
+    const auto kj = kin_jnt<G>(m, j);
+    const int qa = __float_as_int(kj[6]);
+    const float jp[3] = {kj[0], kj[1], kj[2]};
+    const float ja3[3] = {kj[3], kj[4], kj[5]};
     float anc[3], ax[3];
     rot_quat(anc, jp, q);
     for (int i = 0; i < 3; ++i) anc[i] += pos[i];
     rot_quat(ax, ja3, q);
     if (kJoints)
       for (int i = 0; i < 3; ++i) { s[L.xanchor + 3 * j + i] = anc[i]; s[L.xaxis + 3 * j + i] = ax[i]; }
-    const int jt = m.jnt_type[j];
+    const int jt = __float_as_int(kj[7]);
     if (jt == MRS_JNT_SLIDE) {
-      const float dq = s[L.qpos + qa] - m.qpos0[qa];
+      const float dq = s[L.qpos + qa] - kj[8];
       for (int i = 0; i < 3; ++i) pos[i] += ax[i] * dq;
     } else {
       float ql[4];
@@ -1929,7 +1947,7 @@ __device__ __forceinline__ void body_pose(const DevModel& m, lfloat* s, int b, c
         for (int i = 0; i < 4; ++i) ql[i] = s[L.qpos + qa + i];
         quat_normalize(ql);
       } else {
-        axis_angle_quat(ql, ja3, s[L.qpos + qa] - m.qpos0[qa]);
+        axis_angle_quat(ql, ja3, s[L.qpos + qa] - kj[8]);
       }
       quat_mul(q, q, ql);
       float v[3];
@@ -1940,8 +1958,10 @@ __device__ __forceinline__ void body_pose(const DevModel& m, lfloat* s, int b, c
 }
 
 // body frame outputs: xpos, xquat, xmat, inertial frame and the rotational part of cinert
+template <int G>
 __device__ __forceinline__ void body_frame_out(const DevModel& m, lfloat* s, int b, const float pos[3], float q[4]) {
   const LdsLayout& L = m.L;
+  const auto kb = kin_body<G>(m, b);
   quat_normalize(q);
   float xm[9];
   quat2mat(xm, q);
@@ -1949,14 +1969,14 @@ __device__ __forceinline__ void body_frame_out(const DevModel& m, lfloat* s, int
   for (int i = 0; i < 4; ++i) s[L.xquat + 4 * b + i] = q[i];
   for (int i = 0; i < 9; ++i) s[L.xmat + 9 * b + i] = xm[i];
   // inertial frame; world-frame rotational inertia about the body com goes to cinert[0..5]
-  const float ip[3] = {m.body_ipos[3 * b], m.body_ipos[3 * b + 1], m.body_ipos[3 * b + 2]};
-  const float iq[4] = {m.body_iquat[4 * b], m.body_iquat[4 * b + 1], m.body_iquat[4 * b + 2], m.body_iquat[4 * b + 3]};
+  const float ip[3] = {kb[7], kb[8], kb[9]};
+  const float iq[4] = {kb[10], kb[11], kb[12], kb[13]};
   float r[3], qi[4], R[9];
   mat_vec(r, xm, ip);
   for (int i = 0; i < 3; ++i) s[L.xipos + 3 * b + i] = pos[i] + r[i];
   quat_mul(qi, q, iq);
   quat2mat(R, qi);
-  const float I0 = m.body_inertia[3 * b], I1 = m.body_inertia[3 * b + 1], I2 = m.body_inertia[3 * b + 2];
+  const float I0 = kb[14], I1 = kb[15], I2 = kb[16];
   lfloat* ci = s + L.cinert + 10 * b;
   ci[0] = R[0] * I0 * R[0] + R[1] * I1 * R[1] + R[2] * I2 * R[2];
   ci[1] = R[3] * I0 * R[3] + R[4] * I1 * R[4] + R[5] * I2 * R[5];
@@ -1978,7 +1998,7 @@ __device__ void kinematics_levels(ENV_PARAMS) {
   const float P0[3] = {0, 0, 0};
     if (lane == 0) {
       float q1[4] = {1, 0, 0, 0};
-      body_frame_out(m, s, 0, P0, q1);
+      body_frame_out<G>(m, s, 0, P0, q1);
     }
     wsync();
     for (int lev = 1; lev <= m.max_depth; ++lev) {
@@ -1990,8 +2010,8 @@ __device__ void kinematics_levels(ENV_PARAMS) {
         const float P[3] = {s[L.xpos + 3 * p], s[L.xpos + 3 * p + 1], s[L.xpos + 3 * p + 2]};
         const float Q[4] = {s[L.xquat + 4 * p], s[L.xquat + 4 * p + 1], s[L.xquat + 4 * p + 2], s[L.xquat + 4 * p + 3]};
         float pos[3], q[4];
-        body_pose<true>(m, s, b, P, Q, pos, q);
-        body_frame_out(m, s, b, pos, q);
+        body_pose<G, true>(m, s, b, P, Q, pos, q);
+        body_frame_out<G>(m, s, b, pos, q);
       }
       wsync();
     }
@@ -2004,7 +2024,7 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   if (m.nbody <= G) {
     const int b = lane;
     float pos[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0};
-    if (b >= 1 && b < m.nbody) body_pose<false>(m, s, b, P0, Q0, pos, q);
+    if (b >= 1 && b < m.nbody) body_pose<G, false>(m, s, b, P0, Q0, pos, q);
     if (b < m.nbody) {
       for (int i = 0; i < 3; ++i) s[L.xpos + 3 * b + i] = pos[i];
       for (int i = 0; i < 4; ++i) s[L.xquat + 4 * b + i] = q[i];
@@ -2042,11 +2062,11 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
     }
     wsync();
     if (b >= 1 && b < m.nbody) {
-      body_pose<true>(m, s, b, P, Q, pos, q);
-      body_frame_out(m, s, b, pos, q);
+      body_pose<G, true>(m, s, b, P, Q, pos, q);
+      body_frame_out<G>(m, s, b, pos, q);
     } else if (b == 0) {
       float q1[4] = {1, 0, 0, 0};
-      body_frame_out(m, s, 0, P0, q1);
+      body_frame_out<G>(m, s, 0, P0, q1);
     }
     wsync();
   } else {
@@ -2055,10 +2075,11 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
   // geoms
   #pragma unroll 1
   for (int g = lane; g < m.ngeom; g += G) {
-    const int b = m.geom_bodyid[g];
+    const auto kg = kin_geom<G>(m, g);
+    const int b = __float_as_int(kg[0]);
     float bq[4] = {s[L.xquat + 4 * b], s[L.xquat + 4 * b + 1], s[L.xquat + 4 * b + 2], s[L.xquat + 4 * b + 3]};
-    float gp[3] = {m.geom_pos[3 * g], m.geom_pos[3 * g + 1], m.geom_pos[3 * g + 2]};
-    float gq[4] = {m.geom_quat[4 * g], m.geom_quat[4 * g + 1], m.geom_quat[4 * g + 2], m.geom_quat[4 * g + 3]};
+    float gp[3] = {kg[1], kg[2], kg[3]};
+    float gq[4] = {kg[4], kg[5], kg[6], kg[7]};
     float r[3], q[4], gm[9];
     rot_quat(r, gp, bq);
     for (int i = 0; i < 3; ++i) s[L.gxpos + 3 * g + i] = s[L.xpos + 3 * b + i] + r[i];
@@ -2107,11 +2128,12 @@ __device__ MRS_PHASE void com_pos(ENV_PARAMS) {
   }
   #pragma unroll 1
   for (int j = lane; j < m.njnt; j += G) {
-    const int b = m.jnt_bodyid[j], rt = m.body_rootid[b];
-    int dof = m.jnt_dofadr[j];
+    const auto kj = kin_jnt<G>(m, j);
+    const int b = __float_as_int(kj[9]), rt = __float_as_int(kj[11]);
+    int dof = __float_as_int(kj[10]);
     float off[3];
     for (int i = 0; i < 3; ++i) off[i] = s[L.scom + 3 * rt + i] - s[L.xanchor + 3 * j + i];
-    const int jt = m.jnt_type[j];
+    const int jt = __float_as_int(kj[7]);
     if (jt == MRS_JNT_HINGE) {
       lfloat* cd = s + L.cdof + 6 * dof;
       float ax[3] = {s[L.xaxis + 3 * j], s[L.xaxis + 3 * j + 1], s[L.xaxis + 3 * j + 2]}, c[3];
@@ -7257,6 +7279,12 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
       for (int i = threadIdx.x; i < 4 * m.nMpair; i += blockDim.x) shr[m.shr_mpair + i] = m.mpairtab[i];
       #pragma unroll 1
       for (int i = threadIdx.x; i < m.njump * m.nbody; i += blockDim.x) shr[m.shr_jump + i] = __int_as_float(m.jump[i]);
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 25 * m.nbody; i += blockDim.x) shr[m.shr_kbody + i] = m.kinbody[i];
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 13 * m.njnt; i += blockDim.x) shr[m.shr_kjnt + i] = m.kinjnt[i];
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < 9 * m.ngeom; i += blockDim.x) shr[m.shr_kgeom + i] = m.kingeom[i];
     }
   }
   if (helpers && threadIdx.x < 4) *helper_flag(m, threadIdx.x) = 0;
