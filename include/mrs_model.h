@@ -53,7 +53,8 @@ enum { MRS_SENS_ACCELEROMETER = 1, MRS_SENS_GYRO = 3, MRS_SENS_FORCE = 4, MRS_SE
  * elliptic contact block exactly over its cone (mj_solPGS takes a normal / ray step, then the friction
  * by mju_QCQP2 with the normal fixed). */
 enum { MRS_RESTATE_NEWTON_REFINE = 1 << 0, MRS_RESTATE_PGS_ELLIPTIC_BLOCK = 1 << 1,
-       MRS_RESTATE_NO_MPR_POLISH = 1 << 2 /* diagnostics: keep MPR's own contact (no normal polish) */ };
+       MRS_RESTATE_NO_MPR_POLISH = 1 << 2, /* diagnostics: keep MPR's own contact (no normal polish) */
+       MRS_RESTATE_NO_MULTICCD = 1 << 3 /* diagnostics: one MPR contact for face-on polytope pairs too */ };
 /* disable flags (mjtDisableBit subset) */
 enum { MRS_DSBL_CONSTRAINT = 1 << 0, MRS_DSBL_EQUALITY = 1 << 1, MRS_DSBL_FRICTIONLOSS = 1 << 2,
        MRS_DSBL_LIMIT = 1 << 3, MRS_DSBL_CONTACT = 1 << 4, MRS_DSBL_PASSIVE = 1 << 5,
@@ -185,6 +186,15 @@ typedef struct mrs_model_view {
   const double *wrap_prm, *tendon_range /*2*/, *tendon_margin, *tendon_solref_lim /*2*/,
       *tendon_solimp_lim /*5*/, *tendon_frictionloss, *tendon_solref_fri /*2*/, *tendon_solimp_fri /*5*/,
       *tendon_stiffness, *tendon_damping, *tendon_lengthspring /*2*/, *tendon_invweight0, *tendon_length0;
+
+  /* the meshes' convex-hull faces as polygons (coplanar hull triangles merged; collision's face
+   * contacts): mesh k's polygons are [mesh_polyadr[k], + mesh_polynum[k]); polygon p
+   * has the outward unit normal mesh_polynormal[p] (mesh frame) and the vertex ids (relative to
+   * mesh_vertadr) mesh_polyvert[mesh_polyvertadr[p] .. + mesh_polyvertnum[p]), counter-clockwise
+   * about the normal */
+  int nmeshpoly, nmeshpolyvert;
+  const int *mesh_polyadr, *mesh_polynum, *mesh_polyvertadr, *mesh_polyvertnum, *mesh_polyvert;
+  const double *mesh_polynormal /*3*/;
 } mrs_model_view;
 
 #ifdef __cplusplus

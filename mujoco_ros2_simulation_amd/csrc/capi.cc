@@ -133,7 +133,9 @@ int mrs_model_view_get(const mrs_model* m, mrs_model_view* out) {
 int mrs_model_set_restate(mrs_model* m, int flags) {
   return guarded([&] {
     if (!m) throw std::invalid_argument("null model");
-    if (flags & ~(MRS_RESTATE_NEWTON_REFINE | MRS_RESTATE_PGS_ELLIPTIC_BLOCK | MRS_RESTATE_NO_MPR_POLISH)) throw std::invalid_argument("unknown restate bits");
+    if (flags & ~(MRS_RESTATE_NEWTON_REFINE | MRS_RESTATE_PGS_ELLIPTIC_BLOCK | MRS_RESTATE_NO_MPR_POLISH |
+                  MRS_RESTATE_NO_MULTICCD))
+      throw std::invalid_argument("unknown restate bits");
     m->m.restate = flags;
   });
 }

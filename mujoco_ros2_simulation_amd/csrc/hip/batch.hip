@@ -1308,6 +1308,9 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   P.addi(&d.mesh_hulladr, m.mesh_hulladr); P.addi(&d.mesh_hullnum, m.mesh_hullnum); P.addi(&d.mesh_face, bvh_face);
   P.addi(&d.mesh_bvhadr, bvh_adr); P.addi(&d.mesh_bvhnum, bvh_num); P.addf(&d.mesh_bvh, bvh_node);
   P.addi(&d.mesh_hull, m.mesh_hull); P.addf(&d.mesh_vert, m.mesh_vert);
+  P.addi(&d.mesh_polyadr, m.mesh_polyadr); P.addi(&d.mesh_polynum, m.mesh_polynum);
+  P.addi(&d.mesh_polyvertadr, m.mesh_polyvertadr); P.addi(&d.mesh_polyvertnum, m.mesh_polynum_v);
+  P.addi(&d.mesh_polyvert, m.mesh_polyvert); P.addf(&d.mesh_polynormal, m.mesh_polynormal);
   {
     // pre-gathered triangle records in device face order: vertex a, b - a, c - a, formed in fp32 from
     // the fp32 vertices exactly as ray_tri forms them on the device (bit-identical t)

@@ -146,6 +146,9 @@ struct DevModel {
   // meshes (mrs_model.h): vertices in the mesh frame, triangles and convex-hull vertex ids (both
   // relative to the mesh's first vertex)
   CPtr<int> mesh_vertadr, mesh_faceadr, mesh_facenum, mesh_hulladr, mesh_hullnum, mesh_face, mesh_hull;
+  // the hulls' faces as polygons (mrs_model.h mesh_poly*; step.hip poly_face_contacts)
+  CPtr<int> mesh_polyadr, mesh_polynum, mesh_polyvertadr, mesh_polyvertnum, mesh_polyvert;
+  CPtr<float> mesh_polynormal;
   CPtr<float> mesh_vert;
   // ray hierarchies (batch.hip build_mesh_bvh; mesh_face is reordered to their leaves): per mesh the
   // first node and the node count (0: none), 8 floats per node

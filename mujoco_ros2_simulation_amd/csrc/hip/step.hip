@@ -1394,6 +1394,113 @@ __device__ __forceinline__ void shape_of(const DevModel& m, int g, const float* 
     s.nhull = m.mesh_hullnum[id];
   }
 }
+#if MRS_EXT
+// face contacts of two polytopes (box and mesh pairs, at least one mesh; oracle.c col_poly_faces
+// restates the same steps in fp64): the support faces along MPR's normal, and when
+// the better aligned one is within kPolyCos of it, the other face's polygon clipped by its side
+// planes, every clipped vertex within margin of the reference plane a contact (at most
+// kMaxPairCon).  Returns -1 when the pair is not face-on (MPR's single contact stays).  Out of line
+// with its polygons in private memory: only the extended kernels of mesh models reach it.
+constexpr int kPolyMaxV = 16;
+constexpr float kPolyCos = 0.999f;
+struct PolyFace { int n; float v[kPolyMaxV][3]; float nrm[3]; };
+__device__ __forceinline__ float poly_support_face(const DevModel& m, const Shape& s, int g, const float dir[3],
+                                                   PolyFace& f) {
+  const float* R = s.mat;
+  if (s.type == MRS_GEOM_BOX) {
+    float l[3];
+    for (int i = 0; i < 3; ++i) l[i] = R[i] * dir[0] + R[3 + i] * dir[1] + R[6 + i] * dir[2];
+    int ax = 0;
+    for (int i = 1; i < 3; ++i)
+      if (fabsf(l[i]) > fabsf(l[ax])) ax = i;
+    const float sg = l[ax] >= 0 ? 1.0f : -1.0f;
+    const int j = (ax + 1) % 3, k = (ax + 2) % 3;
+    const float cj[4] = {-1, 1, 1, -1}, ck[4] = {-1, -1, 1, 1};
+    f.n = 4;
+    for (int q = 0; q < 4; ++q) {
+      const int qq = sg > 0 ? q : 3 - q;
+      float lp[3];
+      lp[ax] = sg * s.size[ax];
+      lp[j] = cj[qq] * s.size[j];
+      lp[k] = ck[qq] * s.size[k];
+      for (int i = 0; i < 3; ++i) f.v[q][i] = s.pos[i] + (R[3 * i] * lp[0] + R[3 * i + 1] * lp[1] + R[3 * i + 2] * lp[2]);
+    }
+    for (int i = 0; i < 3; ++i) f.nrm[i] = sg * R[3 * i + ax];
+    return fabsf(l[ax]);
+  }
+  const int id = m.geom_dataid[g];
+  int best = -1;
+  float ba = -3;
+  const int q0 = m.mesh_polyadr[id], q1 = q0 + m.mesh_polynum[id];
+  for (int q = q0; q < q1; ++q) {
+    const float nl[3] = {m.mesh_polynormal[3 * q], m.mesh_polynormal[3 * q + 1], m.mesh_polynormal[3 * q + 2]};
+    float a = 0;
+    for (int i = 0; i < 3; ++i) a += (R[3 * i] * nl[0] + R[3 * i + 1] * nl[1] + R[3 * i + 2] * nl[2]) * dir[i];
+    if (a > ba) { ba = a; best = q; }
+  }
+  if (best < 0 || m.mesh_polyvertnum[best] > kPolyMaxV) return -2;
+  const float nl[3] = {m.mesh_polynormal[3 * best], m.mesh_polynormal[3 * best + 1], m.mesh_polynormal[3 * best + 2]};
+  for (int i = 0; i < 3; ++i) f.nrm[i] = R[3 * i] * nl[0] + R[3 * i + 1] * nl[1] + R[3 * i + 2] * nl[2];
+  f.n = m.mesh_polyvertnum[best];
+  const int va = m.mesh_vertadr[id], pa = m.mesh_polyvertadr[best];
+  for (int q = 0; q < f.n; ++q) {
+    const int vi = va + m.mesh_polyvert[pa + q];
+    const float lp[3] = {m.mesh_vert[3 * vi], m.mesh_vert[3 * vi + 1], m.mesh_vert[3 * vi + 2]};
+    for (int i = 0; i < 3; ++i) f.v[q][i] = s.pos[i] + (R[3 * i] * lp[0] + R[3 * i + 1] * lp[1] + R[3 * i + 2] * lp[2]);
+  }
+  return ba;
+}
+__device__ __attribute__((noinline)) int poly_face_contacts(const DevModel& m, const Shape& A, int g1, const Shape& B,
+                                                            int g2, const float nrm[3], float margin, gCon* out) {
+  PolyFace fa, fb;
+  const float nb[3] = {-nrm[0], -nrm[1], -nrm[2]};
+  const float aa = poly_support_face(m, A, g1, nrm, fa), ab = poly_support_face(m, B, g2, nb, fb);
+  if (aa < -1 || ab < -1) return -1;
+  const bool refA = !(ab > aa + 1e-4f);
+  if ((refA ? aa : ab) < kPolyCos) return -1;
+  const PolyFace& ref = refA ? fa : fb;
+  const PolyFace& inc = refA ? fb : fa;
+  float buf[2][2 * kPolyMaxV][3];
+  int cnt = inc.n, cur = 0;
+  for (int q = 0; q < cnt; ++q)
+    for (int i = 0; i < 3; ++i) buf[0][q][i] = inc.v[q][i];
+  for (int e = 0; e < ref.n && cnt > 0; ++e) {
+    const float* r0 = ref.v[e];
+    const float* r1 = ref.v[(e + 1) % ref.n];
+    const float ed[3] = {r1[0] - r0[0], r1[1] - r0[1], r1[2] - r0[2]};
+    float h[3];
+    cross3(h, ref.nrm, ed);
+    int on = 0;
+    for (int q = 0; q < cnt; ++q) {
+      const float* pc = buf[cur][q];
+      const float* pn = buf[cur][(q + 1) % cnt];
+      const float dc = (pc[0] - r0[0]) * h[0] + (pc[1] - r0[1]) * h[1] + (pc[2] - r0[2]) * h[2];
+      const float dn = (pn[0] - r0[0]) * h[0] + (pn[1] - r0[1]) * h[1] + (pn[2] - r0[2]) * h[2];
+      if (dc >= 0 && on < 2 * kPolyMaxV)
+        for (int i = 0; i < 3; ++i) buf[1 - cur][on][i] = pc[i];
+      if (dc >= 0) ++on;
+      if ((dc >= 0) != (dn >= 0) && on < 2 * kPolyMaxV) {
+        const float t = dc / (dc - dn);
+        for (int i = 0; i < 3; ++i) buf[1 - cur][on][i] = pc[i] + t * (pn[i] - pc[i]);
+        ++on;
+      }
+    }
+    cnt = on < 2 * kPolyMaxV ? on : 2 * kPolyMaxV;
+    cur = 1 - cur;
+  }
+  const float sg = refA ? 1.0f : -1.0f;
+  int n = 0;
+  for (int q = 0; q < cnt && n < kMaxPairCon; ++q) {
+    const float* p = buf[cur][q];
+    const float d = (p[0] - ref.v[0][0]) * ref.nrm[0] + (p[1] - ref.v[0][1]) * ref.nrm[1] + (p[2] - ref.v[0][2]) * ref.nrm[2];
+    if (d > margin) continue;
+    gCon& o = out[n++];
+    for (int i = 0; i < 3; ++i) { o.pos[i] = p[i] - 0.5f * d * ref.nrm[i]; o.nrm[i] = sg * ref.nrm[i]; }
+    o.dist = d;
+  }
+  return n > 0 ? n : -1;
+}
+#endif
 __device__ __forceinline__ int convex_convex(const DevModel& m, int g1, int g2, const float* p1, const float* m1, const float* s1,
                              const float* p2, const float* m2, const float* s2, float margin, gCon* out) {
   Shape A, B;
@@ -1401,6 +1508,16 @@ __device__ __forceinline__ int convex_convex(const DevModel& m, int g1, int g2, 
   shape_of(m, g2, p2, m2, s2, 0.5f * margin, B);
   float depth, nrm[3], pos[3];
   if (!mpr_penetration(MeshTab{m.mesh_vert, m.mesh_hull}, A, B, depth, nrm, pos)) return 0;
+#if MRS_EXT
+  {
+    // two polytopes, at least one a mesh: the face contacts when the contact is face-on
+    const bool p1 = A.type == MRS_GEOM_BOX || A.type == MRS_GEOM_MESH, p2 = B.type == MRS_GEOM_BOX || B.type == MRS_GEOM_MESH;
+    if (p1 && p2 && (A.type == MRS_GEOM_MESH || B.type == MRS_GEOM_MESH) && !(m.restate & MRS_RESTATE_NO_MULTICCD)) {
+      const int r = poly_face_contacts(m, A, g1, B, g2, nrm, margin, out);
+      if (r >= 0) return r;
+    }
+  }
+#endif
 #if MRS_EXT
   if (!(m.restate & MRS_RESTATE_NO_MPR_POLISH)) {
     const float n0[3] = {nrm[0], nrm[1], nrm[2]};

@@ -235,6 +235,8 @@ struct MeshRec {
   std::string name;
   std::vector<double> vert;
   std::vector<int> face, hull;
+  std::vector<std::vector<int>> poly;  // hull faces as polygons (hull_polygons)
+  std::vector<double> poly_normal;
   double pos[3] = {0, 0, 0}, quat[4] = {1, 0, 0, 0};
   double volume = 0, inertia[3] = {0, 0, 0}, half[3] = {0, 0, 0}, rbound = 0;
 };
@@ -621,6 +623,7 @@ struct Compiler {
         r.rbound = std::max(r.rbound, norm3(&r.vert[3 * i]));
       }
       r.face = a.face;
+      hull_polygons(r.vert, hull_face, r.poly, r.poly_normal);
       std::string name;
       if (!get_str(e, nullptr, "mesh", "name", name)) {
         if (!has_file) fail(e, "a mesh without a file needs a name");
@@ -1532,6 +1535,14 @@ struct Compiler {
       m.mesh_vert.insert(m.mesh_vert.end(), r.vert.begin(), r.vert.end());
       m.mesh_face.insert(m.mesh_face.end(), r.face.begin(), r.face.end());
       m.mesh_hull.insert(m.mesh_hull.end(), r.hull.begin(), r.hull.end());
+      m.mesh_polyadr.push_back(static_cast<int>(m.mesh_polynum_v.size()));
+      m.mesh_polynum.push_back(static_cast<int>(r.poly.size()));
+      for (size_t q = 0; q < r.poly.size(); ++q) {
+        m.mesh_polyvertadr.push_back(static_cast<int>(m.mesh_polyvert.size()));
+        m.mesh_polynum_v.push_back(static_cast<int>(r.poly[q].size()));
+        m.mesh_polyvert.insert(m.mesh_polyvert.end(), r.poly[q].begin(), r.poly[q].end());
+        for (int k = 0; k < 3; ++k) m.mesh_polynormal.push_back(r.poly_normal[3 * q + k]);
+      }
     }
     m.names[MRS_OBJ_MESH] = names;
   }
@@ -2279,6 +2290,10 @@ mrs_model_view Model::view() const {
   v.nexclude = static_cast<int>(exclude_body1.size());
   MRS_V(expair_geom1); MRS_V(expair_geom2); MRS_V(expair_dim); MRS_V(exclude_body1); MRS_V(exclude_body2);
   MRS_V(expair_friction); MRS_V(expair_solref); MRS_V(expair_solimp); MRS_V(expair_margin); MRS_V(expair_gap);
+  v.nmeshpoly = static_cast<int>(mesh_polynum_v.size());
+  v.nmeshpolyvert = static_cast<int>(mesh_polyvert.size());
+  MRS_V(mesh_polyadr); MRS_V(mesh_polynum); MRS_V(mesh_polyvertadr); MRS_V(mesh_polyvert); MRS_V(mesh_polynormal);
+  v.mesh_polyvertnum = mesh_polynum_v.empty() ? nullptr : mesh_polynum_v.data();
 #undef MRS_V
   return v;
 }

@@ -220,6 +220,78 @@ void convex_hull(const std::vector<double>& vert, std::vector<int>& hull_face, s
   hull_vert.assign(used.begin(), used.end());
 }
 
+void hull_polygons(const std::vector<double>& vert, const std::vector<int>& hull_face,
+                   std::vector<std::vector<int>>& polys, std::vector<double>& normals) {
+  polys.clear();
+  normals.clear();
+  const size_t nt = hull_face.size() / 3;
+  std::vector<double> tn(3 * nt);
+  std::vector<double> ta(nt);
+  for (size_t t = 0; t < nt; ++t) {
+    const double *a = P(vert, hull_face[3 * t]), *b = P(vert, hull_face[3 * t + 1]), *c = P(vert, hull_face[3 * t + 2]);
+    const double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+    double n[3];
+    cross(n, e1, e2);
+    const double l = std::sqrt(dot(n, n));
+    ta[t] = l;
+    for (int k = 0; k < 3; ++k) tn[3 * t + k] = l > 0 ? n[k] / l : 0;
+  }
+  std::vector<int> group(nt, -1);
+  for (size_t t = 0; t < nt; ++t) {
+    if (group[t] >= 0 || !(ta[t] > 0)) continue;
+    const int gid = static_cast<int>(polys.size());
+    double nsum[3] = {0, 0, 0};
+    std::vector<int> ids;
+    for (size_t u = t; u < nt; ++u) {
+      if (group[u] >= 0 || !(ta[u] > 0)) continue;
+      if (dot(&tn[3 * t], &tn[3 * u]) < 1 - 1e-6) continue;
+      group[u] = gid;
+      for (int k = 0; k < 3; ++k) nsum[k] += ta[u] * tn[3 * u + k];
+      for (int k = 0; k < 3; ++k) ids.push_back(hull_face[3 * u + k]);
+    }
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    const double l = std::sqrt(dot(nsum, nsum));
+    const double n[3] = {nsum[0] / l, nsum[1] / l, nsum[2] / l};
+    // order about the centroid in the face plane (u, v, n right-handed: counter-clockwise about n)
+    double cen[3] = {0, 0, 0};
+    for (int i : ids)
+      for (int k = 0; k < 3; ++k) cen[k] += P(vert, i)[k] / ids.size();
+    double uax[3] = {P(vert, ids[0])[0] - cen[0], P(vert, ids[0])[1] - cen[1], P(vert, ids[0])[2] - cen[2]};
+    const double un = dot(uax, n);
+    for (int k = 0; k < 3; ++k) uax[k] -= un * n[k];
+    const double ul = std::sqrt(dot(uax, uax));
+    for (int k = 0; k < 3; ++k) uax[k] /= ul;
+    double vax[3];
+    cross(vax, n, uax);
+    std::vector<std::pair<double, int>> ang;
+    for (int i : ids) {
+      const double d[3] = {P(vert, i)[0] - cen[0], P(vert, i)[1] - cen[1], P(vert, i)[2] - cen[2]};
+      ang.push_back({std::atan2(dot(d, vax), dot(d, uax)), i});
+    }
+    std::sort(ang.begin(), ang.end());
+    std::vector<int> loop;
+    for (auto& a : ang) loop.push_back(a.second);
+    // drop vertices on a straight boundary edge (their neighbours' edge passes through them)
+    double ext = 0;
+    for (int i : loop) {
+      const double d[3] = {P(vert, i)[0] - cen[0], P(vert, i)[1] - cen[1], P(vert, i)[2] - cen[2]};
+      ext = std::max(ext, std::sqrt(dot(d, d)));
+    }
+    std::vector<int> keep;
+    const size_t nl = loop.size();
+    for (size_t q = 0; q < nl; ++q) {
+      const double *pa = P(vert, loop[(q + nl - 1) % nl]), *pb = P(vert, loop[q]), *pc = P(vert, loop[(q + 1) % nl]);
+      const double e1[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]}, e2[3] = {pc[0] - pb[0], pc[1] - pb[1], pc[2] - pb[2]};
+      double c[3];
+      cross(c, e1, e2);
+      if (dot(c, n) > 1e-12 * ext * ext) keep.push_back(loop[q]);
+    }
+    polys.push_back(keep.size() >= 3 ? keep : loop);
+    for (int k = 0; k < 3; ++k) normals.push_back(n[k]);
+  }
+}
+
 void mesh_mass_properties(const std::vector<double>& vert, const std::vector<int>& face, double& volume,
                           double com[3], double inertia[9]) {
   double vol = 0, c1[3] = {0, 0, 0}, C[9] = {0};

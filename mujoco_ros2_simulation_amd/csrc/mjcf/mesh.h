@@ -21,6 +21,12 @@ MeshAsset load_mesh_file(const std::string& path);
 // outward-oriented triangles over vertex indices, and the sorted ids of the hull's vertices.
 void convex_hull(const std::vector<double>& vert, std::vector<int>& hull_face, std::vector<int>& hull_vert);
 
+// The convex hull's faces as polygons: coplanar hull triangles (unit normals within 1e-6) merged, each
+// polygon's vertices counter-clockwise about its outward unit normal, collinear boundary vertices
+// dropped.  polys: vertex ids per polygon; normals: 3 per polygon.
+void hull_polygons(const std::vector<double>& vert, const std::vector<int>& hull_face,
+                   std::vector<std::vector<int>>& polys, std::vector<double>& normals);
+
 // Volume, centre of mass and the inertia tensor about it (unit density) of the solid bounded by the
 // triangles (divergence theorem over signed tetrahedra from the origin).
 void mesh_mass_properties(const std::vector<double>& vert, const std::vector<int>& face, double& volume,

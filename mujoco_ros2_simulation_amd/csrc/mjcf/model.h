@@ -61,6 +61,10 @@ struct Model {
   int nmesh = 0;
   std::vector<int> geom_dataid, mesh_vertadr, mesh_vertnum, mesh_faceadr, mesh_facenum, mesh_hulladr,
       mesh_hullnum, mesh_face, mesh_hull;
+  // hull faces as polygons (mrs_model.h): per mesh polyadr / polynum; per polygon the vertex-list
+  // address and length (mesh_polynum_v) and its outward normal; the vertex ids
+  std::vector<int> mesh_polyadr, mesh_polynum, mesh_polyvertadr, mesh_polynum_v, mesh_polyvert;
+  std::vector<double> mesh_polynormal;
   std::vector<double> mesh_vert;
   // statically admissible collision pairs (mj_collision's broad-phase filters), lower geom type first
   std::vector<int> pair_geom1, pair_geom2;

@@ -30,7 +30,7 @@ OBJ_TENDON = 18
 SENS_ACCELEROMETER, SENS_GYRO, SENS_FORCE, SENS_TORQUE, SENS_RANGEFINDER = 1, 3, 4, 5, 7
 SENS_JOINTPOS, SENS_JOINTVEL, SENS_ACTUATORFRC, SENS_FRAMEPOS, SENS_FRAMEQUAT = 9, 10, 15, 25, 26
 BIAS_NONE, BIAS_AFFINE = 0, 1
-RESTATE_NEWTON_REFINE, RESTATE_PGS_ELLIPTIC_BLOCK, RESTATE_NO_MPR_POLISH = 1, 2, 4
+RESTATE_NEWTON_REFINE, RESTATE_PGS_ELLIPTIC_BLOCK, RESTATE_NO_MPR_POLISH, RESTATE_NO_MULTICCD = 1, 2, 4, 8
 (FIELD_QPOS, FIELD_QVEL, FIELD_CTRL, FIELD_QFRC_APPLIED, FIELD_QACC_WARMSTART, FIELD_QACC,
  FIELD_QFRC_ACTUATOR, FIELD_SENSORDATA, FIELD_TIME, FIELD_WARNING, FIELD_NCON, FIELD_SOLVER_NITER) = range(12)
 # ActuatorType (include/mujoco_ros2_control/data.hpp:43-51 numbering)
@@ -139,6 +139,13 @@ _TEN_ARRAYS = [
     ("tendon_length0", "d", "ntendon", 1),
 ]
 TRN_JOINT, TRN_TENDON = 0, 3
+# mesh hull polygons (after the tendon block)
+_POLY_SIZES = ["nmeshpoly", "nmeshpolyvert"]
+_POLY_ARRAYS = [
+    ("mesh_polyadr", "i", "nmesh", 1), ("mesh_polynum", "i", "nmesh", 1), ("mesh_polyvertadr", "i", "nmeshpoly", 1),
+    ("mesh_polyvertnum", "i", "nmeshpoly", 1), ("mesh_polyvert", "i", "nmeshpolyvert", 1),
+    ("mesh_polynormal", "d", "nmeshpoly", 3),
+]
 
 
 class ModelView(C.Structure):
@@ -159,7 +166,9 @@ class ModelView(C.Structure):
                 [("vis_headlight", C.c_double * 10)] + [(n, C.c_int) for n in _REND_SIZES] +
                 [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _REND_ARRAYS] +
                 [(n, C.c_int) for n in _TEN_SIZES] +
-                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _TEN_ARRAYS])
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _TEN_ARRAYS] +
+                [(n, C.c_int) for n in _POLY_SIZES] +
+                [(n, C.POINTER(C.c_int) if k == "i" else C.POINTER(C.c_double)) for n, k, _, _ in _POLY_ARRAYS])
 
 
 _lib = None
@@ -247,7 +256,7 @@ class Model:
         self.view = ModelView()
         _check(lib().mrs_model_view_get(self._h, C.byref(self.view)))
         v = self.view
-        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES + _REND_SIZES + _TEN_SIZES:
+        for n in _SIZES + _MESH_SIZES + _CONTACT_SIZES + _EQ_SIZES + _REND_SIZES + _TEN_SIZES + _POLY_SIZES:
             setattr(self, n, getattr(v, n))
         for n in ["timestep", "tolerance", "impratio", "ls_tolerance", "ls_iterations", "restate", "integrator", "solver",
                   "iterations", "disableflags",
@@ -256,7 +265,7 @@ class Model:
         self.gravity = np.array(v.gravity[:])
         self.vis_headlight = np.array(v.vis_headlight[:])
         for name, kind, count, width in (_ARRAYS + _MESH_ARRAYS + _CONTACT_ARRAYS + _EQ_ARRAYS + _REND_ARRAYS +
-                                         _TEN_ARRAYS):
+                                         _TEN_ARRAYS + _POLY_ARRAYS):
             n = getattr(v, count)
             w = getattr(v, width) if isinstance(width, str) else width
             ptr = getattr(v, name)

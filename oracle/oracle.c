@@ -1661,12 +1661,137 @@ static int mpr_polish(const orc_shape* A, const orc_shape* B, const double n0[3]
   return 1;
 }
 
+/* ---- face contacts of two polytopes (box and mesh pairs, at least one mesh): this restatement of
+ * MuJoCo's multi-contact convex collision (multiccd) [restated; verify against upstream].  MPR gives
+ * the contact normal n (geom1 -> geom2).  Each shape's support face is the face whose outward normal
+ * is nearest n (geom1) or -n (geom2): a box face, or a polygon of the mesh's hull (mesh_poly*).  When
+ * the better aligned of the two is within POLY_COS of n (a face contact), it is the reference face and
+ * the other the incident face: the incident polygon is clipped by the reference polygon's side planes
+ * (Sutherland-Hodgman, in the incident polygon's vertex order), and every clipped vertex within margin
+ * of the reference plane is a contact (at most 8, in clip order): distance d to the reference plane,
+ * position midway between the vertex and the plane, normal the reference face's (geom1 -> geom2).  A
+ * flat face-on-face rest gets its corners, a box tipped onto an edge the edge's ends.  Otherwise
+ * (edge-edge, vertex contacts) MPR's single contact stays.  The reference face is geom1's unless
+ * geom2's alignment is larger by more than 1e-4 (fp32 and fp64 break a tie between two flat faces
+ * the same way). */
+#define POLY_MAXV 16
+#define POLY_COS 0.999
+typedef struct { int n; double v[POLY_MAXV][3]; double nrm[3]; } orc_poly;
+/* support face of shape s (box or mesh geom g) along dir; returns the alignment n_face.dir, or -2
+ * when the face has more than POLY_MAXV vertices */
+static double poly_support_face(const mrs_model_view* m, const orc_shape* s, int g, const double dir[3], orc_poly* f) {
+  const double* R = s->mat;
+  if (s->type == MRS_GEOM_BOX) {
+    double l[3];
+    matT_vec(l, R, dir);
+    int ax = 0;
+    for (int i = 1; i < 3; ++i)
+      if (fabs(l[i]) > fabs(l[ax])) ax = i;
+    const double sg = l[ax] >= 0 ? 1.0 : -1.0;
+    const int j = (ax + 1) % 3, k = (ax + 2) % 3;
+    /* corners counter-clockwise about the outward normal sg e_ax: (j, k) signs (-,-), (+,-), (+,+),
+     * (-,+) about +e_ax (e_j x e_k = e_ax), reversed about -e_ax */
+    static const double cj[4] = {-1, 1, 1, -1}, ck[4] = {-1, -1, 1, 1};
+    f->n = 4;
+    for (int q = 0; q < 4; ++q) {
+      const int qq = sg > 0 ? q : 3 - q;
+      double lp[3];
+      lp[ax] = sg * s->size[ax];
+      lp[j] = cj[qq] * s->size[j];
+      lp[k] = ck[qq] * s->size[k];
+      double wv[3];
+      mat_vec(wv, R, lp);
+      for (int i = 0; i < 3; ++i) f->v[q][i] = s->pos[i] + wv[i];
+    }
+    for (int i = 0; i < 3; ++i) f->nrm[i] = sg * R[3 * i + ax];
+    return fabs(l[ax]);
+  }
+  const int id = m->geom_dataid[g];
+  int best = -1;
+  double ba = -3;
+  for (int q = m->mesh_polyadr[id]; q < m->mesh_polyadr[id] + m->mesh_polynum[id]; ++q) {
+    double nw[3];
+    mat_vec(nw, R, m->mesh_polynormal + 3 * q);
+    const double a = dot3(nw, dir);
+    if (a > ba) { ba = a; best = q; }
+  }
+  if (best < 0 || m->mesh_polyvertnum[best] > POLY_MAXV) return -2;
+  mat_vec(f->nrm, R, m->mesh_polynormal + 3 * best);
+  f->n = m->mesh_polyvertnum[best];
+  const double* vb = m->mesh_vert + 3 * m->mesh_vertadr[id];
+  for (int q = 0; q < f->n; ++q) {
+    double wv[3];
+    mat_vec(wv, R, vb + 3 * m->mesh_polyvert[m->mesh_polyvertadr[best] + q]);
+    for (int i = 0; i < 3; ++i) f->v[q][i] = s->pos[i] + wv[i];
+  }
+  return ba;
+}
+static int col_poly_faces(const mrs_model_view* m, const orc_shape* A, int g1, const orc_shape* B, int g2,
+                          const double nrm[3], double margin, orc_contact* out, int n) {
+  orc_poly fa, fb;
+  const double nb[3] = {-nrm[0], -nrm[1], -nrm[2]};
+  const double aa = poly_support_face(m, A, g1, nrm, &fa), ab = poly_support_face(m, B, g2, nb, &fb);
+  if (aa < -1 || ab < -1) return -1;
+  const int refA = !(ab > aa + 1e-4);
+  if ((refA ? aa : ab) < POLY_COS) return -1;
+  const orc_poly* ref = refA ? &fa : &fb;
+  const orc_poly* inc = refA ? &fb : &fa;
+  double buf[2][2 * POLY_MAXV][3];
+  int cnt = inc->n, cur = 0;
+  for (int q = 0; q < cnt; ++q)
+    for (int i = 0; i < 3; ++i) buf[0][q][i] = inc->v[q][i];
+  for (int e = 0; e < ref->n && cnt > 0; ++e) {
+    const double* r0 = ref->v[e];
+    const double* r1 = ref->v[(e + 1) % ref->n];
+    const double ed[3] = {r1[0] - r0[0], r1[1] - r0[1], r1[2] - r0[2]};
+    double h[3];
+    cross3(h, ref->nrm, ed); /* inward side normal of the edge */
+    int out_n = 0;
+    for (int q = 0; q < cnt; ++q) {
+      const double* pc = buf[cur][q];
+      const double* pn = buf[cur][(q + 1) % cnt];
+      const double dc = (pc[0] - r0[0]) * h[0] + (pc[1] - r0[1]) * h[1] + (pc[2] - r0[2]) * h[2];
+      const double dn = (pn[0] - r0[0]) * h[0] + (pn[1] - r0[1]) * h[1] + (pn[2] - r0[2]) * h[2];
+      if (dc >= 0 && out_n < 2 * POLY_MAXV)
+        for (int i = 0; i < 3; ++i) buf[1 - cur][out_n][i] = pc[i];
+      if (dc >= 0) ++out_n;
+      if ((dc >= 0) != (dn >= 0) && out_n < 2 * POLY_MAXV) {
+        const double t = dc / (dc - dn);
+        for (int i = 0; i < 3; ++i) buf[1 - cur][out_n][i] = pc[i] + t * (pn[i] - pc[i]);
+        ++out_n;
+      }
+    }
+    cnt = out_n < 2 * POLY_MAXV ? out_n : 2 * POLY_MAXV;
+    cur = 1 - cur;
+  }
+  const double sg = refA ? 1.0 : -1.0;
+  const double cn[3] = {sg * ref->nrm[0], sg * ref->nrm[1], sg * ref->nrm[2]};
+  const int n0 = n;
+  for (int q = 0; q < cnt; ++q) {
+    const double* p = buf[cur][q];
+    const double d = (p[0] - ref->v[0][0]) * ref->nrm[0] + (p[1] - ref->v[0][1]) * ref->nrm[1] +
+                     (p[2] - ref->v[0][2]) * ref->nrm[2];
+    if (d > margin) continue;
+    double pos[3];
+    for (int i = 0; i < 3; ++i) pos[i] = p[i] - 0.5 * d * ref->nrm[i];
+    n = add_contact(out, n, d, pos, cn);
+  }
+  return n > n0 ? n : -1;
+}
 static int col_convex(const mrs_model_view* m, orc_ws* w, int g1, int g2, double margin, orc_contact* out, int n) {
   orc_shape A, B;
   shape_of(m, w, g1, margin, &A);
   shape_of(m, w, g2, margin, &B);
   double depth, nrm[3], pos[3];
   if (!mpr_penetration(&A, &B, &depth, nrm, pos)) return n;
+  {
+    /* two polytopes, at least one a mesh: the face contacts, when the contact is face-on */
+    const int p1 = A.type == MRS_GEOM_BOX || A.type == MRS_GEOM_MESH, p2 = B.type == MRS_GEOM_BOX || B.type == MRS_GEOM_MESH;
+    if (p1 && p2 && (A.type == MRS_GEOM_MESH || B.type == MRS_GEOM_MESH) && !(m->restate & MRS_RESTATE_NO_MULTICCD)) {
+      const int r = col_poly_faces(m, &A, g1, &B, g2, nrm, margin, out, n);
+      if (r >= 0) return r;
+    }
+  }
   static int no_polish = -1;  /* diagnostics: ORC_NO_POLISH=1 keeps MPR's contact (scripts/diag_mpr.py) */
   if (no_polish < 0) no_polish = getenv("ORC_NO_POLISH") != NULL;
   if (!no_polish && !(m->restate & MRS_RESTATE_NO_MPR_POLISH)) mpr_polish(&A, &B, nrm, depth, &depth, nrm, pos);

@@ -79,8 +79,14 @@ def test_mesh_convex_contact_lists(steps):
 
 def test_mesh_scene_rollout():
     """200 steps of the mesh scene from the same start on both sides: qpos within 10x the scene's
-    fp32-state sensitivity + 1e-5 (bodies settling on single-contact convex pairs)"""
+    fp32-state sensitivity + 1e-5 (bodies settling on single-contact convex pairs).  The face contacts
+    of polytope pairs are off here (RESTATE_NO_MULTICCD, both sides): the box landing on the cube gets
+    clipped-polygon contacts whose vertices cross the zero-margin threshold as it settles, and fp32 /
+    fp64 geometry switch such a contact on one step apart, so a free rollout measures that threshold,
+    not the arithmetic -- test_reseeded_mesh_scene_face_contacts holds the same scene with them on,
+    step by step, with every flip explained"""
     model = sim.Model.from_string(MESH_SCENE)
+    model.set_restate(sim.RESTATE_NO_MULTICCD)
     n, steps = 4, 200
     q0 = synth.initial_qpos(model, np.arange(n))
     b = sim.Batch(model, n)
@@ -467,3 +473,80 @@ def test_lit_colour_all_kernels(path, monkeypatch):
     miss = wd >= wd.max()
     assert miss.sum() > 1000 and wrgb[miss][:, 2].max() > 100  # skybox above the horizon
     assert len({tuple(c) for c in wrgb.reshape(-1, 3)[::37]}) > 100
+
+
+def test_reseeded_mesh_scene_face_contacts():
+    """the mesh scene with the polytope face contacts on (the box landing on the cube, the cube on the
+    floor through plane-mesh), one step at a time from the oracle's state: per-step state within 1e-5,
+    contact flips explained as threshold cases (flips.explain_flip)"""
+    from test_gpu_solvers import _reseeded
+    model = sim.Model.from_string(MESH_SCENE)
+    wq, wv, ncon, flips, unexplained = _reseeded(model, 4, 120, settle=90)
+    print(f"mesh scene (face contacts): worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts "
+          f"{ncon.mean():.2f}; flips {flips}")
+    assert ncon.max() >= 14
+    assert flips <= max(1, 0.02 * 4 * 120)
+    assert not unexplained, unexplained[:5]
+    assert wq <= 1e-5 and wv <= 1e-5
+
+
+# ---------------------------------------------------------------- polytope face contacts (multiccd)
+_CUBE = 'vertex="-1 -1 -1 1 -1 -1 1 1 -1 -1 1 -1 -1 -1 1 1 -1 1 1 1 1 -1 1 1" scale="0.08 0.08 0.08"'
+FACE_SCENE = f"""<mujoco><compiler angle="radian"/><option timestep="0.002" solver="PGS" iterations="50"/>
+  <asset><mesh name="cube" {_CUBE}/></asset>
+  <worldbody><geom name="table" type="box" pos="0 0 -0.05" size="1 1 0.05"/>
+    <body name="a" pos="0.3 0.1 0.09" euler="0.02 -0.03 0.2"><freejoint/><geom type="mesh" mesh="cube"/></body>
+    <body name="b" pos="-0.25 -0.2 0.12" euler="0.1 0.05 -0.4"><freejoint/><geom type="mesh" mesh="cube"/></body>
+    <body name="c" pos="0 0.35 0.085"><freejoint/><geom type="mesh" mesh="cube"/></body>
+    <body name="d" pos="0.03 0.36 0.26" euler="0 0 0.5"><freejoint/><geom type="mesh" mesh="cube"/></body>
+    <body name="e" pos="-0.3 0.3 0.2"><freejoint/><geom type="box" size="0.06 0.05 0.04" euler="0.05 0 0.3"/></body>
+  </worldbody></mujoco>"""
+
+
+def _face_kinds(model, d):
+    return {tuple(int(model.geom_type[x]) for x in p) for p in d.contacts()[0]}
+
+
+def test_face_contacts_match_oracle():
+    """mesh cubes resting on a box table, a cube stacked on another (mesh-mesh) and a box (box-mesh):
+    the face contacts of polytope pairs (up to one per clipped polygon vertex) agree with the oracle --
+    the (geom1, geom2) list bit-exact, dist / pos / frame within 1e-4 -- after the cubes have settled"""
+    model = sim.Model.from_string(FACE_SCENE)
+    d = binding.OracleData(model)
+    d.step(300)
+    q = d.qpos.copy()
+    g_ref = d.contacts()[0]
+    per_pair = {}
+    for p in g_ref.tolist():
+        per_pair[tuple(p)] = per_pair.get(tuple(p), 0) + 1
+    assert max(per_pair.values()) >= 4, per_pair  # flat rests give several contacts per pair
+    assert (6, 7) in _face_kinds(model, d) and (7, 7) in _face_kinds(model, d)
+    b = sim.Batch(model, 4)
+    b.set(sim.FIELD_QPOS, np.tile(q, (4, 1)))
+    b.forward()
+    for e in range(4):
+        g, dist, pos, frame = b.contacts(e)
+        r = binding.OracleData(model)
+        r.qpos[:] = q
+        r.forward()
+        gr, dr, pr, fr = r.contacts()
+        assert np.array_equal(g, gr), (g.tolist(), gr.tolist())
+        np.testing.assert_allclose(dist, dr, atol=1e-4)
+        np.testing.assert_allclose(pos, pr, atol=1e-4)
+        np.testing.assert_allclose(frame, fr, atol=1e-4)
+    b.close()
+
+
+def test_reseeded_face_contacts():
+    """the same scene one step at a time from the oracle's state (test_gpu_solvers._reseeded) while
+    the cubes fall, tip and settle: per-step qpos / qvel within 1e-5, contact-count flips explained as
+    threshold cases"""
+    from test_gpu_solvers import _reseeded
+    model = sim.Model.from_string(FACE_SCENE)
+    wq, wv, ncon, flips, unexplained = _reseeded(model, 8, 120, settle=40)
+    print(f"face-contact scene: worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts {ncon.mean():.2f}; "
+          f"flips {flips}")
+    assert ncon.max() >= 12
+    assert flips <= max(1, 0.01 * 8 * 120)
+    assert not unexplained, unexplained[:5]
+    assert wq <= 1e-5 and wv <= 1e-5

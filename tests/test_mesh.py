@@ -140,10 +140,11 @@ def test_mesh_cube_rests_like_box_and_convex_primitives_settle():
     assert d.ncon == 4 + 4 + 1 + 3
 
 
-def _pair(g1, g2, p2, margin=0.0):
+def _pair(g1, g2, p2, margin=0.0, restate=0):
     m = sim.Model.from_string(f"""<mujoco><asset><mesh name="c" vertex="{CUBE}" scale="0.1 0.1 0.1"/></asset>
       <worldbody><body><freejoint/>{g1}</body><body pos="{p2}"><freejoint/>{g2}</body></worldbody></mujoco>"""
                               .replace("<geom ", f'<geom margin="{margin}" '))
+    m.set_restate(restate)
     d = binding.OracleData(m)
     d.forward()
     return d.contacts()
@@ -161,10 +162,18 @@ def test_mpr_sphere_ellipsoid_is_exact():
 
 @pytest.mark.parametrize("margin", [0.0, 0.02])
 def test_mpr_box_mesh_face_depth(margin):
-    """box vs cube mesh, face on face with an offset: depth along z as the SAT box-box gives; a margin
-    inflates both shapes by margin/2 and is subtracted back (dist = margin - depth)"""
+    """box vs cube mesh, face on face with an offset: MPR's depth along z as the SAT box-box gives; a
+    margin inflates both shapes by margin/2 and is subtracted back (dist = margin - depth).  With the
+    face contacts (default) the pair gives the four corners of the faces' overlap at that depth"""
     g, dist, pos, frame = _pair('<geom type="box" size="0.1 0.1 0.1"/>', '<geom type="mesh" mesh="c"/>',
                                 "0.03 0.02 0.19", margin)
+    assert len(dist) == 4
+    np.testing.assert_allclose(dist, -0.01, atol=1e-9)
+    np.testing.assert_allclose(frame[:, :3], np.tile([0, 0, 1.0], (4, 1)), atol=1e-9)
+    np.testing.assert_allclose(sorted({round(p[0], 9) for p in pos}), [-0.07, 0.1], atol=1e-9)
+    np.testing.assert_allclose(sorted({round(p[1], 9) for p in pos}), [-0.08, 0.1], atol=1e-9)
+    g, dist, pos, frame = _pair('<geom type="box" size="0.1 0.1 0.1"/>', '<geom type="mesh" mesh="c"/>',
+                                "0.03 0.02 0.19", margin, restate=sim.RESTATE_NO_MULTICCD)
     assert len(dist) == 1
     # margin rounds the inflated shapes' edges: MPR stops within mpr_tolerance (1e-6) of the surface
     assert dist[0] == pytest.approx(-0.01, abs=1e-9 if margin == 0 else 1e-6)

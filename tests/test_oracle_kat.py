@@ -498,3 +498,66 @@ def test_equality_kats():
         worst = max(worst, abs(d.qpos[0] - 2 * d.qpos[1]))
         reach = max(reach, d.qpos[1])
     assert worst < 5e-3 and reach > 0.2  # the driven joint swings to the target; the coupled one follows
+
+
+# ---------------------------------------------------------------- polytope face contacts (multiccd)
+_CUBE = 'vertex="-1 -1 -1 1 -1 -1 1 1 -1 -1 1 -1 -1 -1 1 1 -1 1 1 1 1 -1 1 1" scale="0.1 0.1 0.1"'
+
+
+def _face_scene(extra_bodies: str) -> str:
+    return f"""<mujoco><compiler angle="radian"/><asset><mesh name="cube" {_CUBE}/></asset>
+    <worldbody><geom name="table" type="box" pos="0 0 -0.05" size="1 1 0.05"/>{extra_bodies}</worldbody></mujoco>"""
+
+
+def test_mesh_cube_resting_flat_gets_four_corner_contacts(built):
+    """a mesh cube (half size 0.1) resting flat on a box, sunk by 1 mm: the face contacts are its four
+    bottom corners, each at distance -1e-3 from the table top, positioned midway (z = -5e-4), normal
+    +z from the table (geom1, the lower type) to the cube; without the face contacts
+    (RESTATE_NO_MULTICCD) MPR gives one contact"""
+    import binding
+    from mujoco_ros2_simulation_amd import sim
+    m = sim.Model.from_string(_face_scene('<body pos="0.3 -0.2 0.099"><freejoint/><geom type="mesh" mesh="cube"/></body>'))
+    d = binding.OracleData(m)
+    d.forward()
+    g, dist, pos, fr = d.contacts()
+    assert len(g) == 4 and all(tuple(x) == (0, 1) for x in g.tolist())
+    np.testing.assert_allclose(dist, -1e-3, atol=1e-12)
+    np.testing.assert_allclose(fr[:, :3], np.tile([0, 0, 1.0], (4, 1)), atol=1e-12)
+    want = {(0.3 + sx * 0.1, -0.2 + sy * 0.1) for sx in (-1, 1) for sy in (-1, 1)}
+    got = {(round(p[0], 9), round(p[1], 9)) for p in pos}
+    assert got == {(round(x, 9), round(y, 9)) for x, y in want}
+    np.testing.assert_allclose(pos[:, 2], -5e-4, atol=1e-12)
+    m.set_restate(sim.RESTATE_NO_MULTICCD)
+    d = binding.OracleData(m)
+    d.forward()
+    assert len(d.contacts()[0]) == 1
+
+
+def test_mesh_cube_tipped_on_edge_and_stacked(built):
+    """a cube tipped by 0.1 rad about x resting on its lower edge gets the edge's two ends (the other
+    two bottom corners are ~2 cm above the table, beyond margin); a cube stacked flat on another cube
+    (mesh-mesh, 1 mm overlap, shifted by 2 cm in x) gets the four corners of the overlap rectangle"""
+    import binding
+    from mujoco_ros2_simulation_amd import sim
+    th = 0.1
+    z = 0.1 * np.cos(th) + 0.1 * np.sin(th) - 1e-3  # lowest edge 1 mm into the table
+    m = sim.Model.from_string(_face_scene(
+        f'<body pos="0 0 {z:.12f}" euler="{th} 0 0"><freejoint/><geom type="mesh" mesh="cube"/></body>'))
+    d = binding.OracleData(m)
+    d.forward()
+    g, dist, pos, fr = d.contacts()
+    assert len(g) == 2, (g, dist)
+    np.testing.assert_allclose(dist, -1e-3, atol=1e-9)
+    np.testing.assert_allclose(sorted(pos[:, 0]), [-0.1, 0.1], atol=1e-9)
+    m = sim.Model.from_string(_face_scene(
+        '<body pos="0 0 0.1"><freejoint/><geom type="mesh" mesh="cube"/></body>'
+        '<body pos="0.02 0 0.299"><freejoint/><geom type="mesh" mesh="cube"/></body>'))
+    d = binding.OracleData(m)
+    d.forward()
+    g, dist, pos, fr = d.contacts()
+    top = [i for i in range(len(g)) if tuple(g[i]) == (1, 2)]
+    assert len(top) == 4, g
+    np.testing.assert_allclose(dist[top], -1e-3, atol=1e-9)
+    xs = sorted({round(p[0], 9) for p in pos[top]})
+    np.testing.assert_allclose(xs, [-0.08, 0.1], atol=1e-9)  # the overlap spans x in [-0.08, 0.1]
+    np.testing.assert_allclose(fr[top, :3], np.tile([0, 0, 1.0], (4, 1)), atol=1e-9)
