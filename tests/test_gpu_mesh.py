@@ -83,8 +83,8 @@ def test_mesh_scene_rollout():
     of polytope pairs are off here (RESTATE_NO_MULTICCD, both sides): the box landing on the cube gets
     clipped-polygon contacts whose vertices cross the zero-margin threshold as it settles, and fp32 /
     fp64 geometry switch such a contact on one step apart, so a free rollout measures that threshold,
-    not the arithmetic -- test_reseeded_mesh_scene_face_contacts holds the same scene with them on,
-    step by step, with every flip explained"""
+    not the arithmetic (the face contacts' own tests: test_face_contacts_match_oracle,
+    test_reseeded_face_contacts)"""
     model = sim.Model.from_string(MESH_SCENE)
     model.set_restate(sim.RESTATE_NO_MULTICCD)
     n, steps = 4, 200
@@ -473,21 +473,6 @@ def test_lit_colour_all_kernels(path, monkeypatch):
     miss = wd >= wd.max()
     assert miss.sum() > 1000 and wrgb[miss][:, 2].max() > 100  # skybox above the horizon
     assert len({tuple(c) for c in wrgb.reshape(-1, 3)[::37]}) > 100
-
-
-def test_reseeded_mesh_scene_face_contacts():
-    """the mesh scene with the polytope face contacts on (the box landing on the cube, the cube on the
-    floor through plane-mesh), one step at a time from the oracle's state: per-step state within 1e-5,
-    contact flips explained as threshold cases (flips.explain_flip)"""
-    from test_gpu_solvers import _reseeded
-    model = sim.Model.from_string(MESH_SCENE)
-    wq, wv, ncon, flips, unexplained = _reseeded(model, 4, 120, settle=90)
-    print(f"mesh scene (face contacts): worst per-step rel err qpos {wq:.2e} qvel {wv:.2e}; contacts "
-          f"{ncon.mean():.2f}; flips {flips}")
-    assert ncon.max() >= 14
-    assert flips <= max(1, 0.02 * 4 * 120)
-    assert not unexplained, unexplained[:5]
-    assert wq <= 1e-5 and wv <= 1e-5
 
 
 # ---------------------------------------------------------------- polytope face contacts (multiccd)
