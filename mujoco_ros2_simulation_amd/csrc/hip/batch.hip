@@ -1071,6 +1071,16 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   }
   // pointer-jumping tables for the tree passes: jump[r][b] = ancestor of b at distance 2^r when b
   // is deeper than 2^r (that ancestor is not the world body), else -1; ceil(log2(max_depth)) rounds
+  d.kin_onepass = 1;
+  for (int bI = 0; bI < m.nbody; ++bI) {
+    const int nj = m.body_jntnum[bI];
+    if (nj > 1) d.kin_onepass = 0;
+    if (nj == 1) {
+      const int t = m.jnt_type[m.body_jntadr[bI]];
+      if (t != MRS_JNT_HINGE && t != MRS_JNT_FREE) d.kin_onepass = 0;
+    }
+  }
+  if (std::getenv("MRS_KIN_TWOPASS")) d.kin_onepass = 0;  // A/B: the joint frames from a second pass
   d.njump = 0;
   while ((1 << d.njump) < m.max_depth) ++d.njump;
   std::vector<int> jump(std::max(1, d.njump * m.nbody), -1);

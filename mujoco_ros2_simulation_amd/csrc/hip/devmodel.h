@@ -79,6 +79,7 @@ struct DevModel {
   ScratchLayout S;
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth, njump;
+  int kin_onepass;  // every body has no joint or one hinge / free joint: kinematics' one-pass joint frames
   int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other, rf_common;
   // kinematic trees with dofs; blocked: M per tree + sparse constraint rows (set when G = 64);
   // pipe_w: dof slots per constraint row in the sparse solver (64 / pipe_w rows in flight per wave)

@@ -2170,6 +2170,35 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
       }
       wsync();
     }
+    if (m.kin_onepass) {
+      // (every body has no joint or one hinge / free joint) the jumps left each body's world pose in
+      // pos / q, and its joint frame follows from that pose: a hinge turns the body about the joint's
+      // anchor and axis, so both are the same before and after the rotation -- xanchor = xpos + R jnt_pos,
+      // xaxis = R jnt_axis (mj_kinematics computes them before applying the joint); a free joint's
+      // anchor is the body position, axis 0.  No second pass from the parents' poses.
+      if (b >= 1 && b < m.nbody) {
+        quat_normalize(q);
+        const auto kb = kin_body<G>(m, b);
+        if (__float_as_int(kb[18]) == 1) {
+          const int j = __float_as_int(kb[17]);
+          const auto kj = kin_jnt<G>(m, j);
+          float anc[3] = {pos[0], pos[1], pos[2]}, ax[3] = {0, 0, 0};
+          if (__float_as_int(kj[7]) == MRS_JNT_HINGE) {
+            const float jp[3] = {kj[0], kj[1], kj[2]}, ja3[3] = {kj[3], kj[4], kj[5]};
+            float r[3];
+            rot_quat(r, jp, q);
+            for (int i = 0; i < 3; ++i) anc[i] += r[i];
+            rot_quat(ax, ja3, q);
+          }
+          for (int i = 0; i < 3; ++i) { s[L.xanchor + 3 * j + i] = anc[i]; s[L.xaxis + 3 * j + i] = ax[i]; }
+        }
+        body_frame_out<G>(m, s, b, pos, q);
+      } else if (b == 0) {
+        float q1[4] = {1, 0, 0, 0};
+        body_frame_out<G>(m, s, 0, P0, q1);
+      }
+      wsync();
+    } else {
     // every body from its parent's world pose (same values up to rounding, plus joint frames)
     float P[3] = {0, 0, 0}, Q[4] = {1, 0, 0, 0};
     if (b >= 1 && b < m.nbody) {
@@ -2186,6 +2215,7 @@ __device__ MRS_PHASE void kinematics(ENV_PARAMS) {
       body_frame_out<G>(m, s, 0, P0, q1);
     }
     wsync();
+    }
   } else {
     MRS_COLD(G, kinematics_levels<G>(ENV_ARGS));
   }
