@@ -1464,7 +1464,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   // force limit flag and range; per dof (16 floats) its single actuator (-1 none, -2 several: the
   // actuator loop runs), that actuator's gear, the joint's actuator-force limit flag and range,
   // joint type, stiffness, qpos address, qpos_spring, the dof's damping, body, subtree end,
-  // whether any body of the subtree has gravcomp and the dof's friction-loss row (-1 none)
+  // whether any body of the subtree has gravcomp, the dof's friction-loss row (-1 none) and its
+  // joint's first dof
   std::vector<float> actrec, dofrec;
   {
     auto fbits = [](int v) { float f; std::memcpy(&f, &v, sizeof f); return f; };
@@ -1495,7 +1496,8 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
                               static_cast<float>(m.jnt_actfrcrange[2 * jid + 1]), fbits(m.jnt_type[jid]),
                               static_cast<float>(m.jnt_stiffness[jid]), fbits(m.jnt_qposadr[jid]),
                               static_cast<float>(m.qpos_spring[m.jnt_qposadr[jid]]), static_cast<float>(m.dof_damping[j]),
-                              fbits(b), fbits(subtree_end[b]), fbits(gc), fbits(fric_row[j]), 0.0f, 0.0f};
+                              fbits(b), fbits(subtree_end[b]), fbits(gc), fbits(fric_row[j]),
+                              fbits(m.jnt_dofadr[jid]), 0.0f};
       dofrec.insert(dofrec.end(), r.begin(), r.end());
     }
   }

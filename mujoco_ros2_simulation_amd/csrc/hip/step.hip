@@ -2351,7 +2351,11 @@ __device__ __forceinline__ void tree_prefix6(const DevModel& m, lfloat* buf, int
   wsync();
   #pragma unroll 1
   for (int r = 0; r < m.njump; ++r) {
-    const int a = (b >= 1 && b < m.nbody) ? m.jump[r * m.nbody + b] : -1;
+    int a = -1;
+    if (b >= 1 && b < m.nbody) {
+      if constexpr (G == 64) a = m.jump[r * m.nbody + b];
+      else a = __float_as_int(shared_lds(m)[m.shr_jump + r * m.nbody + b]);
+    }
     float av[6];
     if (a >= 0)
       for (int i = 0; i < 6; ++i) av[i] = buf[6 * a + i];
@@ -2365,14 +2369,18 @@ __device__ __forceinline__ void tree_prefix6(const DevModel& m, lfloat* buf, int
 }
 
 // cdof_dot of body b's dofs from the velocity of its parent (mj_comVel per body); returns cvel[b]
+// (dof and body indices from the tree tables: workgroup LDS with lane groups)
+template <int G>
 __device__ __forceinline__ void body_comvel(const DevModel& m, lfloat* s, int b, float cv[6]) {
   const LdsLayout& L = m.L;
-  const int da = m.body_dofadr[b], nd = m.body_dofnum[b];
+  const auto bt = body_tab<G>(m, b);
+  const int da = __float_as_int(bt[5]), nd = __float_as_int(bt[6]);
   #pragma unroll 1
   for (int k2 = 0; k2 < nd; ++k2) {
     const int j = da + k2;
-    const int jid = m.dof_jntid[j], jt = m.jnt_type[jid];
-    if (jt == MRS_JNT_FREE && j == m.jnt_dofadr[jid]) {
+    const auto dr = dof_tab<G>(m, j);
+    const int jt = __float_as_int(dr[5]);
+    if (jt == MRS_JNT_FREE && j == __float_as_int(dr[14])) {
       for (int t = 0; t < 3; ++t) {
         const float qv = s[L.qvel + j + t];
         for (int i = 0; i < 6; ++i) {
@@ -2422,7 +2430,7 @@ __device__ MRS_PHASE void com_vel(ENV_PARAMS) {
       const int p = __float_as_int(body_tab<G>(m, b)[3]);
       float cv[6];
       for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
-      body_comvel(m, s, b, cv);
+      body_comvel<G>(m, s, b, cv);
     }
     wsync();
     return;
@@ -2444,7 +2452,7 @@ __device__ void com_vel_levels(ENV_PARAMS) {
       const int p = m.body_parentid[b];
       float cv[6];
       for (int i = 0; i < 6; ++i) cv[i] = s[L.cvel + 6 * p + i];
-      body_comvel(m, s, b, cv);
+      body_comvel<G>(m, s, b, cv);
       for (int i = 0; i < 6; ++i) s[L.cvel + 6 * b + i] = cv[i];
     }
     wsync();
@@ -7028,8 +7036,10 @@ __device__ __forceinline__ void integrate_pos(const DevModel& m, lfloat* s, cons
   const LdsLayout& L = m.L;
   #pragma unroll 1
   for (int j = lane; j < m.njnt; j += G) {
-    int a = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
-    const int jt = m.jnt_type[j];
+    const auto kj = kin_jnt<G>(m, j);  // (workgroup LDS with lane groups: no global load right after
+    //                                   the step's sensordata stores, which it would wait for)
+    int a = __float_as_int(kj[6]), da = __float_as_int(kj[10]);
+    const int jt = __float_as_int(kj[7]);
     if (jt == MRS_JNT_HINGE || jt == MRS_JNT_SLIDE) {
       s[L.qpos + a] += h * vel[da];
       continue;
