@@ -1943,6 +1943,17 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       lds_layout(false);
     }
   }
+  // the integrator's M + h D factored together with M (step.hip cholesky_ih) into M's own LDS slot,
+  // which PGS models no longer read after the factor: 16-lane groups without helper waves (they
+  // factor it on the helper), implicitfast, PGS, and no force-limited actuator (their velocity
+  // derivative depends on the step's actuator forces, which come after the factor).  MRS_NO_FUSE_IH=1
+  // factors it in integrate() instead (A/B)
+  {
+    bool flim = false;
+    for (int a = 0; a < m.nu; ++a) flim |= m.actuator_forcelimited[a] != 0;
+    d.fuse_ih = b.group == 16 && !b.helpers && m.integrator == MRS_INT_IMPLICITFAST && m.solver == MRS_SOL_PGS &&
+                !flim && m.nv <= 16 && !std::getenv("MRS_NO_FUSE_IH") ? 1 : 0;
+  }
   d.blocked = b.group == 64 ? 1 : 0;
   if (b.group == 64) d.shr_total = shr_small;
 

@@ -1831,6 +1831,45 @@ __device__ __forceinline__ void chol_rows16(const lfloat* A, lfloat* Lf, int nv,
     });
 }
 
+// two factors in one pass: M (into Lf) and M + diag(h dg) (into Lh, which may alias A): the same
+// register row form, the two column chains interleaved so each hides the other's latency
+// (DevModel::fuse_ih); the diagonal update is integrate()'s fma, so both factors are bit-identical to
+// the separate ones
+template <int N>
+__device__ __forceinline__ void chol_rows16_dual(const lfloat* A, lfloat* Lf, lfloat* Lh, float h, float dg, int nv,
+                                                 int lane) {
+  float ra[N], rb[N];
+  unroll<N>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    ra[p] = (p < nv && lane < nv) ? A[lane * nv + p] : 0.0f;
+    rb[p] = p == lane ? __builtin_fmaf(h, dg, ra[p]) : ra[p];
+  });
+  unroll<N>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if (k < nv) {
+      float ta = ra[k], tb = rb[k];
+      unroll<k>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        ta -= ra[p] * rowb<k>(ra[p]);
+        tb -= rb[p] * rowb<k>(rb[p]);
+      });
+      const float da = rowb<k>(ta), db = rowb<k>(tb);
+      const float la = sqrtf(da > kMinVal ? da : kMinVal), lb = sqrtf(db > kMinVal ? db : kMinVal);
+      ra[k] = lane == k ? la : (lane > k ? ta / la : ra[k]);
+      rb[k] = lane == k ? lb : (lane > k ? tb / lb : rb[k]);
+    }
+  });
+  wsync();  // (Lh may alias A: every lane has read its row)
+  if (lane < nv)
+    unroll<N>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      if (p < nv) {
+        Lf[lane * nv + p] = p <= lane ? ra[p] : 0.0f;
+        Lh[lane * nv + p] = p <= lane ? rb[p] : 0.0f;
+      }
+    });
+}
+
 template <int G>
 __device__ MRS_PHASE void cholesky(const DevModel* __restrict__ mp, const lfloat* A, lfloat* Lf, int lane) {
   mp = uniform_ptr(mp);
@@ -6968,6 +7007,9 @@ __device__ __forceinline__ bool any_bad_step(ENV_PARAMS, int off, int n) {
   return any_bad<G>(ENV_ARGS, off, n);
 }
 
+template <int G>
+__device__ __forceinline__ void cholesky_ih(ENV_PARAMS);
+
 // full forward pass; returns the contact count.  With acc_bad, *acc_bad is the group's vote on qacc
 // (mj_checkAcc), taken from the solver's lane-per-dof result in registers
 template <int G, bool kPrimal = false>
@@ -6989,7 +7031,8 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
   PH_END(ph_acc, PH_COMPOS);
   MRS_CALL(G, make_M<G>(ENV_ARGS));
   PH_END(ph_acc, PH_MAKEM);
-  MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
+  if (G == 16 && m.fuse_ih) MRS_CALL(G, cholesky_ih<G>(ENV_ARGS));
+  else MRS_CALL(G, cholesky<G>(mp, s + L.M, s + L.L, lane));
   PH_END(ph_acc, PH_CHOL);
   MRS_CALL(G, com_vel<G>(ENV_ARGS));
   PH_END(ph_acc, PH_COMVEL);
@@ -7127,8 +7170,21 @@ __device__ __forceinline__ void integrate_prefactor(ENV_PARAMS) {
   MRS_CALL(G, cholesky<G>(mp, s + L.Lh, s + L.Lh, lane));
 }
 
-// mj_Euler / mj_implicit(implicitfast) + mj_advance (prefac: the factor of M + h D is in L.Lh,
-// built by the helper wave)
+// M's factor (L.L) and, for integrate(), the factor of M + h D in M's slot (DevModel::fuse_ih: 16-lane
+// PGS implicitfast models, whose M is not read after the factor)
+template <int G>
+__device__ __forceinline__ void cholesky_ih(ENV_PARAMS) {
+  ENV_UNPACK;
+  if constexpr (G == 16) {
+    const float dg = integrate_dg<G>(ENV_ARGS);
+    if (m.nv <= 8) chol_rows16_dual<8>(s + L.M, s + L.L, s + L.M, m.timestep, dg, m.nv, lane);
+    else chol_rows16_dual<16>(s + L.M, s + L.L, s + L.M, m.timestep, dg, m.nv, lane);
+    wsync();
+  }
+}
+
+// mj_Euler / mj_implicit(implicitfast) + mj_advance (prefac: the factor of M + h D is in L.Lh, built
+// by the helper wave, or with DevModel::fuse_ih in L.M, built beside M's factor)
 template <int G>
 __device__ MRS_PHASE void integrate(ENV_PARAMS, bool prefac = false) {
   ENV_UNPACK;
@@ -7145,7 +7201,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS, bool prefac = false) {
   if (need_solve) {
     const float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
     if (prefac) {
-      MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + L.Lh, rhs, lane));
+      MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + (m.fuse_ih ? L.M : L.Lh), rhs, lane));
     } else {
       // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
       if (lane < nv) s[L.M + midx<G>(m, lane, lane)] += h * dg;
@@ -7540,7 +7596,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     } else {
       PH_BEGIN();
       // (a re-run step's factor is its own: the helper's was of the first forward's state)
-      MRS_CALL(G, integrate<G>(ENV_ARGS, helpers && L.Lh != 0 && !__any(redo)));
+      MRS_CALL(G, integrate<G>(ENV_ARGS, (helpers && L.Lh != 0 && !__any(redo)) || (G == 16 && m.fuse_ih)));
       PH_END(ph_acc, PH_INTEG);
     }
     time += m.timestep_d;

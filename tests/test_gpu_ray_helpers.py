@@ -14,8 +14,15 @@ ROOT = Path(__file__).resolve().parents[1]
 pytestmark = pytest.mark.gpu
 
 
-def _run(xml: Path, n: int, steps: int, helpers: bool, monkeypatch):
+def _run(xml: Path, n: int, steps: int, helpers: bool, monkeypatch, fuse: bool = False):
     monkeypatch.setenv("MRS_RAY_HELPERS", "1" if helpers else "0")
+    # without helpers, implicitfast PGS models factor M + h D beside M (DevModel::fuse_ih): the same
+    # factor in another instruction order; the bit-identity reference factors it in integrate(), as
+    # the helper does
+    if fuse:
+        monkeypatch.delenv("MRS_NO_FUSE_IH", raising=False)
+    else:
+        monkeypatch.setenv("MRS_NO_FUSE_IH", "1")
     model = sim.Model.load(xml)
     b = sim.Batch(model, n)
     rng = np.random.default_rng(7)
@@ -40,6 +47,12 @@ def test_ray_helpers_bit_identical(scene, n, monkeypatch):
     for k, (x, y) in enumerate(zip(a, c)):
         for name, u, v in zip(("qpos", "qvel", "sensordata"), x, y):
             assert np.array_equal(u, v), (scene, k, name, np.abs(u - v).max())
+    # the fused factor (default without helpers) agrees to fp32 rounding: one-ulp differences of the
+    # factor carried through 50 steps of the stiff position servos (kp 1000) measure ~1e-5 here
+    f = _run(xml, n, 5, False, monkeypatch, fuse=True)
+    for k, (x, y) in enumerate(zip(a, f)):
+        for name, u, v in zip(("qpos", "qvel"), x, y):
+            assert np.max(np.abs(u - v) / np.maximum(np.abs(u), 1)) <= 1e-4, (scene, k, name, np.abs(u - v).max())
     # the lidar saw something (the comparison is not of empty outputs)
     assert np.any(a[-1][2] > 0)
 
