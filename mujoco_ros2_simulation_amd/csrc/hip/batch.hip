@@ -6,6 +6,7 @@
 #include <cmath>
 #include <array>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -360,7 +361,11 @@ __global__ __launch_bounds__(256) void depth_kernel(const int* geom_type, const 
 #ifndef MRS_DEPTH_TILE_H
 #define MRS_DEPTH_TILE_H 16  // measured C4 (2048 frames): 4 rows 2.08 ms, 8 rows 1.70, 16 rows 1.68, 32 rows 2.13
 #endif
-constexpr int kDepthTileW = 64, kDepthTileH = MRS_DEPTH_TILE_H, kDepthGeoms = 64;
+#ifndef MRS_DEPTH_CHUNK
+#define MRS_DEPTH_CHUNK 8  // rows of a tile evaluated together (registers: the chunk's rows only; measured C4 frames alone 1.66 ms at 8, 1.77 at 4 and 16)
+#endif
+constexpr int kDepthTileW = 64, kDepthTileH = MRS_DEPTH_TILE_H, kDepthGeoms = 64, kDepthChunk = MRS_DEPTH_CHUNK;
+static_assert(kDepthTileH % kDepthChunk == 0, "a tile is a whole number of row chunks");
 struct DepthGeom {  // 30 words in LDS
   float lp[3], A[9], size[3];  // row i of A = R'C is also the geom's axis i in the camera frame
   float cc[3], ext[3];         // cull: centre in the camera frame, oriented-box half extents
@@ -437,6 +442,7 @@ __device__ __forceinline__ void stage_depth_geom(DepthGeom* G, const int* geom_t
 // shadow ray of the camera-frame kernels (lit_pixel's occluded): does a shadow-casting geom cross
 // o + s L, 0 <= s < dist?  Geom-frame ray through the staged lp and A (a camera-frame point o maps to
 // lp + A o); a bounding-sphere reject on the culling box first.  Oracle: ray_scene over groups 0-2.
+template <bool kMesh = true>
 __device__ inline bool occluded_staged(const DepthGeom* G, int ngeom, const MeshRef& mesh, const float o[3],
                                        const float L[3], float dist) {
   for (int k = 0; k < ngeom; ++k) {
@@ -456,7 +462,7 @@ __device__ inline bool occluded_staged(const DepthGeom* G, int ngeom, const Mesh
     }
     float t;
     if (h.type == MRS_GEOM_BOX) t = ray_box_slab(h.size, lp, lv);
-    else if (h.type == MRS_GEOM_MESH) {
+    else if (kMesh && h.type == MRS_GEOM_MESH) {
       int tri;
       t = ray_mesh(mesh.tri + 9 * mesh.faceadr[h.dataid], mesh.facenum[h.dataid], h.size, lp, lv,
                    mesh.bvh + 8 * mesh.bvhadr[h.dataid], mesh.bvhnum[h.dataid], &tri);
@@ -465,8 +471,18 @@ __device__ inline bool occluded_staged(const DepthGeom* G, int ngeom, const Mesh
   }
   return false;
 }
-template <bool kRGB>
-__global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, const int* geom_group,
+#ifdef MRS_DEPTH_STATS
+// diagnostics build: tiles, candidate visits and visits whose geom is the nearest hit of some pixel of
+// the tile, summed over every frame (printed when the batch is freed)
+__device__ unsigned long long g_depth_stats[4];
+#endif
+#ifndef MRS_DEPTH_MINBLK
+#define MRS_DEPTH_MINBLK 1
+#endif
+// kMesh: the frame has mesh geoms (their per-pixel hierarchy walk, MRS_DEPTH_V2); frames without
+// them take the instance without that code, whose registers allow more resident workgroups
+template <bool kRGB, bool kMesh>
+__global__ __launch_bounds__(256, MRS_DEPTH_MINBLK) void depth_kernel_v2(const int* geom_type, const int* geom_group,
                                                        const float* geom_size, const float* geom_rgba, int ngeom,
                                                        const float* geom_xpos, const float* geom_xmat,
                                                        const float* cam_xpos, const float* cam_xmat, int ncam, int cam,
@@ -515,14 +531,20 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
     unsigned long long cand = __ballot(keep);
     const int col = tx * kDepthTileW + lane;
     const float dx = (col + 0.5f - 0.5f * W) / f;
-    float best[kDepthTileH], dy[kDepthTileH];
-    int bestg[kDepthTileH];
+    const unsigned long long cand_tile = cand;
+    // the tile's rows in chunks of kDepthChunk under the tile's one cull: only a chunk's rows are
+    // live in registers (the fully unrolled 16-row tile held ~160 VGPRs, 3 workgroups per CU)
+#pragma unroll 1
+    for (int r0 = 0; r0 < kDepthTileH; r0 += kDepthChunk) {
+    float best[kDepthChunk], dy[kDepthChunk];
+    int bestg[kDepthChunk];
 #pragma unroll
-    for (int k = 0; k < kDepthTileH; ++k) {
+    for (int k = 0; k < kDepthChunk; ++k) {
       best[k] = -1;
       bestg[k] = 0;
-      dy[k] = (0.5f * H - (ty * kDepthTileH + k) - 0.5f) / f;
+      dy[k] = (0.5f * H - (ty * kDepthTileH + r0 + k) - 0.5f) / f;
     }
+    cand = cand_tile;
     while (cand) {
       const int g = __builtin_ctzll(cand);
       cand &= cand - 1;
@@ -532,12 +554,12 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
       for (int i = 0; i < 9; ++i) A[i] = o.A[i];
       const int type = o.type;
 #pragma unroll
-      for (int k = 0; k < kDepthTileH; ++k) {
+      for (int k = 0; k < kDepthChunk; ++k) {
         float lv[3];
         pixel_ray(A, dx, dy[k], lv);
         float t;
         if (type == MRS_GEOM_BOX) t = ray_box_slab(sz, lp, lv);
-        else if (type == MRS_GEOM_MESH)
+        else if (kMesh && type == MRS_GEOM_MESH)
         {
           int tri;
           t = ray_mesh(mesh.tri + 9 * mesh.faceadr[o.dataid], mesh.facenum[o.dataid], sz, lp, lv,
@@ -547,16 +569,34 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
         if (t >= znear && (best[k] < 0 || t < best[k])) { best[k] = t; bestg[k] = g; }
       }
     }
+#ifdef MRS_DEPTH_STATS
+    if (r0 == 0) {
+      unsigned long long cc = cand_tile, won = 0;
+      const int ncand = __popcll(cc);
+      while (cc) {
+        const int g = __builtin_ctzll(cc);
+        cc &= cc - 1;
+        bool w = false;
+        for (int k = 0; k < kDepthChunk; ++k) w |= best[k] >= 0 && best[k] <= zfar && bestg[k] == g;
+        if (__any(w)) ++won;
+      }
+      if (lane == 0) {
+        atomicAdd(&g_depth_stats[0], 1ull);
+        atomicAdd(&g_depth_stats[1], static_cast<unsigned long long>(ncand));
+        atomicAdd(&g_depth_stats[2], won);
+      }
+    }
+#endif
     if (col < W) {
 #pragma unroll
-      for (int k = 0; k < kDepthTileH; ++k) {
-        const int row = ty * kDepthTileH + k;
+      for (int k = 0; k < kDepthChunk; ++k) {
+        const int row = ty * kDepthTileH + r0 + k;
         if (row < H) img[static_cast<size_t>(row) * W + col] = (best[k] < 0 || best[k] > zfar) ? zfar : best[k];
       }
       if constexpr (kRGB) {
         unsigned char* frame = rgb + static_cast<size_t>(blockIdx.x) * W * H * 3;
-        for (int k = 0; k < kDepthTileH; ++k) {
-          const int row = ty * kDepthTileH + k;
+        for (int k = 0; k < kDepthChunk; ++k) {
+          const int row = ty * kDepthTileH + r0 + k;
           if (row >= H) break;
           unsigned char* px = frame + (static_cast<size_t>(row) * W + col) * 3;
           if (best[k] < 0 || best[k] > zfar) { lit_sky(LF, dx, dy[k], px); continue; }
@@ -566,7 +606,7 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
           float q[3], nl[3], nc[3], lv[3];
           pixel_ray(o.A, dx, dy[k], lv);
           for (int i = 0; i < 3; ++i) q[i] = o.lp[i] + best[k] * lv[i];
-          if (o.type == MRS_GEOM_MESH) {  // the hit triangle's normal, facing the ray
+          if (kMesh && o.type == MRS_GEOM_MESH) {  // the hit triangle's normal, facing the ray
             const float* mv = mesh.vert + 3 * mesh.vertadr[o.dataid];
             const int* mf = mesh.face + 3 * mesh.faceadr[o.dataid];
             int tri = 0;
@@ -578,10 +618,11 @@ __global__ __launch_bounds__(256) void depth_kernel_v2(const int* geom_type, con
           }
           for (int j = 0; j < 3; ++j) nc[j] = nl[0] * o.A[j] + nl[1] * o.A[3 + j] + nl[2] * o.A[6 + j];
           lit_pixel(LF, lr, g, o.rgba, o.type, o.size, q, dx, dy[k], best[k], nc,
-                    [&](const float* so, const float* sl, float sd) { return occluded_staged(G, ngeom, mesh, so, sl, sd); },
+                    [&](const float* so, const float* sl, float sd) { return occluded_staged<kMesh>(G, ngeom, mesh, so, sl, sd); },
                     px);
         }
       }
+    }
     }
   }
 }
@@ -2089,6 +2130,14 @@ BatchImpl* batch_create(const Model* model, int n_envs, int device, int max_cont
 }
 
 void batch_free(BatchImpl* b) {
+#ifdef MRS_DEPTH_STATS
+  {
+    unsigned long long h[4] = {};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_depth_stats), sizeof h) == hipSuccess && h[0])
+      fprintf(stderr, "depth stats: tiles %llu, candidate visits %llu (%.2f per tile), winning visits %llu (%.1f %%)\n",
+              h[0], h[1], static_cast<double>(h[1]) / h[0], h[2], 100.0 * h[2] / std::max(1ull, h[1]));
+  }
+#endif
   if (!b) return;
   (void)hipSetDevice(b->device);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
@@ -2285,7 +2334,11 @@ void render_launch(BatchImpl* b, int cam, int env0, int n, float* dout, unsigned
                          d.rast_geom.p, d.rast_base.p, d.nrast, d.nrast_pair, b->rast_list, lr);
     }
   } else if (m.ngeom <= kDepthGeoms && !std::getenv("MRS_DEPTH_V1")) {
-    hipLaunchKernelGGL(drgb ? depth_kernel_v2<true> : depth_kernel_v2<false>, dim3(n), dim3(256), 0, stream,
+    const bool has_mesh = d.nrast > 0 || std::any_of(m.geom_type.begin(), m.geom_type.end(),
+                                                      [](int t) { return t == MRS_GEOM_MESH; });
+    auto kern = has_mesh ? (drgb ? depth_kernel_v2<true, true> : depth_kernel_v2<false, true>)
+                         : (drgb ? depth_kernel_v2<true, false> : depth_kernel_v2<false, false>);
+    hipLaunchKernelGGL(kern, dim3(n), dim3(256), 0, stream,
                        d.geom_type.p, d.geom_group.p, d.geom_size.p,
                        d.geom_rgba.p, m.ngeom, ps.gpos, ps.gmat, ps.cpos, ps.cmat, m.ncam,
                        cam, env0, W, H, f, znear, zfar, dout, drgb, mesh, lr);
