@@ -1080,6 +1080,7 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   d.max_depth = m.max_depth;
   d.integrator = m.integrator; d.iterations = m.iterations; d.disableflags = m.disableflags;
   d.solver = m.solver; d.ls_iterations = m.ls_iterations; d.cone = m.cone; d.restate = m.restate;
+  if (std::getenv("MRS_NO_MULTICCD")) d.restate |= MRS_RESTATE_NO_MULTICCD;  // (A/B of the face contacts)
   d.impratio = static_cast<float>(m.impratio); d.ls_tolerance = static_cast<float>(m.ls_tolerance);
   // diagnostic phase ablation for profiling only (bit 0 sensors, 1 collision, 2 constraints)
   d.diag_skip = std::getenv("MRS_DIAG_SKIP") ? std::atoi(std::getenv("MRS_DIAG_SKIP")) : 0;

@@ -1399,9 +1399,11 @@ __device__ __forceinline__ void shape_of(const DevModel& m, int g, const float* 
 // restates the same steps in fp64): the support faces along MPR's normal, and when
 // the better aligned one is within kPolyCos of it, the other face's polygon clipped by its side
 // planes, every clipped vertex within margin of the reference plane a contact (at most
-// kMaxPairCon).  Returns -1 when the pair is not face-on (MPR's single contact stays).  Out of line
-// with its polygons in private memory: only the extended kernels of mesh models reach it.
-constexpr int kPolyMaxV = 16;
+// kMaxPairCon).  Returns -1 when the pair is not face-on or a support face has more than kPolyMaxV
+// vertices (MPR's single contact stays).  Inlined: out of line, its reference arguments forced the
+// caller's model copy and shapes into scratch memory, which cost the mesh robot's extended kernel
+// 10 % (C3m 4.42 -> 4.84 ms per launch) although that scene has no polytope pair.
+constexpr int kPolyMaxV = 8;
 constexpr float kPolyCos = 0.999f;
 struct PolyFace { int n; float v[kPolyMaxV][3]; float nrm[3]; };
 __device__ __forceinline__ float poly_support_face(const DevModel& m, const Shape& s, int g, const float dir[3],
@@ -1450,7 +1452,7 @@ __device__ __forceinline__ float poly_support_face(const DevModel& m, const Shap
   }
   return ba;
 }
-__device__ __attribute__((noinline)) int poly_face_contacts(const DevModel& m, const Shape& A, int g1, const Shape& B,
+__device__ __forceinline__ int poly_face_contacts(const DevModel& m, const Shape& A, int g1, const Shape& B,
                                                             int g2, const float nrm[3], float margin, gCon* out) {
   PolyFace fa, fb;
   const float nb[3] = {-nrm[0], -nrm[1], -nrm[2]};

@@ -1673,8 +1673,8 @@ static int mpr_polish(const orc_shape* A, const orc_shape* B, const double n0[3]
  * flat face-on-face rest gets its corners, a box tipped onto an edge the edge's ends.  Otherwise
  * (edge-edge, vertex contacts) MPR's single contact stays.  The reference face is geom1's unless
  * geom2's alignment is larger by more than 1e-4 (fp32 and fp64 break a tie between two flat faces
- * the same way). */
-#define POLY_MAXV 16
+ * the same way).  Faces of more than POLY_MAXV vertices keep MPR's single contact, as on the device. */
+#define POLY_MAXV 8
 #define POLY_COS 0.999
 typedef struct { int n; double v[POLY_MAXV][3]; double nrm[3]; } orc_poly;
 /* support face of shape s (box or mesh geom g) along dir; returns the alignment n_face.dir, or -2
