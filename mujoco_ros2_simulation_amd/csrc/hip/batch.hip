@@ -1985,16 +1985,26 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
       lds_layout(false);
     }
   }
-  // the integrator's M + h D factored together with M (step.hip cholesky_ih) into M's own LDS slot,
-  // which PGS models no longer read after the factor: 16-lane groups without helper waves (they
-  // factor it on the helper), implicitfast, PGS, and no force-limited actuator (their velocity
-  // derivative depends on the step's actuator forces, which come after the factor).  MRS_NO_FUSE_IH=1
-  // factors it in integrate() instead (A/B)
+  // the integrator's M + h D factored together with M (step.hip cholesky_ih): into M's own LDS slot
+  // for PGS models, which no longer read M after the factor, into the L.Lh slot for Newton / CG
+  // (their primal solve multiplies by M).  16-lane groups without helper waves (they factor it on the
+  // helper), implicitfast, and no force-limited actuator (their velocity derivative depends on the
+  // step's actuator forces, which come after the factor).  MRS_NO_FUSE_IH=1 factors it in integrate()
+  // instead (A/B)
   {
     bool flim = false;
     for (int a = 0; a < m.nu; ++a) flim |= m.actuator_forcelimited[a] != 0;
-    d.fuse_ih = b.group == 16 && !b.helpers && m.integrator == MRS_INT_IMPLICITFAST && m.solver == MRS_SOL_PGS &&
-                !flim && m.nv <= 16 && !std::getenv("MRS_NO_FUSE_IH") ? 1 : 0;
+    d.fuse_ih = b.group == 16 && !b.helpers && m.integrator == MRS_INT_IMPLICITFAST && !flim && m.nv <= 16 &&
+                !std::getenv("MRS_NO_FUSE_IH") ? 1 : 0;
+    if (d.fuse_ih && m.solver != MRS_SOL_PGS && !want_lh) {
+      want_lh = true;
+      lds_layout(false);
+      if ((static_cast<size_t>(L.total) * envs_per_block(b.group, b.wpb16) + d.shr_total) * sizeof(float) > 160 * 1024) {
+        d.fuse_ih = 0;  // (the extra nv x nv slot does not fit the workgroup's LDS: factor in integrate())
+        want_lh = false;
+        lds_layout(false);
+      }
+    }
   }
   d.blocked = b.group == 64 ? 1 : 0;
   if (b.group == 64) d.shr_total = shr_small;
@@ -2159,11 +2169,11 @@ void batch_free(BatchImpl* b) {
 int batch_num_envs(const BatchImpl* b) { return b->n; }
 
 int batch_layout(const BatchImpl* b, int* out, int n) {
-  const int v[13] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
+  const int v[14] = {b->group, b->dm.L.total, b->dm.S.total, b->dm.blocked, b->dm.pipe_w, b->dm.max_efc,
                      b->dm.max_con, b->dm.ntree, b->dm.shr_total, b->dm.rf_common, b->g16_one_wg,
-                     b->group == 16 ? b->wpb16 : 0, b->helpers};
+                     b->group == 16 ? b->wpb16 : 0, b->helpers, b->dm.fuse_ih};
   int k = 0;
-  for (; k < n && k < 13; ++k) out[k] = v[k];
+  for (; k < n && k < 14; ++k) out[k] = v[k];
   return k;
 }
 

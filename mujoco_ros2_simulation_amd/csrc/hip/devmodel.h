@@ -80,7 +80,7 @@ struct DevModel {
   // sizes
   int nq, nv, nu, nbody, njnt, ngeom, nsite, ncam, nsensor, nsensordata, max_depth, njump;
   int kin_onepass;  // every body has no joint or one hinge / free joint: kinematics' one-pass joint frames
-  int fuse_ih;      // 16-lane PGS implicitfast models: M + h D factored beside M (step.hip cholesky_ih)
+  int fuse_ih;      // 16-lane implicitfast models: M + h D factored beside M (step.hip cholesky_ih)
   int nfric, nlim, npair, nrf, nMpair, max_con, max_efc, nrgeom, nrfblk, nsens_other, rf_common;
   // kinematic trees with dofs; blocked: M per tree + sparse constraint rows (set when G = 64);
   // pipe_w: dof slots per constraint row in the sparse solver (64 / pipe_w rows in flight per wave)

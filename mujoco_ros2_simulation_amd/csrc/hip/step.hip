@@ -7172,15 +7172,16 @@ __device__ __forceinline__ void integrate_prefactor(ENV_PARAMS) {
   MRS_CALL(G, cholesky<G>(mp, s + L.Lh, s + L.Lh, lane));
 }
 
-// M's factor (L.L) and, for integrate(), the factor of M + h D in M's slot (DevModel::fuse_ih: 16-lane
-// PGS implicitfast models, whose M is not read after the factor)
+// M's factor (L.L) and, for integrate(), the factor of M + h D (DevModel::fuse_ih: 16-lane implicitfast
+// models) in M's slot for PGS, whose M is not read after the factor, in L.Lh for Newton / CG
 template <int G>
 __device__ __forceinline__ void cholesky_ih(ENV_PARAMS) {
   ENV_UNPACK;
   if constexpr (G == 16) {
     const float dg = integrate_dg<G>(ENV_ARGS);
-    if (m.nv <= 8) chol_rows16_dual<8>(s + L.M, s + L.L, s + L.M, m.timestep, dg, m.nv, lane);
-    else chol_rows16_dual<16>(s + L.M, s + L.L, s + L.M, m.timestep, dg, m.nv, lane);
+    lfloat* ih = s + (m.solver == MRS_SOL_PGS ? L.M : L.Lh);
+    if (m.nv <= 8) chol_rows16_dual<8>(s + L.M, s + L.L, ih, m.timestep, dg, m.nv, lane);
+    else chol_rows16_dual<16>(s + L.M, s + L.L, ih, m.timestep, dg, m.nv, lane);
     wsync();
   }
 }
@@ -7203,7 +7204,7 @@ __device__ MRS_PHASE void integrate(ENV_PARAMS, bool prefac = false) {
   if (need_solve) {
     const float rhs = lane < nv ? s[L.qfrc_smooth + lane] + s[L.qfrc_con + lane] : 0.0f;
     if (prefac) {
-      MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + (m.fuse_ih ? L.M : L.Lh), rhs, lane));
+      MRS_CALL(G, qacc_int = chol_solve_lanes<G>(mp, s + (m.fuse_ih && m.solver == MRS_SOL_PGS ? L.M : L.Lh), rhs, lane));
     } else {
       // M + h*diag(dg) into the M slot (M is rebuilt every step), factor into L
       if (lane < nv) s[L.M + midx<G>(m, lane, lane)] += h * dg;

@@ -362,10 +362,11 @@ class Batch:
     def layout(self) -> dict:
         """kernel configuration of this batch (diagnostics): group width, LDS and scratch floats per
         env, blocked mode, pipe width, row and contact capacity, kinematic trees"""
-        out = np.zeros(13, dtype=np.int32)
-        k = lib().mrs_debug_batch_layout(self._h, out.ctypes.data, 13)
+        out = np.zeros(14, dtype=np.int32)
+        k = lib().mrs_debug_batch_layout(self._h, out.ctypes.data, 14)
         keys = ["group", "lds_floats", "scratch_floats", "blocked", "pipe_w", "max_efc", "max_con", "ntree",
-                "shared_floats", "rf_common", "one_workgroup_per_cu", "waves_per_workgroup", "helper_waves"]
+                "shared_floats", "rf_common", "one_workgroup_per_cu", "waves_per_workgroup", "helper_waves",
+                "fused_integrator_factor"]
         return dict(zip(keys[:k], out[:k].tolist()))
 
     def step(self, n_steps: int = 1) -> None:

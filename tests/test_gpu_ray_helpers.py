@@ -69,3 +69,40 @@ def test_helper_configuration_per_batch_size(monkeypatch):
     lay = c3.layout()
     c3.close()
     assert lay["group"] == 16 and lay["waves_per_workgroup"] == 4 and lay["helper_waves"] == 0, lay
+
+
+@pytest.mark.parametrize("solver", ["Newton", "CG"])
+def test_fused_integrator_factor_primal_solvers(solver, monkeypatch):
+    """implicitfast models under Newton / CG on 16-lane groups factor M + h D beside M into their own
+    LDS slot (the primal solve still multiplies by M): the reference scene (C2's) agrees with the
+    separate factor in integrate() (MRS_NO_FUSE_IH=1) to fp32 rounding"""
+    import re
+    xml = (ROOT / "tests" / "golden" / "ref_scenes" / "scene.xml").read_text()
+    xml = xml.replace("<mujoco model=\"scene\">", f'<mujoco model="scene">\n  <option solver="{solver}"/>', 1)
+    assert re.search(f'solver="{solver}"', xml)
+    base = ROOT / "tests" / "golden" / "ref_scenes"
+    n = 64
+    monkeypatch.setenv("MRS_RAY_HELPERS", "0")  # (64 envs with rangefinders would take helper waves)
+    runs = {}
+    for fuse in (False, True):
+        if fuse:
+            monkeypatch.delenv("MRS_NO_FUSE_IH", raising=False)
+        else:
+            monkeypatch.setenv("MRS_NO_FUSE_IH", "1")
+        model = sim.Model.from_string(xml, str(base))
+        b = sim.Batch(model, n)
+        assert b.layout()["fused_integrator_factor"] == int(fuse), b.layout()
+        rng = np.random.default_rng(3)
+        qpos = b.get(sim.FIELD_QPOS)
+        qpos[:, :] += rng.uniform(-0.5, 0.5, qpos.shape).astype(np.float32)
+        b.set(sim.FIELD_QPOS, qpos)
+        out = []
+        for _ in range(5):
+            b.set(sim.FIELD_CTRL, rng.uniform(-1, 1, (n, model.nu)).astype(np.float32))
+            b.step(10)
+            out.append((b.get(sim.FIELD_QPOS).copy(), b.get(sim.FIELD_QVEL).copy()))
+        b.close()
+        runs[fuse] = out
+    for k, (x, y) in enumerate(zip(runs[False], runs[True])):
+        for name, u, v in zip(("qpos", "qvel"), x, y):
+            assert np.max(np.abs(u - v) / np.maximum(np.abs(u), 1)) <= 1e-4, (solver, k, name, np.abs(u - v).max())
