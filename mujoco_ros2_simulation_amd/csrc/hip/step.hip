@@ -2912,7 +2912,7 @@ __device__ __forceinline__ float sel_slot16(float own, float other) {
 // kUnit: every row's Jacobian is the unit vector of the dof held in lane r's `mydof` (dof friction
 // loss rows), built in registers instead of read from the global rows J
 // KV: the dof loops' unroll bound (>= nv; the call site picks 8 or 16), separate from the row count
-template <bool kUnit = false, int KR = 16, int KV = 16>
+template <bool kUnit = false, int KR = 16, int KV = 16, bool kRegAR = false>
 __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const gfloat* J, gfloat* ff, int nefc, int rmax,
                                              float myR, float myaref, float myb, float myfl, float qacc_s,
                                              int lane, int mydof = -1) {
@@ -2921,6 +2921,7 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   // instantiated per row count KR (the wave's rmax rounded up to 4 at the call site): rows past the
   // wave's own are zero rows, so every row loop runs to the compile-time KR without bound tests
   rmax = KR;
+  unsigned long long t_p = SUB_T();  // (timing builds: set-up / Delassus / warm start / sweeps)
   // J and M^-1 J' columns per row in registers; row scalars (R, aref, b, bound, diagonal of A, force)
   // stay in the row's own lane and reach the other lanes by DPP row broadcasts when used
   float Jt[KR], MJt[KR];
@@ -2962,6 +2963,8 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       });
     }
   });
+  SUB_ADD(PH_REC_SOLVE, t_p);
+  t_p = SUB_T();
   // Delassus rows (mj_solPGS's efc_AR): lane r holds AR_rs = J_r M^-1 J_s' (+ R_r on the diagonal)
   // for every s; each (r, s <= r) product is one group sum, mirrored into lane s
   float AR[KR];
@@ -2973,15 +2976,32 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
       constexpr int c = decltype(sc)::value;
       if (r < rmax) {
         const float a = gsum<16>(Jt[r] * MJt[c]);
-        if constexpr (c == r) {
-          if (lane == r) { AR[r] = a + myR; myA = AR[r]; }
+        // kRegAR: selects, not conditional stores -- the compiler merges the two conditional stores
+        // into one store through a selected address, which keeps AR in a scratch array.  In registers
+        // the out-of-line dense path clobbers more of its caller's registers, which the kernels where
+        // it is cold (C2, C3) pay for in spills around their hot loop; where it is hot (the helper-wave
+        // kernel, C4's contacts every step) the register form is the faster one
+        if constexpr (kRegAR) {
+          if constexpr (c == r) {
+            AR[r] = lane == r ? a + myR : AR[r];
+            myA = lane == r ? AR[r] : myA;
+          } else {
+            AR[c] = lane == r ? a : AR[c];
+            AR[r] = lane == c ? a : AR[r];
+          }
         } else {
-          if (lane == r) AR[c] = a;
-          if (lane == c) AR[r] = a;
+          if constexpr (c == r) {
+            if (lane == r) { AR[r] = a + myR; myA = AR[r]; }
+          } else {
+            if (lane == r) AR[c] = a;
+            if (lane == c) AR[r] = a;
+          }
         }
       }
     });
   });
+  SUB_ADD(PH_CON_DEL, t_p);
+  t_p = SUB_T();
   // warm start: forces of mj_constraintUpdate at qacc_warmstart, kept if the dual cost
   // f' (0.5 AR f + b) is negative.  Lane r owns row r: it alone computes the row's force, which every
   // lane then takes from it by broadcast
@@ -3038,6 +3058,8 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   unroll<KR>([&](auto rc) { ARn[decltype(rc)::value] = nia * AR[decltype(rc)::value]; });
   float mylo = (myfl > 0 ? -myfl : 0.0f) - myf, myhi = (myfl > 0 ? myfl : __builtin_inff()) - myf;
   int nit = 0;  // sweeps done (mjData.solver_niter)
+  SUB_ADD(PH_CON_WARM, t_p);
+  t_p = SUB_T();
   // the sweep is unrolled to the wave's row count rounded up to 4 (rows past rmax are the zero rows,
   // which never move): no per-row bound tests inside the sweep
   auto sweeps = [&](auto nc) {
@@ -3063,6 +3085,7 @@ __device__ __forceinline__ float pgs_small16(const DevModel& m, lfloat* s, const
   else if (KR <= 8 || rmax <= 8) sweeps(std::integral_constant<int, (KR < 8 ? KR : 8)>{});
   else if (KR <= 12 || rmax <= 12) sweeps(std::integral_constant<int, (KR < 12 ? KR : 12)>{});
   else sweeps(std::integral_constant<int, KR>{});
+  SUB_ADD(PH_REC_ROWS, t_p);
   myf = (myfl > 0 ? -myfl : 0.0f) - mylo;
   float f[KR];
   unroll<KR>([&](auto rc) { f[decltype(rc)::value] = rowb<decltype(rc)::value>(myf); });
@@ -5488,12 +5511,12 @@ __device__ __forceinline__ float primal_small16(ENV_PARAMS, const gfloat* J, gfl
   return dof ? qa : 0.0f;
 }
 
-template <int G, bool kPrimal = false>
+template <int G, bool kPrimal = false, bool kHot = false>
 __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_nefc = -1);
 template <int G>
 __device__ int dense_rows(ENV_PARAMS, int ncon);
 
-template <int G, bool kPrimal = false>
+template <int G, bool kPrimal = false, bool kHot = false>
 __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s, int pre_nefc = -1) {
   ENV_UNPACK;
   if constexpr (G == 64) {
@@ -5583,7 +5606,13 @@ __device__ MRS_PHASE float constraints(ENV_PARAMS, int ncon, float qacc_s, int p
   // rows with contacts or active joint limits: the dense row path, out of line -- cold in C3's
   // steady state, and keeping it out of the inlined step loop keeps the hot code footprint small
   float qa;
-  [[clang::noinline]] qa = constraints_dense<G, kPrimal>(ENV_ARGS, ncon, qacc_s, pre_nefc);
+#ifdef MRS_DENSE_INLINE_HOT
+  if constexpr (kHot) {
+    [[clang::always_inline]] qa = constraints_dense<G, kPrimal, kHot>(ENV_ARGS, ncon, qacc_s, pre_nefc);
+    return qa;
+  }
+#endif
+  [[clang::noinline]] qa = constraints_dense<G, kPrimal, kHot>(ENV_ARGS, ncon, qacc_s, pre_nefc);
   return qa;
 }
 
@@ -5987,7 +6016,7 @@ __device__ int dense_rows(ENV_PARAMS, int ncon) {
   return nefc;
 }
 
-template <int G, bool kPrimal>
+template <int G, bool kPrimal, bool kHot>
 __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_nefc) {
   ENV_UNPACK;
   if constexpr (G == 64) ncon = uniform_int(ncon);
@@ -6111,10 +6140,10 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_n
       // exceed the row count: a free body with one contact, an arm with one active limit)
       auto solve = [&](auto kv) {
         constexpr int KV = decltype(kv)::value;
-        if (rmax <= 4) return pgs_small16<false, 4, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
-        if (rmax <= 8) return pgs_small16<false, 8, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
-        if (rmax <= 12) return pgs_small16<false, 12, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
-        return pgs_small16<false, 16, KV>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        if (rmax <= 4) return pgs_small16<false, 4, KV, kHot>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        if (rmax <= 8) return pgs_small16<false, 8, KV, kHot>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        if (rmax <= 12) return pgs_small16<false, 12, KV, kHot>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
+        return pgs_small16<false, 16, KV, kHot>(m, s, J, ff, nefc, rmax, my_R, my_aref, my_b, my_fl, qacc_s, lane);
       };
       float qa = nv <= 8 ? solve(std::integral_constant<int, 8>{}) : solve(std::integral_constant<int, 16>{});
       wsync();
@@ -7014,7 +7043,7 @@ __device__ __forceinline__ void cholesky_ih(ENV_PARAMS);
 
 // full forward pass; returns the contact count.  With acc_bad, *acc_bad is the group's vote on qacc
 // (mj_checkAcc), taken from the solver's lane-per-dof result in registers
-template <int G, bool kPrimal = false>
+template <int G, bool kPrimal = false, bool kHot = false>
 __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bool helper = false,
                                  bool* acc_bad = nullptr) {
   ENV_UNPACK;
@@ -7061,7 +7090,7 @@ __device__ MRS_PHASE int forward(ENV_PARAMS, gfloat* sensordata PH_ACC_PARAM, bo
     // no rows unless constraints() builds some (mrs_batch_get_efc), or the helper's
     scr[S.efc_n] = __int_as_float(pre_nefc >= 0 ? pre_nefc : 0);
   }
-  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = (constraints<G, kPrimal>(ENV_ARGS, ncon, qacc_s, pre_nefc)));
+  if (!(m.diag_skip & 4)) MRS_CALL(G, qacc = (constraints<G, kPrimal, kHot>(ENV_ARGS, ncon, qacc_s, pre_nefc)));
   PH_END(ph_acc, PH_CONSTR);
   if (lane < m.nv) s[L.qacc + lane] = qacc;
   if (acc_bad) *acc_bad = gany<G>(lane < m.nv && is_bad(qacc));
@@ -7562,7 +7591,7 @@ __global__ __launch_bounds__(64 * WavesPerBlock<G>::value, Occupancy<G>::waves) 
     gfloat* sd_step = sensordata;
 #endif
     bool acc_bad = false;
-    MRS_CALL(G, ncon = (forward<G, kPrimal>(ENV_ARGS, sd_step PH_ACC_ARG, helpers, &acc_bad)));
+    MRS_CALL(G, ncon = (forward<G, kPrimal, helpers>(ENV_ARGS, sd_step PH_ACC_ARG, helpers, &acc_bad)));
     if (helpers) helper_barrier(false);  // barrier B: this step's rays are stored
 #if MRS_EXT
     // rangefinders of a model with more than 32 ray geoms (sensors() leaves them to this call)
