@@ -65,6 +65,12 @@ def test_helper_configuration_per_batch_size(monkeypatch):
     lay = c4.layout()
     c4.close()
     assert lay["group"] == 16 and lay["waves_per_workgroup"] == 1 and lay["helper_waves"] == 1, lay
+    # between two and four physics waves per CU: one-wave workgroups without helpers (the helper
+    # kernels run at one wave per SIMD, so physics and helper waves must fit the SIMDs together)
+    mid = sim.Batch(sim.Model.load(ROOT / "scenes" / "mobile_base.xml"), 3072)
+    lay = mid.layout()
+    mid.close()
+    assert lay["group"] == 16 and lay["waves_per_workgroup"] == 1 and lay["helper_waves"] == 0, lay
     c3 = sim.Batch(sim.Model.load(ROOT / "scenes" / "arm7_lidar.xml"), 8192)
     lay = c3.layout()
     c3.close()
