@@ -1976,12 +1976,12 @@ void build_devmodel(BatchImpl& b, int max_con_req) {
   {
     const char* e = std::getenv("MRS_RAY_HELPERS");
     const bool want = e ? std::atoi(e) != 0 : true;
-    // (the PGS helper kernel runs at one wave per SIMD, step.hip MRS_HELPER_OCC: physics plus helper
+    // (the helper kernels run at one wave per SIMD, step.hip MRS_HELPER_OCC: physics plus helper
     // waves must fit the device's SIMDs at once, i.e. at most two physics waves per CU)
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b.device) != hipSuccess) cus = 0;
     const long waves = (static_cast<long>(b.n) * 16 + 63) / 64;
-    const bool fit = cus <= 0 || waves <= 2L * cus || m.solver != MRS_SOL_PGS;
+    const bool fit = cus <= 0 || waves <= 2L * cus;
     b.helpers = want && fit && b.group == 16 && b.wpb16 == 1 && !b.ext && d.nrf > 0 && d.nrgeom <= 32 &&
                 m.integrator != MRS_INT_RK4 && !(m.disableflags & MRS_DSBL_SENSOR) ? 1 : 0;
     // the integrator factor slot (implicit-damping Euler and implicitfast; the full implicit

@@ -7444,16 +7444,15 @@ struct Occupancy { static constexpr int waves = G == 64 ? MRS_G64_WAVES : (G == 
 // kHelpers: the G = 16 step kernel with ray helper waves (DevState::ray_helpers; its own instantiation,
 // so the kernels without helpers keep their code and registers -- the run-time switch alone cost C3 5%)
 template <int G, bool kForwardOnly, bool kPrimal = false, bool kHelpers = false>
-// the PGS helper-wave kernel at one wave per SIMD (up to 512 VGPRs: the physics wave keeps its values
-// in registers around the out-of-line dense constraint path instead of spilling them; C4 31.5 ->
-// 32.5 M, same-box A/B; the Newton / CG helper kernel measured 1.5 % slower so and keeps two):
-// batch.hip takes helpers for PGS models only while physics and helper waves together fit one per
+// the helper-wave kernels at one wave per SIMD (up to 512 VGPRs: the physics wave keeps its values in
+// registers around the out-of-line dense constraint path instead of spilling them, and the frames
+// rendered beside the steps overlap them better; C4 31.5 -> 32.5 M, under Newton 27.7 -> 28.1 M,
+// same-box A/B): batch.hip takes helpers only while physics and helper waves together fit one per
 // SIMD
 #ifndef MRS_HELPER_OCC
 #define MRS_HELPER_OCC 1
 #endif
-__global__ __launch_bounds__(64 * WavesPerBlock<G>::value,
-                             kHelpers && !kPrimal ? MRS_HELPER_OCC : Occupancy<G>::waves) void step_kernel(
+__global__ __launch_bounds__(64 * WavesPerBlock<G>::value, kHelpers ? MRS_HELPER_OCC : Occupancy<G>::waves) void step_kernel(
     const DevModel* __restrict__ mp, DevState st, int n_envs, int n_steps) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int kEnvsPerBlock = G == 16 ? 4 * st.wpb16 : WavesPerBlock<G>::value * 64 / G;
