@@ -6043,7 +6043,9 @@ __device__ float constraints_dense(ENV_PARAMS, int ncon, float qacc_s, int pre_n
     return qacc_s;
   }
   // --- impedance, R, aref, M^-1 J', ARii, b (lane per row); the primal solvers need R and aref only
-  const bool primal = m.solver != MRS_SOL_PGS;
+  // (kPrimal: the kernel instantiated for Newton / CG models, so the dual PGS paths below are not
+  // compiled into it)
+  const bool primal = kPrimal || m.solver != MRS_SOL_PGS;
   // register-resident solvers (dual PGS or primal) for small systems; elliptic blocks take the
   // generic paths below
   const bool small = G == 16 && nefc <= 16 && !(m.cone == MRS_CONE_ELLIPTIC && ncon > 0);
