@@ -329,7 +329,10 @@ def main():
     rend_async, rend_async_ms = [False], []
 
     def period(p: int, timed: bool):
-        batch.set_ctrl_device(d_table[p].data_ptr())
+        # the period's actions, resident in HBM, bound as the launch's ctrl source (zero-copy
+        # mrs_batch_bind_ctrl_device: the kernel loads them at launch start; no copy op between
+        # launches)
+        batch.bind_ctrl_device(d_table[p].data_ptr())
         e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
         if e:
             e[0].record(stream)

@@ -108,6 +108,12 @@ int mrs_batch_get_field(mrs_batch* b, int field, double* host, int env0, int n);
 void* mrs_batch_device_ptr(mrs_batch* b, int field);
 /* copy ctrl for all envs from a device buffer [n_envs][nu] fp32 (device-resident actions) */
 int mrs_batch_set_ctrl_device(mrs_batch* b, const float* d_ctrl);
+/* zero-copy form of the same write (a policy's output tensor as the sim's ctrl): the following step
+ * and forward launches read ctrl from the caller's device buffer [n_envs][nu] fp32, stream-ordered
+ * on the batch stream, until another buffer is bound, NULL is bound, or ctrl is set by
+ * mrs_batch_set_field / mrs_batch_set_ctrl_device (which return to the batch's own buffer).  Reads
+ * of the ctrl field return the bound buffer's values.  The buffer must stay valid while bound. */
+int mrs_batch_bind_ctrl_device(mrs_batch* b, const float* d_ctrl);
 
 /* replaces mj_step (src/mujoco_system_interface.cpp:1691,1731): advance every env n_steps times,
  * fused in one launch; ctrl / qfrc_applied are held constant (zero-order hold) across the n steps,

@@ -221,6 +221,13 @@ int mrs_batch_set_ctrl_device(mrs_batch* b, const float* d_ctrl) {
   });
 }
 
+int mrs_batch_bind_ctrl_device(mrs_batch* b, const float* d_ctrl) {
+  return guarded([&] {
+    if (!b) throw std::invalid_argument("null batch");
+    mrs::batch_bind_ctrl_device(b->impl, d_ctrl);
+  });
+}
+
 int mrs_batch_step(mrs_batch* b, int n_steps) {
   return guarded([&] {
     if (!b) throw std::invalid_argument("null batch");

@@ -910,6 +910,9 @@ struct BatchImpl {
   LdsLayout& L = dm.L;
   ScratchLayout& S = dm.S;
   DevState st{};
+  // a caller's device buffer [n][nu] the step launches read ctrl from (batch_bind_ctrl_device; null:
+  // st.ctrl, the batch's own buffer)
+  const float* ctrl_bound = nullptr;
   void* dblock_f = nullptr;
   void* dblock_i = nullptr;
   std::vector<void*> allocs;
@@ -2220,6 +2223,7 @@ void batch_set(BatchImpl* b, int field, const double* host, int env0, int n) {
   int dim = field_dim(m, field);
   if (dim < 0) throw std::invalid_argument("unknown field");
   if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
+  if (field == MRS_FIELD_CTRL) b->ctrl_bound = nullptr;  // (host ctrl replaces a bound buffer)
   if (n == 0 || dim == 0) return;
   HIP_CHECK(hipSetDevice(b->device));
   const size_t cnt = static_cast<size_t>(n) * dim;
@@ -2252,7 +2256,8 @@ void batch_get(BatchImpl* b, int field, double* host, int env0, int n) {
   if (n == 0 || dim == 0) return;
   HIP_CHECK(hipSetDevice(b->device));
   const size_t cnt = static_cast<size_t>(n) * dim;
-  const char* src = static_cast<const char*>(field_ptr(*b, field));
+  const char* src = field == MRS_FIELD_CTRL && b->ctrl_bound ? reinterpret_cast<const char*>(b->ctrl_bound)
+                                                               : static_cast<const char*>(field_ptr(*b, field));
   if (field == MRS_FIELD_TIME) {
     HIP_CHECK(hipMemcpyAsync(host, src + sizeof(double) * env0, cnt * sizeof(double), hipMemcpyDeviceToHost, b->stream));
     HIP_CHECK(hipStreamSynchronize(b->stream));
@@ -2273,8 +2278,11 @@ void batch_get(BatchImpl* b, int field, double* host, int env0, int n) {
 
 void* batch_device_ptr(BatchImpl* b, int field) { return field_ptr(*b, field); }
 
+void batch_bind_ctrl_device(BatchImpl* b, const float* d_ctrl) { b->ctrl_bound = d_ctrl; }
+
 void batch_set_ctrl_device(BatchImpl* b, const float* d_ctrl) {
   const Model& m = *b->model;
+  b->ctrl_bound = nullptr;
   if (m.nu == 0) return;
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipMemcpyAsync(b->st.ctrl, d_ctrl, static_cast<size_t>(b->n) * m.nu * sizeof(float),
@@ -2285,7 +2293,9 @@ void batch_launch(BatchImpl* b, int n_steps, bool forward_only) {
   if (n_steps < 1) throw std::invalid_argument("n_steps must be positive");
   HIP_CHECK(hipSetDevice(b->device));
   HIP_CHECK(hipEventRecord(b->ev0[0], b->stream));
-  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, b->st, b->n, n_steps, forward_only, b->group,
+  DevState st = b->st;
+  if (b->ctrl_bound) st.ctrl = const_cast<float*>(b->ctrl_bound);  // (read only: loaded at launch start)
+  HIP_CHECK(launch_step(b->d_dm, b->L.total, b->dm.shr_total, st, b->n, n_steps, forward_only, b->group,
                         b->model->solver != MRS_SOL_PGS, b->ext, b->stream));
   HIP_CHECK(hipEventRecord(b->ev1[0], b->stream));
   b->ev_valid[0] = true;
@@ -2508,7 +2518,9 @@ void batch_get_field_device(BatchImpl* b, int field, float* d_out, int env0, int
   if (env0 < 0 || n < 0 || env0 + n > b->n) throw std::invalid_argument("env range out of bounds");
   if (n == 0 || dim == 0) return;
   HIP_CHECK(hipSetDevice(b->device));
-  const float* src = static_cast<const float*>(field_ptr(*b, field)) + static_cast<size_t>(env0) * dim;
+  const float* base = field == MRS_FIELD_CTRL && b->ctrl_bound ? b->ctrl_bound
+                                                               : static_cast<const float*>(field_ptr(*b, field));
+  const float* src = base + static_cast<size_t>(env0) * dim;
   HIP_CHECK(hipMemcpyAsync(d_out, src, static_cast<size_t>(n) * dim * sizeof(float), hipMemcpyDeviceToDevice,
                            b->stream));
 }

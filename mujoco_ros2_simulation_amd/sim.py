@@ -205,6 +205,7 @@ def lib() -> C.CDLL:
         L.mrs_batch_device_ptr.restype = C.c_void_p
         L.mrs_batch_device_ptr.argtypes = [C.c_void_p, C.c_int]
         L.mrs_batch_set_ctrl_device.argtypes = [C.c_void_p, C.c_void_p]
+        L.mrs_batch_bind_ctrl_device.argtypes = [C.c_void_p, C.c_void_p]
         L.mrs_batch_step.argtypes = [C.c_void_p, C.c_int]
         L.mrs_batch_forward.argtypes = [C.c_void_p]
         L.mrs_batch_render_depth.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -383,6 +384,11 @@ class Batch:
 
     def set_ctrl_device(self, ptr: int) -> None:
         _check(lib().mrs_batch_set_ctrl_device(self._h, C.c_void_p(ptr)))
+
+    def bind_ctrl_device(self, ptr: int | None) -> None:
+        """zero-copy ctrl: the following launches read ctrl from this device buffer [n][nu] fp32
+        (None: the batch's own buffer again; set / set_ctrl_device also return to it)"""
+        _check(lib().mrs_batch_bind_ctrl_device(self._h, C.c_void_p(ptr) if ptr else None))
 
     def set_stream(self, stream_ptr: int | None) -> None:
         _check(lib().mrs_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
