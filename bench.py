@@ -213,6 +213,7 @@ def run_c1(args):
     # unpaced: synchronous controller cycles
     s = system(physics_thread="false")
     bh = s.batch_handle()
+    sim.lib().mrs_batch_set_timing(bh, 3)  # (the kernel time of each cycle below)
     for _ in range(args.warmup):
         s.cycle(ctrl_period, args.period)
     kms = []
@@ -315,6 +316,9 @@ def main():
     stream = torch.cuda.Stream(device=local)
     batch = sim.Batch(model, n, device=local)
     batch.set_stream(stream.cuda_stream)
+    # step launches are bracketed by this script's own HIP events (below), not by the batch's (a
+    # second pair around every launch cost ~10 us, mrs_batch_set_timing); frames are timed by the batch
+    batch.set_timing(2)
     batch.set(sim.FIELD_QPOS, synth.initial_qpos(model, env_ids))
     gather = None
     if world > 1 and not args.no_gather:

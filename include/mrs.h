@@ -166,8 +166,12 @@ int mrs_batch_get_field_device(mrs_batch* b, int field, float* d_out, int env0, 
 /* wait for all queued batch work */
 int mrs_batch_sync(mrs_batch* b);
 /* duration in ms of the last step / render kernel measured with HIP events on the batch stream
- * (kind 0 = step, 1 = depth), -1 if unavailable */
+ * (kind 0 = step, 1 = depth), -1 if unavailable (no such launch yet, or its kind is not timed) */
 double mrs_batch_last_kernel_ms(mrs_batch* b, int kind);
+/* which launches the batch brackets with its own HIP events for mrs_batch_last_kernel_ms: bit 0 step
+ * launches, bit 1 frames (default 2: frames only).  A timed step launch costs ~10 us (a C3 10-step
+ * launch 0.420 vs 0.410 ms), so step launches are timed only when asked for */
+int mrs_batch_set_timing(mrs_batch* b, int mask);
 /* diagnostics (no reference counterpart): per-phase wave-cycle totals of the step kernel since the
  * last reset, in phase order kinematics, com_pos, make_M, cholesky, com_vel, rne, smooth_forces,
  * collision, constraints, sensors, integrate, checks.  Only a library built with

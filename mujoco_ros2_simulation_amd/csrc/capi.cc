@@ -317,6 +317,13 @@ int mrs_batch_sync(mrs_batch* b) {
   });
 }
 
+int mrs_batch_set_timing(mrs_batch* b, int mask) {
+  return guarded([&] {
+    if (!b || mask < 0 || mask > 3) throw std::invalid_argument("timing mask must be 0..3");
+    mrs::batch_set_timing(b->impl, mask);
+  });
+}
+
 double mrs_batch_last_kernel_ms(mrs_batch* b, int kind) {
   double ms = -1;
   guarded([&] {

@@ -23,6 +23,7 @@ void batch_get(BatchImpl* b, int field, double* host, int env0, int n);
 void* batch_device_ptr(BatchImpl* b, int field);
 void batch_set_ctrl_device(BatchImpl* b, const float* d_ctrl);
 void batch_bind_ctrl_device(BatchImpl* b, const float* d_ctrl);  // zero-copy ctrl source (null: own buffer)
+void batch_set_timing(BatchImpl* b, int mask);  // launches timed for batch_last_kernel_ms (bit 0 step, 1 frames)
 void batch_launch(BatchImpl* b, int n_steps, bool forward_only);
 // rgb (may be null): n * H * W * 3 bytes, same host/device side as out
 void batch_render_depth(BatchImpl* b, int cam, int env0, int n, float* out, bool device_out, unsigned char* rgb = nullptr);

@@ -206,6 +206,7 @@ def lib() -> C.CDLL:
         L.mrs_batch_device_ptr.argtypes = [C.c_void_p, C.c_int]
         L.mrs_batch_set_ctrl_device.argtypes = [C.c_void_p, C.c_void_p]
         L.mrs_batch_bind_ctrl_device.argtypes = [C.c_void_p, C.c_void_p]
+        L.mrs_batch_set_timing.argtypes = [C.c_void_p, C.c_int]
         L.mrs_batch_step.argtypes = [C.c_void_p, C.c_int]
         L.mrs_batch_forward.argtypes = [C.c_void_p]
         L.mrs_batch_render_depth.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -452,6 +453,10 @@ class Batch:
         """fp32 rows of `field` into a device buffer [n, dim], asynchronous on the batch stream"""
         n = self.n - env0 if n is None else n
         _check(lib().mrs_batch_get_field_device(self._h, field, C.c_void_p(dptr), env0, n))
+
+    def set_timing(self, mask: int) -> None:
+        """launches bracketed by the batch's own HIP events (bit 0 step, bit 1 frames; default 2)"""
+        _check(lib().mrs_batch_set_timing(self._h, mask))
 
     def last_kernel_ms(self, kind: int = 0) -> float:
         return lib().mrs_batch_last_kernel_ms(self._h, kind)

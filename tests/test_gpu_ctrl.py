@@ -59,3 +59,25 @@ def test_device_ctrl_paths_match_host_ctrl(scene, n):
             b.bind_ctrl_device(None)
             assert np.array_equal(b.get(sim.FIELD_CTRL), zero)
         b.close()
+
+
+def test_launch_timing_mask():
+    """mrs_batch_set_timing: step launches timed by the batch's own events only with bit 0 (off by
+    default; bench.py brackets launches itself), frames with bit 1; untimed kinds report -1"""
+    model = sim.Model.load(ROOT / "scenes" / "arm7_lidar.xml")
+    b = sim.Batch(model, 16)
+    b.step(10)
+    assert b.last_kernel_ms(0) == -1  # default: frames only
+    b.set_timing(3)
+    b.step(10)
+    assert b.last_kernel_ms(0) > 0
+    b.set_timing(2)
+    assert b.last_kernel_ms(0) == -1
+    b.step(10)
+    assert b.last_kernel_ms(0) == -1
+    b.set_timing(3)
+    b.step(10)
+    assert b.last_kernel_ms(0) > 0
+    with pytest.raises(sim.MrsError):
+        b.set_timing(4)
+    b.close()
